@@ -1,0 +1,176 @@
+/*
+ * recsys_hip.h -- C ABI of librecsys_hip.so, the MI355X (gfx950) hot path for
+ * SASRec / BERT4Rec training.
+ *
+ * The reference (Furyton/Recommender-Baseline-Model, NerualNetwork/bert4rec&sas4rec,
+ * "BS/" below) has no native code and no FFI: every op on its hot path is a
+ * stock PyTorch module call.  Each entry point here replaces the reference
+ * call(s) cited on it; the Python host side (rbm_amd.ops, bound with ctypes)
+ * keeps the reference's model/trainer API on top.
+ *
+ * Conventions (every function):
+ *   - raw device pointers + sizes, plus a hipStream_t passed as void*; the
+ *     caller passes torch.cuda.current_stream().cuda_stream;
+ *   - nothing is allocated or freed; every buffer, including workspace, is
+ *     owned by the caller (graph-capturable: no sync, no malloc);
+ *   - returns 0 on success, a hipError_t value, or RS_ERR_* (1001 bad argument,
+ *     1002 unsupported shape/dtype);
+ *   - dtype: 0 = fp32 (parity mode: exact f32-input MFMA), 1 = bf16 (storage
+ *     and MFMA operands; fp32 accumulate).  Gradients, LN/softmax statistics,
+ *     biases, LN affine params and the loss are always fp32.
+ *   - ids are int64 (the reference feeds torch.LongTensor / int64 numpy).
+ */
+#ifndef RECSYS_HIP_H
+#define RECSYS_HIP_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RS_ERR_ARG 1001
+#define RS_ERR_UNSUPPORTED 1002
+
+/* Fused GEMM epilogue, applied per output element in this order:
+ *   v = alpha*acc (+ bias[n])
+ *   act: 1 relu / 2 gelu_tanh (pre-activation stored to aux_out if set),
+ *        3 relu_bwd (v *= aux>0), 4 gelu_bwd (v *= gelu'(aux))
+ *   dropout: v *= keep(drop_seed, m*drop_ld+n) / (1-drop_p)
+ *   v += resid[m*ldres+n];  v *= (rowmask_ids[m] != 0);  v += C (accumulate)    */
+typedef struct rs_epilogue {
+  const float* bias;
+  float alpha;
+  int act;
+  const void* aux;
+  void* aux_out;
+  int64_t ldaux;
+  float drop_p;
+  uint64_t drop_seed;          /* site salt */
+  const uint64_t* seed_base;   /* device step seed (nullable) */
+  int64_t drop_ld;
+  const void* resid;
+  int64_t ldres;
+  const int64_t* rowmask_ids;
+  int accumulate;
+} rs_epilogue;
+
+/* C[M,N] = epi(A . B^T).  a_kmajor: A(m,k) at A[k*lda+m] (else A[m*lda+k]);
+ * b_kmajor: B(n,k) at B[k*ldb+n] (else B[n*ldb+k]).  c_f32 selects an fp32 C.
+ * split_k > 1 writes raw fp32 partials to slab[split_k][M][N] (epi ignored);
+ * finish with rs_reduce_slabs.
+ * Replaces: nn.Linear / nn.Conv1d(k=1) forward and autograd backward
+ *   (BS/models/sas_model/sas.py:10-17, torch F.multi_head_attention_forward
+ *   in_proj/out_proj via sas.py:45-47,75; BS/models/bert_modules/attention/
+ *   multi_head.py:18-19,29,40; utils/feed_forward.py:10-16; BS/models/bert.py:10,16). */
+int rs_gemm(int dtype, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
+            const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int c_f32,
+            const rs_epilogue* epi, int split_k, float* slab, void* stream);
+
+/* out[i] (+)= sum_z slab[z*n+i], fixed order (deterministic split-K finish). */
+int rs_reduce_slabs(const float* slab, int splits, int64_t n, float* out, int accumulate, void* stream);
+
+/* out[n] (+)= sum_m X[m*ldx+n] over M rows (bias gradients).  ws: >= 64*N floats. */
+int rs_colsum(int dtype, const void* X, int64_t M, int64_t N, int64_t ldx, float* ws, float* out,
+              int accumulate, void* stream);
+
+/* Embedding stage.  mode 0 = SAS (BS/models/sas_model/sas.py:60-67):
+ *   x = table[ids]*scale + pos[t]; dropout; x *= (ids != 0)
+ * mode 1 = BERT (BS/models/bert_modules/embedding/bert.py:29-31):
+ *   x = table[ids] + pos[t]; dropout.        t = row % T, rows = B*T. */
+int rs_embed_fwd(int dtype, int mode, const int64_t* ids, int64_t rows, int64_t T, const void* table,
+                 const void* pos, int64_t d, float scale, float drop_p, uint64_t seed, const uint64_t* seed_base,
+                 void* out, void* stream);
+/* dtable[ids[r]] += dX*mask*scale (rows with id 0 skipped: padding_idx=0, fp32 atomics);
+ * dpos[t] (+)= sum_b dX[b,t] * mask (deterministic; accumulate flag). */
+int rs_embed_bwd(int dtype, int mode, const int64_t* ids, int64_t rows, int64_t T, const void* dx,
+                 int64_t d, float scale, float drop_p, uint64_t seed, const uint64_t* seed_base,
+                 float* dtable, float* dpos, int accumulate_pos, void* stream);
+
+/* LayerNorm over rows of d.  variant 0 = torch.nn.LayerNorm (biased var,
+ * eps in sqrt; BS/models/sas_model/sas.py:39,42,50); variant 1 = BERT custom
+ * a2*(x-mean)/(std_unbiased+eps)+b2 (BS/models/bert_modules/utils/layer_norm.py:14-17).
+ * Saves mean[M] and rinv[M] (1/sqrt(var+eps), or 1/(std+eps)). */
+int rs_layernorm_fwd(int dtype, int variant, const void* X, int64_t ldx, int64_t M, int64_t d,
+                     const float* gamma, const float* beta, float eps, void* Y, int64_t ldy,
+                     float* mean, float* rinv, void* stream);
+/* dX (+)= LN backward; dgamma/dbeta (+)= column sums (deterministic, ws >= 2*d*256 floats). */
+int rs_layernorm_bwd(int dtype, int variant, const void* X, int64_t ldx, const void* dY, int64_t lddy,
+                     int64_t M, int64_t d, const float* gamma, const float* mean, const float* rinv, float eps,
+                     void* dX, int64_t lddx, int accumulate_dx, float* dgamma, float* dbeta, float* ws,
+                     void* stream);
+
+/* Fused scaled-dot-product attention per (sequence, head), T keys, head dim Dh.
+ * q/k/v/o rows are tokens (b*T + t); head h occupies columns [h*Dh, (h+1)*Dh).
+ * mask_kind 0 = causal, -inf above the diagonal (SAS, sas.py:70 + torch MHA baddbmm);
+ * mask_kind 1 = key padding, scores of keys with ids==0 replaced by -1e9 (BERT,
+ * bert_modules/bert.py:38 + attention/single.py:28).  S = scale * q.k^T;
+ * P = softmax(S); P = dropout(P); O = P.v.  lse[(b*H+h)*T + t] = row logsumexp. */
+int rs_attn_fwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t Dh, const void* q, int64_t ldq,
+                const void* k, int64_t ldk, const void* v, int64_t ldv, void* o, int64_t ldo, float* lse,
+                float scale, int mask_kind, const int64_t* ids, float drop_p, uint64_t seed,
+                const uint64_t* seed_base, void* stream);
+/* Backward: dq, dk, dv (overwritten).  ws: >= B*H*T floats (row deltas). */
+int rs_attn_bwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t Dh, const void* q, int64_t ldq,
+                const void* k, int64_t ldk, const void* v, int64_t ldv, const void* o, int64_t ldo,
+                const void* dout, int64_t lddo, const float* lse, void* dq, int64_t lddq, void* dk,
+                int64_t lddk, void* dv, int64_t lddv, float scale, int mask_kind, const int64_t* ids,
+                float drop_p, uint64_t seed, const uint64_t* seed_base, float* ws, void* stream);
+
+/* SAS sampled tied logits (sas.py:93-100): pl[m] = <f[m], E[pos[m]]>, nl likewise (fp32 out). */
+int rs_sampled_logits_fwd(int dtype, const void* f, int64_t M, int64_t d, const void* E,
+                          const int64_t* pos, const int64_t* neg, float* pl, float* nl, void* stream);
+/* df[m] (+)= dpl*E[pos]+dnl*E[neg];  dE[pos] += dpl*f, dE[neg] += dnl*f (id 0 skipped). */
+int rs_sampled_logits_bwd(int dtype, const void* f, int64_t M, int64_t d, const void* E,
+                          const int64_t* pos, const int64_t* neg, const float* dpl, const float* dnl,
+                          void* df, int accumulate_df, float* dE, void* stream);
+/* SAS loss (BS/trainers/sas.py:40-49): mean BCEWithLogits(pl,1) + mean BCEWithLogits(nl,0)
+ * over valid = (pos != 0).  Writes out[0] = sum of terms, out[1] = count, out[2] = loss
+ * (= pos_sum/count + neg_sum/count, count taken from count_override if non-null -- the DP
+ * global count), out[3] = neg_sum.  out needs 4 floats; ws >= 3*256 floats. */
+int rs_bce_fwd(const float* pl, const float* nl, const int64_t* pos, int64_t M, const float* count_override,
+               float* ws, float* out, void* stream);
+/* dpl, dnl = dloss * (sigmoid(x) - y) / count on valid positions, 0 elsewhere. */
+int rs_bce_bwd(const float* pl, const float* nl, const int64_t* pos, int64_t M, const float* count,
+               const float* dloss, float* dpl, float* dnl, void* stream);
+
+/* BERT loss (BS/trainers/bert.py:36-40): CrossEntropyLoss(ignore_index=0) over
+ * R rows of V1 fp32 logits (leading dim ldl).  out[0] = sum of -log p(label),
+ * out[1] = count, out[2] = loss (count_override as in rs_bce_fwd).
+ * ws >= 3*R floats (row lse + partials). */
+int rs_ce_fwd(const float* logits, int64_t R, int64_t V1, int64_t ldl, const int64_t* labels,
+              const float* count_override, float* ws, float* out, void* stream);
+/* dlogits (may alias logits) = dloss * (softmax - onehot)/count on labelled rows, 0 else; dtype of
+ * dlogits selected by dtype (fp32 or bf16 copy for the following GEMMs). */
+int rs_ce_bwd(int dtype, const float* logits, int64_t R, int64_t V1, int64_t ldl, const int64_t* labels,
+              const float* count, const float* dloss, const float* ws, void* dlogits, int64_t lddl,
+              void* stream);
+
+/* torch.optim.Adam step (BS/trainers/base.py:225-228; amsgrad=False) over a
+ * flat fp32 buffer.  hyper (device fp32[5]) = {lr, beta1, beta2, eps, weight_decay}.
+ * state (device double[4]): rs_adam_prepare does state[0] += 1 (the step count) and
+ * forms state[1] = lr/(1-beta1^step), state[2] = sqrt(1-beta2^step) in double
+ * precision, like torch's Python-float scalars.  rs_adam_step then updates
+ * p, m, v (and writes the bf16 copy of p to p_bf16 when non-null). */
+int rs_adam_prepare(double* state, const float* hyper, void* stream);
+int rs_adam_step(int64_t n, float* p, const float* g, float* m, float* v, void* p_bf16,
+                 const double* state, const float* hyper, void* stream);
+
+/* dst_bf16[i] = bf16(src[i]) */
+int rs_cast_bf16(int64_t n, const float* src, void* dst, void* stream);
+
+/* out = x * keep(seed, m*drop_ld+n)/(1-p) * (rowmask_ids[m] != 0); also (optional)
+ * out_masked = x * (rowmask != 0).  Elementwise backward helper for dropout sites
+ * that feed GEMMs (SAS FFN dropout2 + timeline mask, sas.py:17,84). */
+int rs_dropout_rowmask(int dtype, const void* x, int64_t M, int64_t N, int64_t ld, float drop_p,
+                       uint64_t seed, const uint64_t* seed_base, int64_t drop_ld, const int64_t* rowmask_ids,
+                       void* out, void* out_masked, void* stream);
+
+/* *seed_base += 1 on the stream (advances every dropout mask; capturable). */
+int rs_seed_advance(uint64_t* seed_base, void* stream);
+
+/* ABI version of this header/library pair. */
+int rs_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -46,7 +46,7 @@ def encode(P, x_ids, num_blocks, heads, p=0.0, hp=0.0, masks=None):
     masks = masks or {}
     B, T = x_ids.shape
     key_ok = (x_ids > 0).view(B, 1, 1, T)
-    x = P["bert.embedding.token.weight"][x_ids] + P["bert.embedding.position.pe.weight"].unsqueeze(0)
+    x = F.embedding(x_ids, P["bert.embedding.token.weight"], padding_idx=0) + P["bert.embedding.position.pe.weight"].unsqueeze(0)
     x = _dropout(x, hp, masks.get("emb"))
     d = x.shape[-1]
     dk = d // heads

@@ -49,7 +49,7 @@ def log2feats(P, log_seqs, num_blocks, heads, p=0.0, masks=None):
     E = P["sas.item_emb.weight"]
     d = E.shape[1]
     B, T = log_seqs.shape
-    x = E[log_seqs] * (d ** 0.5)                                   # :60-61
+    x = F.embedding(log_seqs, E, padding_idx=0) * (d ** 0.5)           # :60-61 (padding_idx=0, :30)
     x = x + P["sas.pos_emb.weight"][:T].unsqueeze(0)                # :62-63
     x = _dropout(x, p, masks.get("emb"))                            # :64
     keep = (log_seqs != 0).unsqueeze(-1).to(x.dtype)                # :66-67
@@ -88,7 +88,9 @@ def forward(P, log_seqs, pos_seqs, neg_seqs, num_blocks, heads, p=0.0, masks=Non
     """sas.py:90-105 -> (pos_logits, neg_logits), each (B,T)."""
     f = log2feats(P, log_seqs, num_blocks, heads, p, masks)
     E = P["sas.item_emb.weight"]
-    return (f * E[pos_seqs]).sum(-1), (f * E[neg_seqs]).sum(-1)
+    pe = F.embedding(pos_seqs, E, padding_idx=0)   # padding_idx=0 blocks the row-0 gradient (sas.py:30)
+    ne = F.embedding(neg_seqs, E, padding_idx=0)
+    return (f * pe).sum(-1), (f * ne).sum(-1)
 
 
 def predict(P, log_seqs, item_indices, num_blocks, heads):

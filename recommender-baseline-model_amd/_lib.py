@@ -1,0 +1,93 @@
+"""ctypes binding of librecsys_hip.so (C ABI: include/recsys_hip.h).
+
+The library is loaded on first use.  There is no fallback: if the .so is
+missing or a call returns non-zero, a RuntimeError is raised.  ``import torch``
+happens first so the process's single HIP runtime is torch's (the .so links
+against ``libamdhip64.so.7``, which the dynamic loader resolves to the copy
+torch already mapped).
+"""
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (must be loaded before the HIP library)
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "librecsys_hip.so")
+
+F32, BF16 = 0, 1
+
+i32, i64, u64, f32, vp = C.c_int, C.c_int64, C.c_uint64, C.c_float, C.c_void_p
+
+
+class Epilogue(C.Structure):
+    """Mirror of ``rs_epilogue`` (include/recsys_hip.h)."""
+    _fields_ = [
+        ("bias", vp), ("alpha", f32), ("act", i32),
+        ("aux", vp), ("aux_out", vp), ("ldaux", i64),
+        ("drop_p", f32), ("drop_seed", u64), ("seed_base", vp), ("drop_ld", i64),
+        ("resid", vp), ("ldres", i64),
+        ("rowmask_ids", vp), ("accumulate", i32),
+    ]
+
+
+ACT_NONE, ACT_RELU, ACT_GELU, ACT_RELU_BWD, ACT_GELU_BWD = 0, 1, 2, 3, 4
+
+# name -> argtypes (all return int)
+SIGNATURES = {
+    "rs_gemm": [i32, i32, i32, i64, i64, i64, vp, i64, vp, i64, vp, i64, i32, C.POINTER(Epilogue), i32, vp, vp],
+    "rs_reduce_slabs": [vp, i32, i64, vp, i32, vp],
+    "rs_colsum": [i32, vp, i64, i64, i64, vp, vp, i32, vp],
+    "rs_embed_fwd": [i32, i32, vp, i64, i64, vp, vp, i64, f32, f32, u64, vp, vp, vp],
+    "rs_embed_bwd": [i32, i32, vp, i64, i64, vp, i64, f32, f32, u64, vp, vp, vp, i32, vp],
+    "rs_layernorm_fwd": [i32, i32, vp, i64, i64, i64, vp, vp, f32, vp, i64, vp, vp, vp],
+    "rs_layernorm_bwd": [i32, i32, vp, i64, vp, i64, i64, i64, vp, vp, vp, f32, vp, i64, i32, vp, vp, vp, vp],
+    "rs_attn_fwd": [i32, i64, i64, i64, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp, f32, i32, vp, f32, u64, vp, vp],
+    "rs_attn_bwd": [i32, i64, i64, i64, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, i64,
+                    vp, i64, f32, i32, vp, f32, u64, vp, vp, vp],
+    "rs_sampled_logits_fwd": [i32, vp, i64, i64, vp, vp, vp, vp, vp, vp],
+    "rs_sampled_logits_bwd": [i32, vp, i64, i64, vp, vp, vp, vp, vp, vp, i32, vp, vp],
+    "rs_bce_fwd": [vp, vp, vp, i64, vp, vp, vp, vp],
+    "rs_bce_bwd": [vp, vp, vp, i64, vp, vp, vp, vp, vp],
+    "rs_ce_fwd": [vp, i64, i64, i64, vp, vp, vp, vp, vp],
+    "rs_ce_bwd": [i32, vp, i64, i64, i64, vp, vp, vp, vp, vp, i64, vp],
+    "rs_adam_prepare": [vp, vp, vp],
+    "rs_adam_step": [i64, vp, vp, vp, vp, vp, vp, vp, vp],
+    "rs_cast_bf16": [i64, vp, vp, vp],
+    "rs_dropout_rowmask": [i32, vp, i64, i64, i64, f32, u64, vp, i64, vp, vp, vp, vp],
+    "rs_seed_advance": [vp, vp],
+    "rs_abi_version": [],
+}
+
+_lib = None
+
+
+def lib():
+    """Load (once) and return the native library; raise if it is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"librecsys_hip.so not found at {LIB_PATH}; build it with "
+                "`python recommender-baseline-model_amd/build.py` (there is no CPU fallback)")
+        h = C.CDLL(LIB_PATH)
+        for name, argt in SIGNATURES.items():
+            fn = getattr(h, name)
+            fn.argtypes = argt
+            fn.restype = C.c_int
+        _lib = h
+    return _lib
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise RuntimeError(f"{name} failed with code {rc}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    return None if t is None else t.data_ptr()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream

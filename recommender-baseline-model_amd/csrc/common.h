@@ -1,0 +1,172 @@
+// Shared device helpers for the gfx950 (CDNA4, MI355X) recsys kernels.
+//
+// Storage dtypes: every activation / weight-copy kernel is templated on the
+// element type T in {float, __bf16}.  Arithmetic is always fp32 (MFMA fp32
+// accumulate; LN / softmax / loss statistics in fp32).  fp32 instantiations use
+// the exact f32-input MFMA (v_mfma_f32_16x16x4_f32, a bitwise k-ordered fmaf
+// chain) and are the parity mode; bf16 instantiations use v_mfma_f32_16x16x32_bf16.
+//
+// MFMA operand convention used by every kernel (16x16 output tile, 32-deep k
+// chunk): lane l holds A[row = l&15][k = 8*(l>>4) + j] and B[k = 8*(l>>4) + j][col = l&15]
+// for j = 0..7; the accumulator holds C[row = 4*(l>>4) + r][col = l&15], r = 0..3.
+// For bf16 this is one v_mfma_f32_16x16x32_bf16; for fp32 it is eight
+// v_mfma_f32_16x16x4_f32 (MFMA j consumes element j of every lane, i.e. the
+// k-subset {8g + j}), so one fragment layout serves both dtypes.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <algorithm>
+
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+
+#define RS_DTYPE_F32 0
+#define RS_DTYPE_BF16 1
+
+#define RS_OK 0
+#define RS_ERR_ARG 1001
+#define RS_ERR_UNSUPPORTED 1002
+
+#define WAVE 64
+
+__device__ __forceinline__ float to_f(float x) { return x; }
+__device__ __forceinline__ float to_f(__bf16 x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f(float x);
+template <> __device__ __forceinline__ float from_f<float>(float x) { return x; }
+template <> __device__ __forceinline__ __bf16 from_f<__bf16>(float x) { return (__bf16)x; }
+
+// ---------------------------------------------------------------- fragments
+template <typename T> struct Frag;
+template <> struct Frag<__bf16> { bf16x8 v; };
+template <> struct Frag<float> { float v[8]; };
+
+// 8 contiguous elements (16-B aligned for bf16, 16-B aligned pairs for f32)
+__device__ __forceinline__ void frag_load_vec(Frag<__bf16>& f, const __bf16* p) {
+  f.v = *reinterpret_cast<const bf16x8*>(p);
+}
+__device__ __forceinline__ void frag_load_vec(Frag<float>& f, const float* p) {
+  float4 a = *reinterpret_cast<const float4*>(p);
+  float4 b = *reinterpret_cast<const float4*>(p + 4);
+  f.v[0] = a.x; f.v[1] = a.y; f.v[2] = a.z; f.v[3] = a.w;
+  f.v[4] = b.x; f.v[5] = b.y; f.v[6] = b.z; f.v[7] = b.w;
+}
+// 8 elements with a stride
+__device__ __forceinline__ void frag_load_strided(Frag<__bf16>& f, const __bf16* p, int stride) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f.v[j] = p[j * stride];
+}
+__device__ __forceinline__ void frag_load_strided(Frag<float>& f, const float* p, int stride) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f.v[j] = p[j * stride];
+}
+__device__ __forceinline__ void frag_zero(Frag<__bf16>& f) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f.v[j] = (__bf16)0.0f;
+}
+__device__ __forceinline__ void frag_zero(Frag<float>& f) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f.v[j] = 0.0f;
+}
+__device__ __forceinline__ void frag_set(Frag<__bf16>& f, int j, float x) { f.v[j] = (__bf16)x; }
+__device__ __forceinline__ void frag_set(Frag<float>& f, int j, float x) { f.v[j] = x; }
+
+__device__ __forceinline__ f32x4 mma(const Frag<__bf16>& a, const Frag<__bf16>& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mma(const Frag<float>& a, const Frag<float>& b, f32x4 c) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[j], b.v[j], c, 0, 0, 0);
+  return c;
+}
+
+// ---------------------------------------------------------------- vectors
+// VEC = elements per 16-byte chunk
+template <typename T> struct Vec { static constexpr int N = 16 / sizeof(T); };
+
+template <typename T>
+__device__ __forceinline__ void load_chunk(float* out, const T* p);
+template <>
+__device__ __forceinline__ void load_chunk<float>(float* out, const float* p) {
+  float4 a = *reinterpret_cast<const float4*>(p);
+  out[0] = a.x; out[1] = a.y; out[2] = a.z; out[3] = a.w;
+}
+template <>
+__device__ __forceinline__ void load_chunk<__bf16>(float* out, const __bf16* p) {
+  bf16x8 a = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) out[j] = (float)a[j];
+}
+template <typename T>
+__device__ __forceinline__ void store_chunk(T* p, const float* in);
+template <>
+__device__ __forceinline__ void store_chunk<float>(float* p, const float* in) {
+  *reinterpret_cast<float4*>(p) = make_float4(in[0], in[1], in[2], in[3]);
+}
+template <>
+__device__ __forceinline__ void store_chunk<__bf16>(__bf16* p, const float* in) {
+  bf16x8 a;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = (__bf16)in[j];
+  *reinterpret_cast<bf16x8*>(p) = a;
+}
+
+// ---------------------------------------------------------------- reductions
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// reduce over the 16 lanes that share (l>>4) -- i.e. over the accumulator's columns
+__device__ __forceinline__ float group16_sum(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float group16_max(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---------------------------------------------------------------- dropout RNG
+// Counter-based: keep(seed, idx) is a pure function, so the backward pass
+// regenerates every mask instead of storing it.  splitmix64 finaliser.
+__device__ __forceinline__ uint32_t rng_u32(uint64_t seed, uint64_t ctr) {
+  uint64_t z = seed + ctr * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)(z >> 32);
+}
+// keep with probability 1-p; returns the multiplier (0 or 1/(1-p))
+__device__ __forceinline__ float drop_mul(float p, uint64_t seed, uint64_t idx) {
+  if (p <= 0.0f) return 1.0f;
+  uint32_t thr = (uint32_t)fminf(p * 4294967296.0f, 4294967295.0f);
+  return rng_u32(seed, idx) >= thr ? 1.0f / (1.0f - p) : 0.0f;
+}
+
+// effective per-site seed: host-side site salt mixed with the device-side step
+// seed (a device word advanced by rs_seed_advance, so graph replays re-draw masks)
+__device__ __forceinline__ uint64_t eff_seed(uint64_t salt, const uint64_t* base) {
+  return salt ^ ((base ? *base : 0ull) * 0xD1B54A32D192ED03ull);
+}
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k = 0.7978845608028654f;  // sqrt(2/pi)
+  return 0.5f * x * (1.0f + tanhf(k * (x + 0.044715f * x * x * x)));
+}
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  const float k = 0.7978845608028654f;
+  float u = k * (x + 0.044715f * x * x * x);
+  float t = tanhf(u);
+  return 0.5f * (1.0f + t) + 0.5f * x * (1.0f - t * t) * k * (1.0f + 3.0f * 0.044715f * x * x);
+}
+
+__host__ __device__ static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }

@@ -1,0 +1,175 @@
+// Optimizer and elementwise helpers (gfx950), all HBM-bound streaming kernels.
+//
+//   rs_adam_prepare / rs_adam_step   torch.optim.Adam as built in BS/trainers/base.py:225-228
+//                                    (one fused sweep over the flat fp32 parameter buffer;
+//                                    optionally emits the bf16 weight copy the GEMMs read)
+//   rs_cast_bf16                     fp32 master weights -> bf16 compute copy
+//   rs_colsum                        bias gradients (sum over token rows), deterministic
+//   rs_dropout_rowmask               dropout/timeline-mask backward for SAS FFN dropout2
+//                                    (BS/models/sas_model/sas.py:17,84)
+#include "common.h"
+#include "../../include/recsys_hip.h"
+
+__global__ void adam_prepare_kernel(double* state, const float* hyper) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const double step = state[0] + 1.0;
+  state[0] = step;
+  const double lr = hyper[0], b1 = hyper[1], b2 = hyper[2];
+  const double bc1 = 1.0 - pow(b1, step);
+  const double bc2 = 1.0 - pow(b2, step);
+  state[1] = lr / bc1;            // step_size
+  state[2] = sqrt(bc2);           // bias_correction2_sqrt
+}
+
+template <bool BF16OUT>
+__global__ __launch_bounds__(256) void adam_step_kernel(int64_t n, float* __restrict__ p, const float* __restrict__ g,
+                                                        float* __restrict__ m, float* __restrict__ v,
+                                                        __bf16* __restrict__ pb, const double* __restrict__ state,
+                                                        const float* __restrict__ hyper) {
+  const float b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
+  const float step_size = (float)state[1];
+  const float bc2s = (float)state[2];
+  const int64_t n4 = n / 4;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    float4 pp = reinterpret_cast<float4*>(p)[i];
+    float4 gg = reinterpret_cast<const float4*>(g)[i];
+    float4 mm = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    float* P = &pp.x; float* G = &gg.x; float* Mv = &mm.x; float* Vv = &vv.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float gj = G[j];
+      if (wd != 0.f) gj = gj + wd * P[j];
+      Mv[j] = Mv[j] + (1.f - b1) * (gj - Mv[j]);            // exp_avg.lerp_(grad, 1-beta1)
+      Vv[j] = Vv[j] * b2 + (1.f - b2) * gj * gj;            // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
+      const float denom = sqrtf(Vv[j]) / bc2s + eps;
+      P[j] = P[j] - step_size * (Mv[j] / denom);            // param.addcdiv_(exp_avg, denom, -step_size)
+    }
+    reinterpret_cast<float4*>(p)[i] = pp;
+    reinterpret_cast<float4*>(m)[i] = mm;
+    reinterpret_cast<float4*>(v)[i] = vv;
+    if (BF16OUT) {
+      bf16x4 o;
+      o[0] = (__bf16)P[0]; o[1] = (__bf16)P[1]; o[2] = (__bf16)P[2]; o[3] = (__bf16)P[3];
+      reinterpret_cast<bf16x4*>(pb)[i] = o;
+    }
+  }
+  // tail
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    const int64_t j = n4 * 4 + threadIdx.x;
+    float gj = g[j];
+    if (wd != 0.f) gj = gj + wd * p[j];
+    m[j] = m[j] + (1.f - b1) * (gj - m[j]);
+    v[j] = v[j] * b2 + (1.f - b2) * gj * gj;
+    const float denom = sqrtf(v[j]) / bc2s + eps;
+    p[j] = p[j] - step_size * (m[j] / denom);
+    if (BF16OUT) pb[j] = (__bf16)p[j];
+  }
+}
+
+__global__ __launch_bounds__(256) void cast_bf16_kernel(int64_t n, const float* __restrict__ src, __bf16* __restrict__ dst) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = (__bf16)src[i];
+}
+
+#define COLSUM_BLOCKS 64
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const T* __restrict__ X, int64_t M, int64_t N, int64_t ldx,
+                                                             float* __restrict__ ws) {
+  const int64_t rows_per = cdiv(M, (int64_t)gridDim.x);
+  const int64_t r0 = blockIdx.x * rows_per, r1 = min(M, r0 + rows_per);
+  for (int64_t c = threadIdx.x; c < N; c += blockDim.x) {
+    float s = 0.f;
+    for (int64_t r = r0; r < r1; ++r) s += to_f(X[r * ldx + c]);
+    ws[blockIdx.x * N + c] = s;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void dropout_rowmask_kernel(const T* __restrict__ x, int64_t M, int64_t N, int64_t ld,
+                                                              float p, uint64_t salt, const uint64_t* seed_base,
+                                                              int64_t drop_ld, const int64_t* __restrict__ ids,
+                                                              T* __restrict__ out, T* __restrict__ out_masked) {
+  const uint64_t seed = eff_seed(salt, seed_base);
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= M * N) return;
+  const int64_t m = i / N, c = i % N;
+  float v = to_f(x[m * ld + c]);
+  if (ids && ids[m] == 0) v = 0.f;
+  if (out_masked) out_masked[m * ld + c] = from_f<T>(v);
+  if (p > 0.f) v *= drop_mul(p, seed, (uint64_t)(m * drop_ld + c));
+  out[m * ld + c] = from_f<T>(v);
+}
+
+extern "C" {
+
+int rs_adam_prepare(double* state, const float* hyper, void* stream) {
+  hipLaunchKernelGGL(adam_prepare_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, state, hyper);
+  return (int)hipGetLastError();
+}
+
+int rs_adam_step(int64_t n, float* p, const float* g, float* m, float* v, void* p_bf16, const double* state,
+                 const float* hyper, void* stream) {
+  if (n <= 0 || ((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16) return RS_ERR_ARG;
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(cdiv(n / 4, 256), 8192));
+  hipStream_t s = (hipStream_t)stream;
+  if (p_bf16)
+    hipLaunchKernelGGL((adam_step_kernel<true>), dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
+                       (__bf16*)p_bf16, state, hyper);
+  else
+    hipLaunchKernelGGL((adam_step_kernel<false>), dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
+                       (__bf16*)nullptr, state, hyper);
+  return (int)hipGetLastError();
+}
+
+int rs_cast_bf16(int64_t n, const float* src, void* dst, void* stream) {
+  if (n <= 0) return RS_ERR_ARG;
+  const int64_t blocks = std::min<int64_t>(cdiv(n, 256), 8192);
+  hipLaunchKernelGGL(cast_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, n, src,
+                     (__bf16*)dst);
+  return (int)hipGetLastError();
+}
+
+int rs_reduce_slabs(const float* slab, int splits, int64_t n, float* out, int accumulate, void* stream);
+
+int rs_colsum(int dtype, const void* X, int64_t M, int64_t N, int64_t ldx, float* ws, float* out, int accumulate,
+              void* stream) {
+  if (M <= 0 || N <= 0) return RS_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int nblk = (int)std::min<int64_t>(COLSUM_BLOCKS, M);
+  if (dtype == RS_DTYPE_BF16)
+    hipLaunchKernelGGL((colsum_partial_kernel<__bf16>), dim3(nblk), dim3(256), 0, s, (const __bf16*)X, M, N, ldx, ws);
+  else
+    hipLaunchKernelGGL((colsum_partial_kernel<float>), dim3(nblk), dim3(256), 0, s, (const float*)X, M, N, ldx, ws);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  return rs_reduce_slabs(ws, nblk, N, out, accumulate, stream);
+}
+
+int rs_dropout_rowmask(int dtype, const void* x, int64_t M, int64_t N, int64_t ld, float drop_p, uint64_t seed,
+                       const uint64_t* seed_base, int64_t drop_ld, const int64_t* rowmask_ids, void* out,
+                       void* out_masked, void* stream) {
+  if (M <= 0 || N <= 0) return RS_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((unsigned)cdiv(M * N, 256));
+  if (dtype == RS_DTYPE_BF16)
+    hipLaunchKernelGGL((dropout_rowmask_kernel<__bf16>), grid, dim3(256), 0, s, (const __bf16*)x, M, N, ld, drop_p,
+                       seed, seed_base, drop_ld, rowmask_ids, (__bf16*)out, (__bf16*)out_masked);
+  else
+    hipLaunchKernelGGL((dropout_rowmask_kernel<float>), grid, dim3(256), 0, s, (const float*)x, M, N, ld, drop_p,
+                       seed, seed_base, drop_ld, rowmask_ids, (float*)out, (float*)out_masked);
+  return (int)hipGetLastError();
+}
+
+__global__ void seed_advance_kernel(uint64_t* s) {
+  if (threadIdx.x == 0) *s += 1;
+}
+
+int rs_seed_advance(uint64_t* seed_base, void* stream) {
+  hipLaunchKernelGGL(seed_advance_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, seed_base);
+  return (int)hipGetLastError();
+}
+
+int rs_abi_version(void) { return 1; }
+
+}  // extern "C"

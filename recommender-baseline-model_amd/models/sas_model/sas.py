@@ -1,0 +1,305 @@
+"""SASRec on the MI355X HIP path.
+
+Same constructor arguments, parameter modules, initialisation and
+``state_dict`` keys as the reference ``BS/models/sas_model/sas.py:23-57`` (the
+torch modules below are only parameter containers and initialisers: they never
+run), same ``forward``/``predict`` results (``sas.py:59-118``).  The math runs
+as HIP kernels through the C ABI, orchestrated by :class:`SASEngine`:
+
+forward (per step)                      kernels (include/recsys_hip.h)
+  x = emb*sqrt(d)+pos, drop, mask         rs_embed_fwd
+  per block: Q = LN1(x)                   rs_layernorm_fwd (variant 0, eps 1e-8)
+             q = Q Wq^T+bq; kv = x Wkv^T  rs_gemm x2 (MFMA)
+             o = attn(q, k, v) causal     rs_attn_fwd (mask_kind 0, dropout on P)
+             x1 = Q + o Wo^T + bo         rs_gemm (+bias+residual epilogue)
+             z = LN2(x1)                  rs_layernorm_fwd
+             h = relu(drop(z W1^T + b1))  rs_gemm (+bias+relu+dropout epilogue)
+             x = (drop(h W2^T+b2) + z)*m  rs_gemm (+bias+dropout+residual+rowmask)
+  f = LN(x); pl/nl = <f, E[pos/neg]>      rs_layernorm_fwd, rs_sampled_logits_fwd
+backward: the mirror image (rs_*_bwd, dgrad/wgrad GEMMs, split-K slabs).
+"""
+import math
+
+import torch
+import torch.nn as nn
+
+from ... import ops
+from ...engine_util import Workspace, as_ids, compute_dtype, require_cuda, site_salt
+from ...flat import FlatParams
+
+LN_EPS = 1e-8
+
+
+class PointWiseFeedForward(nn.Module):
+    """Parameter container mirroring ``sas.py:6-14`` (conv1 / conv2 = Conv1d(d, d, 1))."""
+
+    def __init__(self, hidden_units, dropout_rate):
+        super().__init__()
+        self.conv1 = nn.Conv1d(hidden_units, hidden_units, kernel_size=1)
+        self.conv2 = nn.Conv1d(hidden_units, hidden_units, kernel_size=1)
+        self.dropout_rate = dropout_rate
+
+
+class SAS(nn.Module):
+    def __init__(self, args):
+        super().__init__()
+        self.item_num = args.num_items
+        self.device = args.device
+        self.max_len = args.max_len
+        self.hidden = args.sas_hidden_units
+        self.num_blocks = args.sas_num_blocks
+        self.heads = args.sas_heads
+        self.dropout_rate = args.sas_dropout
+        self.cdtype = compute_dtype(args)
+        d = self.hidden
+        if d % self.heads:
+            raise ValueError("sas_hidden_units must be divisible by sas_heads")
+
+        self.item_emb = nn.Embedding(self.item_num + 1, d, padding_idx=0)
+        self.pos_emb = nn.Embedding(args.max_len, d)
+        self.attention_layernorms = nn.ModuleList()
+        self.attention_layers = nn.ModuleList()
+        self.forward_layernorms = nn.ModuleList()
+        self.forward_layers = nn.ModuleList()
+        self.last_layernorm = nn.LayerNorm(d, eps=LN_EPS)
+        for _ in range(self.num_blocks):
+            self.attention_layernorms.append(nn.LayerNorm(d, eps=LN_EPS))
+            self.attention_layers.append(nn.MultiheadAttention(d, self.heads, self.dropout_rate))
+            self.forward_layernorms.append(nn.LayerNorm(d, eps=LN_EPS))
+            self.forward_layers.append(PointWiseFeedForward(d, self.dropout_rate))
+
+        self._flat = None
+        self._engine = None
+        if torch.device(self.device).type == "cuda":
+            self.to(self.device)
+
+    # ---- flat-buffer management ------------------------------------------------------
+    def _apply(self, fn, recurse=True):
+        super()._apply(fn, recurse)
+        p = next(self.parameters())
+        self._flat = FlatParams(self, p.device) if p.device.type == "cuda" else None
+        self._engine = None
+        return self
+
+    def engine(self):
+        p = self.item_emb.weight
+        require_cuda(p.device)
+        if self._flat is None or not self._flat.is_bound(self):
+            self._flat = FlatParams(self, p.device)
+            self._engine = None
+        if self._engine is None:
+            self._engine = SASEngine(self, self._flat)
+        return self._engine
+
+    # ---- reference API ---------------------------------------------------------------
+    def forward(self, log_seqs, pos_seqs, neg_seqs):
+        eng = self.engine()
+        dev = self._flat.device
+        ids, pos, neg = as_ids(log_seqs, dev), as_ids(pos_seqs, dev), as_ids(neg_seqs, dev)
+        params = [p for _, p in self.named_parameters()]
+        return _SASFunction.apply(eng, ids, pos, neg, self.training, *params)
+
+    def log2feats(self, log_seqs):
+        eng = self.engine()
+        ids = as_ids(log_seqs, self._flat.device)
+        with torch.no_grad():
+            return eng.features(ids).clone()
+
+    @torch.no_grad()
+    def predict(self, log_seqs, item_indices):
+        eng = self.engine()
+        dev = self._flat.device
+        return eng.predict(as_ids(log_seqs, dev), as_ids(item_indices, dev))
+
+
+class _SASFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, engine, ids, pos, neg, training, *params):
+        engine.sync_compute_weights()
+        pl, nl, saved = engine.forward(ids, pos, neg, training)
+        ctx.engine = engine
+        ctx.saved = saved
+        return pl, nl
+
+    @staticmethod
+    def backward(ctx, dpl, dnl):
+        eng = ctx.engine
+        grad = torch.zeros(eng.flat.numel, dtype=torch.float32, device=eng.flat.device)
+        eng.backward(ctx.saved, dpl.contiguous().float(), dnl.contiguous().float(), grad)
+        ctx.saved = None
+        grads = [eng.flat.view(n, grad) for n in eng.flat.names]
+        return (None, None, None, None, None, *grads)
+
+
+class SASEngine:
+    """Owns workspaces and issues the HIP kernels of one SAS model."""
+
+    def __init__(self, model: SAS, flat: FlatParams):
+        self.m = model
+        self.flat = flat
+        self.d = model.hidden
+        self.L = model.num_blocks
+        self.H = model.heads
+        self.Dh = self.d // self.H
+        self.p = float(model.dropout_rate)
+        self.dt = model.cdtype
+        self.dev = flat.device
+        if self.dt == torch.bfloat16:
+            flat.enable_bf16()
+        self.ws = Workspace(self.dev)
+        self.seed_base = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        salt0 = int(torch.randint(0, 2 ** 62, (1,)).item())
+        self.salt = {"emb": site_salt(salt0, 0)}
+        for i in range(self.L):
+            self.salt[f"attn{i}"] = site_salt(salt0, 1 + 4 * i)
+            self.salt[f"ffn1_{i}"] = site_salt(salt0, 2 + 4 * i)
+            self.salt[f"ffn2_{i}"] = site_salt(salt0, 3 + 4 * i)
+
+    # compute-dtype weights
+    def sync_compute_weights(self):
+        if self.flat.bf16 is not None:
+            ops.cast_bf16(self.flat.data, self.flat.bf16)
+
+    def W(self, n):
+        return self.flat.cview(n)
+
+    def Wf(self, n):
+        return self.flat.view(n)
+
+    def _buf(self, name, shape, dtype=None):
+        return torch.empty(shape, dtype=dtype or self.dt, device=self.dev)
+
+    # ---- forward -------------------------------------------------------------------
+    def forward(self, ids, pos, neg, training, need_logits=True):
+        B, T = ids.shape
+        M, d, H, Dh, L = B * T, self.d, self.H, self.Dh, self.L
+        p = self.p if training else 0.0
+        if p > 0:
+            ops.seed_advance(self.seed_base)
+        sb = self.seed_base.clone()      # this step's masks, replayed by backward
+        e = self._buf
+        s = {"B": B, "T": T, "p": p, "ids": ids, "pos": pos, "neg": neg, "sb": sb,
+             "x": [], "Q": [], "mu1": [], "r1": [], "q": [], "kv": [], "o": [], "lse": [],
+             "x1": [], "z": [], "mu2": [], "r2": [], "h1": []}
+        x = e("x0", (M, d))
+        ops.embed_fwd(0, ids, T, self.W("item_emb.weight"), self.W("pos_emb.weight"), math.sqrt(d), p,
+                      self.salt["emb"], sb, x)
+        for i in range(L):
+            pre = f"attention_layers.{i}."
+            Q, mu1, r1 = e("Q", (M, d)), e("mu", (M,), torch.float32), e("r", (M,), torch.float32)
+            ops.layernorm_fwd(x, self.Wf(f"attention_layernorms.{i}.weight"),
+                              self.Wf(f"attention_layernorms.{i}.bias"), LN_EPS, Q, mu1, r1, 0)
+            Win, bin_ = self.W(pre + "in_proj_weight"), self.Wf(pre + "in_proj_bias")
+            q, kv = e("q", (M, d)), e("kv", (M, 2 * d))
+            ops.linear_fwd(Q, Win[:d], q, bias=bin_[:d])
+            ops.linear_fwd(x, Win[d:], kv, bias=bin_[d:])
+            o, lse = e("o", (M, d)), e("lse", (B * H * T,), torch.float32)
+            ops.attn_fwd(B, T, H, Dh, q, kv[:, :d], kv[:, d:], o, lse, 1.0 / math.sqrt(Dh), 0, ids, p,
+                         self.salt[f"attn{i}"], sb)
+            x1 = e("x1", (M, d))
+            ops.linear_fwd(o, self.W(pre + "out_proj.weight"), x1, bias=self.Wf(pre + "out_proj.bias"), resid=Q)
+            z, mu2, r2 = e("z", (M, d)), e("mu", (M,), torch.float32), e("r", (M,), torch.float32)
+            ops.layernorm_fwd(x1, self.Wf(f"forward_layernorms.{i}.weight"),
+                              self.Wf(f"forward_layernorms.{i}.bias"), LN_EPS, z, mu2, r2, 0)
+            fw = f"forward_layers.{i}."
+            h1 = e("h1", (M, d))
+            ops.linear_fwd(z, self.W(fw + "conv1.weight").view(d, d), h1, bias=self.Wf(fw + "conv1.bias"),
+                           act=ops.ACT_RELU, drop_p=p, drop_seed=self.salt[f"ffn1_{i}"], seed_base=sb, drop_ld=d)
+            xn = e("x", (M, d))
+            ops.linear_fwd(h1, self.W(fw + "conv2.weight").view(d, d), xn, bias=self.Wf(fw + "conv2.bias"),
+                           drop_p=p, drop_seed=self.salt[f"ffn2_{i}"], seed_base=sb, drop_ld=d, resid=z,
+                           rowmask_ids=ids)
+            for k_, v_ in (("x", x), ("Q", Q), ("mu1", mu1), ("r1", r1), ("q", q), ("kv", kv), ("o", o),
+                           ("lse", lse), ("x1", x1), ("z", z), ("mu2", mu2), ("r2", r2), ("h1", h1)):
+                s[k_].append(v_)
+            x = xn
+        f, muf, rf = e("f", (M, d)), e("mu", (M,), torch.float32), e("r", (M,), torch.float32)
+        ops.layernorm_fwd(x, self.Wf("last_layernorm.weight"), self.Wf("last_layernorm.bias"), LN_EPS, f, muf, rf, 0)
+        s.update(xL=x, f=f, muf=muf, rf=rf)
+        if not need_logits:
+            return None, None, s
+        pl, nl = e("pl", (B, T), torch.float32), e("nl", (B, T), torch.float32)
+        ops.sampled_logits_fwd(f, self.W("item_emb.weight"), pos, neg, pl, nl)
+        return pl, nl, s
+
+    # ---- backward ------------------------------------------------------------------
+    def backward(self, s, dpl, dnl, grad):
+        """Accumulates every parameter gradient into the flat fp32 buffer ``grad``."""
+        B, T, p, ids = s["B"], s["T"], s["p"], s["ids"]
+        M, d, H, Dh, L = B * T, self.d, self.H, self.Dh, self.L
+        sb = s["sb"]
+        e = self._buf
+        G = lambda n: self.flat.view(n, grad)  # noqa: E731
+        slab = self.ws.get("slab", (ops.split_for(M, 2 * d, d) * 2 * d * d,), torch.float32)
+        wsc = self.ws.get("colsum", (64 * 2 * d,), torch.float32)
+        wln = self.ws.get("ln", (2 * 256 * d,), torch.float32)
+        wat = self.ws.get("attn", (B * H * T,), torch.float32)
+
+        df = e("df", (M, d))
+        ops.sampled_logits_bwd(s["f"], self.W("item_emb.weight"), s["pos"], s["neg"], dpl, dnl, df,
+                               G("item_emb.weight"))
+        dx = e("dx", (M, d))
+        ops.layernorm_bwd(s["xL"], df, self.Wf("last_layernorm.weight"), s["muf"], s["rf"], LN_EPS, dx,
+                          G("last_layernorm.weight"), G("last_layernorm.bias"), wln, 0)
+        for i in reversed(range(L)):
+            pre = f"attention_layers.{i}."
+            fw = f"forward_layers.{i}."
+            # x_{i+1} = (drop2(h1 W2^T + b2) + z) * mask
+            dy2, dzres = e("dy2", (M, d)), e("dzres", (M, d))
+            ops.dropout_rowmask(dx, p, self.salt[f"ffn2_{i}"], sb, ids, dy2, dzres)
+            ops.linear_wgrad(dy2, s["h1"][i], G(fw + "conv2.weight").view(d, d), slab)
+            ops.colsum(dy2, G(fw + "conv2.bias"), wsc)
+            da1 = e("da1", (M, d))
+            ops.linear_dgrad(dy2, self.W(fw + "conv2.weight").view(d, d), da1, act=ops.ACT_RELU_BWD,
+                             aux=s["h1"][i], drop_p=p, drop_seed=self.salt[f"ffn1_{i}"], seed_base=sb, drop_ld=d)
+            ops.linear_wgrad(da1, s["z"][i], G(fw + "conv1.weight").view(d, d), slab)
+            ops.colsum(da1, G(fw + "conv1.bias"), wsc)
+            dz = e("dz", (M, d))
+            ops.linear_dgrad(da1, self.W(fw + "conv1.weight").view(d, d), dz, resid=dzres)
+            dx1 = e("dx1", (M, d))
+            ops.layernorm_bwd(s["x1"][i], dz, self.Wf(f"forward_layernorms.{i}.weight"), s["mu2"][i], s["r2"][i],
+                              LN_EPS, dx1, G(f"forward_layernorms.{i}.weight"), G(f"forward_layernorms.{i}.bias"),
+                              wln, 0)
+            # x1 = Q + o Wo^T + bo
+            ops.linear_wgrad(dx1, s["o"][i], G(pre + "out_proj.weight"), slab)
+            ops.colsum(dx1, G(pre + "out_proj.bias"), wsc)
+            do = e("do", (M, d))
+            ops.linear_dgrad(dx1, self.W(pre + "out_proj.weight"), do)
+            dq, dkv = e("dq", (M, d)), e("dkv", (M, 2 * d))
+            kv = s["kv"][i]
+            ops.attn_bwd(B, T, H, Dh, s["q"][i], kv[:, :d], kv[:, d:], s["o"][i], do, s["lse"][i], dq,
+                         dkv[:, :d], dkv[:, d:], 1.0 / math.sqrt(Dh), 0, ids, p, self.salt[f"attn{i}"], sb, wat)
+            Gin, Gb = G(pre + "in_proj_weight"), G(pre + "in_proj_bias")
+            Win = self.W(pre + "in_proj_weight")
+            ops.linear_wgrad(dq, s["Q"][i], Gin[:d], slab)
+            ops.colsum(dq, Gb[:d], wsc)
+            ops.linear_wgrad(dkv, s["x"][i], Gin[d:], slab)
+            ops.colsum(dkv, Gb[d:], wsc)
+            dQ = e("dQ", (M, d))
+            ops.linear_dgrad(dq, Win[:d], dQ, resid=dx1)
+            dxi = e("dxi", (M, d))
+            ops.linear_dgrad(dkv, Win[d:], dxi)
+            ops.layernorm_bwd(s["x"][i], dQ, self.Wf(f"attention_layernorms.{i}.weight"), s["mu1"][i], s["r1"][i],
+                              LN_EPS, dxi, G(f"attention_layernorms.{i}.weight"),
+                              G(f"attention_layernorms.{i}.bias"), wln, 0, accumulate=True)
+            dx = dxi
+        ops.embed_bwd(0, ids, T, dx, math.sqrt(d), p, self.salt["emb"], sb, G("item_emb.weight"),
+                      G("pos_emb.weight"))
+
+    # ---- eval ----------------------------------------------------------------------
+    def features(self, ids):
+        self.sync_compute_weights()
+        _, _, s = self.forward(ids, None, None, False, need_logits=False)
+        B, T = ids.shape
+        return s["f"].view(B, T, self.d)
+
+    def predict(self, ids, cand):
+        f = self.features(ids)[:, -1, :].contiguous()       # sas.py:110
+        B, C = cand.shape
+        # candidate scores <f_b, E[c]> (sas.py:112-114) via the sampled-logit kernel on repeated rows
+        frep = f.unsqueeze(1).expand(B, C, self.d).reshape(B * C, self.d).contiguous()
+        out = torch.empty(B * C, dtype=torch.float32, device=self.dev)
+        junk = torch.empty(B * C, dtype=torch.float32, device=self.dev)
+        cflat = cand.reshape(-1).contiguous()
+        ops.sampled_logits_fwd(frep, self.W("item_emb.weight"), cflat, cflat, out, junk)
+        return out.view(B, C)

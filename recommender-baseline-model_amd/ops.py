@@ -1,0 +1,182 @@
+"""Thin tensor-level wrappers over the C ABI (librecsys_hip.so).
+
+Every function launches HIP kernels on the current torch stream and returns
+nothing; outputs are caller-allocated tensors (the C ABI allocates nothing).
+2-D tensors are passed with their row stride as the leading dimension.
+"""
+import ctypes as C
+
+import torch
+
+from . import _lib
+from ._lib import BF16, F32, Epilogue, call, ptr, stream
+
+ACT_NONE, ACT_RELU, ACT_GELU, ACT_RELU_BWD, ACT_GELU_BWD = (
+    _lib.ACT_NONE, _lib.ACT_RELU, _lib.ACT_GELU, _lib.ACT_RELU_BWD, _lib.ACT_GELU_BWD)
+
+
+def dtype_code(t):
+    if t.dtype == torch.float32:
+        return F32
+    if t.dtype == torch.bfloat16:
+        return BF16
+    raise TypeError(f"unsupported dtype {t.dtype}")
+
+
+def ld(t):
+    return t.stride(0) if t.dim() == 2 else t.shape[-1]
+
+
+def epilogue(bias=None, alpha=1.0, act=ACT_NONE, aux=None, aux_out=None, drop_p=0.0, drop_seed=0,
+             seed_base=None, drop_ld=0, resid=None, rowmask_ids=None, accumulate=False):
+    e = Epilogue()
+    e.bias = ptr(bias)
+    e.alpha = alpha
+    e.act = act
+    e.aux = ptr(aux)
+    e.aux_out = ptr(aux_out)
+    a = aux if aux is not None else aux_out
+    e.ldaux = ld(a) if a is not None else 0
+    e.drop_p = drop_p
+    e.drop_seed = drop_seed
+    e.seed_base = ptr(seed_base)
+    e.drop_ld = drop_ld
+    e.resid = ptr(resid)
+    e.ldres = ld(resid) if resid is not None else 0
+    e.rowmask_ids = ptr(rowmask_ids)
+    e.accumulate = 1 if accumulate else 0
+    return e
+
+
+def gemm(A, B, Cout, M, N, K, a_kmajor=False, b_kmajor=False, epi=None, split_k=1, slab=None):
+    """Cout[M,N] = epi(A . B^T) with the storage conventions of rs_gemm (C may be fp32 for bf16 A/B)."""
+    assert A.dtype == B.dtype, "A and B must share the compute dtype"
+    call("rs_gemm", dtype_code(A), int(a_kmajor), int(b_kmajor), M, N, K, ptr(A), ld(A), ptr(B), ld(B),
+         ptr(Cout), ld(Cout), int(Cout.dtype == torch.float32),
+         C.byref(epi) if epi is not None else None, split_k, ptr(slab), stream())
+
+
+def linear_fwd(X, W, Y, bias=None, **epi_kw):
+    """Y = X W^T (+ fused epilogue).  X [M,K], W [N,K], Y [M,N]."""
+    M, K = X.shape
+    N = W.shape[0]
+    gemm(X, W, Y, M, N, K, False, False, epilogue(bias=bias, **epi_kw))
+
+
+def linear_dgrad(dY, W, dX, **epi_kw):
+    """dX = dY W (+ epilogue).  dY [M,N], W [N,K], dX [M,K]."""
+    M, N = dY.shape
+    K = W.shape[1]
+    gemm(dY, W, dX, M, K, N, False, True, epilogue(**epi_kw))
+
+
+def split_for(M_tok, n_out, k_in):
+    tiles = -(-n_out // 64) * -(-k_in // 64)
+    return int(max(1, min(-(-512 // tiles), -(-M_tok // 128))))
+
+
+def linear_wgrad(dY, X, dW, slab, split_k=None):
+    """dW [N,K] += dY^T X over M token rows (split-K slabs, deterministic reduce)."""
+    M, N = dY.shape
+    K = X.shape[1]
+    s = split_k or split_for(M, N, K)
+    assert slab.numel() >= s * N * K, "slab workspace too small"
+    gemm(dY, X, slab, N, K, M, True, True, None, split_k=s, slab=slab)
+    call("rs_reduce_slabs", ptr(slab), s, N * K, ptr(dW), 1, stream())
+
+
+def colsum(X, out, ws, accumulate=True):
+    M, N = X.shape
+    call("rs_colsum", dtype_code(X), ptr(X), M, N, ld(X), ptr(ws), ptr(out), int(accumulate), stream())
+
+
+def layernorm_fwd(X, gamma, beta, eps, Y, mean, rinv, variant):
+    M, d = X.shape
+    call("rs_layernorm_fwd", dtype_code(X), variant, ptr(X), ld(X), M, d, ptr(gamma), ptr(beta), eps,
+         ptr(Y), ld(Y), ptr(mean), ptr(rinv), stream())
+
+
+def layernorm_bwd(X, dY, gamma, mean, rinv, eps, dX, dgamma, dbeta, ws, variant, accumulate=False):
+    M, d = X.shape
+    call("rs_layernorm_bwd", dtype_code(X), variant, ptr(X), ld(X), ptr(dY), ld(dY), M, d, ptr(gamma),
+         ptr(mean), ptr(rinv), eps, ptr(dX), ld(dX), int(accumulate), ptr(dgamma), ptr(dbeta), ptr(ws), stream())
+
+
+def embed_fwd(mode, ids, T, table, pos, scale, drop_p, seed, seed_base, out):
+    rows = ids.numel()
+    d = table.shape[1]
+    call("rs_embed_fwd", dtype_code(table), mode, ptr(ids), rows, T, ptr(table), ptr(pos), d, scale, drop_p,
+         seed, ptr(seed_base), ptr(out), stream())
+
+
+def embed_bwd(mode, ids, T, dx, scale, drop_p, seed, seed_base, dtable, dpos, accumulate_pos=True):
+    rows = ids.numel()
+    d = dx.shape[-1]
+    call("rs_embed_bwd", dtype_code(dx), mode, ptr(ids), rows, T, ptr(dx), d, scale, drop_p, seed,
+         ptr(seed_base), ptr(dtable), ptr(dpos), int(accumulate_pos), stream())
+
+
+def attn_fwd(B, T, H, Dh, q, k, v, o, lse, scale, mask_kind, ids, drop_p, seed, seed_base):
+    call("rs_attn_fwd", dtype_code(q), B, T, H, Dh, ptr(q), ld(q), ptr(k), ld(k), ptr(v), ld(v), ptr(o), ld(o),
+         ptr(lse), scale, mask_kind, ptr(ids), drop_p, seed, ptr(seed_base), stream())
+
+
+def attn_bwd(B, T, H, Dh, q, k, v, o, do, lse, dq, dk, dv, scale, mask_kind, ids, drop_p, seed, seed_base, ws):
+    call("rs_attn_bwd", dtype_code(q), B, T, H, Dh, ptr(q), ld(q), ptr(k), ld(k), ptr(v), ld(v), ptr(o), ld(o),
+         ptr(do), ld(do), ptr(lse), ptr(dq), ld(dq), ptr(dk), ld(dk), ptr(dv), ld(dv), scale, mask_kind, ptr(ids),
+         drop_p, seed, ptr(seed_base), ptr(ws), stream())
+
+
+def sampled_logits_fwd(f, E, pos, neg, pl, nl):
+    M, d = f.shape
+    call("rs_sampled_logits_fwd", dtype_code(f), ptr(f), M, d, ptr(E), ptr(pos), ptr(neg), ptr(pl), ptr(nl),
+         stream())
+
+
+def sampled_logits_bwd(f, E, pos, neg, dpl, dnl, df, dE, accumulate_df=False):
+    M, d = f.shape
+    call("rs_sampled_logits_bwd", dtype_code(f), ptr(f), M, d, ptr(E), ptr(pos), ptr(neg), ptr(dpl), ptr(dnl),
+         ptr(df), int(accumulate_df), ptr(dE), stream())
+
+
+def bce_fwd(pl, nl, pos, ws, out, count_override=None):
+    call("rs_bce_fwd", ptr(pl), ptr(nl), ptr(pos), pl.numel(), ptr(count_override), ptr(ws), ptr(out), stream())
+
+
+def bce_bwd(pl, nl, pos, count, dloss, dpl, dnl):
+    call("rs_bce_bwd", ptr(pl), ptr(nl), ptr(pos), pl.numel(), ptr(count), ptr(dloss), ptr(dpl), ptr(dnl),
+         stream())
+
+
+def ce_fwd(logits, labels, ws, out, count_override=None):
+    R, V1 = logits.shape
+    call("rs_ce_fwd", ptr(logits), R, V1, ld(logits), ptr(labels), ptr(count_override), ptr(ws), ptr(out),
+         stream())
+
+
+def ce_bwd(logits, labels, count, dloss, ws, dlogits):
+    R, V1 = logits.shape
+    call("rs_ce_bwd", dtype_code(dlogits), ptr(logits), R, V1, ld(logits), ptr(labels), ptr(count), ptr(dloss),
+         ptr(ws), ptr(dlogits), ld(dlogits), stream())
+
+
+def adam_prepare(state, hyper):
+    call("rs_adam_prepare", ptr(state), ptr(hyper), stream())
+
+
+def adam_step(p, g, m, v, p_bf16, state, hyper):
+    call("rs_adam_step", p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), ptr(p_bf16), ptr(state), ptr(hyper), stream())
+
+
+def cast_bf16(src, dst):
+    call("rs_cast_bf16", src.numel(), ptr(src), ptr(dst), stream())
+
+
+def dropout_rowmask(x, drop_p, seed, seed_base, rowmask_ids, out, out_masked=None):
+    M, N = x.shape
+    call("rs_dropout_rowmask", dtype_code(x), ptr(x), M, N, ld(x), drop_p, seed, ptr(seed_base), N,
+         ptr(rowmask_ids), ptr(out), ptr(out_masked), stream())
+
+
+def seed_advance(seed_base):
+    call("rs_seed_advance", ptr(seed_base), stream())
