@@ -36,6 +36,8 @@ def layer_norm(x, w, b, eps=LN_EPS):
 
 
 def _dropout(x, p, mask):
+    if mask is False:                # CPU-baseline timing: torch's own bernoulli dropout, as the reference
+        return F.dropout(x, p, training=True) if p > 0 else x
     if mask is not None:
         return x * mask / (1.0 - p)
     if p > 0:
@@ -43,9 +45,17 @@ def _dropout(x, p, mask):
     return x
 
 
+class RandomDropout(dict):
+    """``masks=RandomDropout()``: every dropout site draws torch bernoulli masks, like the
+    reference's nn.Dropout (used only to time the CPU baseline at the config dropout)."""
+
+    def get(self, key, default=None):
+        return False
+
+
 def log2feats(P, log_seqs, num_blocks, heads, p=0.0, masks=None):
     """sas.py:59-88.  log_seqs: (B,T) int64 tensor.  Returns (B,T,d)."""
-    masks = masks or {}
+    masks = {} if masks is None else masks
     E = P["sas.item_emb.weight"]
     d = E.shape[1]
     B, T = log_seqs.shape
