@@ -67,6 +67,19 @@ int rs_gemm(int dtype, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t
 
 /* out[i] (+)= sum_z slab[z*n+i], fixed order (deterministic split-K finish). */
 int rs_reduce_slabs(const float* slab, int splits, int64_t n, float* out, int accumulate, void* stream);
+/* Same over slabs of n0+n1 floats: the first n0 columns go to out0, the rest to out1. */
+int rs_reduce_slabs2(const float* slab, int splits, int64_t n0, float* out0, int64_t n1, float* out1, int accumulate,
+                     void* stream);
+
+/* Weight + bias gradient of a Linear / Conv1d(k=1) layer over M token rows:
+ *   dW[N,K] (+)= sum_m dY[m,:]^T X[m,:];   db[N] (+)= sum_m dY[m,:]   (db nullable)
+ * split-K over the rows into `splits` fp32 slabs (slab >= splits*(N*K + N) floats), the bias
+ * column sums fused into the GEMM, then one deterministic reduce.  accumulate: += into dW/db.
+ * Replaces the autograd weight/bias gradients of nn.Linear / nn.Conv1d / in_proj / out_proj
+ * (BS/models/sas_model/sas.py:10-17,45-47; BS/models/bert_modules/attention/multi_head.py:18-19;
+ * utils/feed_forward.py:10-11; BS/models/bert.py:10). */
+int rs_linear_wgrad(int dtype, int64_t M, int64_t N, int64_t K, const void* dY, int64_t lddy, const void* X,
+                    int64_t ldx, float* dW, float* db, int accumulate, int splits, float* slab, void* stream);
 
 /* out[n] (+)= sum_m X[m*ldx+n] over M rows (bias gradients).  ws: >= 64*N floats. */
 int rs_colsum(int dtype, const void* X, int64_t M, int64_t N, int64_t ldx, float* ws, float* out,
@@ -92,7 +105,7 @@ int rs_embed_bwd(int dtype, int mode, const int64_t* ids, int64_t rows, int64_t 
 int rs_layernorm_fwd(int dtype, int variant, const void* X, int64_t ldx, int64_t M, int64_t d,
                      const float* gamma, const float* beta, float eps, void* Y, int64_t ldy,
                      float* mean, float* rinv, void* stream);
-/* dX (+)= LN backward; dgamma/dbeta (+)= column sums (deterministic, ws >= 2*d*256 floats). */
+/* dX (+)= LN backward; dgamma/dbeta += column sums (deterministic, ws >= 2*d*128 floats). */
 int rs_layernorm_bwd(int dtype, int variant, const void* X, int64_t ldx, const void* dY, int64_t lddy,
                      int64_t M, int64_t d, const float* gamma, const float* mean, const float* rinv, float eps,
                      void* dX, int64_t lddx, int accumulate_dx, float* dgamma, float* dbeta, float* ws,

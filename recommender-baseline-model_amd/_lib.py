@@ -36,6 +36,8 @@ ACT_NONE, ACT_RELU, ACT_GELU, ACT_RELU_BWD, ACT_GELU_BWD = 0, 1, 2, 3, 4
 SIGNATURES = {
     "rs_gemm": [i32, i32, i32, i64, i64, i64, vp, i64, vp, i64, vp, i64, i32, C.POINTER(Epilogue), i32, vp, vp],
     "rs_reduce_slabs": [vp, i32, i64, vp, i32, vp],
+    "rs_reduce_slabs2": [vp, i32, i64, vp, i64, vp, i32, vp],
+    "rs_linear_wgrad": [i32, i64, i64, i64, vp, i64, vp, i64, vp, vp, i32, i32, vp, vp],
     "rs_colsum": [i32, vp, i64, i64, i64, vp, vp, i32, vp],
     "rs_embed_fwd": [i32, i32, vp, i64, i64, vp, vp, i64, f32, f32, u64, vp, vp, vp],
     "rs_embed_bwd": [i32, i32, vp, i64, i64, vp, i64, f32, f32, u64, vp, vp, vp, i32, vp],

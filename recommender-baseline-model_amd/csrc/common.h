@@ -170,3 +170,8 @@ __device__ __forceinline__ float gelu_tanh_grad(float x) {
 }
 
 __host__ __device__ static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// second pass of every two-level reduction (reduce.hip): out0[i] (+)= sum_z slab[z*n+i] for i < n0,
+// out1[i-n0] likewise for n0 <= i < n (either output may be null to drop that part).
+hipError_t launch_reduce_slabs(const float* slab, int splits, int64_t n, int64_t n0, float* out0, float* out1,
+                               int accumulate, hipStream_t s);

@@ -77,6 +77,46 @@ __global__ __launch_bounds__(256) void embed_bwd_pos_kernel(const int64_t* __res
   }
 }
 
+// vectorized positional-gradient sum: block = position t, 256 threads = CPR chunk-columns x RG
+// batch groups, fixed-order LDS combine (deterministic)
+template <typename T, int CPR>
+__global__ __launch_bounds__(256) void embed_bwd_pos_v_kernel(const int64_t* __restrict__ ids, int64_t rows,
+                                                              int64_t T_, const T* __restrict__ dx, int64_t d,
+                                                              int mode, float drop_p, uint64_t salt,
+                                                              const uint64_t* seed_base, float* __restrict__ dpos,
+                                                              int accumulate) {
+  constexpr int V = Vec<T>::N, RG = 256 / CPR;
+  const uint64_t seed = eff_seed(salt, seed_base);
+  const int64_t t = blockIdx.x, nb = rows / T_;
+  const int cc = threadIdx.x % CPR, rg = threadIdx.x / CPR;
+  float acc[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) acc[j] = 0.f;
+  if (cc * V < d) {
+    for (int64_t b = rg; b < nb; b += RG) {
+      const int64_t r = b * T_ + t;
+      if (mode == 0 && ids[r] == 0) continue;
+      float g[V];
+      load_chunk<T>(g, dx + r * d + cc * V);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        float x = g[j];
+        if (drop_p > 0.f) x *= drop_mul(drop_p, seed, (uint64_t)(r * d + cc * V + j));
+        acc[j] += x;
+      }
+    }
+  }
+  __shared__ float red[RG][CPR * V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) red[rg][cc * V + j] = acc[j];
+  __syncthreads();
+  for (int c = threadIdx.x; c < d; c += 256) {
+    float sum = 0.f;
+    for (int g2 = 0; g2 < RG; ++g2) sum += red[g2][c];
+    dpos[t * d + c] = accumulate ? dpos[t * d + c] + sum : sum;
+  }
+}
+
 // one wave per row m
 template <typename T>
 __global__ __launch_bounds__(256) void sampled_logits_fwd_kernel(const T* __restrict__ f, int64_t M, int64_t d,
@@ -146,9 +186,23 @@ static hipError_t embed_bwd_t(int mode, const int64_t* ids, int64_t rows, int64_
   if (dtable)
     hipLaunchKernelGGL((embed_bwd_table_kernel<T>), dim3((unsigned)cdiv(rows * d, 256)), dim3(256), 0, s, ids, rows,
                        (const T*)dx, d, mode == 0 ? scale : 1.0f, drop_p, seed, seed_base, dtable);
-  if (dpos)
-    hipLaunchKernelGGL((embed_bwd_pos_kernel<T>), dim3((unsigned)T_), dim3(d >= 256 ? 256 : 128), 0, s, ids, rows,
-                       T_, (const T*)dx, d, mode, drop_p, seed, seed_base, dpos, acc_pos);
+  if (dpos) {
+    constexpr int V = Vec<T>::N;
+    const int64_t cpr = d / V;
+    const bool vec = (d % V == 0) && ((uintptr_t)dx % 16 == 0);
+    if (vec && cpr <= 16)
+      hipLaunchKernelGGL((embed_bwd_pos_v_kernel<T, 16>), dim3((unsigned)T_), dim3(256), 0, s, ids, rows, T_,
+                         (const T*)dx, d, mode, drop_p, seed, seed_base, dpos, acc_pos);
+    else if (vec && cpr <= 32)
+      hipLaunchKernelGGL((embed_bwd_pos_v_kernel<T, 32>), dim3((unsigned)T_), dim3(256), 0, s, ids, rows, T_,
+                         (const T*)dx, d, mode, drop_p, seed, seed_base, dpos, acc_pos);
+    else if (vec && cpr <= 64)
+      hipLaunchKernelGGL((embed_bwd_pos_v_kernel<T, 64>), dim3((unsigned)T_), dim3(256), 0, s, ids, rows, T_,
+                         (const T*)dx, d, mode, drop_p, seed, seed_base, dpos, acc_pos);
+    else
+      hipLaunchKernelGGL((embed_bwd_pos_kernel<T>), dim3((unsigned)T_), dim3(d >= 256 ? 256 : 128), 0, s, ids, rows,
+                         T_, (const T*)dx, d, mode, drop_p, seed, seed_base, dpos, acc_pos);
+  }
   return hipGetLastError();
 }
 

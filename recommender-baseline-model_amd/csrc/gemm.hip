@@ -33,7 +33,9 @@ struct GemmArgs {
   void* C; int64_t ldc;
   int c_f32;
   int split_k; int64_t k_per_split;
-  float* slab;  // when non-null: write raw fp32 partials to slab[z][M][N]
+  float* slab;  // when non-null: write raw fp32 partials to slab[z*slab_stride + m*N + n]
+  int64_t slab_stride;
+  int bias_colsum;  // (AK only) also write sum_k A(m,k) of this split to slab[z*slab_stride + M*N + m]
   rs_epilogue epi;
 };
 
@@ -157,11 +159,23 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
     else lb.load(B, a.ldb, k0, n0, kend, a.N, tid);
   };
 
+  // bias gradient fused into the weight-gradient GEMM: the blocks of output
+  // column tile 0 also sum their A (= dY^T, k-major) tiles over k
+  const bool do_colsum = AK && a.bias_colsum && (bid % tiles_n) == 0;
+  float csum = 0.f;
+  auto colsum_tile = [&]() {
+    if (do_colsum && tid < BM) {
+#pragma unroll 8
+      for (int kk = 0; kk < 32; ++kk) csum += to_f(As[kk * LA::LD + tid]);
+    }
+  };
+
   if (kbeg < kend) {
     issue(kbeg);
     la.store(As, tid);
     lb.store(Bs, tid);
     __syncthreads();
+    colsum_tile();
     const int kb = 8 * (lane >> 4), rl = lane & 15;
     for (int64_t k0 = kbeg; k0 < kend; k0 += 32) {
       const bool more = k0 + 32 < kend;
@@ -180,6 +194,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
         la.store(As, tid);
         lb.store(Bs, tid);
         __syncthreads();
+        colsum_tile();
       }
     }
   }
@@ -194,11 +209,13 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
       for (int r = 0; r < 4; ++r) {
         const int64_t m = m0 + wm * (BM / 2) + i * 16 + rq + r;
         if (m < a.M && n < a.N) {
-          if (a.slab) a.slab[((int64_t)z * a.M + m) * a.N + n] = acc[i][j][r];
+          if (a.slab) a.slab[(int64_t)z * a.slab_stride + m * a.N + n] = acc[i][j][r];
           else epilogue_store<T>(a, m, n, acc[i][j][r]);
         }
       }
     }
+  if (do_colsum && tid < BM && m0 + tid < a.M)
+    a.slab[(int64_t)z * a.slab_stride + a.M * a.N + m0 + tid] = csum;
 }
 
 template <typename T, bool AK, bool BK>
@@ -222,15 +239,6 @@ static hipError_t launch_dt(int ak, int bk, GemmArgs& a, hipStream_t s) {
   return launch_t<T, true, false>(a, s);
 }
 
-__global__ void reduce_slabs_kernel(const float* __restrict__ slab, int splits, int64_t n,
-                                    float* __restrict__ out, int accumulate) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    float s = 0.0f;
-    for (int z = 0; z < splits; ++z) s += slab[(int64_t)z * n + i];  // fixed order: deterministic
-    out[i] = accumulate ? out[i] + s : s;
-  }
-}
-
 extern "C" {
 
 int rs_gemm(int dtype, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
@@ -246,6 +254,8 @@ int rs_gemm(int dtype, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t
   a.c_f32 = c_f32; a.split_k = split_k;
   a.k_per_split = split_k > 1 ? cdiv(cdiv(K, split_k), 32) * 32 : (K > 0 ? K : 1);
   a.slab = slab;
+  a.slab_stride = M * N;
+  a.bias_colsum = 0;
   if (epi) a.epi = *epi;
   else { a.epi = rs_epilogue{}; a.epi.alpha = 1.0f; }
   hipStream_t s = (hipStream_t)stream;
@@ -254,12 +264,29 @@ int rs_gemm(int dtype, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t
   return (int)err;
 }
 
-int rs_reduce_slabs(const float* slab, int splits, int64_t n, float* out, int accumulate, void* stream) {
-  if (n <= 0 || splits < 1) return RS_ERR_ARG;
-  int64_t blocks = std::min<int64_t>(cdiv(n, 256), 4096);
-  hipLaunchKernelGGL(reduce_slabs_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
-                     slab, splits, n, out, accumulate);
-  return (int)hipGetLastError();
+// dW[N,K] (+)= sum_m dY[m,:]^T X[m,:]  and  db[N] (+)= sum_m dY[m,:]  (split-K over the M token
+// rows into fp32 slabs, bias column sums fused into the GEMM, one deterministic reduce pass)
+int rs_linear_wgrad(int dtype, int64_t M, int64_t N, int64_t K, const void* dY, int64_t lddy, const void* X,
+                    int64_t ldx, float* dW, float* db, int accumulate, int splits, float* slab, void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || splits < 1 || !slab || !dW) return RS_ERR_ARG;
+  const int esz = dtype == RS_DTYPE_BF16 ? 2 : 4;
+  const int vec = 16 / esz;
+  if ((lddy % vec) || (ldx % vec) || ((uintptr_t)dY % 16) || ((uintptr_t)X % 16) || ((uintptr_t)slab % 16))
+    return RS_ERR_ARG;
+  GemmArgs a;
+  a.M = N; a.N = K; a.K = M; a.A = dY; a.lda = lddy; a.B = X; a.ldb = ldx; a.C = nullptr; a.ldc = 0;
+  a.c_f32 = 1; a.split_k = splits;
+  a.k_per_split = cdiv(cdiv(M, splits), 32) * 32;
+  a.slab = slab;
+  a.slab_stride = N * K + (db ? N : 0);
+  a.bias_colsum = db ? 1 : 0;
+  a.epi = rs_epilogue{};
+  a.epi.alpha = 1.0f;
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t err = dtype == RS_DTYPE_BF16 ? launch_t<__bf16, true, true>(a, s) : launch_t<float, true, true>(a, s);
+  if (err != hipSuccess) return (int)err;
+  // one pass over the slabs: columns [0, N*K) -> dW, [N*K, N*K+N) -> db
+  return (int)launch_reduce_slabs(slab, splits, a.slab_stride, N * K, dW, db, accumulate, s);
 }
 
 }  // extern "C"

@@ -14,6 +14,7 @@
 #include "../../include/recsys_hip.h"
 
 #define LN_MAXV 16  // d <= 64*16
+#define LN_BWD_BLOCKS 128  // affine-partial slabs per LN backward (ws >= 2*d*LN_BWD_BLOCKS floats)
 
 template <typename T, int NV>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ X, int64_t ldx, int64_t M, int d,
@@ -130,23 +131,166 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ X, in
   }
 }
 
-__global__ void ln_affine_reduce_kernel(const float* __restrict__ part, int nblk, int d, float* __restrict__ dgamma,
-                                        float* __restrict__ dbeta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= 2 * d) return;
-  const int which = c / d, col = c % d;
+// ---- vectorized kernels: LPR lanes per row, NCH 16-byte chunks per lane (d = LPR*NCH*V),
+// 64/LPR rows per wave; statistics by shuffles inside the LPR-lane group.
+template <int LPR>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T, int LPR, int NCH>
+__global__ __launch_bounds__(256) void ln_fwd_v_kernel(const T* __restrict__ X, int64_t ldx, int64_t M, int d,
+                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                       float eps, int variant, T* __restrict__ Y, int64_t ldy,
+                                                       float* __restrict__ mean_out, float* __restrict__ rinv_out) {
+  constexpr int V = Vec<T>::N, RPW = 64 / LPR;
+  const int lane = threadIdx.x & 63, sub = lane % LPR;
+  const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR;
+  if (row >= M) return;
+  const T* x = X + row * ldx;
+  float v[NCH][V];
   float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += part[((int64_t)b * 2 + which) * d + col];
-  float* dst = which == 0 ? dgamma : dbeta;
-  if (dst) dst[col] += s;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    load_chunk<T>(v[i], x + (i * LPR + sub) * V);
+#pragma unroll
+    for (int j = 0; j < V; ++j) s += v[i][j];
+  }
+  const float mu = group_sum<LPR>(s) / (float)d;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i)
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const float u = v[i][j] - mu;
+      q += u * u;
+    }
+  q = group_sum<LPR>(q);
+  const float rinv = variant == 0 ? 1.0f / sqrtf(q / (float)d + eps) : 1.0f / (sqrtf(q / (float)(d - 1)) + eps);
+  T* y = Y + row * ldy;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int c0 = (i * LPR + sub) * V;
+    float o[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const float u = v[i][j] - mu;
+      o[j] = variant == 0 ? u * rinv * gamma[c0 + j] + beta[c0 + j] : gamma[c0 + j] * (u * rinv) + beta[c0 + j];
+    }
+    store_chunk<T>(y + c0, o);
+  }
+  if (sub == 0) {
+    mean_out[row] = mu;
+    rinv_out[row] = rinv;
+  }
+}
+
+// backward; the affine partials of each lane's columns are accumulated over all rows the lane
+// group visits (grid-stride), combined over the block's row groups in LDS (fixed order) and
+// written to part[block][2][d] for the deterministic slab reduce.
+template <typename T, int LPR, int NCH>
+__global__ __launch_bounds__(256) void ln_bwd_v_kernel(const T* __restrict__ X, int64_t ldx, const T* __restrict__ dY,
+                                                       int64_t lddy, int64_t M, int d, const float* __restrict__ gamma,
+                                                       const float* __restrict__ mean, const float* __restrict__ rinv,
+                                                       float eps, int variant, T* __restrict__ dX, int64_t lddx,
+                                                       int accumulate, float* __restrict__ part) {
+  constexpr int V = Vec<T>::N, RPW = 64 / LPR, RPB = 4 * RPW;
+  const int lane = threadIdx.x & 63, sub = lane % LPR;
+  const int rgrp = (threadIdx.x >> 6) * RPW + lane / LPR;  // row group within the block
+  float pg[NCH][V], pb[NCH][V], gm[NCH][V];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i)
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      pg[i][j] = 0.f;
+      pb[i][j] = 0.f;
+      gm[i][j] = gamma[(i * LPR + sub) * V + j];
+    }
+  for (int64_t row = (int64_t)blockIdx.x * RPB + rgrp; row < M; row += (int64_t)gridDim.x * RPB) {
+    const float mu = mean[row], a = rinv[row];
+    float u[NCH][V], gq[NCH][V];
+    float sg = 0.f, sgu = 0.f;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int c0 = (i * LPR + sub) * V;
+      float xv[V], dy[V];
+      load_chunk<T>(xv, X + row * ldx + c0);
+      load_chunk<T>(dy, dY + row * lddy + c0);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        u[i][j] = xv[j] - mu;
+        gq[i][j] = dy[j] * gm[i][j];
+        pg[i][j] += dy[j] * (u[i][j] * a);
+        pb[i][j] += dy[j];
+        sg += gq[i][j];
+        sgu += gq[i][j] * u[i][j];
+      }
+    }
+    sg = group_sum<LPR>(sg);
+    sgu = group_sum<LPR>(sgu);
+    const float mg = sg / (float)d;
+    float coef;
+    if (variant == 0) {
+      coef = a * a * a * sgu / (float)d;
+    } else {
+      const float sd = 1.0f / a - eps;
+      coef = sd > 0.f ? a * a * sgu / ((float)(d - 1) * sd) : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int c0 = (i * LPR + sub) * V;
+      float o[V];
+      if (accumulate) load_chunk<T>(o, dX + row * lddx + c0);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const float t = a * (gq[i][j] - mg) - coef * u[i][j];
+        o[j] = accumulate ? o[j] + t : t;
+      }
+      store_chunk<T>(dX + row * lddx + c0, o);
+    }
+  }
+  // combine the RPB row groups: LDS [RPB][d] twice (gamma, beta) in two rounds to bound LDS
+  __shared__ float red[RPB * LPR * NCH * V];
+  for (int which = 0; which < 2; ++which) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i)
+#pragma unroll
+      for (int j = 0; j < V; ++j) red[rgrp * d + (i * LPR + sub) * V + j] = which == 0 ? pg[i][j] : pb[i][j];
+    __syncthreads();
+    for (int c = threadIdx.x; c < d; c += 256) {
+      float t = 0.f;
+      for (int g = 0; g < RPB; ++g) t += red[g * d + c];
+      part[((int64_t)blockIdx.x * 2 + which) * d + c] = t;
+    }
+    __syncthreads();
+  }
 }
 
 template <typename T>
 static hipError_t ln_fwd_t(const void* X, int64_t ldx, int64_t M, int d, const float* gamma, const float* beta,
                            float eps, int variant, void* Y, int64_t ldy, float* mean, float* rinv, hipStream_t s) {
-  dim3 grid((unsigned)cdiv(M, 4)), block(256);
   const T* x = (const T*)X;
   T* y = (T*)Y;
+  {
+    constexpr int V = Vec<T>::N;
+    const bool vec = (d % V == 0) && (ldx % V == 0) && (ldy % V == 0) && ((uintptr_t)X % 16 == 0) &&
+                     ((uintptr_t)Y % 16 == 0);
+    const int cpr = d / V;
+#define LNFV(LPR, NCH) hipLaunchKernelGGL((ln_fwd_v_kernel<T, LPR, NCH>), dim3((unsigned)cdiv(M, 4 * (64 / LPR))), \
+                                          dim3(256), 0, s, x, ldx, M, d, gamma, beta, eps, variant, y, ldy, mean, rinv)
+    if (vec) {
+      if (cpr == 4) { LNFV(4, 1); return hipGetLastError(); }
+      if (cpr == 8) { LNFV(8, 1); return hipGetLastError(); }
+      if (cpr == 16) { LNFV(16, 1); return hipGetLastError(); }
+      if (cpr == 32) { LNFV(32, 1); return hipGetLastError(); }
+      if (cpr == 64) { LNFV(64, 1); return hipGetLastError(); }
+      if (cpr == 128) { LNFV(64, 2); return hipGetLastError(); }
+    }
+#undef LNFV
+  }
+  dim3 grid((unsigned)cdiv(M, 4)), block(256);
 #define LNF(NV) hipLaunchKernelGGL((ln_fwd_kernel<T, NV>), grid, block, 0, s, x, ldx, M, d, gamma, beta, eps, variant, y, ldy, mean, rinv)
   if (d <= 64) LNF(1);
   else if (d <= 128) LNF(2);
@@ -161,11 +305,38 @@ template <typename T>
 static hipError_t ln_bwd_t(const void* X, int64_t ldx, const void* dY, int64_t lddy, int64_t M, int d,
                            const float* gamma, const float* mean, const float* rinv, float eps, int variant,
                            void* dX, int64_t lddx, int acc, float* dgamma, float* dbeta, float* ws, hipStream_t s) {
-  const int nblk = (int)std::min<int64_t>(256, cdiv(M, 4));
-  dim3 grid(nblk), block(256);
   const T* x = (const T*)X;
   const T* dy = (const T*)dY;
   T* dx = (T*)dX;
+  {
+    constexpr int V = Vec<T>::N;
+    const bool vec = (d % V == 0) && (ldx % V == 0) && (lddy % V == 0) && (lddx % V == 0) &&
+                     ((uintptr_t)X % 16 == 0) && ((uintptr_t)dY % 16 == 0) && ((uintptr_t)dX % 16 == 0);
+    const int cpr = d / V;
+    int lpr = 0, nch = 1;
+    if (vec) {
+      if (cpr == 4 || cpr == 8 || cpr == 16 || cpr == 32 || cpr == 64) lpr = cpr;
+      else if (cpr == 128) { lpr = 64; nch = 2; }
+    }
+    if (lpr) {
+      const int64_t rpb = 4 * (64 / lpr);
+      const int nb = (int)std::min<int64_t>(LN_BWD_BLOCKS, cdiv(M, rpb));
+#define LNBV(LPR, NCH) hipLaunchKernelGGL((ln_bwd_v_kernel<T, LPR, NCH>), dim3(nb), dim3(256), 0, s, x, ldx, dy, lddy, \
+                                          M, d, gamma, mean, rinv, eps, variant, dx, lddx, acc, ws)
+      if (lpr == 4) LNBV(4, 1);
+      else if (lpr == 8) LNBV(8, 1);
+      else if (lpr == 16) LNBV(16, 1);
+      else if (lpr == 32) LNBV(32, 1);
+      else if (nch == 1) LNBV(64, 1);
+      else LNBV(64, 2);
+#undef LNBV
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess || !(dgamma || dbeta)) return e;
+      return launch_reduce_slabs(ws, nb, 2 * (int64_t)d, d, dgamma, dbeta, 1, s);
+    }
+  }
+  const int nblk = (int)std::min<int64_t>(LN_BWD_BLOCKS, cdiv(M, 4));
+  dim3 grid(nblk), block(256);
 #define LNB(NV) hipLaunchKernelGGL((ln_bwd_kernel<T, NV>), grid, block, 0, s, x, ldx, dy, lddy, M, d, gamma, mean, rinv, eps, variant, dx, lddx, acc, ws)
   if (d <= 64) LNB(1);
   else if (d <= 128) LNB(2);
@@ -173,10 +344,9 @@ static hipError_t ln_bwd_t(const void* X, int64_t ldx, const void* dY, int64_t l
   else if (d <= 512) LNB(8);
   else LNB(16);
 #undef LNB
-  if (dgamma || dbeta)
-    hipLaunchKernelGGL(ln_affine_reduce_kernel, dim3((unsigned)cdiv(2 * d, 256)), dim3(256), 0, s, ws, nblk, d,
-                       dgamma, dbeta);
-  return hipGetLastError();
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !(dgamma || dbeta)) return e;
+  return launch_reduce_slabs(ws, nblk, 2 * (int64_t)d, d, dgamma, dbeta, 1, s);
 }
 
 extern "C" {

@@ -73,6 +73,38 @@ __global__ __launch_bounds__(256) void cast_bf16_kernel(int64_t n, const float* 
 }
 
 #define COLSUM_BLOCKS 64
+// block = 256 threads = CPR chunk-columns (16 B each) x (256/CPR) row groups; every block sums
+// a contiguous range of rows, the row groups are combined in LDS in a fixed order.
+template <typename T, int CPR>
+__global__ __launch_bounds__(256) void colsum_partial_v_kernel(const T* __restrict__ X, int64_t M, int64_t N,
+                                                               int64_t ldx, float* __restrict__ ws) {
+  constexpr int V = Vec<T>::N, RG = 256 / CPR;
+  const int cc = threadIdx.x % CPR, rg = threadIdx.x / CPR;
+  const int64_t rows_per = cdiv(M, (int64_t)gridDim.x);
+  const int64_t r0 = blockIdx.x * rows_per, r1 = min(M, r0 + rows_per);
+  float acc[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) acc[j] = 0.f;
+  const bool active = cc * V < N;
+  if (active) {
+    for (int64_t r = r0 + rg; r < r1; r += RG) {
+      float v[V];
+      load_chunk<T>(v, X + r * ldx + cc * V);
+#pragma unroll
+      for (int j = 0; j < V; ++j) acc[j] += v[j];
+    }
+  }
+  __shared__ float red[RG][CPR * V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) red[rg][cc * V + j] = acc[j];
+  __syncthreads();
+  for (int c = threadIdx.x; c < N; c += 256) {
+    float t = 0.f;
+    for (int g = 0; g < RG; ++g) t += red[g][c];
+    ws[blockIdx.x * N + c] = t;
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const T* __restrict__ X, int64_t M, int64_t N, int64_t ldx,
                                                              float* __restrict__ ws) {
@@ -83,6 +115,22 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const T* __restrict
     for (int64_t r = r0; r < r1; ++r) s += to_f(X[r * ldx + c]);
     ws[blockIdx.x * N + c] = s;
   }
+}
+
+template <typename T>
+static hipError_t colsum_partial(const T* X, int64_t M, int64_t N, int64_t ldx, float* ws, int nblk, hipStream_t s) {
+  constexpr int V = Vec<T>::N;
+  const bool vec = (N % V == 0) && (ldx % V == 0) && ((uintptr_t)X % 16 == 0);
+  const int64_t cpr = N / V;
+  if (vec && cpr <= 16)
+    hipLaunchKernelGGL((colsum_partial_v_kernel<T, 16>), dim3(nblk), dim3(256), 0, s, X, M, N, ldx, ws);
+  else if (vec && cpr <= 32)
+    hipLaunchKernelGGL((colsum_partial_v_kernel<T, 32>), dim3(nblk), dim3(256), 0, s, X, M, N, ldx, ws);
+  else if (vec && cpr <= 64)
+    hipLaunchKernelGGL((colsum_partial_v_kernel<T, 64>), dim3(nblk), dim3(256), 0, s, X, M, N, ldx, ws);
+  else
+    hipLaunchKernelGGL((colsum_partial_kernel<T>), dim3(nblk), dim3(256), 0, s, X, M, N, ldx, ws);
+  return hipGetLastError();
 }
 
 template <typename T>
@@ -130,20 +178,15 @@ int rs_cast_bf16(int64_t n, const float* src, void* dst, void* stream) {
   return (int)hipGetLastError();
 }
 
-int rs_reduce_slabs(const float* slab, int splits, int64_t n, float* out, int accumulate, void* stream);
-
 int rs_colsum(int dtype, const void* X, int64_t M, int64_t N, int64_t ldx, float* ws, float* out, int accumulate,
               void* stream) {
   if (M <= 0 || N <= 0) return RS_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
-  const int nblk = (int)std::min<int64_t>(COLSUM_BLOCKS, M);
-  if (dtype == RS_DTYPE_BF16)
-    hipLaunchKernelGGL((colsum_partial_kernel<__bf16>), dim3(nblk), dim3(256), 0, s, (const __bf16*)X, M, N, ldx, ws);
-  else
-    hipLaunchKernelGGL((colsum_partial_kernel<float>), dim3(nblk), dim3(256), 0, s, (const float*)X, M, N, ldx, ws);
-  hipError_t e = hipGetLastError();
+  const int nblk = (int)std::min<int64_t>(COLSUM_BLOCKS, cdiv(M, 64));
+  hipError_t e = dtype == RS_DTYPE_BF16 ? colsum_partial<__bf16>((const __bf16*)X, M, N, ldx, ws, nblk, s)
+                                        : colsum_partial<float>((const float*)X, M, N, ldx, ws, nblk, s);
   if (e != hipSuccess) return (int)e;
-  return rs_reduce_slabs(ws, nblk, N, out, accumulate, stream);
+  return (int)launch_reduce_slabs(ws, nblk, N, N, out, nullptr, accumulate, s);
 }
 
 int rs_dropout_rowmask(int dtype, const void* x, int64_t M, int64_t N, int64_t ld, float drop_p, uint64_t seed,

@@ -230,9 +230,8 @@ class SASEngine:
         sb = s["sb"]
         e = self._buf
         G = lambda n: self.flat.view(n, grad)  # noqa: E731
-        slab = self.ws.get("slab", (ops.split_for(M, 2 * d, d) * 2 * d * d,), torch.float32)
-        wsc = self.ws.get("colsum", (64 * 2 * d,), torch.float32)
-        wln = self.ws.get("ln", (2 * 256 * d,), torch.float32)
+        slab = self.ws.get("slab", (ops.wgrad_slab_numel(M, 2 * d, d),), torch.float32)
+        wln = self.ws.get("ln", (2 * 128 * d,), torch.float32)
         wat = self.ws.get("attn", (B * H * T,), torch.float32)
 
         df = e("df", (M, d))
@@ -247,13 +246,11 @@ class SASEngine:
             # x_{i+1} = (drop2(h1 W2^T + b2) + z) * mask
             dy2, dzres = e("dy2", (M, d)), e("dzres", (M, d))
             ops.dropout_rowmask(dx, p, self.salt[f"ffn2_{i}"], sb, ids, dy2, dzres)
-            ops.linear_wgrad(dy2, s["h1"][i], G(fw + "conv2.weight").view(d, d), slab)
-            ops.colsum(dy2, G(fw + "conv2.bias"), wsc)
+            ops.linear_wgrad(dy2, s["h1"][i], G(fw + "conv2.weight").view(d, d), slab, db=G(fw + "conv2.bias"))
             da1 = e("da1", (M, d))
             ops.linear_dgrad(dy2, self.W(fw + "conv2.weight").view(d, d), da1, act=ops.ACT_RELU_BWD,
                              aux=s["h1"][i], drop_p=p, drop_seed=self.salt[f"ffn1_{i}"], seed_base=sb, drop_ld=d)
-            ops.linear_wgrad(da1, s["z"][i], G(fw + "conv1.weight").view(d, d), slab)
-            ops.colsum(da1, G(fw + "conv1.bias"), wsc)
+            ops.linear_wgrad(da1, s["z"][i], G(fw + "conv1.weight").view(d, d), slab, db=G(fw + "conv1.bias"))
             dz = e("dz", (M, d))
             ops.linear_dgrad(da1, self.W(fw + "conv1.weight").view(d, d), dz, resid=dzres)
             dx1 = e("dx1", (M, d))
@@ -261,8 +258,7 @@ class SASEngine:
                               LN_EPS, dx1, G(f"forward_layernorms.{i}.weight"), G(f"forward_layernorms.{i}.bias"),
                               wln, 0)
             # x1 = Q + o Wo^T + bo
-            ops.linear_wgrad(dx1, s["o"][i], G(pre + "out_proj.weight"), slab)
-            ops.colsum(dx1, G(pre + "out_proj.bias"), wsc)
+            ops.linear_wgrad(dx1, s["o"][i], G(pre + "out_proj.weight"), slab, db=G(pre + "out_proj.bias"))
             do = e("do", (M, d))
             ops.linear_dgrad(dx1, self.W(pre + "out_proj.weight"), do)
             dq, dkv = e("dq", (M, d)), e("dkv", (M, 2 * d))
@@ -271,10 +267,8 @@ class SASEngine:
                          dkv[:, :d], dkv[:, d:], 1.0 / math.sqrt(Dh), 0, ids, p, self.salt[f"attn{i}"], sb, wat)
             Gin, Gb = G(pre + "in_proj_weight"), G(pre + "in_proj_bias")
             Win = self.W(pre + "in_proj_weight")
-            ops.linear_wgrad(dq, s["Q"][i], Gin[:d], slab)
-            ops.colsum(dq, Gb[:d], wsc)
-            ops.linear_wgrad(dkv, s["x"][i], Gin[d:], slab)
-            ops.colsum(dkv, Gb[d:], wsc)
+            ops.linear_wgrad(dq, s["Q"][i], Gin[:d], slab, db=Gb[:d])
+            ops.linear_wgrad(dkv, s["x"][i], Gin[d:], slab, db=Gb[d:])
             dQ = e("dQ", (M, d))
             ops.linear_dgrad(dq, Win[:d], dQ, resid=dx1)
             dxi = e("dxi", (M, d))

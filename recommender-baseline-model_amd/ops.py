@@ -71,18 +71,24 @@ def linear_dgrad(dY, W, dX, **epi_kw):
 
 
 def split_for(M_tok, n_out, k_in):
+    """Split-K factor of the weight-gradient GEMM: ~1024 blocks of 64x64 output tiles, >= 256 rows each."""
     tiles = -(-n_out // 64) * -(-k_in // 64)
-    return int(max(1, min(-(-512 // tiles), -(-M_tok // 128))))
+    return int(max(1, min(-(-1024 // tiles), -(-M_tok // 256))))
 
 
-def linear_wgrad(dY, X, dW, slab, split_k=None):
-    """dW [N,K] += dY^T X over M token rows (split-K slabs, deterministic reduce)."""
+def wgrad_slab_numel(M_tok, n_out, k_in):
+    return split_for(M_tok, n_out, k_in) * (n_out * k_in + n_out)
+
+
+def linear_wgrad(dY, X, dW, slab, db=None, split_k=None, accumulate=True):
+    """dW [N,K] (+)= dY^T X and db [N] (+)= colsum(dY) over M token rows (rs_linear_wgrad)."""
     M, N = dY.shape
     K = X.shape[1]
     s = split_k or split_for(M, N, K)
-    assert slab.numel() >= s * N * K, "slab workspace too small"
-    gemm(dY, X, slab, N, K, M, True, True, None, split_k=s, slab=slab)
-    call("rs_reduce_slabs", ptr(slab), s, N * K, ptr(dW), 1, stream())
+    assert slab.numel() >= s * (N * K + N), "slab workspace too small"
+    assert dY.dtype == X.dtype
+    call("rs_linear_wgrad", dtype_code(dY), M, N, K, ptr(dY), ld(dY), ptr(X), ld(X), ptr(dW), ptr(db),
+         int(accumulate), s, ptr(slab), stream())
 
 
 def colsum(X, out, ws, accumulate=True):

@@ -1,0 +1,133 @@
+#!/usr/bin/env python
+"""Per-op micro-benchmark of the C-ABI kernels at a config's shapes (GPU only).
+
+    python tools/kbench.py [--config cfg2] [--dtype bf16] [--reps 50]
+
+Each op is launched `reps` times back to back on one stream and timed with HIP
+events on that stream; prints avg microseconds and the algorithmic HBM rate.
+"""
+import argparse
+import math
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import rbm_amd  # noqa: E402,F401
+from rbm_amd import ops  # noqa: E402
+
+SHAPES = {"cfg2": dict(B=128, T=200, d=128, V=3416, H=1, ff=128),
+          "cfg3": dict(B=64, T=200, d=256, V=26744, H=2, ff=1024),
+          "cfg4": dict(B=128, T=50, d=128, V=54542, H=1, ff=128)}
+
+
+def timeit(fn, reps):
+    for _ in range(3):
+        fn()
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        fn()
+    e1.record(s)
+    e1.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="cfg2")
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--reps", type=int, default=50)
+    a = ap.parse_args()
+    c = SHAPES[a.config]
+    B, T, d, V, H, ff = c["B"], c["T"], c["d"], c["V"], c["H"], c["ff"]
+    M = B * T
+    dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    es = 2 if dt == torch.bfloat16 else 4
+    dev = "cuda"
+    g = torch.Generator(device=dev).manual_seed(0)
+
+    def rn(*shape, dtype=dt):
+        return torch.randn(*shape, device=dev, generator=g).to(dtype)
+
+    ids = torch.randint(1, V + 1, (B, T), device=dev, generator=g)
+    ids[:, :40] = 0
+    pos = torch.randint(1, V + 1, (B, T), device=dev, generator=g)
+    neg = torch.randint(1, V + 1, (B, T), device=dev, generator=g)
+    x, y, z = rn(M, d), rn(M, d), rn(M, d)
+    W, Wff, bias, bff = rn(d, d), rn(ff, d), torch.randn(d, device=dev), torch.randn(ff, device=dev)
+    yff = rn(M, ff)
+    sb = torch.zeros(1, dtype=torch.int64, device=dev)
+    rows = []
+
+    def rec(name, us, nbytes, flops=0.0):
+        rows.append((name, us, nbytes / (us * 1e-6) / 1e9, flops / (us * 1e-6) / 1e12))
+
+    mb = M * d * es
+    rec("linear_fwd d->d +bias", timeit(lambda: ops.linear_fwd(x, W, y, bias=bias), a.reps), 2 * mb, 2 * M * d * d)
+    rec("linear_fwd d->ff +bias+relu+drop", timeit(lambda: ops.linear_fwd(
+        x, Wff, yff, bias=bff, act=ops.ACT_RELU, drop_p=0.2, drop_seed=7, seed_base=sb, drop_ld=ff), a.reps),
+        mb + M * ff * es, 2 * M * d * ff)
+    rec("linear_fwd d->d +bias+drop+resid+rowmask", timeit(lambda: ops.linear_fwd(
+        x, W, y, bias=bias, drop_p=0.2, drop_seed=7, seed_base=sb, drop_ld=d, resid=z, rowmask_ids=ids), a.reps),
+        3 * mb, 2 * M * d * d)
+    rec("linear_dgrad d<-d", timeit(lambda: ops.linear_dgrad(y, W, z), a.reps), 2 * mb, 2 * M * d * d)
+    dW = torch.zeros(d, d, device=dev)
+    db = torch.zeros(d, device=dev)
+    for sk in (None, 16, 32, 64, 128):
+        s = sk or ops.split_for(M, d, d)
+        slab = torch.empty(s * (d * d + d), device=dev)
+        rec(f"linear_wgrad+bias split={s}", timeit(lambda: ops.linear_wgrad(y, x, dW, slab, db=db, split_k=s),
+                                                   a.reps), 2 * mb, 2 * M * d * d)
+    gam, bet = torch.ones(d, device=dev), torch.zeros(d, device=dev)
+    mu, ri = torch.empty(M, device=dev), torch.empty(M, device=dev)
+    rec("layernorm_fwd", timeit(lambda: ops.layernorm_fwd(x, gam, bet, 1e-8, y, mu, ri, 0), a.reps), 2 * mb)
+    ws = torch.empty(2 * 128 * d, device=dev)
+    dg, dbt = torch.zeros(d, device=dev), torch.zeros(d, device=dev)
+    rec("layernorm_bwd", timeit(lambda: ops.layernorm_bwd(x, y, gam, mu, ri, 1e-8, z, dg, dbt, ws, 0), a.reps),
+        3 * mb)
+    wsc = torch.empty(64 * d, device=dev)
+    rec("colsum", timeit(lambda: ops.colsum(y, db, wsc), a.reps), mb)
+    table = rn(V + 1, d)
+    pe = rn(T, d)
+    rec("embed_fwd", timeit(lambda: ops.embed_fwd(0, ids, T, table, pe, math.sqrt(d), 0.2, 5, sb, x), a.reps), 2 * mb)
+    dtab = torch.zeros(V + 1, d, device=dev)
+    dpos = torch.zeros(T, d, device=dev)
+    rec("embed_bwd (table atomics + pos)", timeit(lambda: ops.embed_bwd(0, ids, T, y, math.sqrt(d), 0.2, 5, sb, dtab,
+                                                                      dpos), a.reps), mb + M * d * 4)
+    rec("embed_bwd pos only", timeit(lambda: ops.embed_bwd(0, ids, T, y, math.sqrt(d), 0.2, 5, sb, None, dpos),
+                                     a.reps), mb)
+    pl, nl = torch.empty(M, device=dev), torch.empty(M, device=dev)
+    rec("sampled_logits_fwd", timeit(lambda: ops.sampled_logits_fwd(x, table, pos, neg, pl, nl), a.reps), 3 * mb)
+    rec("sampled_logits_bwd", timeit(lambda: ops.sampled_logits_bwd(x, table, pos, neg, pl, nl, y, dtab), a.reps),
+        4 * mb + 2 * M * d * 4)
+    Dh = d // H
+    q, kv, o = rn(M, d), rn(M, 2 * d), rn(M, d)
+    lse = torch.empty(B * H * T, device=dev)
+    aflops = 2.0 * T * (T + 1) * Dh * B * H
+    rec("attn_fwd causal drop", timeit(lambda: ops.attn_fwd(B, T, H, Dh, q, kv[:, :d], kv[:, d:], o, lse,
+                                                            1 / math.sqrt(Dh), 0, ids, 0.2, 9, sb), a.reps),
+        4 * mb, aflops)
+    dq, dkv = rn(M, d), rn(M, 2 * d)
+    wat = torch.empty(B * H * T, device=dev)
+    rec("attn_bwd causal drop", timeit(lambda: ops.attn_bwd(B, T, H, Dh, q, kv[:, :d], kv[:, d:], o, y, lse, dq,
+                                                            dkv[:, :d], dkv[:, d:], 1 / math.sqrt(Dh), 0, ids, 0.2,
+                                                            9, sb, wat), a.reps), 8 * mb, 2.5 * aflops)
+    n = 662400
+    p, gg, m1, v1 = (torch.randn(n, device=dev) for _ in range(4))
+    v1.abs_()
+    pbf = torch.empty(n, dtype=torch.bfloat16, device=dev)
+    st = torch.tensor([1.0, 0.001, 1.0, 0], dtype=torch.float64, device=dev)
+    hy = torch.tensor([1e-3, 0.9, 0.999, 1e-8, 0.0], device=dev)
+    rec("adam_step (662k params)", timeit(lambda: ops.adam_step(p, gg, m1, v1, pbf, st, hy), a.reps), n * 4 * 7 + n * 2)
+    print(f"{'op':45s} {'us':>9s} {'GB/s':>9s} {'TFLOP/s':>8s}")
+    for name, us, gbs, tf in rows:
+        print(f"{name:45s} {us:9.2f} {gbs:9.1f} {tf:8.2f}")
+
+
+if __name__ == "__main__":
+    main()
