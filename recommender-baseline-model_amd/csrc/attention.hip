@@ -398,6 +398,29 @@ static hipError_t dispatch(bool fwd, int64_t Dh, AttnArgs& a, hipStream_t s) {
   }
 }
 
+bool attn_lds_supported(int64_t T, int64_t Dh);
+hipError_t attn_lds_fwd(int64_t B, int64_t T, int64_t H, int64_t Dh, const void* q, int64_t ldq, const void* k,
+                        int64_t ldk, const void* v, int64_t ldv, void* o, int64_t ldo, float* lse, float scale,
+                        int mask_kind, const int64_t* ids, float drop_p, uint64_t seed, const uint64_t* seed_base,
+                        hipStream_t s);
+hipError_t attn_lds_bwd(int64_t B, int64_t T, int64_t H, int64_t Dh, const void* q, int64_t ldq, const void* k,
+                        int64_t ldk, const void* v, int64_t ldv, const void* o, int64_t ldo, const void* dout,
+                        int64_t lddo, const float* lse, void* dq, int64_t lddq, void* dk, int64_t lddk, void* dv,
+                        int64_t lddv, float scale, int mask_kind, const int64_t* ids, float drop_p, uint64_t seed,
+                        const uint64_t* seed_base, float* delta, hipStream_t s);
+
+// bf16 storage with T <= 256 takes the LDS-resident kernels (attention_lds.hip); fp32 (the
+// parity mode) and anything else the register/LDS-chunk kernels above.  RS_ATTN_LEGACY=1 forces
+// the latter (A/B testing).
+static bool use_lds_path(int dtype, int64_t T, int64_t Dh) {
+  static int legacy = -1;
+  if (legacy < 0) {
+    const char* e = getenv("RS_ATTN_LEGACY");
+    legacy = (e && e[0] == '1') ? 1 : 0;
+  }
+  return !legacy && dtype == RS_DTYPE_BF16 && attn_lds_supported(T, Dh);
+}
+
 static int check(int dtype, int64_t T, int64_t Dh, const int64_t* lds, int n) {
   if (T <= 0 || T > 256) return RS_ERR_UNSUPPORTED;
   if (Dh != 32 && Dh != 64 && Dh != 128) return RS_ERR_UNSUPPORTED;
@@ -418,10 +441,13 @@ int rs_attn_fwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t Dh, const vo
   if (c) return c;
   if (mask_kind == 1 && !ids) return RS_ERR_ARG;
   AttnArgs a = {};
+  hipStream_t s = (hipStream_t)stream;
+  if (use_lds_path(dtype, T, Dh))
+    return (int)attn_lds_fwd(B, T, H, Dh, q, ldq, k, ldk, v, ldv, o, ldo, lse, scale, mask_kind, ids, drop_p, seed,
+                             seed_base, s);
   a.B = B; a.T = T; a.H = H; a.q = q; a.ldq = ldq; a.k = k; a.ldk = ldk; a.v = v; a.ldv = ldv;
   a.o = o; a.ldo = ldo; a.lse = lse; a.scale = scale; a.mask_kind = mask_kind; a.ids = ids;
   a.drop_p = drop_p; a.seed = seed; a.seed_base = seed_base;
-  hipStream_t s = (hipStream_t)stream;
   return (int)(dtype == RS_DTYPE_BF16 ? dispatch<__bf16>(true, Dh, a, s) : dispatch<float>(true, Dh, a, s));
 }
 
@@ -434,6 +460,9 @@ int rs_attn_bwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t Dh, const vo
   int c = check(dtype, T, Dh, lds, 8);
   if (c) return c;
   if (mask_kind == 1 && !ids) return RS_ERR_ARG;
+  if (use_lds_path(dtype, T, Dh))
+    return (int)attn_lds_bwd(B, T, H, Dh, q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, dq, lddq, dk, lddk, dv,
+                             lddv, scale, mask_kind, ids, drop_p, seed, seed_base, ws, (hipStream_t)stream);
   AttnArgs a = {};
   a.B = B; a.T = T; a.H = H; a.q = q; a.ldq = ldq; a.k = k; a.ldk = ldk; a.v = v; a.ldv = ldv;
   a.o = const_cast<void*>(o); a.ldo = ldo; a.dout = dout; a.lddo = lddo; a.dq = dq; a.lddq = lddq;

@@ -1,0 +1,502 @@
+// LDS-resident attention for bf16, T <= 256, head dim 32/64/128 (gfx950).
+//
+// Same math and masks as attention.hip (the reference call sites are listed
+// there): S = scale * q.k^T, causal -inf (SAS) or key-padding -1e9 (BERT),
+// P = softmax(S), dropout(P), O = P.v; backward recomputes P from the row
+// logsumexp.  Design (CDNA4):
+//
+//  * one workgroup = 4 waves = one (sequence, head) and a 1/nsplit share of its
+//    16-row tiles; the two operands every tile needs (K,V forward and for dQ;
+//    Q,dO for dK/dV) are staged ONCE into LDS as row-major images with a
+//    32-byte row pad (T*Dh*2 B each: 51 KB at T=200, Dh=128), so HBM/L2 sees
+//    each of q,k,v,o,dO about once per split;
+//  * "key on the register axis": the first product of each pair is computed
+//    transposed (S^T = K.Q^T in the forward / dQ pass, S = Q.K^T in the dK/dV
+//    pass) so that its 16x16 accumulator tiles, packed pairwise to bf16, ARE
+//    the B operand of the second product (O^T = V^T.P^T, dQ^T = K^T.dS^T,
+//    dV^T = dO^T.P, dK^T = Q^T.dS): no P/dS round trip through LDS.  The k order
+//    inside a 32-deep step is then {16(j>>2) + 4g + (j&3)}, and the matching A
+//    operand (the transposed image) is read with ds_read_b64_tr_b16;
+//  * softmax statistics per query live on one lane (+2 cross-group shuffles).
+#include "common.h"
+#include "../../include/recsys_hip.h"
+
+typedef __attribute__((ext_vector_type(4))) __bf16 bf4;
+typedef __bf16 bf16;
+
+struct AttnLdsArgs {
+  int64_t B, T, H;
+  const bf16* q; int64_t ldq;
+  const bf16* k; int64_t ldk;
+  const bf16* v; int64_t ldv;
+  const bf16* o; int64_t ldo;
+  const bf16* dout; int64_t lddo;
+  bf16* out; int64_t ldout;     // forward: O
+  bf16* dq; int64_t lddq;
+  bf16* dk; int64_t lddk;
+  bf16* dv; int64_t lddv;
+  float* lse;                    // forward writes; backward reads
+  float* delta;                  // dQ pass writes, dK/dV pass reads
+  float scale;
+  int mask_kind;                 // 0 causal (-inf), 1 key padding (-1e9)
+  const int64_t* ids;
+  float drop_p;
+  uint64_t seed;
+  const uint64_t* seed_base;
+  int nsplit;
+};
+
+#define NEG_INF (-__builtin_inff())
+
+template <int DH> struct Img { static constexpr int LD = DH + 16; };  // row stride (elements), +32 B pad
+
+__device__ __forceinline__ bf16x8 cat8(bf4 a, bf4 b) {
+  return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// A operand = X^T for a 32-row k step starting at image row rb, columns c0..c0+15 (X row-major image)
+__device__ __forceinline__ bf16x8 tr_frag(const bf16* img, int ld, int rb, int c0, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const bf16* a0 = img + (rb + 4 * g + q) * ld + c0 + 4 * p;
+  const bf4 x = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf4*)a0);
+  const bf4 y = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf4*)(a0 + 16 * ld));
+  return cat8(x, y);
+}
+
+// row fragment (A or B operand in natural k order) from an LDS image
+__device__ __forceinline__ bf16x8 row_frag(const bf16* img, int ld, int row, int col) {
+  return *reinterpret_cast<const bf16x8*>(img + row * ld + col);
+}
+
+__device__ __forceinline__ bf16x8 pack8(const f32x4& a, const f32x4& b) {
+  bf16x8 r;
+  r[0] = (bf16)a[0]; r[1] = (bf16)a[1]; r[2] = (bf16)a[2]; r[3] = (bf16)a[3];
+  r[4] = (bf16)b[0]; r[5] = (bf16)b[1]; r[6] = (bf16)b[2]; r[7] = (bf16)b[3];
+  return r;
+}
+
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// global row chunk (zero beyond T)
+__device__ __forceinline__ bf16x8 gload8(const bf16* base, int64_t ld, int64_t row, int64_t T, int col) {
+  if (row < T) return *reinterpret_cast<const bf16x8*>(base + row * ld + col);
+  bf16x8 z;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) z[j] = (bf16)0.0f;
+  return z;
+}
+
+// stage rows [0, rows) of a (T x DH) head slice into an LDS image (rows >= T zero)
+template <int DH>
+__device__ __forceinline__ void stage(bf16* img, const bf16* src, int64_t ld, int64_t T, int rows, int tid) {
+  constexpr int CPR = DH / 8, LD = Img<DH>::LD;
+  for (int i = tid; i < rows * CPR; i += 256) {
+    const int r = i / CPR, c = (i % CPR) * 8;
+    *reinterpret_cast<bf16x8*>(img + r * LD + c) = gload8(src, ld, r, T, c);
+  }
+}
+
+// 1.0 where the key is masked by key padding (mask_kind 1), else 0; keys >= T are handled separately
+__device__ __forceinline__ void stage_keymask(float* km, const AttnLdsArgs& a, int64_t b, int rows, int tid) {
+  for (int i = tid; i < rows; i += 256)
+    km[i] = (a.mask_kind == 1 && i < a.T && a.ids[b * a.T + i] == 0) ? 1.f : 0.f;
+}
+
+// 0 = live score, 1 = -inf (causal / beyond the sequence), 2 = filled with -1e9 (key padding)
+__device__ __forceinline__ int mask_state(const AttnLdsArgs& a, const float* km, int64_t q, int64_t key) {
+  if (key >= a.T) return 1;
+  if (a.mask_kind == 0) return key > q ? 1 : 0;
+  return km[key] != 0.f ? 2 : 0;
+}
+__device__ __forceinline__ float apply_mask(int st, float s) { return st == 0 ? s : (st == 1 ? NEG_INF : -1e9f); }
+__device__ __forceinline__ float masked(const AttnLdsArgs& a, const float* km, int64_t q, int64_t key, float s) {
+  return apply_mask(mask_state(a, km, q, key), s);
+}
+
+// tiles of 16 queries handled by this workgroup: split, split+nsplit, ...
+__device__ __forceinline__ int last_tile_of_split(int nq, int split, int nsplit) {
+  return split + ((nq - 1 - split) / nsplit) * nsplit;
+}
+
+// ------------------------------------------------------------------ forward
+template <int DH>
+__global__ __launch_bounds__(256) void attn_fwd_lds_kernel(AttnLdsArgs a) {
+  constexpr int LD = Img<DH>::LD, KC = DH / 32, DT = DH / 16, NKT = 16;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
+  const int64_t bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int split = blockIdx.x, T = (int)a.T;
+  const int nq = (T + 15) / 16;
+  if (split >= nq) return;
+  const int lastq = last_tile_of_split(nq, split, a.nsplit);
+  const int kneed = a.mask_kind == 0 ? min(T, 16 * (lastq + 1)) : T;
+  const int rows = ((kneed + 31) / 32) * 32;
+  bf16* Ks = reinterpret_cast<bf16*>(smem);
+  bf16* Vs = Ks + rows * LD;
+  float* km = reinterpret_cast<float*>(Vs + rows * LD);
+  const bf16* Kg = a.k + b * a.T * a.ldk + h * DH;
+  const bf16* Vg = a.v + b * a.T * a.ldv + h * DH;
+  const bf16* Qg = a.q + b * a.T * a.ldq + h * DH;
+  stage<DH>(Ks, Kg, a.ldk, a.T, rows, tid);
+  stage<DH>(Vs, Vg, a.ldv, a.T, rows, tid);
+  stage_keymask(km, a, b, rows, tid);
+  __syncthreads();
+  const uint64_t seed = eff_seed(a.seed, a.seed_base);
+
+  for (int qt = split + wave * a.nsplit; qt < nq; qt += 4 * a.nsplit) {
+    const int q0 = qt * 16;
+    const int64_t qrow = q0 + cl;  // this lane's query
+    bf16x8 qf[KC];
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) qf[kc] = gload8(Qg, a.ldq, qrow, a.T, kc * 32 + 8 * g);
+    const int nkt = a.mask_kind == 0 ? qt + 1 : nq;
+    f32x4 s[NKT];
+    float mx = NEG_INF;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      s[kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      if (kt < nkt) {
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) s[kt] = mfma16(row_frag(Ks, LD, kt * 16 + cl, kc * 32 + 8 * g), qf[kc], s[kt]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float x = masked(a, km, qrow, kt * 16 + 4 * g + r, s[kt][r] * a.scale);
+          s[kt][r] = x;
+          mx = fmaxf(mx, x);
+        }
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float sm = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      if (kt < nkt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = s[kt][r] == NEG_INF ? 0.f : __expf(s[kt][r] - mx);
+          s[kt][r] = e;
+          sm += e;
+        }
+      }
+    }
+    sm += __shfl_xor(sm, 16, 64);
+    sm += __shfl_xor(sm, 32, 64);
+    const float inv = 1.f / sm;
+    if (g == 0 && qrow < a.T) a.lse[bh * a.T + qrow] = mx + __logf(sm);
+    // P^T (+ dropout), packed pairwise as the B operand of O^T = V^T P^T
+    f32x4 o[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < NKT / 2; ++c) {
+      if (2 * c < nkt) {
+        f32x4 p0 = s[2 * c], p1 = s[2 * c + 1];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t k0 = (2 * c) * 16 + 4 * g + r, k1 = k0 + 16;
+          float x0 = p0[r] * inv, x1 = (2 * c + 1 < nkt) ? p1[r] * inv : 0.f;
+          if (a.drop_p > 0.f) {
+            x0 *= drop_mul(a.drop_p, seed, (uint64_t)((bh * a.T + qrow) * a.T + k0));
+            x1 *= drop_mul(a.drop_p, seed, (uint64_t)((bh * a.T + qrow) * a.T + k1));
+          }
+          p0[r] = x0;
+          p1[r] = x1;
+        }
+        const bf16x8 pb = pack8(p0, p1);
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) o[dt] = mfma16(tr_frag(Vs, LD, 32 * c, 16 * dt, lane), pb, o[dt]);
+      }
+    }
+    if (qrow < a.T) {
+      bf16* O = a.out + (b * a.T + qrow) * a.ldout + h * DH;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        bf4 w;
+        w[0] = (bf16)o[dt][0]; w[1] = (bf16)o[dt][1]; w[2] = (bf16)o[dt][2]; w[3] = (bf16)o[dt][3];
+        *reinterpret_cast<bf4*>(O + 16 * dt + 4 * g) = w;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ backward: delta + dQ
+template <int DH>
+__global__ __launch_bounds__(256) void attn_bwd_dq_lds_kernel(AttnLdsArgs a) {
+  constexpr int LD = Img<DH>::LD, KC = DH / 32, DT = DH / 16;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
+  const int64_t bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int split = blockIdx.x, T = (int)a.T;
+  const int nq = (T + 15) / 16;
+  if (split >= nq) return;
+  const int lastq = last_tile_of_split(nq, split, a.nsplit);
+  const int kneed = a.mask_kind == 0 ? min(T, 16 * (lastq + 1)) : T;
+  const int rows = ((kneed + 31) / 32) * 32;
+  bf16* Ks = reinterpret_cast<bf16*>(smem);
+  bf16* Vs = Ks + rows * LD;
+  float* km = reinterpret_cast<float*>(Vs + rows * LD);
+  stage<DH>(Ks, a.k + b * a.T * a.ldk + h * DH, a.ldk, a.T, rows, tid);
+  stage<DH>(Vs, a.v + b * a.T * a.ldv + h * DH, a.ldv, a.T, rows, tid);
+  stage_keymask(km, a, b, rows, tid);
+  __syncthreads();
+  const uint64_t seed = eff_seed(a.seed, a.seed_base);
+  const bf16* Qg = a.q + b * a.T * a.ldq + h * DH;
+  const bf16* Og = a.o + b * a.T * a.ldo + h * DH;
+  const bf16* dOg = a.dout + b * a.T * a.lddo + h * DH;
+
+  for (int qt = split + wave * a.nsplit; qt < nq; qt += 4 * a.nsplit) {
+    const int q0 = qt * 16;
+    const int64_t qrow = q0 + cl;
+    bf16x8 qf[KC], df[KC];
+    float dl = 0.f;
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      qf[kc] = gload8(Qg, a.ldq, qrow, a.T, kc * 32 + 8 * g);
+      df[kc] = gload8(dOg, a.lddo, qrow, a.T, kc * 32 + 8 * g);
+      const bf16x8 of = gload8(Og, a.ldo, qrow, a.T, kc * 32 + 8 * g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dl += (float)df[kc][j] * (float)of[j];
+    }
+    dl += __shfl_xor(dl, 16, 64);
+    dl += __shfl_xor(dl, 32, 64);  // delta = rowsum(dO * O) for query qrow
+    if (g == 0 && qrow < a.T) a.delta[bh * a.T + qrow] = dl;
+    const float lq = qrow < a.T ? a.lse[bh * a.T + qrow] : 0.f;
+    const int nkt = a.mask_kind == 0 ? qt + 1 : nq;
+    f32x4 acc[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) acc[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; 2 * c < nkt; ++c) {
+      f32x4 ds2[2];
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const int t = 2 * c + hf;
+        f32x4 s = (f32x4){0.f, 0.f, 0.f, 0.f}, dp = (f32x4){0.f, 0.f, 0.f, 0.f};
+        if (t < nkt) {
+#pragma unroll
+          for (int kc = 0; kc < KC; ++kc) {
+            s = mfma16(row_frag(Ks, LD, t * 16 + cl, kc * 32 + 8 * g), qf[kc], s);
+            dp = mfma16(row_frag(Vs, LD, t * 16 + cl, kc * 32 + 8 * g), df[kc], dp);
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t key = t * 16 + 4 * g + r;
+          // masked_fill has no gradient: dS = 0 on masked scores (-inf and -1e9 alike)
+          const bool live = t < nkt && qrow < a.T && mask_state(a, km, qrow, key) == 0;
+          const float p = live ? __expf(s[r] * a.scale - lq) : 0.f;
+          float dpe = dp[r];
+          if (a.drop_p > 0.f) dpe *= drop_mul(a.drop_p, seed, (uint64_t)((bh * a.T + qrow) * a.T + key));
+          ds2[hf][r] = live ? p * (dpe - dl) * a.scale : 0.f;
+        }
+      }
+      const bf16x8 bds = pack8(ds2[0], ds2[1]);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) acc[dt] = mfma16(tr_frag(Ks, LD, 32 * c, 16 * dt, lane), bds, acc[dt]);
+    }
+    if (qrow < a.T) {
+      bf16* dQ = a.dq + (b * a.T + qrow) * a.lddq + h * DH;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        bf4 w;
+        w[0] = (bf16)acc[dt][0]; w[1] = (bf16)acc[dt][1]; w[2] = (bf16)acc[dt][2]; w[3] = (bf16)acc[dt][3];
+        *reinterpret_cast<bf4*>(dQ + 16 * dt + 4 * g) = w;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ backward: dK, dV
+template <int DH>
+__global__ __launch_bounds__(256) void attn_bwd_dkv_lds_kernel(AttnLdsArgs a) {
+  constexpr int LD = Img<DH>::LD, KC = DH / 32, DT = DH / 16;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
+  const int64_t bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int split = blockIdx.x, T = (int)a.T;
+  const int nk = (T + 15) / 16;  // key tiles
+  if (split >= nk) return;
+  // queries needed: causal -> from the first key tile of this split on (all queries of the
+  // sequence, kept simple: the image always starts at query 0)
+  const int rows = ((T + 31) / 32) * 32;
+  bf16* Qs = reinterpret_cast<bf16*>(smem);
+  bf16* dOs = Qs + rows * LD;
+  float* lse_s = reinterpret_cast<float*>(dOs + rows * LD);
+  float* dl_s = lse_s + rows;
+  float* km = dl_s + rows;
+  stage<DH>(Qs, a.q + b * a.T * a.ldq + h * DH, a.ldq, a.T, rows, tid);
+  stage<DH>(dOs, a.dout + b * a.T * a.lddo + h * DH, a.lddo, a.T, rows, tid);
+  for (int i = tid; i < rows; i += 256) {
+    lse_s[i] = i < T ? a.lse[bh * a.T + i] : 0.f;
+    dl_s[i] = i < T ? a.delta[bh * a.T + i] : 0.f;
+  }
+  stage_keymask(km, a, b, rows, tid);
+  __syncthreads();
+  const uint64_t seed = eff_seed(a.seed, a.seed_base);
+  const bf16* Kg = a.k + b * a.T * a.ldk + h * DH;
+  const bf16* Vg = a.v + b * a.T * a.ldv + h * DH;
+  const int nqc = (T + 31) / 32;  // 32-query chunks
+
+  for (int kt = split + wave * a.nsplit; kt < nk; kt += 4 * a.nsplit) {
+    const int64_t key = kt * 16 + cl;  // this lane's key
+    bf16x8 kf[KC], vf[KC];
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      kf[kc] = gload8(Kg, a.ldk, key, a.T, kc * 32 + 8 * g);
+      vf[kc] = gload8(Vg, a.ldv, key, a.T, kc * 32 + 8 * g);
+    }
+    f32x4 dk[DT], dv[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      dk[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      dv[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+    const int c0 = a.mask_kind == 0 ? kt / 2 : 0;
+    for (int c = c0; c < nqc; ++c) {
+      f32x4 pd2[2], ds2[2];
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const int t = 2 * c + hf;
+        f32x4 s = (f32x4){0.f, 0.f, 0.f, 0.f}, dp = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+          s = mfma16(row_frag(Qs, LD, t * 16 + cl, kc * 32 + 8 * g), kf[kc], s);
+          dp = mfma16(row_frag(dOs, LD, t * 16 + cl, kc * 32 + 8 * g), vf[kc], dp);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t qr = t * 16 + 4 * g + r;
+          const int st = qr < a.T ? mask_state(a, km, qr, key) : 1;
+          const float p = st == 1 ? 0.f : __expf(apply_mask(st, s[r] * a.scale) - lse_s[qr]);
+          const float m = a.drop_p > 0.f ? drop_mul(a.drop_p, seed, (uint64_t)((bh * a.T + qr) * a.T + key)) : 1.f;
+          pd2[hf][r] = p * m;
+          ds2[hf][r] = st == 0 ? p * (dp[r] * m - dl_s[qr]) * a.scale : 0.f;
+        }
+      }
+      const bf16x8 bp = pack8(pd2[0], pd2[1]);
+      const bf16x8 bds = pack8(ds2[0], ds2[1]);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        dv[dt] = mfma16(tr_frag(dOs, LD, 32 * c, 16 * dt, lane), bp, dv[dt]);
+        dk[dt] = mfma16(tr_frag(Qs, LD, 32 * c, 16 * dt, lane), bds, dk[dt]);
+      }
+    }
+    if (key < a.T) {
+      bf16* dK = a.dk + (b * a.T + key) * a.lddk + h * DH;
+      bf16* dV = a.dv + (b * a.T + key) * a.lddv + h * DH;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        bf4 wk, wv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          wk[r] = (bf16)dk[dt][r];
+          wv[r] = (bf16)dv[dt][r];
+        }
+        *reinterpret_cast<bf4*>(dK + 16 * dt + 4 * g) = wk;
+        *reinterpret_cast<bf4*>(dV + 16 * dt + 4 * g) = wv;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ launchers
+template <int DH>
+static size_t fwd_lds_bytes(int T) {
+  const int rows = ((T + 31) / 32) * 32;
+  return (size_t)2 * rows * Img<DH>::LD * 2 + rows * 4;
+}
+template <int DH>
+static size_t dkv_lds_bytes(int T) {
+  const int rows = ((T + 31) / 32) * 32;
+  return (size_t)2 * rows * Img<DH>::LD * 2 + 3 * rows * 4;
+}
+
+static int pick_split(int64_t BH, int ntiles) {
+  // aim for >= 256 workgroups (one per CU at T ~ 200), at least 2 tiles per wave group
+  int s = 1;
+  while (BH * s < 256 && s * 2 <= std::max(1, ntiles / 4)) s *= 2;
+  return s;
+}
+
+bool attn_lds_supported(int64_t T, int64_t Dh) {
+  if (T <= 0 || T > 256) return false;
+  if (Dh != 32 && Dh != 64 && Dh != 128) return false;
+  const size_t need = Dh == 128 ? dkv_lds_bytes<128>((int)T) : Dh == 64 ? dkv_lds_bytes<64>((int)T)
+                                                                            : dkv_lds_bytes<32>((int)T);
+  return need <= 160 * 1024;
+}
+
+template <int DH>
+static hipError_t fwd_t(AttnLdsArgs& a, hipStream_t s) {
+  const int nq = (int)cdiv(a.T, 16);
+  a.nsplit = pick_split(a.B * a.H, nq);
+  const size_t lds = fwd_lds_bytes<DH>((int)a.T);
+  hipLaunchKernelGGL((attn_fwd_lds_kernel<DH>), dim3((unsigned)a.nsplit, (unsigned)(a.B * a.H)), dim3(256), lds, s,
+                     a);
+  return hipGetLastError();
+}
+
+template <int DH>
+static hipError_t bwd_t(AttnLdsArgs& a, hipStream_t s) {
+  const int nq = (int)cdiv(a.T, 16);
+  a.nsplit = pick_split(a.B * a.H, nq);
+  hipLaunchKernelGGL((attn_bwd_dq_lds_kernel<DH>), dim3((unsigned)a.nsplit, (unsigned)(a.B * a.H)), dim3(256),
+                     fwd_lds_bytes<DH>((int)a.T), s, a);
+  hipLaunchKernelGGL((attn_bwd_dkv_lds_kernel<DH>), dim3((unsigned)a.nsplit, (unsigned)(a.B * a.H)), dim3(256),
+                     dkv_lds_bytes<DH>((int)a.T), s, a);
+  return hipGetLastError();
+}
+
+template <int DH>
+static void set_lds_limits() {
+  hipFuncSetAttribute((const void*)attn_fwd_lds_kernel<DH>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipFuncSetAttribute((const void*)attn_bwd_dq_lds_kernel<DH>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                      160 * 1024);
+  hipFuncSetAttribute((const void*)attn_bwd_dkv_lds_kernel<DH>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                      160 * 1024);
+}
+
+static void init_once() {
+  static bool done = false;
+  if (!done) {
+    set_lds_limits<32>();
+    set_lds_limits<64>();
+    set_lds_limits<128>();
+    done = true;
+  }
+}
+
+hipError_t attn_lds_fwd(int64_t B, int64_t T, int64_t H, int64_t Dh, const void* q, int64_t ldq, const void* k,
+                        int64_t ldk, const void* v, int64_t ldv, void* o, int64_t ldo, float* lse, float scale,
+                        int mask_kind, const int64_t* ids, float drop_p, uint64_t seed, const uint64_t* seed_base,
+                        hipStream_t s) {
+  init_once();
+  AttnLdsArgs a = {};
+  a.B = B; a.T = T; a.H = H;
+  a.q = (const bf16*)q; a.ldq = ldq; a.k = (const bf16*)k; a.ldk = ldk; a.v = (const bf16*)v; a.ldv = ldv;
+  a.out = (bf16*)o; a.ldout = ldo; a.lse = lse; a.scale = scale; a.mask_kind = mask_kind; a.ids = ids;
+  a.drop_p = drop_p; a.seed = seed; a.seed_base = seed_base;
+  if (Dh == 128) return fwd_t<128>(a, s);
+  if (Dh == 64) return fwd_t<64>(a, s);
+  return fwd_t<32>(a, s);
+}
+
+hipError_t attn_lds_bwd(int64_t B, int64_t T, int64_t H, int64_t Dh, const void* q, int64_t ldq, const void* k,
+                        int64_t ldk, const void* v, int64_t ldv, const void* o, int64_t ldo, const void* dout,
+                        int64_t lddo, const float* lse, void* dq, int64_t lddq, void* dk, int64_t lddk, void* dv,
+                        int64_t lddv, float scale, int mask_kind, const int64_t* ids, float drop_p, uint64_t seed,
+                        const uint64_t* seed_base, float* delta, hipStream_t s) {
+  init_once();
+  AttnLdsArgs a = {};
+  a.B = B; a.T = T; a.H = H;
+  a.q = (const bf16*)q; a.ldq = ldq; a.k = (const bf16*)k; a.ldk = ldk; a.v = (const bf16*)v; a.ldv = ldv;
+  a.o = (const bf16*)o; a.ldo = ldo; a.dout = (const bf16*)dout; a.lddo = lddo;
+  a.dq = (bf16*)dq; a.lddq = lddq; a.dk = (bf16*)dk; a.lddk = lddk; a.dv = (bf16*)dv; a.lddv = lddv;
+  a.lse = const_cast<float*>(lse); a.delta = delta; a.scale = scale; a.mask_kind = mask_kind; a.ids = ids;
+  a.drop_p = drop_p; a.seed = seed; a.seed_base = seed_base;
+  if (Dh == 128) return bwd_t<128>(a, s);
+  if (Dh == 64) return bwd_t<64>(a, s);
+  return bwd_t<32>(a, s);
+}

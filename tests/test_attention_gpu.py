@@ -1,0 +1,103 @@
+"""rs_attn_fwd / rs_attn_bwd vs a plain PyTorch fp32 reference of the same op.
+
+The reference op is the attention core both models run:
+  SAS  (mask_kind 0): torch F.multi_head_attention_forward's baddbmm(-inf causal mask) /
+       softmax / bmm, called at BS/models/sas_model/sas.py:75
+  BERT (mask_kind 1): BS/models/bert_modules/attention/single.py:13-35 -- masked_fill(key
+       padding, -1e9) / softmax / matmul
+bf16 runs the LDS-resident kernels (attention_lds.hip), fp32 the chunked kernels.
+"""
+import math
+
+import pytest
+import torch
+
+from conftest import rel
+
+pytestmark = pytest.mark.gpu
+
+TOL = {torch.float32: 2e-5, torch.bfloat16: 2e-2}
+
+
+def ref_attention(q, k, v, ids, B, T, H, Dh, mask_kind):
+    """q,k,v: (B*T, H*Dh) fp32 -> o (B*T, H*Dh)"""
+    def heads(x):
+        return x.view(B, T, H, Dh).transpose(1, 2)
+    s = heads(q) @ heads(k).transpose(-1, -2) / math.sqrt(Dh)
+    if mask_kind == 0:
+        blocked = torch.triu(torch.ones(T, T, dtype=torch.bool, device=q.device), 1)
+        s = s.masked_fill(blocked, float("-inf"))
+    else:
+        s = s.masked_fill((ids == 0).view(B, 1, 1, T), -1e9)
+    p = torch.softmax(s, -1)
+    return (p @ heads(v)).transpose(1, 2).reshape(B * T, H * Dh)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("mask_kind", [0, 1])
+@pytest.mark.parametrize("B,T,H,Dh", [(3, 200, 1, 128), (2, 50, 2, 64), (2, 16, 2, 32), (2, 256, 2, 128),
+                                      (3, 37, 1, 64), (2, 200, 2, 128)])
+def test_attention_matches_torch(dtype, mask_kind, B, T, H, Dh):
+    import rbm_amd  # noqa: F401
+    from rbm_amd import ops
+    torch.manual_seed(B * T + H * Dh + mask_kind)
+    d = H * Dh
+    dev = "cuda"
+    ids = torch.randint(1, 50, (B, T), device=dev)
+    for b in range(B):                   # left padding of different lengths (the reference pads left)
+        ids[b, : (b * T) // (B + 1)] = 0
+    q = torch.randn(B * T, d, device=dev)
+    kv = torch.randn(B * T, 2 * d, device=dev)
+    q16, kv16 = q.to(dtype), kv.to(dtype)
+    qr, kr, vr = (t.float().clone().requires_grad_(True) for t in (q16, kv16[:, :d], kv16[:, d:]))
+    o_ref = ref_attention(qr, kr, vr, ids, B, T, H, Dh, mask_kind)
+    do = torch.randn_like(o_ref).to(dtype)
+    o_ref.backward(do.float())
+
+    o = torch.empty(B * T, d, device=dev, dtype=dtype)
+    lse = torch.empty(B * H * T, device=dev)
+    sc = 1.0 / math.sqrt(Dh)
+    ops.attn_fwd(B, T, H, Dh, q16, kv16[:, :d], kv16[:, d:], o, lse, sc, mask_kind, ids, 0.0, 0, None)
+    dq = torch.empty_like(q16)
+    dkv = torch.empty_like(kv16)
+    ws = torch.empty(B * H * T, device=dev)
+    ops.attn_bwd(B, T, H, Dh, q16, kv16[:, :d], kv16[:, d:], o, do, lse, dq, dkv[:, :d], dkv[:, d:], sc, mask_kind,
+                 ids, 0.0, 0, None, ws)
+    torch.cuda.synchronize()
+    tol = TOL[dtype]
+    assert rel(o.float().cpu(), o_ref.detach().cpu()) < tol
+    assert rel(dq.float().cpu(), qr.grad.cpu()) < 2 * tol
+    assert rel(dkv[:, :d].float().cpu(), kr.grad.cpu()) < 2 * tol
+    assert rel(dkv[:, d:].float().cpu(), vr.grad.cpu()) < 2 * tol
+
+
+@pytest.mark.parametrize("mask_kind", [0, 1])
+def test_attention_dropout_is_consistent_between_fwd_and_bwd(mask_kind):
+    """With dropout on, the backward must regenerate exactly the forward's mask: check the
+    bf16 kernels against the fp32 kernels run with the same seed (same counter-based RNG)."""
+    import rbm_amd  # noqa: F401
+    from rbm_amd import ops
+    torch.manual_seed(5)
+    B, T, H, Dh = 2, 200, 1, 128
+    d = H * Dh
+    dev = "cuda"
+    ids = torch.randint(1, 50, (B, T), device=dev)
+    ids[0, :60] = 0
+    q = torch.randn(B * T, d, device=dev)
+    kv = torch.randn(B * T, 2 * d, device=dev)
+    do = torch.randn(B * T, d, device=dev)
+    sb = torch.full((1,), 3, dtype=torch.int64, device=dev)
+    outs = {}
+    for dt in (torch.float32, torch.bfloat16):
+        qq, kk, dd = q.to(dt), kv.to(dt), do.to(dt)
+        o = torch.empty(B * T, d, device=dev, dtype=dt)
+        lse = torch.empty(B * H * T, device=dev)
+        ops.attn_fwd(B, T, H, Dh, qq, kk[:, :d], kk[:, d:], o, lse, 0.1, mask_kind, ids, 0.2, 77, sb)
+        dq, dkv = torch.empty_like(qq), torch.empty_like(kk)
+        ws = torch.empty(B * H * T, device=dev)
+        ops.attn_bwd(B, T, H, Dh, qq, kk[:, :d], kk[:, d:], o, dd, lse, dq, dkv[:, :d], dkv[:, d:], 0.1, mask_kind,
+                     ids, 0.2, 77, sb, ws)
+        outs[dt] = [t.float().cpu() for t in (o, dq, dkv)]
+    torch.cuda.synchronize()
+    for a, b in zip(outs[torch.bfloat16], outs[torch.float32]):
+        assert rel(a, b) < 3e-2
