@@ -35,7 +35,10 @@ extern "C" {
  *   act: 1 relu / 2 gelu_tanh (pre-activation stored to aux_out if set),
  *        3 relu_bwd (v *= aux>0), 4 gelu_bwd (v *= gelu'(aux))
  *   dropout: v *= keep(drop_seed, m*drop_ld+n) / (1-drop_p)
- *   v += resid[m*ldres+n];  v *= (rowmask_ids[m] != 0);  v += C (accumulate)    */
+ *   v += resid[m*ldres+n];  v *= (rowmask_ids[m] != 0);
+ *   post dropout: v *= keep(post_drop_seed, m*drop_ld+n) / (1-post_drop_p);  v += C (accumulate)
+ * rows_dev (nullable, device int): only rows m < min(M, *rows_dev) are computed/stored -- the
+ * row count of a device-side compaction (BERT labelled rows) without a host sync.           */
 typedef struct rs_epilogue {
   const float* bias;
   float alpha;
@@ -51,6 +54,9 @@ typedef struct rs_epilogue {
   int64_t ldres;
   const int64_t* rowmask_ids;
   int accumulate;
+  float post_drop_p;
+  uint64_t post_drop_seed;
+  const int* rows_dev;
 } rs_epilogue;
 
 /* C[M,N] = epi(A . B^T).  a_kmajor: A(m,k) at A[k*lda+m] (else A[m*lda+k]);
@@ -75,11 +81,13 @@ int rs_reduce_slabs2(const float* slab, int splits, int64_t n0, float* out0, int
  *   dW[N,K] (+)= sum_m dY[m,:]^T X[m,:];   db[N] (+)= sum_m dY[m,:]   (db nullable)
  * split-K over the rows into `splits` fp32 slabs (slab >= splits*(N*K + N) floats), the bias
  * column sums fused into the GEMM, then one deterministic reduce.  accumulate: += into dW/db.
+ * rows_dev (nullable, device int): only the first min(M, *rows_dev) rows contribute.
  * Replaces the autograd weight/bias gradients of nn.Linear / nn.Conv1d / in_proj / out_proj
  * (BS/models/sas_model/sas.py:10-17,45-47; BS/models/bert_modules/attention/multi_head.py:18-19;
  * utils/feed_forward.py:10-11; BS/models/bert.py:10). */
 int rs_linear_wgrad(int dtype, int64_t M, int64_t N, int64_t K, const void* dY, int64_t lddy, const void* X,
-                    int64_t ldx, float* dW, float* db, int accumulate, int splits, float* slab, void* stream);
+                    int64_t ldx, float* dW, float* db, int accumulate, int splits, float* slab, const int* rows_dev,
+                    void* stream);
 
 /* out[n] (+)= sum_m X[m*ldx+n] over M rows (bias gradients).  ws: >= 64*N floats. */
 int rs_colsum(int dtype, const void* X, int64_t M, int64_t N, int64_t ldx, float* ws, float* out,
@@ -148,14 +156,27 @@ int rs_bce_bwd(const float* pl, const float* nl, const int64_t* pos, int64_t M, 
 /* BERT loss (BS/trainers/bert.py:36-40): CrossEntropyLoss(ignore_index=0) over
  * R rows of V1 fp32 logits (leading dim ldl).  out[0] = sum of -log p(label),
  * out[1] = count, out[2] = loss (count_override as in rs_bce_fwd).
- * ws >= 3*R floats (row lse + partials). */
+ * ws >= 3*R floats (row lse + partials).  rows_dev (nullable): rows >= *rows_dev are skipped (the
+ * tail of a labelled-row compaction, see rs_compact_rows). */
 int rs_ce_fwd(const float* logits, int64_t R, int64_t V1, int64_t ldl, const int64_t* labels,
-              const float* count_override, float* ws, float* out, void* stream);
+              const float* count_override, float* ws, float* out, const int* rows_dev, void* stream);
 /* dlogits (may alias logits) = dloss * (softmax - onehot)/count on labelled rows, 0 else; dtype of
  * dlogits selected by dtype (fp32 or bf16 copy for the following GEMMs). */
 int rs_ce_bwd(int dtype, const float* logits, int64_t R, int64_t V1, int64_t ldl, const int64_t* labels,
               const float* count, const float* dloss, const float* ws, void* dlogits, int64_t lddl,
-              void* stream);
+              const int* rows_dev, void* stream);
+
+/* Labelled-row compaction for the BERT loss head (BS/trainers/bert.py:36-40 drops label-0 rows).
+ * idx[i] = i-th row with labels != 0 (ascending, i < cap), rank[r] = position of row r in idx or -1,
+ * *count = min(#labelled, cap) -- all on the device (the count bounds later GEMMs via rows_dev). */
+int rs_compact_rows(const int64_t* labels, int64_t n, int64_t cap, int32_t* idx, int32_t* rank, int32_t* count,
+                    void* stream);
+/* dst[i,:] = src[idx[i],:] for i < *count, zero rows up to cap; lab_out[i] = labels[idx[i]] (0 beyond). */
+int rs_gather_rows(int dtype, const void* src, int64_t lds, int64_t d, const int32_t* idx, const int32_t* count,
+                   int64_t cap, void* dst, int64_t ldd, const int64_t* labels, int64_t* lab_out, void* stream);
+/* dst[r,:] = rank[r] >= 0 ? src[rank[r],:] : 0 for r < n (the hidden-state gradient scattered back). */
+int rs_scatter_rows(int dtype, const void* src, int64_t lds, int64_t d, const int32_t* rank, int64_t n, void* dst,
+                    int64_t ldd, void* stream);
 
 /* torch.optim.Adam step (BS/trainers/base.py:225-228; amsgrad=False) over a
  * flat fp32 buffer.  hyper (device fp32[5]) = {lr, beta1, beta2, eps, weight_decay}.

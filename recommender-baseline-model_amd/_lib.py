@@ -27,6 +27,7 @@ class Epilogue(C.Structure):
         ("drop_p", f32), ("drop_seed", u64), ("seed_base", vp), ("drop_ld", i64),
         ("resid", vp), ("ldres", i64),
         ("rowmask_ids", vp), ("accumulate", i32),
+        ("post_drop_p", f32), ("post_drop_seed", u64), ("rows_dev", vp),
     ]
 
 
@@ -37,7 +38,7 @@ SIGNATURES = {
     "rs_gemm": [i32, i32, i32, i64, i64, i64, vp, i64, vp, i64, vp, i64, i32, C.POINTER(Epilogue), i32, vp, vp],
     "rs_reduce_slabs": [vp, i32, i64, vp, i32, vp],
     "rs_reduce_slabs2": [vp, i32, i64, vp, i64, vp, i32, vp],
-    "rs_linear_wgrad": [i32, i64, i64, i64, vp, i64, vp, i64, vp, vp, i32, i32, vp, vp],
+    "rs_linear_wgrad": [i32, i64, i64, i64, vp, i64, vp, i64, vp, vp, i32, i32, vp, vp, vp],
     "rs_colsum": [i32, vp, i64, i64, i64, vp, vp, i32, vp],
     "rs_embed_fwd": [i32, i32, vp, i64, i64, vp, vp, i64, f32, f32, u64, vp, vp, vp],
     "rs_embed_bwd": [i32, i32, vp, i64, i64, vp, i64, f32, f32, u64, vp, vp, vp, i32, vp],
@@ -50,8 +51,11 @@ SIGNATURES = {
     "rs_sampled_logits_bwd": [i32, vp, i64, i64, vp, vp, vp, vp, vp, vp, i32, vp, vp],
     "rs_bce_fwd": [vp, vp, vp, i64, vp, vp, vp, vp],
     "rs_bce_bwd": [vp, vp, vp, i64, vp, vp, vp, vp, vp],
-    "rs_ce_fwd": [vp, i64, i64, i64, vp, vp, vp, vp, vp],
-    "rs_ce_bwd": [i32, vp, i64, i64, i64, vp, vp, vp, vp, vp, i64, vp],
+    "rs_ce_fwd": [vp, i64, i64, i64, vp, vp, vp, vp, vp, vp],
+    "rs_ce_bwd": [i32, vp, i64, i64, i64, vp, vp, vp, vp, vp, i64, vp, vp],
+    "rs_compact_rows": [vp, i64, i64, vp, vp, vp, vp],
+    "rs_gather_rows": [i32, vp, i64, i64, vp, vp, i64, vp, i64, vp, vp, vp],
+    "rs_scatter_rows": [i32, vp, i64, i64, vp, i64, vp, i64, vp],
     "rs_adam_prepare": [vp, vp, vp],
     "rs_adam_step": [i64, vp, vp, vp, vp, vp, vp, vp, vp],
     "rs_cast_bf16": [i64, vp, vp, vp],

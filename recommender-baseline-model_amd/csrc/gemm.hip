@@ -107,6 +107,8 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& a, int64_t m, int
   if (e.drop_p > 0.0f) v *= drop_mul(e.drop_p, eff_seed(e.drop_seed, e.seed_base), (uint64_t)(m * e.drop_ld + n));
   if (e.resid) v += to_f(reinterpret_cast<const T*>(e.resid)[m * e.ldres + n]);
   if (e.rowmask_ids) v = (e.rowmask_ids[m] != 0) ? v : 0.0f;
+  if (e.post_drop_p > 0.0f)
+    v *= drop_mul(e.post_drop_p, eff_seed(e.post_drop_seed, e.seed_base), (uint64_t)(m * e.drop_ld + n));
   if (a.c_f32) {
     float* C = reinterpret_cast<float*>(a.C) + m * a.ldc + n;
     *C = e.accumulate ? *C + v : v;
@@ -138,8 +140,12 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
   }
   const int64_t m0 = (bid / tiles_n) * BM, n0 = (bid % tiles_n) * BN;
   const int z = blockIdx.z;
+  // device-side row bound (rows of a compaction): M rows for the A-row-major GEMMs, K for wgrad
+  const int64_t Mb = (!AK && a.epi.rows_dev) ? min(a.M, (int64_t)*a.epi.rows_dev) : a.M;
+  const int64_t Kb = (AK && a.epi.rows_dev) ? min(a.K, (int64_t)*a.epi.rows_dev) : a.K;
+  if (m0 >= Mb) return;
   const int64_t kbeg = (int64_t)z * a.k_per_split;
-  const int64_t kend = min(a.K, kbeg + a.k_per_split);
+  const int64_t kend = min(Kb, kbeg + a.k_per_split);
 
   const T* A = reinterpret_cast<const T*>(a.A);
   const T* B = reinterpret_cast<const T*>(a.B);
@@ -153,7 +159,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
   LA la;
   LB lb;
   auto issue = [&](int64_t k0) {
-    if (!AK) la.load(A, a.lda, m0, k0, a.M, kend, tid);
+    if (!AK) la.load(A, a.lda, m0, k0, Mb, kend, tid);
     else la.load(A, a.lda, k0, m0, kend, a.M, tid);
     if (!BK) lb.load(B, a.ldb, n0, k0, a.N, kend, tid);
     else lb.load(B, a.ldb, k0, n0, kend, a.N, tid);
@@ -208,7 +214,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t m = m0 + wm * (BM / 2) + i * 16 + rq + r;
-        if (m < a.M && n < a.N) {
+        if (m < Mb && n < a.N) {
           if (a.slab) a.slab[(int64_t)z * a.slab_stride + m * a.N + n] = acc[i][j][r];
           else epilogue_store<T>(a, m, n, acc[i][j][r]);
         }
@@ -267,7 +273,8 @@ int rs_gemm(int dtype, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t
 // dW[N,K] (+)= sum_m dY[m,:]^T X[m,:]  and  db[N] (+)= sum_m dY[m,:]  (split-K over the M token
 // rows into fp32 slabs, bias column sums fused into the GEMM, one deterministic reduce pass)
 int rs_linear_wgrad(int dtype, int64_t M, int64_t N, int64_t K, const void* dY, int64_t lddy, const void* X,
-                    int64_t ldx, float* dW, float* db, int accumulate, int splits, float* slab, void* stream) {
+                    int64_t ldx, float* dW, float* db, int accumulate, int splits, float* slab, const int* rows_dev,
+                    void* stream) {
   if (M <= 0 || N <= 0 || K <= 0 || splits < 1 || !slab || !dW) return RS_ERR_ARG;
   const int esz = dtype == RS_DTYPE_BF16 ? 2 : 4;
   const int vec = 16 / esz;
@@ -282,6 +289,7 @@ int rs_linear_wgrad(int dtype, int64_t M, int64_t N, int64_t K, const void* dY, 
   a.bias_colsum = db ? 1 : 0;
   a.epi = rs_epilogue{};
   a.epi.alpha = 1.0f;
+  a.epi.rows_dev = rows_dev;
   hipStream_t s = (hipStream_t)stream;
   hipError_t err = dtype == RS_DTYPE_BF16 ? launch_t<__bf16, true, true>(a, s) : launch_t<float, true, true>(a, s);
   if (err != hipSuccess) return (int)err;

@@ -68,8 +68,13 @@ __global__ __launch_bounds__(256) void bce_bwd_kernel(const float* __restrict__ 
 // ---- cross entropy: one block per row, online (max, sum) over the vocabulary
 __global__ __launch_bounds__(256) void ce_row_kernel(const float* __restrict__ logits, int64_t R, int64_t V1,
                                                      int64_t ldl, const int64_t* __restrict__ labels,
-                                                     float* __restrict__ lse_out, float* __restrict__ part) {
+                                                     float* __restrict__ lse_out, float* __restrict__ part,
+                                                     const int* __restrict__ rows_dev) {
   const int64_t r = blockIdx.x;
+  if (rows_dev && r >= *rows_dev) {
+    if (threadIdx.x == 0) { lse_out[r] = 0.f; part[r * 2] = 0.f; part[r * 2 + 1] = 0.f; }
+    return;
+  }
   const int64_t lab = labels[r];
   const float* x = logits + r * ldl;
   float m = -__builtin_inff(), s = 0.f;
@@ -123,8 +128,10 @@ template <typename T>
 __global__ __launch_bounds__(256) void ce_bwd_kernel(const float* __restrict__ logits, int64_t R, int64_t V1,
                                                      int64_t ldl, const int64_t* __restrict__ labels,
                                                      const float* __restrict__ count, const float* __restrict__ dloss,
-                                                     const float* __restrict__ lse, T* __restrict__ dl, int64_t lddl) {
+                                                     const float* __restrict__ lse, T* __restrict__ dl, int64_t lddl,
+                                                     const int* __restrict__ rows_dev) {
   const int64_t r = blockIdx.y;
+  if (rows_dev && r >= *rows_dev) return;
   const int64_t lab = labels[r];
   const float sc = (dloss ? *dloss : 1.f) / *count;
   const float L = lse[r];
@@ -156,26 +163,27 @@ int rs_bce_bwd(const float* pl, const float* nl, const int64_t* pos, int64_t M, 
 }
 
 int rs_ce_fwd(const float* logits, int64_t R, int64_t V1, int64_t ldl, const int64_t* labels,
-              const float* count_override, float* ws, float* out, void* stream) {
+              const float* count_override, float* ws, float* out, const int* rows_dev, void* stream) {
   // ws layout: [R] lse, then [R][2] partials
   if (R <= 0 || V1 <= 0) return RS_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(ce_row_kernel, dim3((unsigned)R), dim3(256), 0, s, logits, R, V1, ldl, labels, ws, ws + R);
+  hipLaunchKernelGGL(ce_row_kernel, dim3((unsigned)R), dim3(256), 0, s, logits, R, V1, ldl, labels, ws, ws + R, rows_dev);
   hipLaunchKernelGGL(ce_finish_kernel, dim3(1), dim3(256), 0, s, ws + R, R, count_override, out);
   return (int)hipGetLastError();
 }
 
 int rs_ce_bwd(int dtype, const float* logits, int64_t R, int64_t V1, int64_t ldl, const int64_t* labels,
-              const float* count, const float* dloss, const float* ws, void* dlogits, int64_t lddl, void* stream) {
+              const float* count, const float* dloss, const float* ws, void* dlogits, int64_t lddl,
+              const int* rows_dev, void* stream) {
   if (R <= 0 || V1 <= 0 || !count) return RS_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((unsigned)std::min<int64_t>(cdiv(V1, 256), 64), (unsigned)R);
   if (dtype == RS_DTYPE_BF16)
     hipLaunchKernelGGL((ce_bwd_kernel<__bf16>), grid, dim3(256), 0, s, logits, R, V1, ldl, labels, count, dloss, ws,
-                       (__bf16*)dlogits, lddl);
+                       (__bf16*)dlogits, lddl, rows_dev);
   else
     hipLaunchKernelGGL((ce_bwd_kernel<float>), grid, dim3(256), 0, s, logits, R, V1, ldl, labels, count, dloss, ws,
-                       (float*)dlogits, lddl);
+                       (float*)dlogits, lddl, rows_dev);
   return (int)hipGetLastError();
 }
 

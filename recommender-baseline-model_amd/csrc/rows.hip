@@ -1,0 +1,138 @@
+// Labelled-row compaction for the BERT4Rec loss head (gfx950).
+//
+// The reference computes the full-vocabulary logits of EVERY position and lets
+// CrossEntropyLoss(ignore_index=0) drop the unlabelled ones
+// (BS/models/bert.py:16, BS/trainers/bert.py:36-40).  Rows with label 0
+// contribute neither loss nor gradient, so the build runs the vocabulary GEMMs
+// only on the labelled rows: these kernels build the ordered list of those rows
+// on the device (no host sync, graph-capturable), gather their hidden states,
+// and scatter the hidden-state gradient back.  The compacted row count stays on
+// the device (rows_dev) and bounds the following GEMMs.
+#include "common.h"
+#include "../../include/recsys_hip.h"
+
+// one 1024-thread block: contiguous chunk per thread, block-wide exclusive scan
+__global__ __launch_bounds__(1024) void compact_kernel(const int64_t* __restrict__ labels, int64_t n,
+                                                       int64_t cap, int32_t* __restrict__ idx,
+                                                       int32_t* __restrict__ rank, int32_t* __restrict__ count) {
+  __shared__ int32_t part[1024];
+  const int tid = threadIdx.x;
+  const int64_t per = cdiv(n, (int64_t)1024);
+  const int64_t r0 = tid * per, r1 = min(n, r0 + per);
+  int32_t c = 0;
+  for (int64_t r = r0; r < r1; ++r) c += labels[r] != 0;
+  part[tid] = c;
+  __syncthreads();
+  // Hillis-Steele inclusive scan over 1024 partials
+  for (int off = 1; off < 1024; off <<= 1) {
+    const int32_t v = tid >= off ? part[tid - off] : 0;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  int32_t pos = part[tid] - c;  // exclusive prefix
+  for (int64_t r = r0; r < r1; ++r) {
+    if (labels[r] != 0) {
+      if (pos < cap) {
+        idx[pos] = (int32_t)r;
+        rank[r] = pos;
+      } else {
+        rank[r] = -1;
+      }
+      ++pos;
+    } else {
+      rank[r] = -1;
+    }
+  }
+  if (tid == 1023) *count = (int32_t)min((int64_t)part[1023], cap);
+  // unused slots of the list point at row 0 (never read for real rows: bounded by count)
+  for (int64_t i = (int64_t)part[1023] + tid; i < cap; i += 1024) idx[i] = -1;
+}
+
+// dst[i] = src[idx[i]] for i < count, zero rows for count <= i < cap; lab_out[i] = labels[idx[i]] or 0
+template <typename T>
+__global__ __launch_bounds__(256) void gather_rows_kernel(const T* __restrict__ src, int64_t lds, int64_t d,
+                                                          const int32_t* __restrict__ idx,
+                                                          const int32_t* __restrict__ count, int64_t cap,
+                                                          T* __restrict__ dst, int64_t ldd,
+                                                          const int64_t* __restrict__ labels,
+                                                          int64_t* __restrict__ lab_out) {
+  constexpr int V = Vec<T>::N;
+  const int64_t cpr = d / V;
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= cap * cpr) return;
+  const int64_t r = i / cpr, c = (i % cpr) * V;
+  const int32_t n = *count;
+  float v[V];
+  if (r < n) {
+    const int64_t s = idx[r];
+    load_chunk<T>(v, src + s * lds + c);
+    if (c == 0 && lab_out) lab_out[r] = labels[s];
+  } else {
+#pragma unroll
+    for (int j = 0; j < V; ++j) v[j] = 0.f;
+    if (c == 0 && lab_out) lab_out[r] = 0;
+  }
+  store_chunk<T>(dst + r * ldd + c, v);
+}
+
+// dst[r] = rank[r] >= 0 ? src[rank[r]] : 0   over all n rows
+template <typename T>
+__global__ __launch_bounds__(256) void scatter_rows_kernel(const T* __restrict__ src, int64_t lds, int64_t d,
+                                                           const int32_t* __restrict__ rank, int64_t n,
+                                                           T* __restrict__ dst, int64_t ldd) {
+  constexpr int V = Vec<T>::N;
+  const int64_t cpr = d / V;
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n * cpr) return;
+  const int64_t r = i / cpr, c = (i % cpr) * V;
+  const int32_t k = rank[r];
+  float v[V];
+  if (k >= 0) load_chunk<T>(v, src + (int64_t)k * lds + c);
+  else {
+#pragma unroll
+    for (int j = 0; j < V; ++j) v[j] = 0.f;
+  }
+  store_chunk<T>(dst + r * ldd + c, v);
+}
+
+extern "C" {
+
+int rs_compact_rows(const int64_t* labels, int64_t n, int64_t cap, int32_t* idx, int32_t* rank, int32_t* count,
+                    void* stream) {
+  if (n <= 0 || cap <= 0) return RS_ERR_ARG;
+  hipLaunchKernelGGL(compact_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, labels, n, cap, idx, rank, count);
+  return (int)hipGetLastError();
+}
+
+int rs_gather_rows(int dtype, const void* src, int64_t lds, int64_t d, const int32_t* idx, const int32_t* count,
+                   int64_t cap, void* dst, int64_t ldd, const int64_t* labels, int64_t* lab_out, void* stream) {
+  const int vec = dtype == RS_DTYPE_BF16 ? 8 : 4;
+  if (cap <= 0 || d <= 0 || d % vec || lds % vec || ldd % vec) return RS_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t n = cap * (d / vec);
+  if (dtype == RS_DTYPE_BF16)
+    hipLaunchKernelGGL((gather_rows_kernel<__bf16>), dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s,
+                       (const __bf16*)src, lds, d, idx, count, cap, (__bf16*)dst, ldd, labels, lab_out);
+  else
+    hipLaunchKernelGGL((gather_rows_kernel<float>), dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s,
+                       (const float*)src, lds, d, idx, count, cap, (float*)dst, ldd, labels, lab_out);
+  return (int)hipGetLastError();
+}
+
+int rs_scatter_rows(int dtype, const void* src, int64_t lds, int64_t d, const int32_t* rank, int64_t n, void* dst,
+                    int64_t ldd, void* stream) {
+  const int vec = dtype == RS_DTYPE_BF16 ? 8 : 4;
+  if (n <= 0 || d <= 0 || d % vec || lds % vec || ldd % vec) return RS_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t m = n * (d / vec);
+  if (dtype == RS_DTYPE_BF16)
+    hipLaunchKernelGGL((scatter_rows_kernel<__bf16>), dim3((unsigned)cdiv(m, 256)), dim3(256), 0, s,
+                       (const __bf16*)src, lds, d, rank, n, (__bf16*)dst, ldd);
+  else
+    hipLaunchKernelGGL((scatter_rows_kernel<float>), dim3((unsigned)cdiv(m, 256)), dim3(256), 0, s,
+                       (const float*)src, lds, d, rank, n, (float*)dst, ldd);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -14,8 +14,15 @@ ALIGN = 64
 
 
 class FlatParams:
-    def __init__(self, module: nn.Module, device):
+    def __init__(self, module: nn.Module, device, order=None):
+        """order: optional callable(list of names) -> the same names in storage order (e.g. to keep the
+        q/k/v projection weights of a block adjacent so that one GEMM computes all three)."""
         named = list(module.named_parameters())
+        if order is not None:
+            pos = {n: i for i, (n, _) in enumerate(named)}
+            names = order([n for n, _ in named])
+            assert sorted(names) == sorted(pos), "order() must permute the parameter names"
+            named = [named[pos[n]] for n in names]
         self.names = [n for n, _ in named]
         self.shapes = {n: tuple(p.shape) for n, p in named}
         self.offsets = {}
@@ -64,6 +71,30 @@ class FlatParams:
     def enable_bf16(self):
         if self.bf16 is None:
             self.bf16 = torch.zeros(self.numel, dtype=torch.bfloat16, device=self.device)
+
+    def adjacent(self, names):
+        """True when the listed parameters are stored back to back (one contiguous region)."""
+        off = self.offsets[names[0]]
+        for n in names:
+            if self.offsets[n] != off:
+                return False
+            k = 1
+            for s in self.shapes[n]:
+                k *= s
+            off += k
+        return True
+
+    def span(self, names, buf=None, rows=None):
+        """A 2-D view over adjacent parameters (concatenated along dim 0)."""
+        assert self.adjacent(names), names
+        buf = self.data if buf is None else buf
+        o = self.offsets[names[0]]
+        n = sum(self.shapes[k][0] for k in names)
+        inner = 1
+        for s in self.shapes[names[0]][1:]:
+            inner *= s
+        t = buf[o:o + n * inner]
+        return t.view(n, inner) if inner > 1 else t
 
     def is_bound(self, module: nn.Module):
         for n, p in module.named_parameters():

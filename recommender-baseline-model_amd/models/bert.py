@@ -1,12 +1,50 @@
-"""BERTModel wrapper -- same API as the reference ``BS/models/bert.py:6-16``."""
+"""BERTModel -- same API as the reference ``BS/models/bert.py:6-16``.
+
+``forward(x)`` returns the full-vocabulary logits (B, T, V+1) like the
+reference; training through :class:`rbm_amd.train_step.FusedTrainStep` uses the
+labelled-rows-only loss head instead (same loss and gradients).
+"""
+import torch
+import torch.nn as nn
+
+from ..engine_util import as_ids, compute_dtype, require_cuda
 from .base import BaseModel
+from .bert_model.bert import BERT, BERTEngine, _BERTFunction, build_flat
 
 
 class BERTModel(BaseModel):
     def __init__(self, args):
         super().__init__(args)
-        raise NotImplementedError("BERT4Rec HIP path: in progress")
+        self.bert = BERT(args)
+        self.out = nn.Linear(self.bert.hidden, args.num_items + 1)
+        self.cdtype = compute_dtype(args)
+        self._flat = None
+        self._engine = None
+        if torch.device(getattr(args, "device", "cpu")).type == "cuda":
+            self.to(args.device)
 
     @classmethod
     def code(cls):
         return 'bert'
+
+    def _apply(self, fn, recurse=True):
+        super()._apply(fn, recurse)
+        self._flat = None
+        self._engine = None
+        return self
+
+    def engine(self):
+        p = self.out.weight
+        require_cuda(p.device)
+        if self._flat is None or not self._flat.is_bound(self):
+            self._flat = build_flat(self, p.device)
+            self._engine = None
+        if self._engine is None:
+            self._engine = BERTEngine(self, self._flat)
+        return self._engine
+
+    def forward(self, x):
+        eng = self.engine()
+        ids = as_ids(x, self._flat.device)
+        params = [p for _, p in self.named_parameters()]
+        return _BERTFunction.apply(eng, ids, self.training, *params)

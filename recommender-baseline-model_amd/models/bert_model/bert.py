@@ -1,0 +1,395 @@
+"""BERT4Rec on the MI355X HIP path.
+
+Parameter modules, construction order (so ``model_init_seed`` gives the
+reference's exact initial weights) and ``state_dict`` keys are those of the
+reference ``BS/models/bert.py:6-16`` + ``BS/models/bert_modules/**``; the torch
+modules here are only parameter containers and initialisers.  The math runs as
+HIP kernels through the C ABI (include/recsys_hip.h), issued by
+:class:`BERTEngine`:
+
+forward (per step)                         kernels
+  x = tok[ids] + pe; drop                    rs_embed_fwd (mode 1)          embedding/bert.py:29-31
+  per block: h = LN1(x)                      rs_layernorm_fwd (variant 1)   utils/layer_norm.py:14-17
+             qkv = h Wqkv^T + b              rs_gemm (one GEMM, q/k/v weights stored adjacent)
+             o = attn(q,k,v) key-padding     rs_attn_fwd (mask_kind 1)      attention/single.py:13-35
+             x1 = x + drop(o Wo^T + bo)      rs_gemm (+bias+dropout+residual)  sublayer.py:16-18
+             g = drop(gelu(LN2(x1) W1^T+b1)) rs_layernorm_fwd, rs_gemm (+bias+gelu+dropout) feed_forward.py:15-16
+             x = drop(x1 + drop(g W2^T+b2))  rs_gemm (+bias+dropout+residual+post-dropout) transformer.py:28-32
+  logits = x Wout^T + bout                   rs_gemm                        BS/models/bert.py:16
+training loss (BS/trainers/bert.py:30-41): CE(ignore_index=0) only needs the
+labelled rows, so the fused step compacts them on the device (rs_compact_rows /
+rs_gather_rows), runs the vocabulary GEMM + CE on those rows only, and scatters
+the hidden-state gradient back (rs_scatter_rows).
+"""
+import math
+import random
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from ... import ops
+from ...engine_util import Workspace, as_ids, compute_dtype, require_cuda, site_salt
+from ...flat import FlatParams
+
+LN_EPS = 1e-6  # utils/layer_norm.py:8
+
+
+# ---------------------------------------------------------------- parameter containers (reference layout)
+class LayerNorm(nn.Module):
+    def __init__(self, features):
+        super().__init__()
+        self.a_2 = nn.Parameter(torch.ones(features))
+        self.b_2 = nn.Parameter(torch.zeros(features))
+
+
+class SublayerConnection(nn.Module):
+    def __init__(self, size):
+        super().__init__()
+        self.norm = LayerNorm(size)
+
+
+class MultiHeadedAttention(nn.Module):
+    def __init__(self, h, d_model):
+        super().__init__()
+        assert d_model % h == 0
+        self.d_k = d_model // h
+        self.h = h
+        self.linear_layers = nn.ModuleList([nn.Linear(d_model, d_model) for _ in range(3)])
+        self.output_linear = nn.Linear(d_model, d_model)
+
+
+class PositionwiseFeedForward(nn.Module):
+    def __init__(self, d_model, d_ff):
+        super().__init__()
+        self.w_1 = nn.Linear(d_model, d_ff)
+        self.w_2 = nn.Linear(d_ff, d_model)
+
+
+class TransformerBlock(nn.Module):
+    def __init__(self, hidden, attn_heads, feed_forward_hidden):
+        super().__init__()
+        self.attention = MultiHeadedAttention(h=attn_heads, d_model=hidden)
+        self.feed_forward = PositionwiseFeedForward(d_model=hidden, d_ff=feed_forward_hidden)
+        self.input_sublayer = SublayerConnection(size=hidden)
+        self.output_sublayer = SublayerConnection(size=hidden)
+
+
+class PositionalEmbedding(nn.Module):
+    def __init__(self, max_len, d_model):
+        super().__init__()
+        self.pe = nn.Embedding(max_len, d_model)
+
+
+class BERTEmbedding(nn.Module):
+    def __init__(self, vocab_size, embed_size, max_len):
+        super().__init__()
+        self.token = nn.Embedding(vocab_size, embed_size, padding_idx=0)
+        self.position = PositionalEmbedding(max_len=max_len, d_model=embed_size)
+
+
+def fix_random_seed_as(seed):
+    """BS/utils.py:65-71 (called by BERT.__init__, bert_modules/bert.py:12)."""
+    random.seed(seed)
+    torch.manual_seed(seed)
+    torch.cuda.manual_seed_all(seed)
+    np.random.seed(seed)
+
+
+class BERT(nn.Module):
+    """Mirror of ``bert_modules/bert.py:8-46`` (parameters only)."""
+
+    def __init__(self, args):
+        super().__init__()
+        fix_random_seed_as(args.model_init_seed)
+        self.max_len = args.max_len
+        self.hidden = args.bert_hidden_units
+        self.heads = args.bert_num_heads
+        self.num_blocks = args.bert_num_blocks
+        self.dropout = float(args.bert_dropout)
+        self.hidden_dropout = float(args.bert_hidden_dropout)
+        vocab_size = args.num_items + 2          # [MASK] = num_items + 1, padding = 0
+        self.embedding = BERTEmbedding(vocab_size=vocab_size, embed_size=self.hidden, max_len=self.max_len)
+        self.transformer_blocks = nn.ModuleList(
+            [TransformerBlock(self.hidden, self.heads, self.hidden * 4) for _ in range(self.num_blocks)])
+
+
+def _storage_order(names):
+    """Keep each block's q/k/v weights (then biases) adjacent so one GEMM computes all three."""
+    out, seen = [], set()
+    for n in names:
+        if n in seen:
+            continue
+        if ".attention.linear_layers.0." in n:
+            stem, leaf = n.split(".attention.linear_layers.0.")
+            group = [f"{stem}.attention.linear_layers.{j}.{leaf}" for j in range(3)]
+            out += group
+            seen.update(group)
+        elif ".attention.linear_layers." in n:
+            continue   # emitted with its .0. sibling
+        else:
+            out.append(n)
+            seen.add(n)
+    return out
+
+
+class BERTEngine:
+    """Owns workspaces and issues the HIP kernels of one BERT4Rec model."""
+
+    def __init__(self, model, flat: FlatParams):
+        self.m = model
+        self.flat = flat
+        b = model.bert
+        self.d = b.hidden
+        self.L = b.num_blocks
+        self.H = b.heads
+        self.Dh = self.d // self.H
+        self.F = 4 * self.d
+        self.p = b.dropout
+        self.hp = b.hidden_dropout
+        self.T = b.max_len
+        self.V1 = model.out.weight.shape[0]
+        self.V1p = -(-self.V1 // 64) * 64
+        self.dt = model.cdtype
+        self.dev = flat.device
+        if self.dt == torch.bfloat16:
+            flat.enable_bf16()
+        self.ws = Workspace(self.dev)
+        self.seed_base = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        salt0 = int(torch.randint(0, 2 ** 62, (1,)).item())
+        self.salt = {"emb": site_salt(salt0, 0)}
+        for i in range(self.L):
+            for j, k in enumerate(("attn", "res1", "ffn", "res2", "blk")):
+                self.salt[f"{k}{i}"] = site_salt(salt0, 1 + 5 * i + j)
+        self.qkv_fused = all(flat.adjacent([self._qkv(i, j, leaf) for j in range(3)])
+                             for i in range(self.L) for leaf in ("weight", "bias"))
+
+    @staticmethod
+    def _qkv(i, j, leaf):
+        return f"bert.transformer_blocks.{i}.attention.linear_layers.{j}.{leaf}"
+
+    def sync_compute_weights(self):
+        if self.flat.bf16 is not None:
+            ops.cast_bf16(self.flat.data, self.flat.bf16)
+
+    def W(self, n):
+        return self.flat.cview(n)
+
+    def Wf(self, n):
+        return self.flat.view(n)
+
+    def _buf(self, shape, dtype=None):
+        return torch.empty(shape, dtype=dtype or self.dt, device=self.dev)
+
+    def Wqkv(self, i, buf=None):
+        names = [self._qkv(i, j, "weight") for j in range(3)]
+        return self.flat.span(names, buf if buf is not None else (self.flat.bf16 if self.flat.bf16 is not None
+                                                                   else self.flat.data))
+
+    def bqkv(self, i, buf=None):
+        return self.flat.span([self._qkv(i, j, "bias") for j in range(3)], buf)
+
+    # ---- encoder forward -------------------------------------------------------------
+    def encode(self, ids, training):
+        B, T = ids.shape
+        if T != self.T:
+            raise ValueError(f"sequence length {T} must equal max_len {self.T} (position.py:14-16 adds the "
+                             "whole positional table)")
+        M, d, H, Dh, L, Fd = B * T, self.d, self.H, self.Dh, self.L, self.F
+        p = self.p if training else 0.0
+        hp = self.hp if training else 0.0
+        if p > 0 or hp > 0:
+            ops.seed_advance(self.seed_base)
+        sb = self.seed_base.clone()
+        e = self._buf
+        s = {"B": B, "T": T, "p": p, "hp": hp, "ids": ids, "sb": sb, "blocks": []}
+        x = e((M, d))
+        ops.embed_fwd(1, ids, T, self.W("bert.embedding.token.weight"), self.W("bert.embedding.position.pe.weight"),
+                      1.0, hp, self.salt["emb"], sb, x)
+        for i in range(L):
+            pre = f"bert.transformer_blocks.{i}."
+            h, mu1, r1 = e((M, d)), e((M,), torch.float32), e((M,), torch.float32)
+            ops.layernorm_fwd(x, self.Wf(pre + "input_sublayer.norm.a_2"), self.Wf(pre + "input_sublayer.norm.b_2"),
+                              LN_EPS, h, mu1, r1, 1)
+            qkv = e((M, 3 * d))
+            if self.qkv_fused:
+                ops.linear_fwd(h, self.Wqkv(i), qkv, bias=self.bqkv(i))
+            else:
+                for j in range(3):
+                    ops.linear_fwd(h, self.W(self._qkv(i, j, "weight")), qkv[:, j * d:(j + 1) * d],
+                                   bias=self.Wf(self._qkv(i, j, "bias")))
+            o, lse = e((M, d)), e((B * H * T,), torch.float32)
+            ops.attn_fwd(B, T, H, Dh, qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, lse, 1.0 / math.sqrt(Dh), 1,
+                         ids, p, self.salt[f"attn{i}"], sb)
+            x1 = e((M, d))
+            ops.linear_fwd(o, self.W(pre + "attention.output_linear.weight"), x1,
+                           bias=self.Wf(pre + "attention.output_linear.bias"), drop_p=hp,
+                           drop_seed=self.salt[f"res1{i}"], seed_base=sb, drop_ld=d, resid=x)
+            h2, mu2, r2 = e((M, d)), e((M,), torch.float32), e((M,), torch.float32)
+            ops.layernorm_fwd(x1, self.Wf(pre + "output_sublayer.norm.a_2"),
+                              self.Wf(pre + "output_sublayer.norm.b_2"), LN_EPS, h2, mu2, r2, 1)
+            a_pre, g = e((M, Fd)), e((M, Fd))
+            ops.linear_fwd(h2, self.W(pre + "feed_forward.w_1.weight"), g, bias=self.Wf(pre + "feed_forward.w_1.bias"),
+                           act=ops.ACT_GELU, aux_out=a_pre, drop_p=hp, drop_seed=self.salt[f"ffn{i}"], seed_base=sb,
+                           drop_ld=Fd)
+            xn = e((M, d))
+            ops.linear_fwd(g, self.W(pre + "feed_forward.w_2.weight"), xn, bias=self.Wf(pre + "feed_forward.w_2.bias"),
+                           drop_p=hp, drop_seed=self.salt[f"res2{i}"], seed_base=sb, drop_ld=d, resid=x1,
+                           post_drop_p=hp, post_drop_seed=self.salt[f"blk{i}"])
+            s["blocks"].append(dict(x=x, h=h, mu1=mu1, r1=r1, qkv=qkv, o=o, lse=lse, x1=x1, h2=h2, mu2=mu2, r2=r2,
+                                    a_pre=a_pre, g=g))
+            x = xn
+        s["xL"] = x
+        return x, s
+
+    # ---- encoder backward ------------------------------------------------------------
+    def encode_backward(self, s, dx, grad):
+        """dx: (M, d) compute-dtype gradient of the last hidden state; accumulates parameter grads."""
+        B, T, hp, ids, sb = s["B"], s["T"], s["hp"], s["ids"], s["sb"]
+        M, d, H, Dh, L, Fd = B * T, self.d, self.H, self.Dh, self.L, self.F
+        e = self._buf
+        G = lambda n: self.flat.view(n, grad)  # noqa: E731
+        slab = self.ws.get("slab", (max(ops.wgrad_slab_numel(M, Fd, d), ops.wgrad_slab_numel(M, d, Fd),
+                                        ops.wgrad_slab_numel(M, 3 * d, d)),), torch.float32)
+        wln = self.ws.get("ln", (2 * 128 * d,), torch.float32)
+        wat = self.ws.get("attn", (B * H * T,), torch.float32)
+        for i in reversed(range(L)):
+            a = s["blocks"][i]
+            pre = f"bert.transformer_blocks.{i}."
+            # x_out = drop_blk(x1 + drop_res2(g W2^T + b2))
+            if hp > 0:
+                dx2, dy = e((M, d)), e((M, d))
+                ops.dropout_rowmask(dx, hp, self.salt[f"blk{i}"], sb, None, dx2)
+                ops.dropout_rowmask(dx2, hp, self.salt[f"res2{i}"], sb, None, dy)
+            else:
+                dx2, dy = dx, dx
+            ops.linear_wgrad(dy, a["g"], G(pre + "feed_forward.w_2.weight"), slab, db=G(pre + "feed_forward.w_2.bias"))
+            da = e((M, Fd))
+            ops.linear_dgrad(dy, self.W(pre + "feed_forward.w_2.weight"), da, act=ops.ACT_GELU_BWD, aux=a["a_pre"],
+                             drop_p=hp, drop_seed=self.salt[f"ffn{i}"], seed_base=sb, drop_ld=Fd)
+            ops.linear_wgrad(da, a["h2"], G(pre + "feed_forward.w_1.weight"), slab, db=G(pre + "feed_forward.w_1.bias"))
+            dh2 = e((M, d))
+            ops.linear_dgrad(da, self.W(pre + "feed_forward.w_1.weight"), dh2)
+            ops.layernorm_bwd(a["x1"], dh2, self.Wf(pre + "output_sublayer.norm.a_2"), a["mu2"], a["r2"], LN_EPS, dx2,
+                              G(pre + "output_sublayer.norm.a_2"), G(pre + "output_sublayer.norm.b_2"), wln, 1,
+                              accumulate=True)
+            # x1 = x + drop_res1(o Wo^T + bo)
+            if hp > 0:
+                dyo = e((M, d))
+                ops.dropout_rowmask(dx2, hp, self.salt[f"res1{i}"], sb, None, dyo)
+            else:
+                dyo = dx2
+            ops.linear_wgrad(dyo, a["o"], G(pre + "attention.output_linear.weight"), slab,
+                             db=G(pre + "attention.output_linear.bias"))
+            do = e((M, d))
+            ops.linear_dgrad(dyo, self.W(pre + "attention.output_linear.weight"), do)
+            qkv = a["qkv"]
+            dqkv = e((M, 3 * d))
+            ops.attn_bwd(B, T, H, Dh, qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], a["o"], do, a["lse"],
+                         dqkv[:, :d], dqkv[:, d:2 * d], dqkv[:, 2 * d:], 1.0 / math.sqrt(Dh), 1, ids, s["p"],
+                         self.salt[f"attn{i}"], sb, wat)
+            dh = e((M, d))
+            if self.qkv_fused:
+                ops.linear_wgrad(dqkv, a["h"], self.Wqkv(i, grad), slab, db=self.bqkv(i, grad))
+                ops.linear_dgrad(dqkv, self.Wqkv(i), dh)
+            else:
+                for j in range(3):
+                    ops.linear_wgrad(dqkv[:, j * d:(j + 1) * d], a["h"], G(self._qkv(i, j, "weight")), slab,
+                                     db=G(self._qkv(i, j, "bias")))
+                    ops.linear_dgrad(dqkv[:, j * d:(j + 1) * d], self.W(self._qkv(i, j, "weight")), dh,
+                                     accumulate=j > 0)
+            ops.layernorm_bwd(a["x"], dh, self.Wf(pre + "input_sublayer.norm.a_2"), a["mu1"], a["r1"], LN_EPS, dx2,
+                              G(pre + "input_sublayer.norm.a_2"), G(pre + "input_sublayer.norm.b_2"), wln, 1,
+                              accumulate=True)
+            dx = dx2
+        ops.embed_bwd(1, ids, T, dx, 1.0, hp, self.salt["emb"], sb, G("bert.embedding.token.weight"),
+                      G("bert.embedding.position.pe.weight"))
+
+    # ---- full-vocabulary logits (the reference forward API) ---------------------------
+    def logits(self, xL):
+        M = xL.shape[0]
+        out = torch.empty((M, self.V1p), dtype=torch.float32, device=self.dev)[:, :self.V1]
+        ops.linear_fwd(xL, self.W("out.weight"), out, bias=self.Wf("out.bias"))
+        return out
+
+    def logits_backward(self, xL, dlogits, grad):
+        """dlogits (M, V+1) fp32 -> out.weight/out.bias grads and dx_L (compute dtype)."""
+        M = xL.shape[0]
+        d = self.d
+        dl = self.ws.get("dlogits_full", (M, self.V1p), self.dt)[:, :self.V1]
+        dl.copy_(dlogits)
+        slab = self.ws.get("slab_out", (ops.wgrad_slab_numel(M, self.V1, d),), torch.float32)
+        ops.linear_wgrad(dl, xL, self.flat.view("out.weight", grad), slab, db=self.flat.view("out.bias", grad))
+        dx = self._buf((M, d))
+        ops.linear_dgrad(dl, self.W("out.weight"), dx)
+        return dx
+
+    # ---- fused training loss (labelled rows only) -------------------------------------
+    def train_loss_and_backward(self, tokens, labels, loss_out, global_count, grad, max_labelled=None):
+        """Forward + CE(ignore_index=0) + backward of one batch.  loss_out[0] = loss sum, [1] = local
+        labelled count, [2] = local mean; ``global_count(local)`` returns the divisor (DP)."""
+        xL, s = self.encode(tokens, True)
+        B, T = tokens.shape
+        M, d = B * T, self.d
+        cap = int(max_labelled or M)
+        idx = self.ws.get("cidx", (cap,), torch.int32)
+        rank = self.ws.get("crank", (M,), torch.int32)
+        cnt = self.ws.get("ccount", (1,), torch.int32)
+        ops.compact_rows(labels, cap, idx, rank, cnt)
+        hl = self.ws.get("hl", (cap, d), self.dt)
+        lab = self.ws.get("lab", (cap,), torch.int64)
+        ops.gather_rows(xL, idx, cnt, cap, hl, labels, lab)
+        logits = self.ws.get("logits", (cap, self.V1p), torch.float32)[:, :self.V1]
+        ops.linear_fwd(hl, self.W("out.weight"), logits, bias=self.Wf("out.bias"), rows_dev=cnt)
+        wce = self.ws.get("wce", (3 * cap,), torch.float32)
+        ops.ce_fwd(logits, lab, wce, loss_out, None, rows_dev=cnt)
+        count = global_count(loss_out[1:2])
+        if self.dt == torch.float32:
+            dl = logits                                   # in place
+        else:
+            dl = self.ws.get("dlogits", (cap, self.V1p), self.dt)[:, :self.V1]
+        ops.ce_bwd(logits, lab, count, None, wce, dl, rows_dev=cnt)
+        slab = self.ws.get("slab_out", (ops.wgrad_slab_numel(cap, self.V1, d),), torch.float32)
+        ops.linear_wgrad(dl, hl, self.flat.view("out.weight", grad), slab, db=self.flat.view("out.bias", grad),
+                         rows_dev=cnt)
+        dhl = self.ws.get("dhl", (cap, d), self.dt)
+        ops.linear_dgrad(dl, self.W("out.weight"), dhl, rows_dev=cnt)
+        dxL = self._buf((M, d))
+        ops.scatter_rows(dhl, rank, dxL)
+        self.encode_backward(s, dxL, grad)
+
+
+class _BERTFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, engine, ids, training, *params):
+        engine.sync_compute_weights()
+        xL, s = engine.encode(ids, training)
+        logits = engine.logits(xL)
+        ctx.engine, ctx.saved, ctx.xL = engine, s, xL
+        B, T = ids.shape
+        return logits.view(B, T, -1)
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        eng = ctx.engine
+        grad = torch.zeros(eng.flat.numel, dtype=torch.float32, device=eng.flat.device)
+        B, T, V1 = dlogits.shape
+        dx = eng.logits_backward(ctx.xL, dlogits.reshape(B * T, V1), grad)
+        eng.encode_backward(ctx.saved, dx, grad)
+        ctx.saved = None
+        return (None, None, None, *[eng.flat.view(n, grad) for n in eng.flat.names_in_module_order])
+
+
+def build_flat(model, device):
+    flat = FlatParams(model, device, order=_storage_order)
+    flat.names_in_module_order = [n for n, _ in model.named_parameters()]
+    return flat
+
+
+def require(model):
+    p = model.out.weight
+    require_cuda(p.device)
+    return p.device
+
+
+__all__ = ["BERT", "BERTEngine", "_BERTFunction", "build_flat", "as_ids", "compute_dtype", "require"]

@@ -28,7 +28,8 @@ def ld(t):
 
 
 def epilogue(bias=None, alpha=1.0, act=ACT_NONE, aux=None, aux_out=None, drop_p=0.0, drop_seed=0,
-             seed_base=None, drop_ld=0, resid=None, rowmask_ids=None, accumulate=False):
+             seed_base=None, drop_ld=0, resid=None, rowmask_ids=None, accumulate=False, post_drop_p=0.0,
+             post_drop_seed=0, rows_dev=None):
     e = Epilogue()
     e.bias = ptr(bias)
     e.alpha = alpha
@@ -45,6 +46,9 @@ def epilogue(bias=None, alpha=1.0, act=ACT_NONE, aux=None, aux_out=None, drop_p=
     e.ldres = ld(resid) if resid is not None else 0
     e.rowmask_ids = ptr(rowmask_ids)
     e.accumulate = 1 if accumulate else 0
+    e.post_drop_p = post_drop_p
+    e.post_drop_seed = post_drop_seed
+    e.rows_dev = ptr(rows_dev)
     return e
 
 
@@ -80,7 +84,7 @@ def wgrad_slab_numel(M_tok, n_out, k_in):
     return split_for(M_tok, n_out, k_in) * (n_out * k_in + n_out)
 
 
-def linear_wgrad(dY, X, dW, slab, db=None, split_k=None, accumulate=True):
+def linear_wgrad(dY, X, dW, slab, db=None, split_k=None, accumulate=True, rows_dev=None):
     """dW [N,K] (+)= dY^T X and db [N] (+)= colsum(dY) over M token rows (rs_linear_wgrad)."""
     M, N = dY.shape
     K = X.shape[1]
@@ -88,7 +92,7 @@ def linear_wgrad(dY, X, dW, slab, db=None, split_k=None, accumulate=True):
     assert slab.numel() >= s * (N * K + N), "slab workspace too small"
     assert dY.dtype == X.dtype
     call("rs_linear_wgrad", dtype_code(dY), M, N, K, ptr(dY), ld(dY), ptr(X), ld(X), ptr(dW), ptr(db),
-         int(accumulate), s, ptr(slab), stream())
+         int(accumulate), s, ptr(slab), ptr(rows_dev), stream())
 
 
 def colsum(X, out, ws, accumulate=True):
@@ -154,16 +158,31 @@ def bce_bwd(pl, nl, pos, count, dloss, dpl, dnl):
          stream())
 
 
-def ce_fwd(logits, labels, ws, out, count_override=None):
+def ce_fwd(logits, labels, ws, out, count_override=None, rows_dev=None):
     R, V1 = logits.shape
     call("rs_ce_fwd", ptr(logits), R, V1, ld(logits), ptr(labels), ptr(count_override), ptr(ws), ptr(out),
-         stream())
+         ptr(rows_dev), stream())
 
 
-def ce_bwd(logits, labels, count, dloss, ws, dlogits):
+def ce_bwd(logits, labels, count, dloss, ws, dlogits, rows_dev=None):
     R, V1 = logits.shape
     call("rs_ce_bwd", dtype_code(dlogits), ptr(logits), R, V1, ld(logits), ptr(labels), ptr(count), ptr(dloss),
-         ptr(ws), ptr(dlogits), ld(dlogits), stream())
+         ptr(ws), ptr(dlogits), ld(dlogits), ptr(rows_dev), stream())
+
+
+def compact_rows(labels, cap, idx, rank, count):
+    call("rs_compact_rows", ptr(labels), labels.numel(), cap, ptr(idx), ptr(rank), ptr(count), stream())
+
+
+def gather_rows(src, idx, count, cap, dst, labels=None, lab_out=None):
+    d = src.shape[1]
+    call("rs_gather_rows", dtype_code(src), ptr(src), ld(src), d, ptr(idx), ptr(count), cap, ptr(dst), ld(dst),
+         ptr(labels), ptr(lab_out), stream())
+
+
+def scatter_rows(src, rank, dst):
+    n, d = dst.shape
+    call("rs_scatter_rows", dtype_code(src), ptr(src), ld(src), d, ptr(rank), n, ptr(dst), ld(dst), stream())
 
 
 def adam_prepare(state, hyper):

@@ -43,12 +43,12 @@ class FusedAdam:
 
 
 class FusedTrainStep:
-    def __init__(self, model, lr=1e-3, weight_decay=0.0, process_group=None, dp=None):
-        """model: rbm_amd SASModel or BERTModel on a CUDA device."""
+    def __init__(self, model, lr=1e-3, weight_decay=0.0, process_group=None, dp=None, max_labelled=None):
+        """model: rbm_amd SASModel or BERTModel on a CUDA device.  max_labelled (BERT): upper bound
+        on labelled rows per batch (sizes the compacted vocabulary-logit buffers; default B*T)."""
         self.model = model
         self.kind = model.code()
-        self.inner = model.sas if self.kind == "sas" else model.bert
-        self.engine = self.inner.engine()
+        self.engine = model.sas.engine() if self.kind == "sas" else model.engine()
         self.flat = self.engine.flat
         self.engine.sync_compute_weights()
         self.opt = FusedAdam(self.flat, lr=lr, weight_decay=weight_decay)
@@ -59,6 +59,7 @@ class FusedTrainStep:
         self.count = torch.zeros(1, dtype=torch.float32, device=dev)
         self.graph = None
         self.static = None
+        self.max_labelled = max_labelled
 
     # ---------------------------------------------------------------- one step
     def step(self, *batch):
@@ -77,7 +78,8 @@ class FusedTrainStep:
             eng.backward(saved, dpl, dnl, self.flat.grad)
         else:
             tokens, labels = batch
-            eng.train_loss_and_backward(tokens, labels, self.loss_out, self._global_count, self.flat.grad)
+            eng.train_loss_and_backward(tokens, labels, self.loss_out, self._global_count, self.flat.grad,
+                                        max_labelled=self.max_labelled)
         if self.dp:
             dist.all_reduce(self.flat.grad, group=self.pg)
         self.opt.step()

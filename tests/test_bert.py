@@ -1,0 +1,139 @@
+"""BERT4Rec: the HIP path vs the reference (golden vectors) and the CPU oracle.
+
+* CPU: ``BERTModel(args)`` builds bit-identical initial weights to the reference for the
+  same ``model_init_seed`` (BS/models/bert_modules/bert.py:12 seeds before construction) and
+  the same state_dict keys -- checked against the weights the reference itself produced.
+* GPU: forward logits / CE loss / every gradient through librecsys_hip.so, both through the
+  reference API (``model(x)`` full-vocabulary logits + torch CE on top) and through the fused
+  labelled-rows-only training step; fp32 within the fp32 tolerance, bf16 within the bf16 one.
+"""
+import argparse
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_params, load_golden, rel
+
+FWD_TOL_F32, GRAD_TOL_F32 = 1e-5, 1e-4
+FWD_TOL_BF16, GRAD_TOL_BF16 = 3e-2, 0.15
+SEEDS = {"bert_tiny": 3, "bert_mid": 4, "bert_curve": 7}   # tools/gen_golden.py
+
+
+def bert_args(z, device="cuda", dtype="fp32", seed=0, p=0.0, hp=0.0):
+    return argparse.Namespace(model_code="bert", num_items=int(z["V"]), max_len=int(z["T"]), device=device,
+                              bert_hidden_units=int(z["d"]), bert_num_blocks=int(z["L"]), bert_num_heads=int(z["h"]),
+                              bert_dropout=p, bert_hidden_dropout=hp, bert_mask_prob=0.2, model_init_seed=seed,
+                              rs_dtype=dtype)
+
+
+@pytest.mark.parametrize("name", ["bert_tiny", "bert_mid", "bert_curve"])
+def test_bert_init_matches_reference(name):
+    import rbm_amd  # noqa: F401
+    from rbm_amd.models import model_factory
+    z = load_golden(name)
+    m = model_factory(bert_args(z, device="cpu", seed=SEEDS[name]))
+    sd = m.state_dict()
+    ref = golden_params(z)
+    assert sorted(sd) == sorted(ref)
+    for k in ref:
+        assert torch.equal(sd[k], ref[k]), k
+
+
+def make_model(z, dtype):
+    import rbm_amd  # noqa: F401
+    from rbm_amd.models import model_factory
+    m = model_factory(bert_args(z, dtype=dtype))
+    m.load_state_dict({k[2:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("p/")})
+    return m
+
+
+def check_grads(grads, z, tol):
+    scale = max(np.linalg.norm(z["g/" + k]) for k in grads)
+    for k, g in grads.items():
+        r = z["g/" + k]
+        if "linear_layers.1.bias" in k:       # key bias: analytically zero (softmax shift invariance)
+            assert np.linalg.norm(g) <= max(1e-5, tol) * scale, k
+            continue
+        if np.linalg.norm(r) == 0:
+            assert np.linalg.norm(g) <= 1e-6 * scale, k
+            continue
+        assert rel(g, r) < tol, (k, rel(g, r))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("name", ["bert_tiny", "bert_mid"])
+def test_bert_api_matches_reference(name, dtype):
+    """model(x) -> (B,T,V+1) logits, torch CE(ignore_index=0) on top, backward through the HIP path."""
+    z = load_golden(name)
+    m = make_model(z, dtype)
+    m.train()
+    tok = torch.from_numpy(z["tokens"]).cuda()
+    lab = torch.from_numpy(z["labels"]).cuda()
+    logits = m(tok)
+    loss = torch.nn.functional.cross_entropy(logits.reshape(-1, logits.shape[-1]), lab.reshape(-1), ignore_index=0)
+    loss.backward()
+    torch.cuda.synchronize()
+    ftol, gtol = (FWD_TOL_F32, GRAD_TOL_F32) if dtype == "fp32" else (FWD_TOL_BF16, GRAD_TOL_BF16)
+    assert rel(logits.detach().cpu().numpy(), z["logits"]) < ftol
+    assert abs(loss.item() - float(z["loss"])) < ftol * max(1.0, float(z["loss"]))
+    check_grads({k: p.grad.cpu().numpy() for k, p in m.named_parameters()}, z, gtol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("name", ["bert_tiny", "bert_mid"])
+def test_bert_fused_step_matches_reference(name, dtype):
+    """The fused training step (labelled-row compaction + vocab GEMM + CE on those rows only)
+    gives the reference loss and gradients."""
+    from rbm_amd.train_step import FusedTrainStep
+    z = load_golden(name)
+    m = make_model(z, dtype)
+    m.train()
+    tr = FusedTrainStep(m, lr=0.0)
+    tok = torch.from_numpy(z["tokens"]).cuda()
+    lab = torch.from_numpy(z["labels"]).cuda()
+    tr.flat.grad.zero_()
+    tr.engine.sync_compute_weights()
+    tr.engine.train_loss_and_backward(tok, lab, tr.loss_out, tr._global_count, tr.flat.grad)
+    torch.cuda.synchronize()
+    ftol, gtol = (FWD_TOL_F32, GRAD_TOL_F32) if dtype == "fp32" else (FWD_TOL_BF16, GRAD_TOL_BF16)
+    loss = float(tr.loss_out[2].item())
+    assert abs(loss - float(z["loss"])) < ftol * max(1.0, float(z["loss"]))
+    assert int(tr.loss_out[1].item()) == int((z["labels"] != 0).sum())
+    check_grads({k: tr.flat.view(k, tr.flat.grad).cpu().numpy() for k, _ in m.named_parameters()}, z, gtol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("V,T,d,L,h,B,cap", [(26744, 200, 256, 2, 2, 2, None), (500, 50, 64, 1, 1, 3, 64),
+                                             (300, 37, 128, 2, 4, 2, None)])
+def test_bert_fp32_matches_oracle_shapes(V, T, d, L, h, B, cap):
+    """cfg3 shape (V=26,744, T=200, d=256, 2 heads) and odd shapes vs the fp64 oracle, fused step,
+    including a compaction cap above the labelled count."""
+    import rbm_amd  # noqa: F401
+    import rbm_amd.data as synth
+    from oracle import bert as obert
+    from rbm_amd.models import model_factory
+    from rbm_amd.train_step import FusedTrainStep
+    a = argparse.Namespace(model_code="bert", num_items=V, max_len=T, device="cuda", bert_hidden_units=d,
+                           bert_num_blocks=L, bert_num_heads=h, bert_dropout=0.0, bert_hidden_dropout=0.0,
+                           bert_mask_prob=0.2, model_init_seed=V, rs_dtype="fp32")
+    m = model_factory(a)
+    rng = np.random.default_rng(T)
+    tok, lab = synth.bert_batch(rng, B, T, V, mask_prob=0.2)
+    tr = FusedTrainStep(m, lr=0.0, max_labelled=cap)
+    tr.flat.grad.zero_()
+    tr.engine.train_loss_and_backward(torch.from_numpy(tok).cuda(), torch.from_numpy(lab).cuda(), tr.loss_out,
+                                      tr._global_count, tr.flat.grad, max_labelled=cap)
+    torch.cuda.synchronize()
+    P = {k: v.detach().cpu().double() for k, v in m.state_dict().items()}
+    l64, _, g64 = obert.loss_and_grads(P, torch.from_numpy(tok), torch.from_numpy(lab), L, h)
+    assert abs(tr.loss_out[2].item() - l64.item()) < 1e-5 * max(1, abs(l64.item()))
+    scale = max(float(v.norm()) for v in g64.values())
+    for k in g64:
+        g = tr.flat.view(k, tr.flat.grad).cpu().double()
+        if "linear_layers.1.bias" in k or float(g64[k].norm()) == 0:
+            assert float(g.norm()) <= 1e-5 * scale, k
+            continue
+        assert rel(g.numpy(), g64[k].numpy()) < GRAD_TOL_F32, (k, rel(g.numpy(), g64[k].numpy()))

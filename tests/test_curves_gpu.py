@@ -1,0 +1,85 @@
+"""Loss curves: the fused HIP training step (forward + loss + backward + fused Adam, fp32
+parity mode) replays the reference's own training run step for step.
+
+tests/golden/sas_curve.npz holds 1000 per-step losses of the reference
+(SASTrainer.calculate_loss + backward + torch.optim.Adam, BS/trainers/base.py:114-123,228)
+on the deterministic batch stream ``rbm_amd.data.sas_batch(default_rng(seed), ...)``;
+bert_curve.npz 300 BERT steps likewise.  North-star bar: |loss - reference| <= 1e-3 at
+every step.
+
+That bar is only meaningful while the reference's own fp32 run stays on the exact-math
+trajectory: tools/gen_curve_floor.py replays the same 1000 SAS steps with the fp64 oracle
+(*_curve_oracle64.npz) and the reference's fp32 curve drifts up to 2.4e-2 from it (step 717;
+chaotic amplification of fp32 rounding, 1.8e-4 by step 300).  So the SAS test holds the
+per-step 1e-3 bar over the first 300 steps and, over all 1000, the reference's own noise
+envelope (max |fp64 - fp32 reference|) plus a 50-step moving-average bar; the BERT run stays
+on the exact trajectory (drift 8e-7) and keeps the 1e-3 bar at every step.
+"""
+import argparse
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(kind, z, steps, dtype="fp32"):
+    import rbm_amd  # noqa: F401
+    import rbm_amd.data as synth
+    from rbm_amd.models import model_factory
+    from rbm_amd.train_step import FusedTrainStep
+    V, T, d, L, h, B = (int(z[k]) for k in ("V", "T", "d", "L", "h", "B"))
+    if kind == "sas":
+        a = argparse.Namespace(model_code="sas", num_items=V, max_len=T, device="cuda", sas_hidden_units=d,
+                               sas_num_blocks=L, sas_heads=h, sas_dropout=0.0, l2_emb=0.0, rs_dtype=dtype)
+    else:
+        a = argparse.Namespace(model_code="bert", num_items=V, max_len=T, device="cuda", bert_hidden_units=d,
+                               bert_num_blocks=L, bert_num_heads=h, bert_dropout=0.0, bert_hidden_dropout=0.0,
+                               bert_mask_prob=0.3, model_init_seed=int(z["seed"]), rs_dtype=dtype)
+    m = model_factory(a)
+    m.load_state_dict({k[2:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("p/")})
+    m.train()
+    tr = FusedTrainStep(m, lr=float(z["lr"]))
+    rng = np.random.default_rng(int(z["seed"]))
+    zipf = synth.ZipfItems(V)
+    out = []
+    for _ in range(steps):
+        if kind == "sas":
+            batch = synth.sas_batch(rng, B, T, V, zipf=zipf)
+        else:
+            batch = synth.bert_batch(rng, B, T, V, mask_prob=0.3, zipf=zipf)
+        loss = tr.step(*(torch.from_numpy(x).cuda() for x in batch))
+        out.append(loss.clone())
+    return np.array([float(x.item()) for x in out]), m
+
+
+def test_sas_loss_curve_matches_reference_1000_steps():
+    z = load_golden("sas_curve")
+    losses, _ = _run("sas", z, int(z["steps"]))
+    ref = z["losses"]
+    err = np.abs(losses - ref)
+    floor = np.abs(load_golden("sas_curve_oracle64")["losses"] - ref)
+    assert err[:300].max() <= 1e-3, (err[:300].max(), int(err[:300].argmax()))
+    assert err.max() <= 1.5 * floor.max(), (err.max(), floor.max())
+
+    def ma(x):
+        return np.convolve(x, np.ones(50) / 50, mode="valid")
+    assert np.abs(ma(losses) - ma(ref)).max() <= 2e-3
+
+
+def test_bert_loss_curve_matches_reference_300_steps():
+    z = load_golden("bert_curve")
+    losses, _ = _run("bert", z, int(z["steps"]))
+    err = np.abs(losses - z["losses"])
+    assert err.max() <= 1e-3, (err.max(), int(err.argmax()))
+
+
+def test_sas_loss_curve_bf16_tracks_reference():
+    """bf16 storage / MFMA (fp32 accumulate, fp32 master weights): reported, looser bound."""
+    z = load_golden("sas_curve")
+    losses, _ = _run("sas", z, 300, dtype="bf16")
+    err = np.abs(losses - z["losses"][:300])
+    assert err.mean() <= 2e-2 and err.max() <= 1e-1, (err.mean(), err.max())
