@@ -182,9 +182,12 @@ int rs_scatter_rows(int dtype, const void* src, int64_t lds, int64_t d, const in
  * flat fp32 buffer.  hyper (device fp32[5]) = {lr, beta1, beta2, eps, weight_decay}.
  * state (device double[4]): rs_adam_prepare does state[0] += 1 (the step count) and
  * forms state[1] = lr/(1-beta1^step), state[2] = sqrt(1-beta2^step) in double
- * precision, like torch's Python-float scalars.  rs_adam_step then updates
+ * precision, like torch's Python-float scalars, and state[3] = 1/(*grad_divisor) (1 when null: the
+ * data-parallel step all-reduces UNnormalised gradients plus the valid-position count and
+ * divides here, so the summed gradient equals the single-device mean's).  rs_adam_step then
+ * updates (grad scaled by state[3])
  * p, m, v (and writes the bf16 copy of p to p_bf16 when non-null). */
-int rs_adam_prepare(double* state, const float* hyper, void* stream);
+int rs_adam_prepare(double* state, const float* hyper, const float* grad_divisor, void* stream);
 int rs_adam_step(int64_t n, float* p, const float* g, float* m, float* v, void* p_bf16,
                  const double* state, const float* hyper, void* stream);
 

@@ -10,8 +10,9 @@
 #include "common.h"
 #include "../../include/recsys_hip.h"
 
-__global__ void adam_prepare_kernel(double* state, const float* hyper) {
+__global__ void adam_prepare_kernel(double* state, const float* hyper, const float* divisor) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  state[3] = divisor ? 1.0 / (double)divisor[0] : 1.0;
   const double step = state[0] + 1.0;
   state[0] = step;
   const double lr = hyper[0], b1 = hyper[1], b2 = hyper[2];
@@ -29,6 +30,7 @@ __global__ __launch_bounds__(256) void adam_step_kernel(int64_t n, float* __rest
   const float b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
   const float step_size = (float)state[1];
   const float bc2s = (float)state[2];
+  const float gs = (float)state[3];
   const int64_t n4 = n / 4;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
     float4 pp = reinterpret_cast<float4*>(p)[i];
@@ -38,7 +40,7 @@ __global__ __launch_bounds__(256) void adam_step_kernel(int64_t n, float* __rest
     float* P = &pp.x; float* G = &gg.x; float* Mv = &mm.x; float* Vv = &vv.x;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      float gj = G[j];
+      float gj = gs == 1.f ? G[j] : G[j] * gs;
       if (wd != 0.f) gj = gj + wd * P[j];
       Mv[j] = Mv[j] + (1.f - b1) * (gj - Mv[j]);            // exp_avg.lerp_(grad, 1-beta1)
       Vv[j] = Vv[j] * b2 + (1.f - b2) * gj * gj;            // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
@@ -57,7 +59,7 @@ __global__ __launch_bounds__(256) void adam_step_kernel(int64_t n, float* __rest
   // tail
   if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
     const int64_t j = n4 * 4 + threadIdx.x;
-    float gj = g[j];
+    float gj = gs == 1.f ? g[j] : g[j] * gs;
     if (wd != 0.f) gj = gj + wd * p[j];
     m[j] = m[j] + (1.f - b1) * (gj - m[j]);
     v[j] = v[j] * b2 + (1.f - b2) * gj * gj;
@@ -151,8 +153,8 @@ __global__ __launch_bounds__(256) void dropout_rowmask_kernel(const T* __restric
 
 extern "C" {
 
-int rs_adam_prepare(double* state, const float* hyper, void* stream) {
-  hipLaunchKernelGGL(adam_prepare_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, state, hyper);
+int rs_adam_prepare(double* state, const float* hyper, const float* grad_divisor, void* stream) {
+  hipLaunchKernelGGL(adam_prepare_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, state, hyper, grad_divisor);
   return (int)hipGetLastError();
 }
 

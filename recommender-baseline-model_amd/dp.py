@@ -1,0 +1,42 @@
+"""Data-parallel gradient exchange (one process per GPU, torch.distributed over RCCL/xGMI).
+
+The reference has no working multi-GPU path for SAS (``nn.DataParallel`` replicates the numpy
+batch, BS/trainers/base.py:32-34 + BS/trainers/sas.py:36-37), so the target is the single-device
+math on the global batch: both losses are MEANS over the valid positions of
+the whole batch (BS/trainers/sas.py:49, BS/trainers/bert.py:40).  Each rank therefore
+back-propagates its UNnormalised loss sum, writes (loss sum, valid count) into the two aux
+floats at the tail of its flat gradient buffer, and ONE all-reduce(SUM) of that buffer yields
+the global gradient sum, loss sum and count; the optimizer divides by the count
+(rs_adam_prepare's grad_divisor).  Averaging per-rank means instead is wrong whenever ranks see
+different valid counts.
+
+These helpers only move tensors; they work for any device / backend (gloo on CPU in the tests).
+"""
+import torch
+import torch.distributed as dist
+
+LOSS_SUM, COUNT = 0, 1   # aux slots
+
+
+def world():
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
+def allreduce_grads(flat_grad, group=None, bucket_numel=None):
+    """SUM all-reduce of the flat gradient buffer (parameters + aux tail), in place.
+
+    bucket_numel: split into buckets of that many floats (None = one call); buckets are issued
+    back to back on the current stream, RCCL pipelines them over the xGMI links."""
+    if world() == 1:
+        return flat_grad
+    if not bucket_numel or bucket_numel >= flat_grad.numel():
+        dist.all_reduce(flat_grad, group=group)
+        return flat_grad
+    for o in range(0, flat_grad.numel(), bucket_numel):
+        dist.all_reduce(flat_grad[o:o + bucket_numel], group=group)
+    return flat_grad
+
+
+def global_mean_loss(aux):
+    """Loss of the global batch from an all-reduced aux tail (a device scalar, no sync)."""
+    return aux[LOSS_SUM:LOSS_SUM + 1] / aux[COUNT:COUNT + 1]

@@ -11,6 +11,7 @@ import torch
 import torch.nn as nn
 
 ALIGN = 64
+AUX = 64   # fp32 scalars riding at the tail of the gradient buffer (DP: loss sum, valid count)
 
 
 class FlatParams:
@@ -33,7 +34,10 @@ class FlatParams:
         self.numel = off
         self.device = torch.device(device)
         self.data = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
-        self.grad = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+        # the gradient buffer carries AUX extra floats after the parameters: the data-parallel step
+        # puts its local loss sum and valid-position count there, so ONE all-reduce sums both
+        self.grad = torch.zeros(self.numel + AUX, dtype=torch.float32, device=self.device)
+        self.aux = self.grad[self.numel:]
         self.bf16 = None
         for n, p in named:
             if p.dtype != torch.float32:

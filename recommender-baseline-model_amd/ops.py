@@ -185,8 +185,8 @@ def scatter_rows(src, rank, dst):
     call("rs_scatter_rows", dtype_code(src), ptr(src), ld(src), d, ptr(rank), n, ptr(dst), ld(dst), stream())
 
 
-def adam_prepare(state, hyper):
-    call("rs_adam_prepare", ptr(state), ptr(hyper), stream())
+def adam_prepare(state, hyper, grad_divisor=None):
+    call("rs_adam_prepare", ptr(state), ptr(hyper), ptr(grad_divisor), stream())
 
 
 def adam_step(p, g, m, v, p_bf16, state, hyper):

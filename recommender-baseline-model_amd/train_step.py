@@ -2,24 +2,27 @@
 
 One call = the reference trainer's inner-loop body (``BS/trainers/base.py:114-123``):
 ``optimizer.zero_grad(); loss = calculate_loss(batch); loss.backward();
-optimizer.step()`` -- with every op a HIP kernel on the current stream and no
-host synchronisation (the reference's ``loss.item()`` is left to the caller).
+optimizer.step()`` -- every op a HIP kernel on the current stream, no host
+synchronisation (the reference's ``loss.item()`` is left to the caller).
 
-Data parallel (one process per GPU, ``torch.distributed`` over RCCL):
-  1. the loss kernel produces this rank's valid-position count;
-  2. one all-reduce of that scalar gives the global count, which is the
-     divisor of every rank's loss gradient (so the summed gradients equal the
-     single-device mean's gradient exactly, SURVEY.md §8(e));
-  3. one all-reduce (SUM) of the flat fp32 gradient buffer, then the fused Adam
-     sweep -- identical on every rank, so the replicas stay bit-identical.
+Single device: the loss kernels divide by the batch's valid-position count
+exactly like the reference's mean (BS/trainers/sas.py:49, BS/trainers/bert.py:40).
 
-The step can be captured once into a HIP graph (``capture``) and replayed
-(``replay``) with new batches copied into its static input buffers; the
+Data parallel (one process per GPU, ``torch.distributed`` over RCCL; see
+:mod:`rbm_amd.dp`): each rank back-propagates its UNnormalised loss sum, puts
+(loss sum, valid count) into the aux tail of its flat gradient buffer, ONE
+all-reduce(SUM) of the buffer follows, and the fused Adam divides by the global
+count -- the summed gradient then equals the single-device mean's gradient
+ and the replicas stay bit-identical.
+
+``capture`` records the step into HIP graphs (one graph on a single device;
+compute and optimizer graphs around the eager RCCL call under DP) and
+``replay`` runs it on new batches copied into the graphs' static inputs; the
 dropout step-seed lives in device memory and is advanced inside the graph.
 """
 import torch
-import torch.distributed as dist
 
+from . import dp as dpx
 from . import ops
 
 
@@ -35,17 +38,21 @@ class FusedAdam:
         self.hyper = torch.tensor([lr, betas[0], betas[1], eps, weight_decay], dtype=torch.float32, device=dev)
 
     def set_lr(self, lr):
+        """StepLR hook (BS/trainers/base.py:40,87): lives on the device, so graph replays see it."""
         self.hyper[0] = lr
 
-    def step(self):
-        ops.adam_prepare(self.state, self.hyper)
+    def step(self, grad_divisor=None):
+        ops.adam_prepare(self.state, self.hyper, grad_divisor)
         ops.adam_step(self.flat.data, self.flat.grad, self.m, self.v, self.flat.bf16, self.state, self.hyper)
 
 
 class FusedTrainStep:
-    def __init__(self, model, lr=1e-3, weight_decay=0.0, process_group=None, dp=None, max_labelled=None):
-        """model: rbm_amd SASModel or BERTModel on a CUDA device.  max_labelled (BERT): upper bound
-        on labelled rows per batch (sizes the compacted vocabulary-logit buffers; default B*T)."""
+    def __init__(self, model, lr=1e-3, weight_decay=0.0, process_group=None, dp=None, max_labelled=None,
+                 bucket_numel=None):
+        """model: rbm_amd SASModel or BERTModel on a CUDA device.
+        dp: data-parallel mode (default: torch.distributed initialised with world size > 1).
+        max_labelled (BERT): upper bound on labelled rows per batch (sizes the compacted
+        vocabulary-logit buffers; default B*T).  bucket_numel: all-reduce bucket size (floats)."""
         self.model = model
         self.kind = model.code()
         self.engine = model.sas.engine() if self.kind == "sas" else model.engine()
@@ -53,18 +60,27 @@ class FusedTrainStep:
         self.engine.sync_compute_weights()
         self.opt = FusedAdam(self.flat, lr=lr, weight_decay=weight_decay)
         self.pg = process_group
-        self.dp = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1 if dp is None else dp
+        self.dp = dpx.world() > 1 if dp is None else bool(dp)
+        self.bucket_numel = bucket_numel
+        self.max_labelled = max_labelled
         dev = self.flat.device
         self.loss_out = torch.zeros(4, dtype=torch.float32, device=dev)
         self.count = torch.zeros(1, dtype=torch.float32, device=dev)
-        self.graph = None
+        self.one = torch.ones(1, dtype=torch.float32, device=dev)
+        self.loss_val = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.graphs = None
         self.static = None
-        self.max_labelled = max_labelled
 
-    # ---------------------------------------------------------------- one step
-    def step(self, *batch):
-        """batch: SAS (seq, pos, neg) / BERT (tokens, labels) int64 device tensors.  Returns the
-        device loss tensor (this rank's share of the global mean under DP)."""
+    # ---------------------------------------------------------------- pieces
+    def _divisor(self, local_count):
+        """Divisor of the loss gradient: the local count (single device, = reference mean) or 1
+        (DP: unnormalised; the optimizer divides by the all-reduced global count)."""
+        if self.dp:
+            return self.one
+        self.count.copy_(local_count)
+        return self.count
+
+    def _compute(self, *batch):
         self.flat.grad.zero_()
         eng = self.engine
         if self.kind == "sas":
@@ -72,30 +88,42 @@ class FusedTrainStep:
             pl, nl, saved = eng.forward(seq, pos, neg, True)
             ws = eng.ws.get("bce", (3 * 256,), torch.float32)
             ops.bce_fwd(pl, nl, pos, ws, self.loss_out)
-            cnt = self._global_count(self.loss_out[1:2])
-            dpl, dnl = torch.empty_like(pl), torch.empty_like(nl)
-            ops.bce_bwd(pl, nl, pos, cnt, None, dpl, dnl)
+            div = self._divisor(self.loss_out[1:2])
+            dpl, dnl = eng.ws.get("dpl", pl.shape, torch.float32), eng.ws.get("dnl", nl.shape, torch.float32)
+            ops.bce_bwd(pl, nl, pos, div, None, dpl, dnl)
             eng.backward(saved, dpl, dnl, self.flat.grad)
         else:
             tokens, labels = batch
-            eng.train_loss_and_backward(tokens, labels, self.loss_out, self._global_count, self.flat.grad,
+            eng.train_loss_and_backward(tokens, labels, self.loss_out, self._divisor, self.flat.grad,
                                         max_labelled=self.max_labelled)
         if self.dp:
-            dist.all_reduce(self.flat.grad, group=self.pg)
-        self.opt.step()
-        return self.loss_out[0:1] / self.count if self.dp else self.loss_out[2:3]
+            self.flat.aux[dpx.LOSS_SUM:dpx.COUNT + 1].copy_(self.loss_out[0:2])
 
-    def _global_count(self, local_count):
-        if not self.dp:
-            self.count.copy_(local_count)
-            return self.count
-        self.count.copy_(local_count)
-        dist.all_reduce(self.count, group=self.pg)
-        return self.count
+    def _exchange(self):
+        if self.dp:
+            dpx.allreduce_grads(self.flat.grad, self.pg, self.bucket_numel)
 
-    # ---------------------------------------------------------------- HIP graph
+    def _update(self):
+        if self.dp:
+            self.opt.step(grad_divisor=self.flat.aux[dpx.COUNT:dpx.COUNT + 1])
+            torch.div(self.flat.aux[dpx.LOSS_SUM:dpx.LOSS_SUM + 1], self.flat.aux[dpx.COUNT:dpx.COUNT + 1],
+                      out=self.loss_val)
+        else:
+            self.opt.step()
+            self.loss_val.copy_(self.loss_out[2:3])
+
+    # ---------------------------------------------------------------- one step
+    def step(self, *batch):
+        """batch: SAS (seq, pos, neg) / BERT (tokens, labels) int64 device tensors.  Returns the
+        device loss (the global batch's mean loss, as the reference's calculate_loss)."""
+        self._compute(*batch)
+        self._exchange()
+        self._update()
+        return self.loss_val
+
+    # ---------------------------------------------------------------- HIP graphs
     def capture(self, *example_batch, warmup=2):
-        """Capture one step into a HIP graph.  example_batch fixes the shapes."""
+        """Capture the step into HIP graphs; example_batch fixes the shapes."""
         self.static = [t.clone() for t in example_batch]
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
@@ -104,13 +132,26 @@ class FusedTrainStep:
                 self.step(*self.static)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self.static_loss = self.step(*self.static)
+        if self.dp:
+            g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g1):
+                self._compute(*self.static)
+            with torch.cuda.graph(g2):
+                self._update()
+            self.graphs = (g1, g2)
+        else:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._compute(*self.static)
+                self._update()
+            self.graphs = (g,)
         return self
 
     def replay(self, *batch):
         for dst, src in zip(self.static, batch):
             dst.copy_(src, non_blocking=True)
-        self.graph.replay()
-        return self.static_loss
+        self.graphs[0].replay()
+        if self.dp:
+            self._exchange()            # RCCL all-reduce, eager, on the current stream
+            self.graphs[1].replay()
+        return self.loss_val

@@ -96,7 +96,7 @@ def test_bert_fused_step_matches_reference(name, dtype):
     lab = torch.from_numpy(z["labels"]).cuda()
     tr.flat.grad.zero_()
     tr.engine.sync_compute_weights()
-    tr.engine.train_loss_and_backward(tok, lab, tr.loss_out, tr._global_count, tr.flat.grad)
+    tr.engine.train_loss_and_backward(tok, lab, tr.loss_out, tr._divisor, tr.flat.grad)
     torch.cuda.synchronize()
     ftol, gtol = (FWD_TOL_F32, GRAD_TOL_F32) if dtype == "fp32" else (FWD_TOL_BF16, GRAD_TOL_BF16)
     loss = float(tr.loss_out[2].item())
@@ -125,7 +125,7 @@ def test_bert_fp32_matches_oracle_shapes(V, T, d, L, h, B, cap):
     tr = FusedTrainStep(m, lr=0.0, max_labelled=cap)
     tr.flat.grad.zero_()
     tr.engine.train_loss_and_backward(torch.from_numpy(tok).cuda(), torch.from_numpy(lab).cuda(), tr.loss_out,
-                                      tr._global_count, tr.flat.grad, max_labelled=cap)
+                                      tr._divisor, tr.flat.grad, max_labelled=cap)
     torch.cuda.synchronize()
     P = {k: v.detach().cpu().double() for k, v in m.state_dict().items()}
     l64, _, g64 = obert.loss_and_grads(P, torch.from_numpy(tok), torch.from_numpy(lab), L, h)

@@ -1,0 +1,103 @@
+"""Data-parallel exchange on CPU (gloo, world_size 2): the product's rbm_amd.dp helpers applied to
+per-rank UNnormalised gradients + (loss sum, count) aux give exactly the single-process gradient
+of the mean loss on the concatenated batch -- the reference's semantics (BS/trainers/sas.py:49,
+BS/trainers/bert.py:40) -- even when the ranks hold different valid counts.  The per-rank
+gradients come from the CPU oracle (the GPU kernels compute the same quantity; the single-GPU
+DP path is covered by tests/test_dp_gpu.py)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import ROOT, load_golden
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _flat(grads, names, loss_sum, count):
+    v = torch.cat([grads[k].reshape(-1) for k in names] + [torch.tensor([loss_sum, count], dtype=grads[names[0]].dtype)])
+    return v
+
+
+def _worker(rank, world, port, kind, bucket, out_dir):
+    import sys
+    sys.path.insert(0, ROOT)
+    import rbm_amd  # noqa: F401
+    from rbm_amd import dp
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        names, flat, _ = _local(kind, rank, world)
+        dp.allreduce_grads(flat, bucket_numel=bucket)
+        loss = dp.global_mean_loss(flat[-2:])
+        g = flat[:-2] / flat[-1]
+        torch.save({"g": g, "loss": loss}, os.path.join(out_dir, f"r{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def _local(kind, rank, world):
+    """This rank's share of the batch (rank r takes rows r, r+world, ...): unnormalised grads."""
+    from oracle import bert as obert
+    from oracle import sas as osas
+    if kind == "sas":
+        z = load_golden("sas_mid")
+        P = {k[2:]: torch.from_numpy(z[k]).double() for k in z.files if k.startswith("p/")}
+        seq, pos, neg = (torch.from_numpy(z[k])[rank::world] for k in ("seq", "pos", "neg"))
+        loss, _, _, g = osas.loss_and_grads(P, seq, pos, neg, int(z["L"]), int(z["h"]))
+        cnt = float((pos != 0).sum())
+    else:
+        z = load_golden("bert_mid")
+        P = {k[2:]: torch.from_numpy(z[k]).double() for k in z.files if k.startswith("p/")}
+        tok, lab = (torch.from_numpy(z[k])[rank::world] for k in ("tokens", "labels"))
+        loss, _, g = obert.loss_and_grads(P, tok, lab, int(z["L"]), int(z["h"]))
+        cnt = float((lab != 0).sum())
+    names = list(P)
+    ung = {k: g[k] * cnt for k in names}          # gradient of the loss SUM
+    return names, _flat(ung, names, float(loss) * cnt, cnt), cnt
+
+
+@pytest.mark.parametrize("kind", ["sas", "bert"])
+@pytest.mark.parametrize("bucket", [None, 4096])
+def test_dp_two_ranks_equal_single_device(kind, bucket, tmp_path):
+    import sys
+    sys.path.insert(0, ROOT)
+    from oracle import bert as obert
+    from oracle import sas as osas
+    port = _free_port()
+    mp.spawn(_worker, args=(2, port, kind, bucket, str(tmp_path)), nprocs=2, join=True)
+    r0 = torch.load(tmp_path / "r0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "r1.pt", weights_only=True)
+    assert torch.equal(r0["g"], r1["g"])                  # replicas apply the same update
+    if kind == "sas":
+        z = load_golden("sas_mid")
+        P = {k[2:]: torch.from_numpy(z[k]).double() for k in z.files if k.startswith("p/")}
+        loss, _, _, g = osas.loss_and_grads(P, *(torch.from_numpy(z[k]) for k in ("seq", "pos", "neg")),
+                                            int(z["L"]), int(z["h"]))
+    else:
+        z = load_golden("bert_mid")
+        P = {k[2:]: torch.from_numpy(z[k]).double() for k in z.files if k.startswith("p/")}
+        loss, _, g = obert.loss_and_grads(P, torch.from_numpy(z["tokens"]), torch.from_numpy(z["labels"]),
+                                          int(z["L"]), int(z["h"]))
+    ref = torch.cat([g[k].reshape(-1) for k in P])
+    assert abs(float(r0["loss"]) - float(loss)) < 1e-10 * max(1.0, abs(float(loss)))
+    assert float((r0["g"] - ref).norm() / ref.norm()) < 1e-12
+
+
+def test_ranks_have_different_counts():
+    """The case the global-count normalisation exists for: per-rank means would be wrong."""
+    z = load_golden("sas_mid")
+    pos = z["pos"]
+    counts = [int((pos[r::2] != 0).sum()) for r in range(2)]
+    assert counts[0] != counts[1]
+    _ = np

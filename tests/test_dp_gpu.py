@@ -1,0 +1,73 @@
+"""The data-parallel training step on the GPU through RCCL (a world_size-1 'nccl' process group:
+one MI355X per test box), eager and HIP-graph-captured: unnormalised backward + aux
+(loss sum, count) + all-reduce + Adam-side division gives the same update as the
+single-device step (which divides inside the loss kernel like the reference)."""
+import argparse
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+
+from conftest import rel
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def nccl_group():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    yield
+    dist.destroy_process_group()
+
+
+def _model(kind, seed):
+    import rbm_amd  # noqa: F401
+    from rbm_amd.models import model_factory
+    torch.manual_seed(seed)
+    if kind == "sas":
+        a = argparse.Namespace(model_code="sas", num_items=500, max_len=50, device="cuda", sas_hidden_units=64,
+                               sas_num_blocks=2, sas_heads=1, sas_dropout=0.0, l2_emb=0.0, rs_dtype="fp32")
+    else:
+        a = argparse.Namespace(model_code="bert", num_items=500, max_len=50, device="cuda", bert_hidden_units=64,
+                               bert_num_blocks=2, bert_num_heads=2, bert_dropout=0.0, bert_hidden_dropout=0.0,
+                               bert_mask_prob=0.2, model_init_seed=seed, rs_dtype="fp32")
+    return model_factory(a)
+
+
+def _batches(kind, n):
+    import rbm_amd.data as synth
+    rng = np.random.default_rng(11)
+    out = []
+    for _ in range(n):
+        b = synth.sas_batch(rng, 6, 50, 500) if kind == "sas" else synth.bert_batch(rng, 6, 50, 500)
+        out.append(tuple(torch.from_numpy(x).cuda() for x in b))
+    return out
+
+
+@pytest.mark.parametrize("graph", [False, True])
+@pytest.mark.parametrize("kind", ["sas", "bert"])
+def test_dp_step_equals_single_device_step(nccl_group, kind, graph):
+    from rbm_amd.train_step import FusedTrainStep
+    batches = _batches(kind, 4)
+    res = {}
+    for dp in (False, True):
+        m = _model(kind, 3)
+        tr = FusedTrainStep(m, lr=1e-3, dp=dp, bucket_numel=8192 if dp else None)
+        if graph:
+            tr.capture(*batches[0])
+            # capture() ran warm-up steps: restart from the same weights for both arms
+        losses = []
+        for b in batches:
+            losses.append(float((tr.replay(*b) if graph else tr.step(*b)).item()))
+        res[dp] = (losses, tr.flat.data.detach().cpu().clone())
+    l0, p0 = res[False]
+    l1, p1 = res[True]
+    assert np.allclose(l0, l1, rtol=1e-5, atol=1e-6), (l0, l1)
+    assert rel(p1.numpy(), p0.numpy()) < 1e-6

@@ -121,7 +121,7 @@ def main():
     p, gg, m1, v1 = (torch.randn(n, device=dev) for _ in range(4))
     v1.abs_()
     pbf = torch.empty(n, dtype=torch.bfloat16, device=dev)
-    st = torch.tensor([1.0, 0.001, 1.0, 0], dtype=torch.float64, device=dev)
+    st = torch.tensor([1.0, 0.001, 1.0, 1.0], dtype=torch.float64, device=dev)
     hy = torch.tensor([1e-3, 0.9, 0.999, 1e-8, 0.0], device=dev)
     rec("adam_step (662k params)", timeit(lambda: ops.adam_step(p, gg, m1, v1, pbf, st, hy), a.reps), n * 4 * 7 + n * 2)
     print(f"{'op':45s} {'us':>9s} {'GB/s':>9s} {'TFLOP/s':>8s}")
