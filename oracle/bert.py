@@ -34,6 +34,8 @@ def gelu(x):
 
 
 def _dropout(x, p, mask):
+    if mask is False:                # CPU-baseline timing: torch's own bernoulli dropout, as the reference
+        return F.dropout(x, p, training=True) if p > 0 else x
     if mask is not None:
         return x * mask / (1.0 - p)
     if p > 0:
@@ -42,8 +44,9 @@ def _dropout(x, p, mask):
 
 
 def encode(P, x_ids, num_blocks, heads, p=0.0, hp=0.0, masks=None):
-    """BERT.forward (bert_modules/bert.py:36-43) -> hidden (B,T,d)."""
-    masks = masks or {}
+    """BERT.forward (bert_modules/bert.py:36-43) -> hidden (B,T,d).  masks: per-site dropout masks,
+    or ``oracle.sas.RandomDropout()`` for torch bernoulli dropout (CPU-baseline timing only)."""
+    masks = {} if masks is None else masks
     B, T = x_ids.shape
     key_ok = (x_ids > 0).view(B, 1, 1, T)
     x = F.embedding(x_ids, P["bert.embedding.token.weight"], padding_idx=0) + P["bert.embedding.position.pe.weight"].unsqueeze(0)
