@@ -28,8 +28,11 @@ class BERTModel(BaseModel):
         return 'bert'
 
     def _apply(self, fn, recurse=True):
+        # (re)build the flat parameter buffer eagerly on .to(cuda), before any optimizer is created over
+        # model.parameters() (the reference builds its Adam after model.to(device), base.py:21,38)
         super()._apply(fn, recurse)
-        self._flat = None
+        p = self.out.weight
+        self._flat = build_flat(self, p.device) if p.device.type == "cuda" else None
         self._engine = None
         return self
 
