@@ -57,8 +57,12 @@ def test_reference_sas_trainer_loop_on_hip_model():
         oopt.step([g[k] for k in P])
         assert abs(loss.item() - l64.item()) < 1e-4 * max(1.0, abs(l64.item()))
     sd = model.state_dict()
+    d = int(z["d"])
     for k in P:
-        assert rel(sd[k].cpu().numpy(), P[k].numpy()) < 1e-4, k
+        a, b = sd[k].cpu().numpy(), P[k].numpy()
+        if k.endswith("in_proj_bias"):   # the key-bias third: noise-level gradient, Adam steps it by ~lr
+            a, b = np.concatenate([a[:d], a[2 * d:]]), np.concatenate([b[:d], b[2 * d:]])
+        assert rel(a, b) < 1e-4, k
 
 
 def test_reference_bert_trainer_loop_on_hip_model():
