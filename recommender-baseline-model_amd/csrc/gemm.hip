@@ -17,27 +17,7 @@
 // AK/BK = 0, m/n-contiguous rows for AK/BK = 1), register-staged prefetch of
 // tile k+1 under the MFMAs of tile k.  The block->tile map is XCD-aware: blocks
 // b and b+8 share an XCD, so consecutive tile ids go to the same XCD's L2.
-#include "common.h"
-#include "../../include/recsys_hip.h"
-
-#define ACT_NONE 0
-#define ACT_RELU 1
-#define ACT_GELU 2
-#define ACT_RELU_BWD 3
-#define ACT_GELU_BWD 4
-
-struct GemmArgs {
-  int64_t M, N, K;
-  const void* A; int64_t lda;
-  const void* B; int64_t ldb;
-  void* C; int64_t ldc;
-  int c_f32;
-  int split_k; int64_t k_per_split;
-  float* slab;  // when non-null: write raw fp32 partials to slab[z*slab_stride + m*N + n]
-  int64_t slab_stride;
-  int bias_colsum;  // (AK only) also write sum_k A(m,k) of this split to slab[z*slab_stride + M*N + m]
-  rs_epilogue epi;
-};
+#include "gemm_common.h"
 
 template <typename T, bool KMAJ, int ROWS>
 struct TileLoader {
@@ -258,14 +238,14 @@ int rs_gemm(int dtype, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t
   GemmArgs a;
   a.M = M; a.N = N; a.K = K; a.A = A; a.lda = lda; a.B = B; a.ldb = ldb; a.C = C; a.ldc = ldc;
   a.c_f32 = c_f32; a.split_k = split_k;
-  a.k_per_split = split_k > 1 ? cdiv(cdiv(K, split_k), 32) * 32 : (K > 0 ? K : 1);
+  a.k_per_split = split_k > 1 ? cdiv(cdiv(K, split_k), 64) * 64 : (K > 0 ? K : 1);
   a.slab = slab;
   a.slab_stride = M * N;
   a.bias_colsum = 0;
   if (epi) a.epi = *epi;
   else { a.epi = rs_epilogue{}; a.epi.alpha = 1.0f; }
   hipStream_t s = (hipStream_t)stream;
-  hipError_t err = dtype == RS_DTYPE_BF16 ? launch_dt<__bf16>(a_kmajor, b_kmajor, a, s)
+  hipError_t err = dtype == RS_DTYPE_BF16 ? gemm_bf16_launch(a_kmajor, b_kmajor, a, s)
                                           : launch_dt<float>(a_kmajor, b_kmajor, a, s);
   return (int)err;
 }
@@ -283,7 +263,7 @@ int rs_linear_wgrad(int dtype, int64_t M, int64_t N, int64_t K, const void* dY, 
   GemmArgs a;
   a.M = N; a.N = K; a.K = M; a.A = dY; a.lda = lddy; a.B = X; a.ldb = ldx; a.C = nullptr; a.ldc = 0;
   a.c_f32 = 1; a.split_k = splits;
-  a.k_per_split = cdiv(cdiv(M, splits), 32) * 32;
+  a.k_per_split = cdiv(cdiv(M, splits), 64) * 64;
   a.slab = slab;
   a.slab_stride = N * K + (db ? N : 0);
   a.bias_colsum = db ? 1 : 0;
@@ -291,7 +271,7 @@ int rs_linear_wgrad(int dtype, int64_t M, int64_t N, int64_t K, const void* dY, 
   a.epi.alpha = 1.0f;
   a.epi.rows_dev = rows_dev;
   hipStream_t s = (hipStream_t)stream;
-  hipError_t err = dtype == RS_DTYPE_BF16 ? launch_t<__bf16, true, true>(a, s) : launch_t<float, true, true>(a, s);
+  hipError_t err = dtype == RS_DTYPE_BF16 ? gemm_bf16_launch(1, 1, a, s) : launch_t<float, true, true>(a, s);
   if (err != hipSuccess) return (int)err;
   // one pass over the slabs: columns [0, N*K) -> dW, [N*K, N*K+N) -> db
   return (int)launch_reduce_slabs(slab, splits, a.slab_stride, N * K, dW, db, accumulate, s);

@@ -1,0 +1,28 @@
+// Shared declarations of the two GEMM implementations (gemm.hip: fp32 parity path and generic;
+// gemm_bf16.hip: the bf16 throughput path).
+#pragma once
+#include "common.h"
+#include "../../include/recsys_hip.h"
+
+#define ACT_NONE 0
+#define ACT_RELU 1
+#define ACT_GELU 2
+#define ACT_RELU_BWD 3
+#define ACT_GELU_BWD 4
+
+struct GemmArgs {
+  int64_t M, N, K;
+  const void* A; int64_t lda;
+  const void* B; int64_t ldb;
+  void* C; int64_t ldc;
+  int c_f32;
+  int split_k; int64_t k_per_split;
+  float* slab;  // when non-null: write raw fp32 partials to slab[z*slab_stride + m*N + n]
+  int64_t slab_stride;
+  int bias_colsum;  // (AK only) also write sum_k A(m,k) of this split to slab[z*slab_stride + M*N + m]
+  rs_epilogue epi;
+  int vec_ok;  // (bf16 path) 8-column vectorised epilogue legal for this call
+};
+
+
+hipError_t gemm_bf16_launch(int ak, int bk, GemmArgs& a, hipStream_t s);

@@ -117,6 +117,24 @@ def main():
     rec("attn_bwd causal drop", timeit(lambda: ops.attn_bwd(B, T, H, Dh, q, kv[:, :d], kv[:, d:], o, y, lse, dq,
                                                             dkv[:, :d], dkv[:, d:], 1 / math.sqrt(Dh), 0, ids, 0.2,
                                                             9, sb, wat), a.reps), 8 * mb, 2.5 * aflops)
+    if a.config in ("cfg3", "cfg5"):
+        V1 = V + 1
+        R = 1792
+        V1p = -(-V1 // 64) * 64
+        h = rn(R, d)
+        Wo = (0.05 * torch.randn(V1, d, device=dev, generator=g)).to(dt)
+        bo = torch.zeros(V1, device=dev)
+        lg = torch.empty(R, V1p, device=dev)[:, :V1]
+        rec("vocab logits fwd (fp32 out)", timeit(lambda: ops.linear_fwd(h, Wo, lg, bias=bo), a.reps),
+            R * V1 * 4 + V1 * d * es, 2 * R * V1 * d)
+        dl = torch.randn(R, V1p, device=dev, generator=g).to(dt)[:, :V1]
+        dh = rn(R, d)
+        rec("vocab dgrad", timeit(lambda: ops.linear_dgrad(dl, Wo, dh), a.reps), R * V1 * es + V1 * d * es,
+            2 * R * V1 * d)
+        dWo = torch.zeros(V1, d, device=dev)
+        slab_o = torch.empty(ops.wgrad_slab_numel(R, V1, d), device=dev)
+        rec("vocab wgrad+bias", timeit(lambda: ops.linear_wgrad(dl, h, dWo, slab_o, db=bo), a.reps),
+            R * V1 * es + V1 * d * 4, 2 * R * V1 * d)
     n = 662400
     p, gg, m1, v1 = (torch.randn(n, device=dev) for _ in range(4))
     v1.abs_()
