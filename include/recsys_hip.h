@@ -113,7 +113,7 @@ int rs_embed_bwd(int dtype, int mode, const int64_t* ids, int64_t rows, int64_t 
 int rs_layernorm_fwd(int dtype, int variant, const void* X, int64_t ldx, int64_t M, int64_t d,
                      const float* gamma, const float* beta, float eps, void* Y, int64_t ldy,
                      float* mean, float* rinv, void* stream);
-/* dX (+)= LN backward; dgamma/dbeta += column sums (deterministic, ws >= 2*d*128 floats). */
+/* dX (+)= LN backward; dgamma/dbeta += column sums (deterministic, ws >= 2*d*512 floats). */
 int rs_layernorm_bwd(int dtype, int variant, const void* X, int64_t ldx, const void* dY, int64_t lddy,
                      int64_t M, int64_t d, const float* gamma, const float* mean, const float* rinv, float eps,
                      void* dX, int64_t lddx, int accumulate_dx, float* dgamma, float* dbeta, float* ws,

@@ -79,22 +79,36 @@ __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, f32x4 
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-// global row chunk (zero beyond T)
+// global row chunk (zero beyond T).  Branch-free: the load always reads a valid row (clamped) and
+// the result is masked afterwards -- a branch around the load makes hipcc wait vmcnt(0) per chunk.
 __device__ __forceinline__ bf16x8 gload8(const bf16* base, int64_t ld, int64_t row, int64_t T, int col) {
-  if (row < T) return *reinterpret_cast<const bf16x8*>(base + row * ld + col);
-  bf16x8 z;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) z[j] = (bf16)0.0f;
-  return z;
+  const int64_t rc = row < T ? row : T - 1;
+  typedef __attribute__((ext_vector_type(4))) unsigned u4;
+  u4 v = *reinterpret_cast<const u4*>(base + rc * ld + col);
+  const unsigned keep = row < T ? 0xffffffffu : 0u;
+  v &= keep;
+  return __builtin_bit_cast(bf16x8, v);
 }
 
-// stage rows [0, rows) of a (T x DH) head slice into an LDS image (rows >= T zero)
+// stage rows [0, rows) of a (T x DH) head slice into an LDS image (rows >= T zero).
+// Batches of 8 chunks per thread: all 8 loads are issued before the first LDS store, so a
+// 51 KB image takes ~2 dependent HBM round trips instead of one per chunk.
 template <int DH>
 __device__ __forceinline__ void stage(bf16* img, const bf16* src, int64_t ld, int64_t T, int rows, int tid) {
-  constexpr int CPR = DH / 8, LD = Img<DH>::LD;
-  for (int i = tid; i < rows * CPR; i += 256) {
-    const int r = i / CPR, c = (i % CPR) * 8;
-    *reinterpret_cast<bf16x8*>(img + r * LD + c) = gload8(src, ld, r, T, c);
+  constexpr int CPR = DH / 8, LD = Img<DH>::LD, U = 8;
+  const int n = rows * CPR;
+  for (int i0 = tid; i0 < n; i0 += 256 * U) {
+    bf16x8 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = min(i0 + u * 256, n - 1);
+      v[u] = gload8(src, ld, i / CPR, T, (i % CPR) * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * 256;
+      if (i < n) *reinterpret_cast<bf16x8*>(img + (i / CPR) * LD + (i % CPR) * 8) = v[u];
+    }
   }
 }
 

@@ -136,20 +136,37 @@ __device__ __forceinline__ float group16_max(float v) {
 }
 
 // ---------------------------------------------------------------- dropout RNG
-// Counter-based: keep(seed, idx) is a pure function, so the backward pass
-// regenerates every mask instead of storing it.  splitmix64 finaliser.
-__device__ __forceinline__ uint32_t rng_u32(uint64_t seed, uint64_t ctr) {
-  uint64_t z = seed + ctr * 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return (uint32_t)(z >> 32);
+// Counter-based: keep(seed, idx) is a pure function of (site/step seed, element index), so the
+// backward pass regenerates every mask instead of storing it.  One 32-bit avalanche hash
+// (lowbias32) per PAIR of elements {2j, 2j+1} gives two 16-bit uniforms; thresholds have 2^-16
+// resolution (p = 0.2 keeps 1 - 13107/65536).  Cost: ~6 VALU per element.
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
 }
+__device__ __forceinline__ uint32_t seed32(uint64_t seed) { return (uint32_t)seed ^ (uint32_t)(seed >> 32) * 0x27d4eb2fU; }
+__device__ __forceinline__ uint32_t pair_hash(uint32_t s32, uint64_t idx) {
+  return hash32(((uint32_t)(idx >> 1) * 0x9E3779B1U) ^ s32 ^ ((uint32_t)(idx >> 33) * 0x85EBCA77U));
+}
+__device__ __forceinline__ uint32_t drop_thr(float p) { return (uint32_t)fminf(p * 65536.0f, 65535.0f); }
 // keep with probability 1-p; returns the multiplier (0 or 1/(1-p))
 __device__ __forceinline__ float drop_mul(float p, uint64_t seed, uint64_t idx) {
   if (p <= 0.0f) return 1.0f;
-  uint32_t thr = (uint32_t)fminf(p * 4294967296.0f, 4294967295.0f);
-  return rng_u32(seed, idx) >= thr ? 1.0f / (1.0f - p) : 0.0f;
+  const uint32_t h = pair_hash(seed32(seed), idx);
+  const uint32_t u = (idx & 1) ? (h >> 16) : (h & 0xFFFFu);
+  return u >= drop_thr(p) ? 1.0f / (1.0f - p) : 0.0f;
+}
+// the two multipliers of elements idx, idx+1 (idx even) from one hash
+__device__ __forceinline__ void drop_mul2(float p, uint32_t s32, uint64_t idx_even, float& m0, float& m1) {
+  const uint32_t h = pair_hash(s32, idx_even);
+  const uint32_t thr = drop_thr(p);
+  const float k = 1.0f / (1.0f - p);
+  m0 = (h & 0xFFFFu) >= thr ? k : 0.0f;
+  m1 = (h >> 16) >= thr ? k : 0.0f;
 }
 
 // effective per-site seed: host-side site salt mixed with the device-side step

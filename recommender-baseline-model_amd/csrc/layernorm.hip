@@ -14,7 +14,7 @@
 #include "../../include/recsys_hip.h"
 
 #define LN_MAXV 16  // d <= 64*16
-#define LN_BWD_BLOCKS 128  // affine-partial slabs per LN backward (ws >= 2*d*LN_BWD_BLOCKS floats)
+#define LN_BWD_BLOCKS 512  // affine-partial slabs per LN backward (ws >= 2*d*LN_BWD_BLOCKS floats)
 
 template <typename T, int NV>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ X, int64_t ldx, int64_t M, int d,
@@ -140,10 +140,13 @@ __device__ __forceinline__ float group_sum(float v) {
   return v;
 }
 
-template <typename T, int LPR, int NCH>
+// (hipcc pitfall: a per-element `variant ? a : b` around the gamma/beta loads made it branch and
+// wait vmcnt(0) per element -- 16 dependent L2 round trips, 4x the kernel time; the variant is a
+// template parameter and gamma/beta are loaded as float4 vectors up front)
+template <typename T, int LPR, int NCH, int VAR>
 __global__ __launch_bounds__(256) void ln_fwd_v_kernel(const T* __restrict__ X, int64_t ldx, int64_t M, int d,
                                                        const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                       float eps, int variant, T* __restrict__ Y, int64_t ldy,
+                                                       float eps, T* __restrict__ Y, int64_t ldy,
                                                        float* __restrict__ mean_out, float* __restrict__ rinv_out) {
   constexpr int V = Vec<T>::N, RPW = 64 / LPR;
   const int lane = threadIdx.x & 63, sub = lane % LPR;
@@ -168,16 +171,22 @@ __global__ __launch_bounds__(256) void ln_fwd_v_kernel(const T* __restrict__ X, 
       q += u * u;
     }
   q = group_sum<LPR>(q);
-  const float rinv = variant == 0 ? 1.0f / sqrtf(q / (float)d + eps) : 1.0f / (sqrtf(q / (float)(d - 1)) + eps);
+  const float rinv = VAR == 0 ? 1.0f / sqrtf(q / (float)d + eps) : 1.0f / (sqrtf(q / (float)(d - 1)) + eps);
   T* y = Y + row * ldy;
 #pragma unroll
   for (int i = 0; i < NCH; ++i) {
     const int c0 = (i * LPR + sub) * V;
-    float o[V];
+    float gm[V], bt[V], o[V];
+    load_chunk<float>(gm, gamma + c0);
+    load_chunk<float>(bt, beta + c0);
+    if (V == 8) {
+      load_chunk<float>(gm + 4, gamma + c0 + 4);
+      load_chunk<float>(bt + 4, beta + c0 + 4);
+    }
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       const float u = v[i][j] - mu;
-      o[j] = variant == 0 ? u * rinv * gamma[c0 + j] + beta[c0 + j] : gamma[c0 + j] * (u * rinv) + beta[c0 + j];
+      o[j] = VAR == 0 ? u * rinv * gm[j] + bt[j] : gm[j] * (u * rinv) + bt[j];
     }
     store_chunk<T>(y + c0, o);
   }
@@ -190,12 +199,12 @@ __global__ __launch_bounds__(256) void ln_fwd_v_kernel(const T* __restrict__ X, 
 // backward; the affine partials of each lane's columns are accumulated over all rows the lane
 // group visits (grid-stride), combined over the block's row groups in LDS (fixed order) and
 // written to part[block][2][d] for the deterministic slab reduce.
-template <typename T, int LPR, int NCH>
+template <typename T, int LPR, int NCH, int VAR, bool ACC>
 __global__ __launch_bounds__(256) void ln_bwd_v_kernel(const T* __restrict__ X, int64_t ldx, const T* __restrict__ dY,
                                                        int64_t lddy, int64_t M, int d, const float* __restrict__ gamma,
                                                        const float* __restrict__ mean, const float* __restrict__ rinv,
-                                                       float eps, int variant, T* __restrict__ dX, int64_t lddx,
-                                                       int accumulate, float* __restrict__ part) {
+                                                       float eps, T* __restrict__ dX, int64_t lddx,
+                                                       float* __restrict__ part) {
   constexpr int V = Vec<T>::N, RPW = 64 / LPR, RPB = 4 * RPW;
   const int lane = threadIdx.x & 63, sub = lane % LPR;
   const int rgrp = (threadIdx.x >> 6) * RPW + lane / LPR;  // row group within the block
@@ -208,47 +217,68 @@ __global__ __launch_bounds__(256) void ln_bwd_v_kernel(const T* __restrict__ X, 
       pb[i][j] = 0.f;
       gm[i][j] = gamma[(i * LPR + sub) * V + j];
     }
-  for (int64_t row = (int64_t)blockIdx.x * RPB + rgrp; row < M; row += (int64_t)gridDim.x * RPB) {
-    const float mu = mean[row], a = rinv[row];
-    float u[NCH][V], gq[NCH][V];
-    float sg = 0.f, sgu = 0.f;
+  // U rows per lane group per iteration, all their loads issued before any of them is used
+  constexpr int U = 4;
+  const int64_t stride = (int64_t)gridDim.x * RPB;
+  for (int64_t row0 = (int64_t)blockIdx.x * RPB + rgrp; row0 < M; row0 += stride * U) {
+    float xv[U][NCH][V], dyv[U][NCH][V], ov[U][NCH][V], mu[U], ra[U];
 #pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      const int c0 = (i * LPR + sub) * V;
-      float xv[V], dy[V];
-      load_chunk<T>(xv, X + row * ldx + c0);
-      load_chunk<T>(dy, dY + row * lddy + c0);
+    for (int uu = 0; uu < U; ++uu) {
+      const int64_t row = row0 + uu * stride;
+      const int64_t rr = row < M ? row : M - 1;
+      mu[uu] = mean[rr];
+      ra[uu] = rinv[rr];
 #pragma unroll
-      for (int j = 0; j < V; ++j) {
-        u[i][j] = xv[j] - mu;
-        gq[i][j] = dy[j] * gm[i][j];
-        pg[i][j] += dy[j] * (u[i][j] * a);
-        pb[i][j] += dy[j];
-        sg += gq[i][j];
-        sgu += gq[i][j] * u[i][j];
+      for (int i = 0; i < NCH; ++i) {
+        const int c0 = (i * LPR + sub) * V;
+        load_chunk<T>(xv[uu][i], X + rr * ldx + c0);
+        load_chunk<T>(dyv[uu][i], dY + rr * lddy + c0);
+        if constexpr (ACC) load_chunk<T>(ov[uu][i], dX + rr * lddx + c0);
       }
     }
-    sg = group_sum<LPR>(sg);
-    sgu = group_sum<LPR>(sgu);
-    const float mg = sg / (float)d;
-    float coef;
-    if (variant == 0) {
-      coef = a * a * a * sgu / (float)d;
-    } else {
-      const float sd = 1.0f / a - eps;
-      coef = sd > 0.f ? a * a * sgu / ((float)(d - 1) * sd) : 0.f;
-    }
 #pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      const int c0 = (i * LPR + sub) * V;
-      float o[V];
-      if (accumulate) load_chunk<T>(o, dX + row * lddx + c0);
+    for (int uu = 0; uu < U; ++uu) {
+      const int64_t row = row0 + uu * stride;
+      const bool valid = row < M;
+      const float a = ra[uu];
+      float u[NCH][V], gq[NCH][V];
+      float sg = 0.f, sgu = 0.f;
 #pragma unroll
-      for (int j = 0; j < V; ++j) {
-        const float t = a * (gq[i][j] - mg) - coef * u[i][j];
-        o[j] = accumulate ? o[j] + t : t;
+      for (int i = 0; i < NCH; ++i)
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          const float dy = valid ? dyv[uu][i][j] : 0.f;
+          u[i][j] = xv[uu][i][j] - mu[uu];
+          gq[i][j] = dy * gm[i][j];
+          pg[i][j] += dy * (u[i][j] * a);
+          pb[i][j] += dy;
+          sg += gq[i][j];
+          sgu += gq[i][j] * u[i][j];
+        }
+      sg = group_sum<LPR>(sg);
+      sgu = group_sum<LPR>(sgu);
+      const float mg = sg / (float)d;
+      float coef;
+      if (VAR == 0) {
+        coef = a * a * a * sgu / (float)d;
+      } else {
+        const float sd = 1.0f / a - eps;
+        coef = sd > 0.f ? a * a * sgu / ((float)(d - 1) * sd) : 0.f;
       }
-      store_chunk<T>(dX + row * lddx + c0, o);
+      if (valid) {
+#pragma unroll
+        for (int i = 0; i < NCH; ++i) {
+          const int c0 = (i * LPR + sub) * V;
+          float o[V];
+#pragma unroll
+          for (int j = 0; j < V; ++j) {
+            const float t = a * (gq[i][j] - mg) - coef * u[i][j];
+            if constexpr (ACC) o[j] = ov[uu][i][j] + t;
+            else o[j] = t;
+          }
+          store_chunk<T>(dX + row * lddx + c0, o);
+        }
+      }
     }
   }
   // combine the RPB row groups: LDS [RPB][d] twice (gamma, beta) in two rounds to bound LDS
@@ -276,10 +306,17 @@ static hipError_t ln_fwd_t(const void* X, int64_t ldx, int64_t M, int d, const f
   {
     constexpr int V = Vec<T>::N;
     const bool vec = (d % V == 0) && (ldx % V == 0) && (ldy % V == 0) && ((uintptr_t)X % 16 == 0) &&
-                     ((uintptr_t)Y % 16 == 0);
+                     ((uintptr_t)Y % 16 == 0) && ((uintptr_t)gamma % 16 == 0) && ((uintptr_t)beta % 16 == 0);
     const int cpr = d / V;
-#define LNFV(LPR, NCH) hipLaunchKernelGGL((ln_fwd_v_kernel<T, LPR, NCH>), dim3((unsigned)cdiv(M, 4 * (64 / LPR))), \
-                                          dim3(256), 0, s, x, ldx, M, d, gamma, beta, eps, variant, y, ldy, mean, rinv)
+#define LNFV(LPR, NCH)                                                                                       \
+  do {                                                                                                       \
+    if (variant == 0)                                                                                        \
+      hipLaunchKernelGGL((ln_fwd_v_kernel<T, LPR, NCH, 0>), dim3((unsigned)cdiv(M, 4 * (64 / LPR))), dim3(256), \
+                         0, s, x, ldx, M, d, gamma, beta, eps, y, ldy, mean, rinv);                          \
+    else                                                                                                     \
+      hipLaunchKernelGGL((ln_fwd_v_kernel<T, LPR, NCH, 1>), dim3((unsigned)cdiv(M, 4 * (64 / LPR))), dim3(256), \
+                         0, s, x, ldx, M, d, gamma, beta, eps, y, ldy, mean, rinv);                          \
+  } while (0)
     if (vec) {
       if (cpr == 4) { LNFV(4, 1); return hipGetLastError(); }
       if (cpr == 8) { LNFV(8, 1); return hipGetLastError(); }
@@ -320,9 +357,18 @@ static hipError_t ln_bwd_t(const void* X, int64_t ldx, const void* dY, int64_t l
     }
     if (lpr) {
       const int64_t rpb = 4 * (64 / lpr);
-      const int nb = (int)std::min<int64_t>(LN_BWD_BLOCKS, cdiv(M, rpb));
-#define LNBV(LPR, NCH) hipLaunchKernelGGL((ln_bwd_v_kernel<T, LPR, NCH>), dim3(nb), dim3(256), 0, s, x, ldx, dy, lddy, \
-                                          M, d, gamma, mean, rinv, eps, variant, dx, lddx, acc, ws)
+      const int nb = (int)std::min<int64_t>(LN_BWD_BLOCKS / 2, cdiv(M, rpb * 4));
+#define LNBV1(LPR, NCH, VAR, ACC)                                                                          \
+  hipLaunchKernelGGL((ln_bwd_v_kernel<T, LPR, NCH, VAR, ACC>), dim3(nb), dim3(256), 0, s, x, ldx, dy, lddy, M, d, \
+                     gamma, mean, rinv, eps, dx, lddx, ws)
+#define LNBV(LPR, NCH)                                                \
+  do {                                                                \
+    if (variant == 0) {                                               \
+      if (acc) LNBV1(LPR, NCH, 0, true); else LNBV1(LPR, NCH, 0, false); \
+    } else {                                                          \
+      if (acc) LNBV1(LPR, NCH, 1, true); else LNBV1(LPR, NCH, 1, false); \
+    }                                                                 \
+  } while (0)
       if (lpr == 4) LNBV(4, 1);
       else if (lpr == 8) LNBV(8, 1);
       else if (lpr == 16) LNBV(16, 1);
@@ -330,6 +376,7 @@ static hipError_t ln_bwd_t(const void* X, int64_t ldx, const void* dY, int64_t l
       else if (nch == 1) LNBV(64, 1);
       else LNBV(64, 2);
 #undef LNBV
+#undef LNBV1
       hipError_t e = hipGetLastError();
       if (e != hipSuccess || !(dgamma || dbeta)) return e;
       return launch_reduce_slabs(ws, nb, 2 * (int64_t)d, d, dgamma, dbeta, 1, s);

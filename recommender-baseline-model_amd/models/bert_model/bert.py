@@ -190,7 +190,7 @@ class BERTEngine:
         return self.flat.span([self._qkv(i, j, "bias") for j in range(3)], buf)
 
     # ---- encoder forward -------------------------------------------------------------
-    def encode(self, ids, training):
+    def encode(self, ids, training, clone_seed=True):
         B, T = ids.shape
         if T != self.T:
             raise ValueError(f"sequence length {T} must equal max_len {self.T} (position.py:14-16 adds the "
@@ -200,7 +200,7 @@ class BERTEngine:
         hp = self.hp if training else 0.0
         if p > 0 or hp > 0:
             ops.seed_advance(self.seed_base)
-        sb = self.seed_base.clone()
+        sb = self.seed_base.clone() if clone_seed else self.seed_base
         e = self._buf
         s = {"B": B, "T": T, "p": p, "hp": hp, "ids": ids, "sb": sb, "blocks": []}
         x = e((M, d))
@@ -251,7 +251,7 @@ class BERTEngine:
         G = lambda n: self.flat.view(n, grad)  # noqa: E731
         slab = self.ws.get("slab", (max(ops.wgrad_slab_numel(M, Fd, d), ops.wgrad_slab_numel(M, d, Fd),
                                         ops.wgrad_slab_numel(M, 3 * d, d)),), torch.float32)
-        wln = self.ws.get("ln", (2 * 128 * d,), torch.float32)
+        wln = self.ws.get("ln", (2 * 512 * d,), torch.float32)
         wat = self.ws.get("attn", (B * H * T,), torch.float32)
         for i in reversed(range(L)):
             a = s["blocks"][i]
@@ -328,7 +328,7 @@ class BERTEngine:
     def train_loss_and_backward(self, tokens, labels, loss_out, global_count, grad, max_labelled=None):
         """Forward + CE(ignore_index=0) + backward of one batch.  loss_out[0] = loss sum, [1] = local
         labelled count, [2] = local mean; ``global_count(local)`` returns the divisor (DP)."""
-        xL, s = self.encode(tokens, True)
+        xL, s = self.encode(tokens, True, clone_seed=False)
         B, T = tokens.shape
         M, d = B * T, self.d
         cap = int(max_labelled or M)
@@ -353,7 +353,11 @@ class BERTEngine:
         ops.linear_wgrad(dl, hl, self.flat.view("out.weight", grad), slab, db=self.flat.view("out.bias", grad),
                          rows_dev=cnt)
         dhl = self.ws.get("dhl", (cap, d), self.dt)
-        ops.linear_dgrad(dl, self.W("out.weight"), dhl, rows_dev=cnt)
+        # contraction over the whole vocabulary with few rows: split-K (slabs + deterministic reduce)
+        sk = int(max(1, min(64, -(-self.V1 // 2048))))
+        slab_d = self.ws.get("slab_dh", (sk * cap * d,), torch.float32)
+        acc = self.ws.get("dhl_f32", (cap, d), torch.float32) if self.dt != torch.float32 else None
+        ops.linear_dgrad_splitk(dl, self.W("out.weight"), dhl, slab_d, sk, acc_f32=acc, rows_dev=cnt)
         dxL = self._buf((M, d))
         ops.scatter_rows(dhl, rank, dxL)
         self.encode_backward(s, dxL, grad)

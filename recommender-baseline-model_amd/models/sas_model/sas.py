@@ -170,13 +170,15 @@ class SASEngine:
         return torch.empty(shape, dtype=dtype or self.dt, device=self.dev)
 
     # ---- forward -------------------------------------------------------------------
-    def forward(self, ids, pos, neg, training, need_logits=True):
+    def forward(self, ids, pos, neg, training, need_logits=True, clone_seed=True):
         B, T = ids.shape
         M, d, H, Dh, L = B * T, self.d, self.H, self.Dh, self.L
         p = self.p if training else 0.0
         if p > 0:
             ops.seed_advance(self.seed_base)
-        sb = self.seed_base.clone()      # this step's masks, replayed by backward
+        # this step's masks, replayed by backward (the fused step runs backward before the next
+        # advance, so it reads the live word; the autograd API may interleave forwards: snapshot)
+        sb = self.seed_base.clone() if clone_seed else self.seed_base
         e = self._buf
         s = {"B": B, "T": T, "p": p, "ids": ids, "pos": pos, "neg": neg, "sb": sb,
              "x": [], "Q": [], "mu1": [], "r1": [], "q": [], "kv": [], "o": [], "lse": [],
@@ -231,7 +233,7 @@ class SASEngine:
         e = self._buf
         G = lambda n: self.flat.view(n, grad)  # noqa: E731
         slab = self.ws.get("slab", (ops.wgrad_slab_numel(M, 2 * d, d),), torch.float32)
-        wln = self.ws.get("ln", (2 * 128 * d,), torch.float32)
+        wln = self.ws.get("ln", (2 * 512 * d,), torch.float32)
         wat = self.ws.get("attn", (B * H * T,), torch.float32)
 
         df = e("df", (M, d))

@@ -74,6 +74,21 @@ def linear_dgrad(dY, W, dX, **epi_kw):
     gemm(dY, W, dX, M, K, N, False, True, epilogue(**epi_kw))
 
 
+def linear_dgrad_splitk(dY, W, dX, slab, splits, acc_f32=None, rows_dev=None):
+    """dX = dY W for a long contraction (dY [M,N] with N >> M, e.g. the vocabulary gradient):
+    split-K into fp32 slabs (rs_gemm with split_k) + one deterministic reduce (+ cast when dX is
+    bf16, through ``acc_f32`` [M,K] fp32)."""
+    M, N = dY.shape
+    K = W.shape[1]
+    assert slab.numel() >= splits * M * K
+    gemm(dY, W, slab, M, K, N, False, True, epilogue(rows_dev=rows_dev), split_k=splits, slab=slab)
+    out = dX if dX.dtype == torch.float32 else acc_f32
+    assert out is not None and out.is_contiguous() and out.shape == (M, K)
+    call("rs_reduce_slabs", ptr(slab), splits, M * K, ptr(out), 0, stream())
+    if out is not dX:
+        cast_bf16(out, dX)
+
+
 def split_for(M_tok, n_out, k_in):
     """Split-K factor of the weight-gradient GEMM: ~1024 blocks of 64x64 output tiles, >= 256 rows each."""
     tiles = -(-n_out // 64) * -(-k_in // 64)

@@ -75,17 +75,14 @@ class FusedTrainStep:
     def _divisor(self, local_count):
         """Divisor of the loss gradient: the local count (single device, = reference mean) or 1
         (DP: unnormalised; the optimizer divides by the all-reduced global count)."""
-        if self.dp:
-            return self.one
-        self.count.copy_(local_count)
-        return self.count
+        return self.one if self.dp else local_count
 
     def _compute(self, *batch):
         self.flat.grad.zero_()
         eng = self.engine
         if self.kind == "sas":
             seq, pos, neg = batch
-            pl, nl, saved = eng.forward(seq, pos, neg, True)
+            pl, nl, saved = eng.forward(seq, pos, neg, True, clone_seed=False)
             ws = eng.ws.get("bce", (3 * 256,), torch.float32)
             ops.bce_fwd(pl, nl, pos, ws, self.loss_out)
             div = self._divisor(self.loss_out[1:2])
@@ -110,7 +107,6 @@ class FusedTrainStep:
                       out=self.loss_val)
         else:
             self.opt.step()
-            self.loss_val.copy_(self.loss_out[2:3])
 
     # ---------------------------------------------------------------- one step
     def step(self, *batch):
@@ -119,7 +115,7 @@ class FusedTrainStep:
         self._compute(*batch)
         self._exchange()
         self._update()
-        return self.loss_val
+        return self.loss_val if self.dp else self.loss_out[2:3]
 
     # ---------------------------------------------------------------- HIP graphs
     def capture(self, *example_batch, warmup=2):
@@ -154,4 +150,4 @@ class FusedTrainStep:
         if self.dp:
             self._exchange()            # RCCL all-reduce, eager, on the current stream
             self.graphs[1].replay()
-        return self.loss_val
+        return self.loss_val if self.dp else self.loss_out[2:3]

@@ -86,7 +86,7 @@ def main():
     gam, bet = torch.ones(d, device=dev), torch.zeros(d, device=dev)
     mu, ri = torch.empty(M, device=dev), torch.empty(M, device=dev)
     rec("layernorm_fwd", timeit(lambda: ops.layernorm_fwd(x, gam, bet, 1e-8, y, mu, ri, 0), a.reps), 2 * mb)
-    ws = torch.empty(2 * 128 * d, device=dev)
+    ws = torch.empty(2 * 512 * d, device=dev)
     dg, dbt = torch.zeros(d, device=dev), torch.zeros(d, device=dev)
     rec("layernorm_bwd", timeit(lambda: ops.layernorm_bwd(x, y, gam, mu, ri, 1e-8, z, dg, dbt, ws, 0), a.reps),
         3 * mb)
