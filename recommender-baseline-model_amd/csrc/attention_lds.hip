@@ -47,6 +47,16 @@ struct AttnLdsArgs {
 };
 
 #define NEG_INF (-__builtin_inff())
+// 8 waves per workgroup (2 per SIMD): with ~7 tiles per workgroup every tile gets its own wave,
+// and a SIMD always has a second wave to issue while the first waits on LDS / exp / MFMA results
+#define NW 8
+#define NT (64 * NW)
+#define LOG2E 1.4426950408889634f
+#define LN2 0.6931471805599453f
+// softmax in the log2 domain: scores are scaled by scale*log2(e) once, exponentials are the raw
+// v_exp_f32 (2^x); the reference's -1e9 fill (applied after scaling) becomes -1e9*log2(e)
+#define MASK2 (-1e9f * LOG2E)
+__device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 template <int DH> struct Img { static constexpr int LD = DH + 16; };  // row stride (elements), +32 B pad
 
@@ -97,16 +107,16 @@ template <int DH>
 __device__ __forceinline__ void stage(bf16* img, const bf16* src, int64_t ld, int64_t T, int rows, int tid) {
   constexpr int CPR = DH / 8, LD = Img<DH>::LD, U = 8;
   const int n = rows * CPR;
-  for (int i0 = tid; i0 < n; i0 += 256 * U) {
+  for (int i0 = tid; i0 < n; i0 += NT * U) {
     bf16x8 v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int i = min(i0 + u * 256, n - 1);
+      const int i = min(i0 + u * NT, n - 1);
       v[u] = gload8(src, ld, i / CPR, T, (i % CPR) * 8);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int i = i0 + u * 256;
+      const int i = i0 + u * NT;
       if (i < n) *reinterpret_cast<bf16x8*>(img + (i / CPR) * LD + (i % CPR) * 8) = v[u];
     }
   }
@@ -114,7 +124,7 @@ __device__ __forceinline__ void stage(bf16* img, const bf16* src, int64_t ld, in
 
 // 1.0 where the key is masked by key padding (mask_kind 1), else 0; keys >= T are handled separately
 __device__ __forceinline__ void stage_keymask(float* km, const AttnLdsArgs& a, int64_t b, int rows, int tid) {
-  for (int i = tid; i < rows; i += 256)
+  for (int i = tid; i < rows; i += NT)
     km[i] = (a.mask_kind == 1 && i < a.T && a.ids[b * a.T + i] == 0) ? 1.f : 0.f;
 }
 
@@ -136,7 +146,7 @@ __device__ __forceinline__ int last_tile_of_split(int nq, int split, int nsplit)
 
 // ------------------------------------------------------------------ forward
 template <int DH>
-__global__ __launch_bounds__(256) void attn_fwd_lds_kernel(AttnLdsArgs a) {
+__global__ __launch_bounds__(NT) void attn_fwd_lds_kernel(AttnLdsArgs a) {
   constexpr int LD = Img<DH>::LD, KC = DH / 32, DT = DH / 16, NKT = 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
@@ -159,13 +169,15 @@ __global__ __launch_bounds__(256) void attn_fwd_lds_kernel(AttnLdsArgs a) {
   __syncthreads();
   const uint64_t seed = eff_seed(a.seed, a.seed_base);
 
-  for (int qt = split + wave * a.nsplit; qt < nq; qt += 4 * a.nsplit) {
+  for (int qt = split + wave * a.nsplit; qt < nq; qt += NW * a.nsplit) {
     const int q0 = qt * 16;
     const int64_t qrow = q0 + cl;  // this lane's query
     bf16x8 qf[KC];
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) qf[kc] = gload8(Qg, a.ldq, qrow, a.T, kc * 32 + 8 * g);
     const int nkt = a.mask_kind == 0 ? qt + 1 : nq;
+    const float sl2 = a.scale * LOG2E;
+    const int qi = q0 + cl;
     f32x4 s[NKT];
     float mx = NEG_INF;
 #pragma unroll
@@ -174,9 +186,17 @@ __global__ __launch_bounds__(256) void attn_fwd_lds_kernel(AttnLdsArgs a) {
       if (kt < nkt) {
 #pragma unroll
         for (int kc = 0; kc < KC; ++kc) s[kt] = mfma16(row_frag(Ks, LD, kt * 16 + cl, kc * 32 + 8 * g), qf[kc], s[kt]);
+        // per-element masking only where a tile can hold masked scores (wave-uniform test)
+        const bool need = a.mask_kind != 0 || kt == qt || kt * 16 + 16 > T;
+        const int kb = kt * 16 + 4 * g;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float x = masked(a, km, qrow, kt * 16 + 4 * g + r, s[kt][r] * a.scale);
+          float x = s[kt][r] * sl2;
+          if (need) {
+            const int k = kb + r;
+            if (k >= T || (a.mask_kind == 0 && k > qi)) x = NEG_INF;
+            else if (a.mask_kind == 1 && km[k] != 0.f) x = MASK2;
+          }
           s[kt][r] = x;
           mx = fmaxf(mx, x);
         }
@@ -190,7 +210,7 @@ __global__ __launch_bounds__(256) void attn_fwd_lds_kernel(AttnLdsArgs a) {
       if (kt < nkt) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = s[kt][r] == NEG_INF ? 0.f : __expf(s[kt][r] - mx);
+          const float e = ex2(s[kt][r] - mx);
           s[kt][r] = e;
           sm += e;
         }
@@ -199,27 +219,34 @@ __global__ __launch_bounds__(256) void attn_fwd_lds_kernel(AttnLdsArgs a) {
     sm += __shfl_xor(sm, 16, 64);
     sm += __shfl_xor(sm, 32, 64);
     const float inv = 1.f / sm;
-    if (g == 0 && qrow < a.T) a.lse[bh * a.T + qrow] = mx + __logf(sm);
-    // P^T (+ dropout), packed pairwise as the B operand of O^T = V^T P^T
+    if (g == 0 && qrow < a.T) a.lse[bh * a.T + qrow] = (mx + __builtin_amdgcn_logf(sm)) * LN2;
+    // P^T (+ dropout: one hash per pair of adjacent keys), packed pairwise as the B operand of O^T = V^T P^T
+    const uint32_t s32 = seed32(seed);
+    const uint32_t rowidx = (uint32_t)(((int)bh * T + qi) * T);
     f32x4 o[DT];
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int c = 0; c < NKT / 2; ++c) {
       if (2 * c < nkt) {
-        f32x4 p0 = s[2 * c], p1 = s[2 * c + 1];
+        f32x4 pp[2] = {s[2 * c], s[2 * c + 1]};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int64_t k0 = (2 * c) * 16 + 4 * g + r, k1 = k0 + 16;
-          float x0 = p0[r] * inv, x1 = (2 * c + 1 < nkt) ? p1[r] * inv : 0.f;
+        for (int hf = 0; hf < 2; ++hf) {
+          const int t = 2 * c + hf;
+          const float sc = t < nkt ? inv : 0.f;
           if (a.drop_p > 0.f) {
-            x0 *= drop_mul(a.drop_p, seed, (uint64_t)((bh * a.T + qrow) * a.T + k0));
-            x1 *= drop_mul(a.drop_p, seed, (uint64_t)((bh * a.T + qrow) * a.T + k1));
+            float m[4];
+            const uint32_t base = rowidx + (uint32_t)(t * 16 + 4 * g);
+            drop_mul2(a.drop_p, s32, base, m[0], m[1]);
+            drop_mul2(a.drop_p, s32, base + 2, m[2], m[3]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) pp[hf][r] *= sc * m[r];
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) pp[hf][r] *= sc;
           }
-          p0[r] = x0;
-          p1[r] = x1;
         }
-        const bf16x8 pb = pack8(p0, p1);
+        const bf16x8 pb = pack8(pp[0], pp[1]);
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) o[dt] = mfma16(tr_frag(Vs, LD, 32 * c, 16 * dt, lane), pb, o[dt]);
       }
@@ -238,7 +265,7 @@ __global__ __launch_bounds__(256) void attn_fwd_lds_kernel(AttnLdsArgs a) {
 
 // ------------------------------------------------------------------ backward: delta + dQ
 template <int DH>
-__global__ __launch_bounds__(256) void attn_bwd_dq_lds_kernel(AttnLdsArgs a) {
+__global__ __launch_bounds__(NT) void attn_bwd_dq_lds_kernel(AttnLdsArgs a) {
   constexpr int LD = Img<DH>::LD, KC = DH / 32, DT = DH / 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
@@ -261,7 +288,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_lds_kernel(AttnLdsArgs a) {
   const bf16* Og = a.o + b * a.T * a.ldo + h * DH;
   const bf16* dOg = a.dout + b * a.T * a.lddo + h * DH;
 
-  for (int qt = split + wave * a.nsplit; qt < nq; qt += 4 * a.nsplit) {
+  for (int qt = split + wave * a.nsplit; qt < nq; qt += NW * a.nsplit) {
     const int q0 = qt * 16;
     const int64_t qrow = q0 + cl;
     bf16x8 qf[KC], df[KC];
@@ -277,7 +304,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_lds_kernel(AttnLdsArgs a) {
     dl += __shfl_xor(dl, 16, 64);
     dl += __shfl_xor(dl, 32, 64);  // delta = rowsum(dO * O) for query qrow
     if (g == 0 && qrow < a.T) a.delta[bh * a.T + qrow] = dl;
-    const float lq = qrow < a.T ? a.lse[bh * a.T + qrow] : 0.f;
+    const float lq2 = (qrow < a.T ? a.lse[bh * a.T + qrow] : 0.f) * LOG2E;
+    const float sl2 = a.scale * LOG2E;
+    const int qi = q0 + cl;
+    const uint32_t s32 = seed32(seed);
+    const uint32_t rowidx = (uint32_t)(((int)bh * T + qi) * T);
+    const bool qok = qi < T;
     const int nkt = a.mask_kind == 0 ? qt + 1 : nq;
     f32x4 acc[DT];
 #pragma unroll
@@ -287,23 +319,31 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_lds_kernel(AttnLdsArgs a) {
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
         const int t = 2 * c + hf;
-        f32x4 s = (f32x4){0.f, 0.f, 0.f, 0.f}, dp = (f32x4){0.f, 0.f, 0.f, 0.f};
+        f32x4 sv = (f32x4){0.f, 0.f, 0.f, 0.f}, dp = (f32x4){0.f, 0.f, 0.f, 0.f};
         if (t < nkt) {
 #pragma unroll
           for (int kc = 0; kc < KC; ++kc) {
-            s = mfma16(row_frag(Ks, LD, t * 16 + cl, kc * 32 + 8 * g), qf[kc], s);
+            sv = mfma16(row_frag(Ks, LD, t * 16 + cl, kc * 32 + 8 * g), qf[kc], sv);
             dp = mfma16(row_frag(Vs, LD, t * 16 + cl, kc * 32 + 8 * g), df[kc], dp);
           }
         }
+        const bool need = a.mask_kind != 0 || t >= qt || t * 16 + 16 > T;
+        const int kb = t * 16 + 4 * g;
+        float m[4] = {1.f, 1.f, 1.f, 1.f};
+        if (a.drop_p > 0.f) {
+          drop_mul2(a.drop_p, s32, rowidx + (uint32_t)kb, m[0], m[1]);
+          drop_mul2(a.drop_p, s32, rowidx + (uint32_t)kb + 2, m[2], m[3]);
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int64_t key = t * 16 + 4 * g + r;
           // masked_fill has no gradient: dS = 0 on masked scores (-inf and -1e9 alike)
-          const bool live = t < nkt && qrow < a.T && mask_state(a, km, qrow, key) == 0;
-          const float p = live ? __expf(s[r] * a.scale - lq) : 0.f;
-          float dpe = dp[r];
-          if (a.drop_p > 0.f) dpe *= drop_mul(a.drop_p, seed, (uint64_t)((bh * a.T + qrow) * a.T + key));
-          ds2[hf][r] = live ? p * (dpe - dl) * a.scale : 0.f;
+          bool live = t < nkt && qok;
+          if (need) {
+            const int k = kb + r;
+            live = live && k < T && !(a.mask_kind == 0 && k > qi) && !(a.mask_kind == 1 && km[k] != 0.f);
+          }
+          const float p = ex2(sv[r] * sl2 - lq2);
+          ds2[hf][r] = live ? p * (dp[r] * m[r] - dl) * a.scale : 0.f;
         }
       }
       const bf16x8 bds = pack8(ds2[0], ds2[1]);
@@ -324,7 +364,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_lds_kernel(AttnLdsArgs a) {
 
 // ------------------------------------------------------------------ backward: dK, dV
 template <int DH>
-__global__ __launch_bounds__(256) void attn_bwd_dkv_lds_kernel(AttnLdsArgs a) {
+__global__ __launch_bounds__(NT) void attn_bwd_dkv_lds_kernel(AttnLdsArgs a) {
   constexpr int LD = Img<DH>::LD, KC = DH / 32, DT = DH / 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
@@ -342,8 +382,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_lds_kernel(AttnLdsArgs a) {
   float* km = dl_s + rows;
   stage<DH>(Qs, a.q + b * a.T * a.ldq + h * DH, a.ldq, a.T, rows, tid);
   stage<DH>(dOs, a.dout + b * a.T * a.lddo + h * DH, a.lddo, a.T, rows, tid);
-  for (int i = tid; i < rows; i += 256) {
-    lse_s[i] = i < T ? a.lse[bh * a.T + i] : 0.f;
+  for (int i = tid; i < rows; i += NT) {
+    lse_s[i] = i < T ? a.lse[bh * a.T + i] * LOG2E : 0.f;
     dl_s[i] = i < T ? a.delta[bh * a.T + i] : 0.f;
   }
   stage_keymask(km, a, b, rows, tid);
@@ -353,8 +393,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_lds_kernel(AttnLdsArgs a) {
   const bf16* Vg = a.v + b * a.T * a.ldv + h * DH;
   const int nqc = (T + 31) / 32;  // 32-query chunks
 
-  for (int kt = split + wave * a.nsplit; kt < nk; kt += 4 * a.nsplit) {
+  const float sl2 = a.scale * LOG2E;
+  for (int kt = split + wave * a.nsplit; kt < nk; kt += NW * a.nsplit) {
     const int64_t key = kt * 16 + cl;  // this lane's key
+    const int ki = kt * 16 + cl;
     bf16x8 kf[KC], vf[KC];
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
@@ -379,12 +421,18 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_lds_kernel(AttnLdsArgs a) {
           s = mfma16(row_frag(Qs, LD, t * 16 + cl, kc * 32 + 8 * g), kf[kc], s);
           dp = mfma16(row_frag(dOs, LD, t * 16 + cl, kc * 32 + 8 * g), vf[kc], dp);
         }
+        const bool need = a.mask_kind != 0 || t <= kt || t * 16 + 16 > T || kt * 16 + 16 > T;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int64_t qr = t * 16 + 4 * g + r;
-          const int st = qr < a.T ? mask_state(a, km, qr, key) : 1;
-          const float p = st == 1 ? 0.f : __expf(apply_mask(st, s[r] * a.scale) - lse_s[qr]);
-          const float m = a.drop_p > 0.f ? drop_mul(a.drop_p, seed, (uint64_t)((bh * a.T + qr) * a.T + key)) : 1.f;
+          const int qr = t * 16 + 4 * g + r;
+          int st = 0;   // 0 live, 1 -inf, 2 -1e9 fill
+          if (need) {
+            if (qr >= T || ki >= T || (a.mask_kind == 0 && ki > qr)) st = 1;
+            else if (a.mask_kind == 1 && km[ki] != 0.f) st = 2;
+          }
+          const float x2 = st == 0 ? s[r] * sl2 : MASK2;
+          const float p = st == 1 ? 0.f : ex2(x2 - lse_s[qr]);
+          const float m = a.drop_p > 0.f ? drop_mul(a.drop_p, seed, (uint64_t)(((int)bh * T + qr) * T + ki)) : 1.f;
           pd2[hf][r] = p * m;
           ds2[hf][r] = st == 0 ? p * (dp[r] * m - dl_s[qr]) * a.scale : 0.f;
         }
@@ -430,7 +478,7 @@ static size_t dkv_lds_bytes(int T) {
 static int pick_split(int64_t BH, int ntiles) {
   // aim for >= 256 workgroups (one per CU at T ~ 200), at least 2 tiles per wave group
   int s = 1;
-  while (BH * s < 256 && s * 2 <= std::max(1, ntiles / 4)) s *= 2;
+  while (BH * s < 256 && s * 2 <= std::max(1, ntiles / 4)) s *= 2;   // ~7 tiles per 8-wave group at T=200
   return s;
 }
 
@@ -447,7 +495,7 @@ static hipError_t fwd_t(AttnLdsArgs& a, hipStream_t s) {
   const int nq = (int)cdiv(a.T, 16);
   a.nsplit = pick_split(a.B * a.H, nq);
   const size_t lds = fwd_lds_bytes<DH>((int)a.T);
-  hipLaunchKernelGGL((attn_fwd_lds_kernel<DH>), dim3((unsigned)a.nsplit, (unsigned)(a.B * a.H)), dim3(256), lds, s,
+  hipLaunchKernelGGL((attn_fwd_lds_kernel<DH>), dim3((unsigned)a.nsplit, (unsigned)(a.B * a.H)), dim3(NT), lds, s,
                      a);
   return hipGetLastError();
 }
@@ -456,9 +504,9 @@ template <int DH>
 static hipError_t bwd_t(AttnLdsArgs& a, hipStream_t s) {
   const int nq = (int)cdiv(a.T, 16);
   a.nsplit = pick_split(a.B * a.H, nq);
-  hipLaunchKernelGGL((attn_bwd_dq_lds_kernel<DH>), dim3((unsigned)a.nsplit, (unsigned)(a.B * a.H)), dim3(256),
+  hipLaunchKernelGGL((attn_bwd_dq_lds_kernel<DH>), dim3((unsigned)a.nsplit, (unsigned)(a.B * a.H)), dim3(NT),
                      fwd_lds_bytes<DH>((int)a.T), s, a);
-  hipLaunchKernelGGL((attn_bwd_dkv_lds_kernel<DH>), dim3((unsigned)a.nsplit, (unsigned)(a.B * a.H)), dim3(256),
+  hipLaunchKernelGGL((attn_bwd_dkv_lds_kernel<DH>), dim3((unsigned)a.nsplit, (unsigned)(a.B * a.H)), dim3(NT),
                      dkv_lds_bytes<DH>((int)a.T), s, a);
   return hipGetLastError();
 }
