@@ -204,6 +204,27 @@ int rs_dropout_rowmask(int dtype, const void* x, int64_t M, int64_t N, int64_t l
 /* *seed_base += 1 on the stream (advances every dropout mask; capturable). */
 int rs_seed_advance(uint64_t* seed_base, void* stream);
 
+/* ---- fused SAS sublayers (bf16, d in {64, 128}; rowfused.hip) ----------------------------
+ * One workgroup per 64 token rows, activations kept in LDS.  Same outputs, saved tensors and
+ * dropout masks as the unfused kernel sequence, so rs_* backward kernels consume them unchanged.
+ *
+ * Replaces, for SASRec block i (BS/models/sas_model/sas.py:73-76, the attention input side):
+ *   Q = LN1(x) [mean/rstd saved];  q = Q Wq^T + bq;  kv = x Wkv^T + bkv   (kv: [M][2d])
+ * Wq = in_proj_weight[:d], Wkv = in_proj_weight[d:] (bf16, torch [out][in] layout).
+ * Returns RS_ERR_UNSUPPORTED for other d: callers fall back to the unfused sequence. */
+int rs_sas_block_in(int64_t M, int64_t d, const void* x, int64_t ldx, const float* ln_w, const float* ln_b,
+                    float eps, void* Q, float* mean, float* rstd, const void* Wq, const float* bq, void* q,
+                    const void* Wkv, const float* bkv, void* kv, void* stream);
+/* The output side (sas.py:75-84, PointWiseFeedForward sas.py:8-24):
+ *   x1 = Q + o Wo^T + bo;  z = LN2(x1);  h1 = relu(drop(z W1^T + b1, salt1));
+ *   xn = (drop(h1 W2^T + b2, salt2) + z) * (ids != 0)
+ * Dropout element index m*d + n, seeds eff_seed(salt, *seed_base) as rs_gemm's epilogue. */
+int rs_sas_block_out(int64_t M, int64_t d, const void* o, const void* Q, const void* Wo, const float* bo, void* x1,
+                     const float* ln_w, const float* ln_b, float eps, void* z, float* mean, float* rstd,
+                     const void* W1, const float* b1, void* h1, const void* W2, const float* b2, void* xn,
+                     const int64_t* ids, float drop_p, uint64_t salt1, uint64_t salt2, const uint64_t* seed_base,
+                     void* stream);
+
 /* ABI version of this header/library pair. */
 int rs_abi_version(void);
 

@@ -61,6 +61,9 @@ SIGNATURES = {
     "rs_cast_bf16": [i64, vp, vp, vp],
     "rs_dropout_rowmask": [i32, vp, i64, i64, i64, f32, u64, vp, i64, vp, vp, vp, vp],
     "rs_seed_advance": [vp, vp],
+    "rs_sas_block_in": [i64, i64, vp, i64, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
+    "rs_sas_block_out": [i64, i64, vp, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32,
+                         u64, u64, vp, vp],
     "rs_abi_version": [],
 }
 

@@ -148,8 +148,8 @@ __device__ __forceinline__ void epi8(const GemmArgs& a, int64_t m, int64_t n, fl
     else if (e.act == 2) x = gelu_tanh(x);
     else if (e.act == 3) x = auxv[j] > 0.f ? x : 0.f;
     else if (e.act == 4) x *= gelu_tanh_grad(auxv[j]);
-    if (e.drop_p > 0.f) x *= drop_mul(e.drop_p, s1, (uint64_t)(m * e.drop_ld + n + j));
-    if (res) x += resv[j];
+    const float dmj = e.drop_p > 0.f ? drop_mul(e.drop_p, s1, (uint64_t)(m * e.drop_ld + n + j)) : 1.0f;
+    x = res ? __builtin_fmaf(x, dmj, resv[j]) : x * dmj;
     if (!rowkeep) x = 0.f;
     if (e.post_drop_p > 0.f) x *= drop_mul(e.post_drop_p, s2, (uint64_t)(m * e.drop_ld + n + j));
     v[j] = x;
@@ -230,8 +230,9 @@ __device__ __forceinline__ void epi8_t(const GemmArgs& a, int64_t m, int64_t n, 
     if constexpr (ACT == 2) x = gelu_tanh(x);
     if constexpr (ACT == 3) x = auxv[j] > 0.f ? x : 0.f;
     if constexpr (ACT == 4) x *= gelu_tanh_grad(auxv[j]);
-    if constexpr ((EC & ED) != 0) x *= dm[j];
-    if constexpr ((EC & ER) != 0) x += resv[j];
+    if constexpr ((EC & ED) != 0 && (EC & ER) != 0) x = __builtin_fmaf(x, dm[j], resv[j]);  // one rounding
+    else if constexpr ((EC & ED) != 0) x *= dm[j];
+    else if constexpr ((EC & ER) != 0) x += resv[j];
     if constexpr ((EC & EM) != 0) x = keep ? x : 0.f;
     if constexpr ((EC & EP) != 0) x *= pm[j];
     v[j] = x;

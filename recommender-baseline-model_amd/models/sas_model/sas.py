@@ -186,31 +186,44 @@ class SASEngine:
         x = e("x0", (M, d))
         ops.embed_fwd(0, ids, T, self.W("item_emb.weight"), self.W("pos_emb.weight"), math.sqrt(d), p,
                       self.salt["emb"], sb, x)
+        fused = ops.sas_block_fused_ok(d, self.dt)
         for i in range(L):
             pre = f"attention_layers.{i}."
             Q, mu1, r1 = e("Q", (M, d)), e("mu", (M,), torch.float32), e("r", (M,), torch.float32)
-            ops.layernorm_fwd(x, self.Wf(f"attention_layernorms.{i}.weight"),
-                              self.Wf(f"attention_layernorms.{i}.bias"), LN_EPS, Q, mu1, r1, 0)
             Win, bin_ = self.W(pre + "in_proj_weight"), self.Wf(pre + "in_proj_bias")
             q, kv = e("q", (M, d)), e("kv", (M, 2 * d))
-            ops.linear_fwd(Q, Win[:d], q, bias=bin_[:d])
-            ops.linear_fwd(x, Win[d:], kv, bias=bin_[d:])
             o, lse = e("o", (M, d)), e("lse", (B * H * T,), torch.float32)
-            ops.attn_fwd(B, T, H, Dh, q, kv[:, :d], kv[:, d:], o, lse, 1.0 / math.sqrt(Dh), 0, ids, p,
-                         self.salt[f"attn{i}"], sb)
             x1 = e("x1", (M, d))
-            ops.linear_fwd(o, self.W(pre + "out_proj.weight"), x1, bias=self.Wf(pre + "out_proj.bias"), resid=Q)
             z, mu2, r2 = e("z", (M, d)), e("mu", (M,), torch.float32), e("r", (M,), torch.float32)
-            ops.layernorm_fwd(x1, self.Wf(f"forward_layernorms.{i}.weight"),
-                              self.Wf(f"forward_layernorms.{i}.bias"), LN_EPS, z, mu2, r2, 0)
             fw = f"forward_layers.{i}."
-            h1 = e("h1", (M, d))
-            ops.linear_fwd(z, self.W(fw + "conv1.weight").view(d, d), h1, bias=self.Wf(fw + "conv1.bias"),
-                           act=ops.ACT_RELU, drop_p=p, drop_seed=self.salt[f"ffn1_{i}"], seed_base=sb, drop_ld=d)
-            xn = e("x", (M, d))
-            ops.linear_fwd(h1, self.W(fw + "conv2.weight").view(d, d), xn, bias=self.Wf(fw + "conv2.bias"),
-                           drop_p=p, drop_seed=self.salt[f"ffn2_{i}"], seed_base=sb, drop_ld=d, resid=z,
-                           rowmask_ids=ids)
+            h1, xn = e("h1", (M, d)), e("x", (M, d))
+            if fused:
+                # one row-block kernel on each side of the attention core (rowfused.hip)
+                ops.sas_block_in(x, self.Wf(f"attention_layernorms.{i}.weight"),
+                                 self.Wf(f"attention_layernorms.{i}.bias"), LN_EPS, Q, mu1, r1, Win[:d], bin_[:d], q,
+                                 Win[d:], bin_[d:], kv)
+                ops.attn_fwd(B, T, H, Dh, q, kv[:, :d], kv[:, d:], o, lse, 1.0 / math.sqrt(Dh), 0, ids, p,
+                             self.salt[f"attn{i}"], sb)
+                ops.sas_block_out(o, Q, self.W(pre + "out_proj.weight"), self.Wf(pre + "out_proj.bias"), x1,
+                                  self.Wf(f"forward_layernorms.{i}.weight"), self.Wf(f"forward_layernorms.{i}.bias"),
+                                  LN_EPS, z, mu2, r2, self.W(fw + "conv1.weight"), self.Wf(fw + "conv1.bias"), h1,
+                                  self.W(fw + "conv2.weight"), self.Wf(fw + "conv2.bias"), xn, ids, p,
+                                  self.salt[f"ffn1_{i}"], self.salt[f"ffn2_{i}"], sb)
+            else:
+                ops.layernorm_fwd(x, self.Wf(f"attention_layernorms.{i}.weight"),
+                                  self.Wf(f"attention_layernorms.{i}.bias"), LN_EPS, Q, mu1, r1, 0)
+                ops.linear_fwd(Q, Win[:d], q, bias=bin_[:d])
+                ops.linear_fwd(x, Win[d:], kv, bias=bin_[d:])
+                ops.attn_fwd(B, T, H, Dh, q, kv[:, :d], kv[:, d:], o, lse, 1.0 / math.sqrt(Dh), 0, ids, p,
+                             self.salt[f"attn{i}"], sb)
+                ops.linear_fwd(o, self.W(pre + "out_proj.weight"), x1, bias=self.Wf(pre + "out_proj.bias"), resid=Q)
+                ops.layernorm_fwd(x1, self.Wf(f"forward_layernorms.{i}.weight"),
+                                  self.Wf(f"forward_layernorms.{i}.bias"), LN_EPS, z, mu2, r2, 0)
+                ops.linear_fwd(z, self.W(fw + "conv1.weight").view(d, d), h1, bias=self.Wf(fw + "conv1.bias"),
+                               act=ops.ACT_RELU, drop_p=p, drop_seed=self.salt[f"ffn1_{i}"], seed_base=sb, drop_ld=d)
+                ops.linear_fwd(h1, self.W(fw + "conv2.weight").view(d, d), xn, bias=self.Wf(fw + "conv2.bias"),
+                               drop_p=p, drop_seed=self.salt[f"ffn2_{i}"], seed_base=sb, drop_ld=d, resid=z,
+                               rowmask_ids=ids)
             for k_, v_ in (("x", x), ("Q", Q), ("mu1", mu1), ("r1", r1), ("q", q), ("kv", kv), ("o", o),
                            ("lse", lse), ("x1", x1), ("z", z), ("mu2", mu2), ("r2", r2), ("h1", h1)):
                 s[k_].append(v_)

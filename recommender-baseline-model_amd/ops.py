@@ -5,6 +5,7 @@ nothing; outputs are caller-allocated tensors (the C ABI allocates nothing).
 2-D tensors are passed with their row stride as the leading dimension.
 """
 import ctypes as C
+import os
 
 import torch
 
@@ -220,3 +221,23 @@ def dropout_rowmask(x, drop_p, seed, seed_base, rowmask_ids, out, out_masked=Non
 
 def seed_advance(seed_base):
     call("rs_seed_advance", ptr(seed_base), stream())
+
+
+# ---- fused SAS sublayers (rowfused.hip) ----------------------------------------------------
+def sas_block_fused_ok(d, dtype):
+    """rs_sas_block_in/out cover bf16 with d in {64, 128}; anything else runs the unfused kernels."""
+    return dtype == torch.bfloat16 and d in (64, 128) and os.environ.get("RS_SAS_UNFUSED", "0") != "1"
+
+
+def sas_block_in(x, ln_w, ln_b, eps, Q, mean, rstd, Wq, bq, q, Wkv, bkv, kv):
+    M, d = x.shape
+    call("rs_sas_block_in", M, d, ptr(x), ld(x), ptr(ln_w), ptr(ln_b), eps, ptr(Q), ptr(mean), ptr(rstd),
+         ptr(Wq), ptr(bq), ptr(q), ptr(Wkv), ptr(bkv), ptr(kv), stream())
+
+
+def sas_block_out(o, Q, Wo, bo, x1, ln_w, ln_b, eps, z, mean, rstd, W1, b1, h1, W2, b2, xn, ids, drop_p,
+                  salt1, salt2, seed_base):
+    M, d = o.shape
+    call("rs_sas_block_out", M, d, ptr(o), ptr(Q), ptr(Wo), ptr(bo), ptr(x1), ptr(ln_w), ptr(ln_b), eps, ptr(z),
+         ptr(mean), ptr(rstd), ptr(W1), ptr(b1), ptr(h1), ptr(W2), ptr(b2), ptr(xn), ptr(ids), drop_p, salt1,
+         salt2, ptr(seed_base), stream())

@@ -141,3 +141,39 @@ def test_sas_all_padding_rows_and_zero_negatives():
     ref = {k: g64[k].numpy() for k in grads}
     scale = max(np.linalg.norm(v) for v in ref.values())
     check_grads(grads, ref, d, GRAD_TOL_F32, scale)
+
+
+@pytest.mark.parametrize("V,T,d,L,h,B", [(500, 37, 64, 2, 2, 3), (400, 200, 128, 2, 1, 5), (300, 50, 128, 1, 4, 2)])
+def test_sas_fused_block_matches_unfused(V, T, d, L, h, B, monkeypatch):
+    """rowfused.hip (rs_sas_block_in/out) against the unfused kernel sequence: same saved tensors,
+    dropout masks and logits (training mode, p=0.2, ragged last row block), same gradients."""
+    import rbm_amd  # noqa: F401
+    import rbm_amd.data as synth
+    from rbm_amd import ops
+    from rbm_amd.models import model_factory
+    torch.manual_seed(V)
+    m = model_factory(sas_args(V, T, d, L, h, p=0.2, dtype="bf16"))
+    eng = m.sas.engine()
+    eng.sync_compute_weights()
+    rng = np.random.default_rng(T)
+    seq, pos, neg = (torch.from_numpy(a).cuda() for a in synth.sas_batch(rng, B, T, V))
+    seq[0, :5] = 0                                          # padding rows hit the timeline mask
+    runs = []
+    for unfused in ("0", "1"):
+        monkeypatch.setenv("RS_SAS_UNFUSED", unfused)
+        assert ops.sas_block_fused_ok(d, torch.bfloat16) == (unfused == "0")
+        eng.seed_base.fill_(41)
+        pl, nl, s = eng.forward(seq, pos, neg, True)
+        grad = torch.zeros(eng.flat.numel, dtype=torch.float32, device="cuda")
+        eng.backward(s, torch.ones_like(pl) / pl.numel(), -torch.ones_like(nl) / nl.numel(), grad)
+        torch.cuda.synchronize()
+        runs.append((pl.clone(), nl.clone(), {k: [t.clone() for t in s[k]] for k in
+                                              ("x", "Q", "mu1", "r1", "q", "kv", "x1", "z", "mu2", "r2", "h1")},
+                     s["xL"].clone(), grad))
+    (pa, na, sa, xa, ga), (pb, nb, sb, xb, gb) = runs
+    bad = [(k, i, int((u != v).sum().item()), (u.float() - v.float()).abs().max().item())
+           for k in sa for i, (u, v) in enumerate(zip(sa[k], sb[k])) if not torch.equal(u, v)]
+    assert not bad, bad
+    assert torch.equal(xa, xb) and torch.equal(pa, pb) and torch.equal(na, nb)
+    assert rel(ga.cpu().numpy(), gb.cpu().numpy()) < 1e-5     # embedding grads use fp32 atomics
+    assert (sa["h1"][0] == 0).float().mean().item() > 0.5 * 0.2   # relu + dropout zeros present
