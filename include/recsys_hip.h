@@ -225,6 +225,57 @@ int rs_sas_block_out(int64_t M, int64_t d, const void* o, const void* Q, const v
                      const int64_t* ids, float drop_p, uint64_t salt1, uint64_t salt2, const uint64_t* seed_base,
                      void* stream);
 
+/* Backward of rs_sas_block_out (sas.py:75-84 reversed), one 64-row block per workgroup:
+ *   dzres = dxn*(ids!=0); dy2 = drop2(dzres) [out]; da1 = relu'(h1)*drop1(dy2 W2) [out];
+ *   dz = da1 W1 + dzres; dx1 = LN2'(x1, dz) [out]; dout = dx1 Wo [out];
+ *   part[b][0][:] / part[b][1][:] = LN2 dgamma / dbeta partials of 64-row block b (part >= 2*d*ceil(M/64)
+ *   floats; sum them with rs_reduce_segments / rs_wgrad_grouped: stride 2d, splits ceil(M/64)).
+ *   W*T are bf16 TRANSPOSED weights ([in][out], rs_transpose_bf16).
+ * Replaces rs_dropout_rowmask + 3 rs_gemm dgrads + rs_layernorm_bwd of the unfused sequence. */
+int rs_sas_block_out_bwd(int64_t M, int64_t d, const void* dxn, const int64_t* ids, const void* h1, const void* x1,
+                         const float* mean2, const float* rstd2, const float* ln_w, const void* W2T, const void* W1T,
+                         const void* WoT, void* dy2, void* da1, void* dx1, void* dout, float* part, float drop_p,
+                         uint64_t salt1, uint64_t salt2, const uint64_t* seed_base, void* stream);
+/* Backward of rs_sas_block_in (sas.py:73-76 reversed):
+ *   dQ = dq Wq + dx1;  dx = dk Wk + dv Wv + LN1'(x, dQ) [out];  LN1 affine partials -> part (as above).
+ * WinT = in_proj_weight^T ([d][3d] bf16). */
+int rs_sas_block_in_bwd(int64_t M, int64_t d, const void* dq, const void* dkv, const void* dx1, const void* x,
+                        const float* mean1, const float* rstd1, const float* ln_w, const void* WinT, void* dx,
+                        float* part, void* stream);
+/* Batched bf16 transpose: for m < nmat, desc[6m..6m+5] = {rows, cols, src_off, lds, dst_off, ldd}
+ * (elements): dst[dst_off + c*ldd + r] = src[src_off + r*lds + c].  Grid x = max_tiles >= the
+ * largest ceil(rows/64)*ceil(cols/64). */
+int rs_transpose_bf16(int64_t nmat, const int64_t* desc, int64_t max_tiles, const void* src, void* dst,
+                      void* stream);
+
+/* ---- grouped weight gradients (wgrad.hip) ---------------------------------------------------
+ * Every Linear / Conv1d(k=1) weight gradient of a backward pass, dW[N][K] += dY^T X and
+ * db[N] += colsum(dY) over the M token rows (the autograd accumulation of nn.Linear's backward,
+ * BS/models/sas_model/sas.py:8-24,67-84; bert_modules/*), in ONE GEMM launch (problems x output
+ * tiles x row splits) followed by ONE deterministic grouped reduction of the split partials.
+ * bf16 dY/X (16-byte aligned, ld % 8 == 0), fp32 dW/db accumulated; N, K multiples of 64. */
+typedef struct {
+  const void* dY; int64_t lddy;   /* [M][N] bf16 */
+  const void* X;  int64_t ldx;    /* [M][K] bf16 */
+  int64_t N, K;
+  float* dW;                      /* [N][K] fp32, += */
+  float* db;                      /* [N] fp32, += (or NULL) */
+} rs_wgrad_problem;
+/* A partial-sum set: out[i] (+)= sum_{z < splits} src[z*stride + i], i < n (n, stride multiples
+ * of 4; src/out 16-byte aligned). */
+typedef struct {
+  const float* src; int64_t stride; int64_t splits; int64_t n; float* out;
+} rs_reduce_segment;
+/* slab floats needed by rs_wgrad_grouped for these problems (splits = ceil(M / rows_per_split)). */
+int64_t rs_wgrad_grouped_slab_numel(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_t rows_per_split);
+/* nprob <= 16 problems; rows_per_split % 64 == 0; the extra segments (<= 64, e.g. LayerNorm
+ * affine partials from rs_sas_block_*_bwd) are summed into their outputs (+=) by the same
+ * reduction launch.  Returns RS_ERR_UNSUPPORTED for shapes outside the contract. */
+int rs_wgrad_grouped(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_t rows_per_split, float* slab,
+                     int64_t slab_numel, int nextra, const rs_reduce_segment* extra, void* stream);
+/* The reduction alone: out (+)= sum over splits, for nseg segments (any number, 64 per launch). */
+int rs_reduce_segments(int nseg, const rs_reduce_segment* segs, int accumulate, void* stream);
+
 /* ABI version of this header/library pair. */
 int rs_abi_version(void);
 

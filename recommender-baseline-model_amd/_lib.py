@@ -31,6 +31,16 @@ class Epilogue(C.Structure):
     ]
 
 
+class WgradProblem(C.Structure):
+    """Mirror of ``rs_wgrad_problem``."""
+    _fields_ = [("dY", vp), ("lddy", i64), ("X", vp), ("ldx", i64), ("N", i64), ("K", i64), ("dW", vp), ("db", vp)]
+
+
+class ReduceSegment(C.Structure):
+    """Mirror of ``rs_reduce_segment``."""
+    _fields_ = [("src", vp), ("stride", i64), ("splits", i64), ("n", i64), ("out", vp)]
+
+
 ACT_NONE, ACT_RELU, ACT_GELU, ACT_RELU_BWD, ACT_GELU_BWD = 0, 1, 2, 3, 4
 
 # name -> argtypes (all return int)
@@ -64,8 +74,17 @@ SIGNATURES = {
     "rs_sas_block_in": [i64, i64, vp, i64, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "rs_sas_block_out": [i64, i64, vp, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32,
                          u64, u64, vp, vp],
+    "rs_sas_block_out_bwd": [i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32, u64, u64,
+                             vp, vp],
+    "rs_sas_block_in_bwd": [i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
+    "rs_wgrad_grouped": [i32, C.POINTER(WgradProblem), i64, i64, vp, i64, i32, C.POINTER(ReduceSegment), vp],
+    "rs_reduce_segments": [i32, C.POINTER(ReduceSegment), i32, vp],
+    "rs_wgrad_grouped_slab_numel": [i32, C.POINTER(WgradProblem), i64, i64],
+    "rs_transpose_bf16": [i64, vp, i64, vp, vp, vp],
     "rs_abi_version": [],
 }
+
+RESTYPES = {"rs_wgrad_grouped_slab_numel": C.c_int64}
 
 _lib = None
 
@@ -82,7 +101,7 @@ def lib():
         for name, argt in SIGNATURES.items():
             fn = getattr(h, name)
             fn.argtypes = argt
-            fn.restype = C.c_int
+            fn.restype = RESTYPES.get(name, C.c_int)
         _lib = h
     return _lib
 

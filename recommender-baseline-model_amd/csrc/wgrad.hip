@@ -1,0 +1,298 @@
+// Grouped weight-gradient GEMMs + grouped slab reduction (bf16 operands, fp32 results).
+//
+// In a SASRec / BERT4Rec backward every Linear / Conv1d(k=1) weight gradient is
+//   dW[N][K] += sum_m dY[m][n] X[m][k],   db[N] += sum_m dY[m][n]
+// with M = B*T token rows (25.6k at the headline shape) and N, K = d or 2d (<= 256): a tall-skinny
+// reduction whose output is tiny.  One launch per weight (the generic split-K GEMM + a reduce
+// launch each) is latency-bound: every workgroup runs a handful of 64-row stages between a cold
+// prologue and a slab epilogue.  Here ALL weight gradients of the backward pass run in ONE launch
+// (problems x output tiles x row splits workgroups, each streaming its row range through
+// double-buffered LDS stages and MFMA-accumulating a whole 64x64 / 128x128 output tile), and ALL
+// their split partials -- plus any extra partial sets such as the LayerNorm affine partials the
+// fused row-block kernels leave -- are summed by ONE deterministic grouped reduction.
+//
+// Bias gradients ride on the same MFMAs (dY^T against a ones operand) in the k-tile-0 blocks.
+#include "gemm_bf16_impl.h"
+
+namespace wg {
+
+typedef __bf16 bf16;
+constexpr int MAXP = 16;
+
+struct Prob {
+  const bf16* dY;
+  const bf16* X;
+  int64_t lddy, ldx;
+  int N, K, tiles_k, tile0;    // tile0: first global tile index of this problem
+  int64_t slab_off;            // float offset of split 0; split stride = N*K + N
+};
+
+struct Args {
+  Prob p[MAXP];
+  int nprob, ntiles, splits, rows_per_split;
+  int64_t M;
+  float* slab;
+};
+
+template <int T>
+__global__ __launch_bounds__(256) void wgrad_group_kernel(Args a) {
+  using I = gbf::Img<true, T>;          // k-major stage image [64 rows][T + 8]
+  constexpr int STAGE = 2 * I::ELEMS;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * STAGE];
+  constexpr int BKT = gbf::BKT;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
+  constexpr int FM = T / 32, FN = T / 32;
+
+  const int t = (int)(blockIdx.x % (unsigned)a.ntiles);
+  const int s = (int)(blockIdx.x / (unsigned)a.ntiles);
+  int pi = 0;
+#pragma unroll 1
+  for (int q = 1; q < a.nprob; ++q)
+    if (t >= a.p[q].tile0) pi = q;
+  const Prob& P = a.p[pi];
+  const int lt = t - P.tile0;
+  const int tn = lt / P.tiles_k, tk = lt - tn * P.tiles_k;
+  const int64_t n0 = (int64_t)tn * T, c0 = (int64_t)tk * T;
+  const int64_t kbeg = (int64_t)s * a.rows_per_split;
+  const int64_t kend = min(a.M, kbeg + a.rows_per_split);
+  const int nk = kend > kbeg ? (int)((kend - kbeg + BKT - 1) / BKT) : 0;
+  const bool do_colsum = tk == 0 && wn == 0;
+
+  f32x4 acc[FM][FN], accb[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    accb[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
+
+  gbf::Stage<true, T> sa, sb;
+  sa.tid_ = tid;
+  sb.tid_ = tid;
+  const bool interior = ((kend - kbeg) % BKT) == 0;
+  auto kloop = [&](auto edge_tag) {
+    constexpr bool EDGE = decltype(edge_tag)::value;
+    auto issue = [&](int64_t k0) {
+      if (!EDGE) {
+        sa.load_next();
+        sb.load_next();
+        return;
+      }
+      sa.load_checked(P.dY, P.lddy, k0, n0, kend, P.N, tid);
+      sb.load_checked(P.X, P.ldx, k0, c0, kend, P.K, tid);
+    };
+    if (!EDGE) {
+      sa.init(P.dY, P.lddy, kbeg, n0, tid);
+      sb.init(P.X, P.ldx, kbeg, c0, tid);
+    }
+    issue(kbeg);
+    sa.store(smem, tid);
+    sb.store(smem + I::ELEMS, tid);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const bf16* cur = smem + (kt & 1) * STAGE;
+      const bool more = kt + 1 < nk;
+      if (more) issue(kbeg + (int64_t)(kt + 1) * BKT);
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        bf16x8 fa[FM], fb[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) fa[i] = gbf::frag<true, T>(cur, wm * (T / 2) + 16 * i, ss, lane);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) fb[j] = gbf::frag<true, T>(cur + I::ELEMS, wn * (T / 2) + 16 * j, ss, lane);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        if (do_colsum) {
+#pragma unroll
+          for (int i = 0; i < FM; ++i) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], ones, accb[i], 0, 0, 0);
+        }
+      }
+      if (more) {
+        bf16* nxt = smem + ((kt + 1) & 1) * STAGE;
+        sa.store(nxt, tid);
+        sb.store(nxt + I::ELEMS, tid);
+      }
+      __syncthreads();
+    }
+  };
+  if (nk > 0) {
+    if (interior) kloop(std::integral_constant<bool, false>{});
+    else kloop(std::integral_constant<bool, true>{});
+  }
+
+  // split partial -> slab (each 16-lane group stores 64 contiguous bytes per row)
+  float* S = a.slab + P.slab_off + (int64_t)s * ((int64_t)P.N * P.K + P.N);
+  const int g = lane >> 4, cl = lane & 15;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t n = n0 + wm * (T / 2) + 16 * i + 4 * g + r;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) S[n * P.K + c0 + wn * (T / 2) + 16 * j + cl] = acc[i][j][r];
+      if (do_colsum && cl == 0) S[(int64_t)P.N * P.K + n] = accb[i][r];
+    }
+}
+
+// ---------------------------------------------------------------- grouped slab reduction
+constexpr int MAXS = 64;
+struct Seg {
+  const float* src;   // split z at src + z*stride
+  int64_t stride;
+  int splits, n;      // n floats (multiple of 4, 16-byte aligned src/out)
+  float* out;
+};
+struct RArgs {
+  Seg s[MAXS];
+  int blk0[MAXS + 1];
+  int nseg, accumulate;
+};
+
+// block = 16 float4 columns x 16 split groups; group g sums splits g, g+16, ... ; fixed-order
+// combine in LDS (deterministic)
+__global__ __launch_bounds__(256) void reduce_segments_kernel(RArgs a) {
+  constexpr int C = 16, G = 16;
+  const int b = blockIdx.x;
+  int si = 0;
+#pragma unroll 1
+  for (int q = 1; q < a.nseg; ++q)
+    if (b >= a.blk0[q]) si = q;
+  const Seg& S = a.s[si];
+  const int col = threadIdx.x % C, grp = threadIdx.x / C;
+  const int64_t i4 = (int64_t)(b - a.blk0[si]) * C + col;
+  const int64_t n4 = S.n / 4;
+  const float4* src = reinterpret_cast<const float4*>(S.src);
+  const int64_t st4 = S.stride / 4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i4 < n4) {
+    int z = grp;
+    for (; z + 3 * G < S.splits; z += 4 * G) {
+      const float4 u0 = src[(int64_t)z * st4 + i4];
+      const float4 u1 = src[(int64_t)(z + G) * st4 + i4];
+      const float4 u2 = src[(int64_t)(z + 2 * G) * st4 + i4];
+      const float4 u3 = src[(int64_t)(z + 3 * G) * st4 + i4];
+      acc.x += u0.x; acc.y += u0.y; acc.z += u0.z; acc.w += u0.w;
+      acc.x += u1.x; acc.y += u1.y; acc.z += u1.z; acc.w += u1.w;
+      acc.x += u2.x; acc.y += u2.y; acc.z += u2.z; acc.w += u2.w;
+      acc.x += u3.x; acc.y += u3.y; acc.z += u3.z; acc.w += u3.w;
+    }
+    for (; z < S.splits; z += G) {
+      const float4 u = src[(int64_t)z * st4 + i4];
+      acc.x += u.x; acc.y += u.y; acc.z += u.z; acc.w += u.w;
+    }
+  }
+  __shared__ float4 red[G][C];
+  red[grp][col] = acc;
+  __syncthreads();
+  if (grp == 0 && i4 < n4) {
+    float4 tot = red[0][col];
+#pragma unroll
+    for (int q = 1; q < G; ++q) {
+      const float4 u = red[q][col];
+      tot.x += u.x; tot.y += u.y; tot.z += u.z; tot.w += u.w;
+    }
+    float4* o = reinterpret_cast<float4*>(S.out) + i4;
+    if (a.accumulate) {
+      const float4 p = *o;
+      tot.x += p.x; tot.y += p.y; tot.z += p.z; tot.w += p.w;
+    }
+    *o = tot;
+  }
+}
+
+}  // namespace wg
+
+static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+static int launch_segments(int nseg, const rs_reduce_segment* segs, int accumulate, hipStream_t s) {
+  if (nseg <= 0) return 0;
+  for (int base = 0; base < nseg; base += wg::MAXS) {
+    wg::RArgs ra{};
+    ra.nseg = min(wg::MAXS, nseg - base);
+    ra.accumulate = accumulate;
+    int blk = 0;
+    for (int q = 0; q < ra.nseg; ++q) {
+      const rs_reduce_segment& g = segs[base + q];
+      if (g.n <= 0 || g.n % 4 || g.stride % 4 || g.splits < 1 || !al16(g.src) || !al16(g.out)) return RS_ERR_ARG;
+      ra.s[q] = {g.src, g.stride, (int)g.splits, (int)g.n, g.out};
+      ra.blk0[q] = blk;
+      blk += (int)cdiv(g.n / 4, 16);
+    }
+    ra.blk0[ra.nseg] = blk;
+    hipLaunchKernelGGL(wg::reduce_segments_kernel, dim3((unsigned)blk), dim3(256), 0, s, ra);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+  }
+  return 0;
+}
+
+extern "C" {
+
+int64_t rs_wgrad_grouped_slab_numel(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_t rows_per_split) {
+  if (nprob <= 0 || M <= 0 || rows_per_split <= 0) return -1;
+  const int64_t splits = cdiv(M, rows_per_split);
+  int64_t tot = 0;
+  for (int q = 0; q < nprob; ++q) tot += splits * (probs[q].N * probs[q].K + probs[q].N);
+  return tot;
+}
+
+int rs_reduce_segments(int nseg, const rs_reduce_segment* segs, int accumulate, void* stream) {
+  return launch_segments(nseg, segs, accumulate, (hipStream_t)stream);
+}
+
+int rs_wgrad_grouped(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_t rows_per_split, float* slab,
+                     int64_t slab_numel, int nextra, const rs_reduce_segment* extra, void* stream) {
+  if (nprob <= 0 || nprob > wg::MAXP || M <= 0 || rows_per_split <= 0 || rows_per_split % 64 || !slab)
+    return RS_ERR_ARG;
+  int64_t T = 128;
+  for (int q = 0; q < nprob; ++q)
+    if (probs[q].N % 128 || probs[q].K % 128) T = 64;
+  const int64_t splits = cdiv(M, rows_per_split);
+  wg::Args a{};
+  a.nprob = nprob;
+  a.M = M;
+  a.rows_per_split = (int)rows_per_split;
+  a.splits = (int)splits;
+  a.slab = slab;
+  int tiles = 0;
+  int64_t off = 0;
+  for (int q = 0; q < nprob; ++q) {
+    const rs_wgrad_problem& p = probs[q];
+    if (p.N <= 0 || p.K <= 0 || p.N % T || p.K % T || p.lddy % 8 || p.ldx % 8 || !al16(p.dY) || !al16(p.X) ||
+        !p.dW)
+      return RS_ERR_UNSUPPORTED;
+    a.p[q] = {(const __bf16*)p.dY, (const __bf16*)p.X, p.lddy, p.ldx, (int)p.N, (int)p.K, (int)(p.K / T), tiles, off};
+    tiles += (int)((p.N / T) * (p.K / T));
+    off += splits * (p.N * p.K + p.N);
+  }
+  if (off > slab_numel) return RS_ERR_ARG;
+  a.ntiles = tiles;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((unsigned)(tiles * splits));
+  if (T == 128) hipLaunchKernelGGL(wg::wgrad_group_kernel<128>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(wg::wgrad_group_kernel<64>, grid, dim3(256), 0, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  // reduce: per problem its W segment and (optional) bias segment, then the caller's extra segments
+  rs_reduce_segment segs[2 * wg::MAXP + wg::MAXS];
+  int ns = 0;
+  off = 0;
+  for (int q = 0; q < nprob; ++q) {
+    const rs_wgrad_problem& p = probs[q];
+    const int64_t stride = p.N * p.K + p.N;
+    segs[ns++] = {slab + off, stride, splits, p.N * p.K, p.dW};
+    if (p.db) segs[ns++] = {slab + off + p.N * p.K, stride, splits, p.N, p.db};
+    off += splits * stride;
+  }
+  if (nextra < 0 || nextra > wg::MAXS) return RS_ERR_ARG;
+  for (int q = 0; q < nextra; ++q) segs[ns++] = extra[q];
+  return launch_segments(ns, segs, 1, s);
+}
+
+}  // extern "C"

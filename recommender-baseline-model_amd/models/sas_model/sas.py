@@ -19,6 +19,7 @@ forward (per step)                      kernels (include/recsys_hip.h)
 backward: the mirror image (rs_*_bwd, dgrad/wgrad GEMMs, split-K slabs).
 """
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -255,6 +256,9 @@ class SASEngine:
         dx = e("dx", (M, d))
         ops.layernorm_bwd(s["xL"], df, self.Wf("last_layernorm.weight"), s["muf"], s["rf"], LN_EPS, dx,
                           G("last_layernorm.weight"), G("last_layernorm.bias"), wln, 0)
+        if ops.sas_block_fused_ok(d, self.dt):
+            self._backward_blocks_fused(s, dx, grad, slab)
+            return
         for i in reversed(range(L)):
             pre = f"attention_layers.{i}."
             fw = f"forward_layers.{i}."
@@ -294,6 +298,79 @@ class SASEngine:
             dx = dxi
         ops.embed_bwd(0, ids, T, dx, math.sqrt(d), p, self.salt["emb"], sb, G("item_emb.weight"),
                       G("pos_emb.weight"))
+
+    def _refresh_transposed(self):
+        """bf16 [in][out] copies of the block weights for the fused backward's input-gradient
+        GEMMs (rs_transpose_bf16, one launch); per layer: in_proj^T [d][3d], out_proj^T, conv1^T,
+        conv2^T [d][d]."""
+        d, L = self.d, self.L
+        if getattr(self, "_wT", None) is None:
+            self._wT = torch.empty(L * 6 * d * d, dtype=torch.bfloat16, device=self.dev)
+            desc = []
+            for i in range(L):
+                base = i * 6 * d * d
+                pre, fw = f"attention_layers.{i}.", f"forward_layers.{i}."
+                for name, rows, off in ((pre + "in_proj_weight", 3 * d, 0), (pre + "out_proj.weight", d, 3 * d * d),
+                                        (fw + "conv1.weight", d, 4 * d * d), (fw + "conv2.weight", d, 5 * d * d)):
+                    desc.append([rows, d, self.flat.offsets[name], d, base + off, rows])
+            self._wT_desc = torch.tensor(desc, dtype=torch.int64, device=self.dev)
+            self._wT_tiles = max(-(-r // 64) * -(-c // 64) for r, c, *_ in desc)
+        ops.transpose_bf16(self._wT_desc, self._wT_tiles, self.flat.bf16, self._wT)
+        return self._wT
+
+    def _backward_blocks_fused(self, s, dx, grad, slab):
+        """SAS blocks' backward with rs_sas_block_out_bwd / rs_sas_block_in_bwd (rowfused.hip) for the
+        row-local chains; then ALL ten weight gradients and the four LayerNorm affine partial sets in
+        one grouped GEMM launch + one grouped reduction (rs_wgrad_grouped, wgrad.hip)."""
+        B, T, p, ids, sb = s["B"], s["T"], s["p"], s["ids"], s["sb"]
+        M, d, H, Dh, L = B * T, self.d, self.H, self.Dh, self.L
+        e = self._buf
+        G = lambda n: self.flat.view(n, grad)  # noqa: E731
+        wT = self._refresh_transposed().view(L, 6, d, d)
+        nb = -(-M // 64)
+        lnp = self.ws.get("lnp", (L, 2, 2 * d * nb), torch.float32)
+        wat = self.ws.get("attn", (B * H * T,), torch.float32)
+        probs, segs = [], []
+        for i in reversed(range(L)):
+            pre, fw = f"attention_layers.{i}.", f"forward_layers.{i}."
+            inT = wT[i, 0:3].reshape(d, 3 * d)
+            dy2, da1, dx1, do = e("dy2", (M, d)), e("da1", (M, d)), e("dx1", (M, d)), e("do", (M, d))
+            ops.sas_block_out_bwd(dx, ids, s["h1"][i], s["x1"][i], s["mu2"][i], s["r2"][i],
+                                  self.Wf(f"forward_layernorms.{i}.weight"), wT[i, 5], wT[i, 4], wT[i, 3],
+                                  dy2, da1, dx1, do, lnp[i, 0], p, self.salt[f"ffn1_{i}"], self.salt[f"ffn2_{i}"], sb)
+            dq, dkv = e("dq", (M, d)), e("dkv", (M, 2 * d))
+            kv = s["kv"][i]
+            ops.attn_bwd(B, T, H, Dh, s["q"][i], kv[:, :d], kv[:, d:], s["o"][i], do, s["lse"][i], dq,
+                         dkv[:, :d], dkv[:, d:], 1.0 / math.sqrt(Dh), 0, ids, p, self.salt[f"attn{i}"], sb, wat)
+            dxi = e("dxi", (M, d))
+            ops.sas_block_in_bwd(dq, dkv, dx1, s["x"][i], s["mu1"][i], s["r1"][i],
+                                 self.Wf(f"attention_layernorms.{i}.weight"), inT, dxi, lnp[i, 1])
+            Gin, Gb = G(pre + "in_proj_weight"), G(pre + "in_proj_bias")
+            probs += [(dy2, s["h1"][i], G(fw + "conv2.weight"), G(fw + "conv2.bias")),
+                      (da1, s["z"][i], G(fw + "conv1.weight"), G(fw + "conv1.bias")),
+                      (dx1, s["o"][i], G(pre + "out_proj.weight"), G(pre + "out_proj.bias")),
+                      (dq, s["Q"][i], Gin[:d], Gb[:d]),
+                      (dkv, s["x"][i], Gin[d:], Gb[d:])]
+            segs += ops.ln_partial_segments(lnp[i, 0], M, d, G(f"forward_layernorms.{i}.weight"),
+                                            G(f"forward_layernorms.{i}.bias"))
+            segs += ops.ln_partial_segments(lnp[i, 1], M, d, G(f"attention_layernorms.{i}.weight"),
+                                            G(f"attention_layernorms.{i}.bias"))
+            dx = dxi
+        rows = self._wgrad_rows(M, L * 6)
+        wslab = self.ws.get("wslab", (ops.wgrad_grouped_slab_numel([(d, d)] * 4 * L + [(2 * d, d)] * L, M, rows),),
+                            torch.float32)
+        ops.wgrad_grouped(probs, M, rows, wslab, extra=segs)
+        ops.embed_bwd(0, ids, T, dx, math.sqrt(d), p, self.salt["emb"], sb, G("item_emb.weight"),
+                      G("pos_emb.weight"))
+
+    @staticmethod
+    def _wgrad_rows(M, tiles):
+        """rows per split of the grouped weight-gradient launch: ~480 workgroups (2 per CU)."""
+        env = os.environ.get("RS_WGRAD_ROWS")
+        if env:
+            return int(env)
+        splits = max(1, 480 // tiles)
+        return max(64, -(-(-(-M // splits)) // 64) * 64)
 
     # ---- eval ----------------------------------------------------------------------
     def features(self, ids):

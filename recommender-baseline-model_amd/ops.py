@@ -241,3 +241,59 @@ def sas_block_out(o, Q, Wo, bo, x1, ln_w, ln_b, eps, z, mean, rstd, W1, b1, h1, 
     call("rs_sas_block_out", M, d, ptr(o), ptr(Q), ptr(Wo), ptr(bo), ptr(x1), ptr(ln_w), ptr(ln_b), eps, ptr(z),
          ptr(mean), ptr(rstd), ptr(W1), ptr(b1), ptr(h1), ptr(W2), ptr(b2), ptr(xn), ptr(ids), drop_p, salt1,
          salt2, ptr(seed_base), stream())
+
+
+def sas_block_out_bwd(dxn, ids, h1, x1, mean2, rstd2, ln_w, W2T, W1T, WoT, dy2, da1, dx1, dout, part, drop_p, salt1,
+                      salt2, seed_base):
+    """part: fp32 >= 2*d*ceil(M/64), receives the LN2 affine partials (ln_partial_segments)."""
+    M, d = dxn.shape
+    call("rs_sas_block_out_bwd", M, d, ptr(dxn), ptr(ids), ptr(h1), ptr(x1), ptr(mean2), ptr(rstd2), ptr(ln_w),
+         ptr(W2T), ptr(W1T), ptr(WoT), ptr(dy2), ptr(da1), ptr(dx1), ptr(dout), ptr(part), drop_p, salt1, salt2,
+         ptr(seed_base), stream())
+
+
+def sas_block_in_bwd(dq, dkv, dx1, x, mean1, rstd1, ln_w, WinT, dx, part):
+    M, d = dq.shape
+    call("rs_sas_block_in_bwd", M, d, ptr(dq), ptr(dkv), ptr(dx1), ptr(x), ptr(mean1), ptr(rstd1), ptr(ln_w),
+         ptr(WinT), ptr(dx), ptr(part), stream())
+
+
+def ln_partial_segments(part, M, d, dgamma, dbeta):
+    """The two reduce segments of a fused kernel's LayerNorm partials (part[b][2][d], b < ceil(M/64))."""
+    nb = -(-M // 64)
+    return [(part, 2 * d, nb, d, dgamma), (part[d:], 2 * d, nb, d, dbeta)]
+
+
+def _segments(segs):
+    arr = (_lib.ReduceSegment * max(1, len(segs)))()
+    for i, (src, stride, splits, n, out) in enumerate(segs):
+        arr[i] = _lib.ReduceSegment(ptr(src), stride, splits, n, ptr(out))
+    return arr
+
+
+def wgrad_grouped(problems, M, rows_per_split, slab, extra=()):
+    """problems: [(dY, X, dW, db|None)] with dW [N][K] fp32 (+=); extra: reduce segments
+    (src, stride, splits, n, out) summed (+=) in the same reduction launch."""
+    arr = (_lib.WgradProblem * len(problems))()
+    for i, (dY, X, dW, db) in enumerate(problems):
+        N, K = dY.shape[1], X.shape[1]
+        assert dW.numel() == N * K and dY.shape[0] >= M and X.shape[0] >= M
+        arr[i] = _lib.WgradProblem(ptr(dY), ld(dY), ptr(X), ld(X), N, K, ptr(dW), ptr(db) if db is not None else None)
+    segs = _segments(list(extra))
+    call("rs_wgrad_grouped", len(problems), arr, M, rows_per_split, ptr(slab), slab.numel(), len(extra), segs,
+         stream())
+
+
+def wgrad_grouped_slab_numel(shapes, M, rows_per_split):
+    """shapes: [(N, K)] of the problems."""
+    splits = -(-M // rows_per_split)
+    return sum(splits * (N * K + N) for N, K in shapes)
+
+
+def reduce_segments(segs, accumulate=True):
+    call("rs_reduce_segments", len(segs), _segments(list(segs)), int(accumulate), stream())
+
+
+def transpose_bf16(desc, max_tiles, src, dst):
+    """desc: int64 device tensor [nmat][6] (rows, cols, src_off, lds, dst_off, ldd)."""
+    call("rs_transpose_bf16", desc.shape[0], ptr(desc), max_tiles, ptr(src), ptr(dst), stream())

@@ -11,7 +11,7 @@ HEADER = os.path.join(ROOT, "include", "recsys_hip.h")
 
 def declared_symbols():
     text = open(HEADER).read()
-    return sorted(set(re.findall(r"^int (rs_\w+)\(", text, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|int64_t) (rs_\w+)\(", text, flags=re.M)))
 
 
 def test_header_declares_the_hot_path():
@@ -30,6 +30,16 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(h, s), s
     assert set(L.SIGNATURES) == set(declared_symbols())
     assert L.lib().rs_abi_version() == 1
+
+
+def test_grouped_wgrad_slab_size_host_function():
+    """rs_wgrad_grouped_slab_numel is host-only: the Python sizing helper must agree with it."""
+    import rbm_amd._lib as L
+    from rbm_amd import ops
+    shapes = [(128, 128), (256, 128), (64, 64)]
+    arr = (L.WgradProblem * 3)(*[L.WgradProblem(None, N, None, K, N, K, None, None) for N, K in shapes])
+    for M, rows in [(25600, 640), (111, 64), (64, 128)]:
+        assert L.lib().rs_wgrad_grouped_slab_numel(3, arr, M, rows) == ops.wgrad_grouped_slab_numel(shapes, M, rows)
 
 
 def test_product_path_does_not_import_oracle():

@@ -1,0 +1,59 @@
+"""Grouped weight-gradient GEMMs + grouped reduction (wgrad.hip) vs a torch fp32 reference.
+
+dW[N][K] += dY^T X and db[N] += colsum(dY) for several problems in one launch, with ragged
+row counts (the last split partial) and extra partial-sum segments reduced by the same launch.
+Operands are bf16, accumulation fp32: the reference is the fp32 product of the same bf16 values.
+"""
+import pytest
+import torch
+
+from conftest import rel
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("d,M,rows", [(128, 25600, 640), (128, 1000, 128), (64, 111, 64), (64, 3000, 256)])
+def test_wgrad_grouped_matches_torch(d, M, rows):
+    import rbm_amd  # noqa: F401
+    from rbm_amd import ops
+    g = torch.Generator(device="cuda").manual_seed(d + M)
+    dev = "cuda"
+    shapes = [(d, d), (2 * d, d), (d, d)]
+    probs, refs = [], []
+    for N, K in shapes:
+        dY = torch.randn(M, N, device=dev, generator=g).bfloat16()
+        X = torch.randn(M, K, device=dev, generator=g).bfloat16()
+        dW = torch.randn(N, K, device=dev, generator=g)
+        db = torch.randn(N, device=dev, generator=g)
+        refs.append((dW + dY.float().t() @ X.float(), db + dY.float().sum(0)))
+        probs.append((dY, X, dW, db))
+    probs[2] = probs[2][:3] + (None,)                       # a problem without a bias
+    # an extra segment set: 37 partials of 2*64 floats each summed into two outputs
+    part = torch.randn(37, 2, 64, device=dev, generator=g)
+    o1, o2 = torch.ones(64, device=dev), torch.zeros(64, device=dev)
+    e1, e2 = o1 + part[:, 0].sum(0), o2 + part[:, 1].sum(0)
+    extra = [(part.view(-1), 128, 37, 64, o1), (part.view(-1)[64:], 128, 37, 64, o2)]
+    slab = torch.empty(ops.wgrad_grouped_slab_numel(shapes, M, rows), device=dev)
+    ops.wgrad_grouped(probs, M, rows, slab, extra=extra)
+    torch.cuda.synchronize()
+    for i, ((dY, X, dW, db), (rW, rb)) in enumerate(zip(probs, refs)):
+        assert rel(dW.cpu().numpy(), rW.cpu().numpy()) < 1e-5, i
+        if db is not None:
+            assert rel(db.cpu().numpy(), rb.cpu().numpy()) < 1e-5, i
+    assert rel(o1.cpu().numpy(), e1.cpu().numpy()) < 1e-6 and rel(o2.cpu().numpy(), e2.cpu().numpy()) < 1e-6
+
+
+def test_wgrad_grouped_is_deterministic():
+    import rbm_amd  # noqa: F401
+    from rbm_amd import ops
+    M, d = 5000, 128
+    dY = torch.randn(M, d, device="cuda").bfloat16()
+    X = torch.randn(M, d, device="cuda").bfloat16()
+    outs = []
+    for _ in range(2):
+        dW = torch.zeros(d, d, device="cuda")
+        db = torch.zeros(d, device="cuda")
+        slab = torch.empty(ops.wgrad_grouped_slab_numel([(d, d)], M, 128), device="cuda")
+        ops.wgrad_grouped([(dY, X, dW, db)], M, 128, slab)
+        outs.append((dW.clone(), db.clone()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
