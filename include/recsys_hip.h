@@ -276,6 +276,39 @@ int rs_wgrad_grouped(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_
 /* The reduction alone: out (+)= sum over splits, for nseg segments (any number, 64 per launch). */
 int rs_reduce_segments(int nseg, const rs_reduce_segment* segs, int accumulate, void* stream);
 
+/* ---- item-table gradient by inverted index (itemgrad.hip) ------------------------------------
+ * dtable[v] += sum over the rows keyed v of: source 0  scale * dropout(m*d + c) * dx[m]  (the
+ * embedding lookup, sas.py:59-66), source 1  w1[m] * f[m], source 2  w2[m] * f[m]  (the tied
+ * sampled logits, sas.py:91-98); key 0 (padding_idx) skipped.  Deterministic: a stable radix
+ * sort of the keys, per-key sums in fixed order, one writer per table row, no float atomics.
+ * Build the index once per batch (the keys are step inputs), then rs_item_grad after the
+ * backward pass.  ws: rs_item_index_ws_bytes() bytes (device). */
+int64_t rs_item_index_ws_bytes(int nsrc, int64_t rows, int64_t table_rows, int64_t d);
+int rs_item_index_build(int nsrc, const int64_t* keys0, const int64_t* keys1, const int64_t* keys2, int64_t rows,
+                        int64_t table_rows, int64_t d, void* ws, int64_t ws_bytes, void* stream);
+/* dx, f: bf16 [rows][d] (d in {64, 128, 256}); w1, w2: fp32 [rows]; dtable fp32 [table_rows][d]. */
+int rs_item_grad(const void* ws, int nsrc, int64_t rows, int64_t table_rows, int64_t d, const void* dx, float scale,
+                 float drop_p, uint64_t salt, const uint64_t* seed_base, const void* f, const float* w1,
+                 const float* w2, float* dtable, void* stream);
+
+/* ---- fused SASRec output head (head.hip), bf16, d in {64, 128, 256} ----------------------------
+ * Forward (sas.py:87-100 + BCE of trainers/sas.py:40-49): f = LN_last(x) [f, mean, rstd saved];
+ * pl = <f, E[pos]>, nl = <f, E[neg]> (E = item_emb); part[b][3] = per-64-row-block sums of
+ * softplus(-pl), softplus(nl) and the valid count (pos != 0).  part >= 3*ceil(M/64) floats. */
+int rs_sas_head_fwd(int64_t M, int64_t d, const void* x, const float* ln_w, const float* ln_b, float eps, void* f,
+                    float* mean, float* rstd, const void* E, const int64_t* pos, const int64_t* neg, float* pl,
+                    float* nl, float* part, void* stream);
+/* Backward: with dpl_in == NULL the BCE gradient is formed here: dpl = (sigmoid(pl)-1)/c,
+ * dnl = sigmoid(nl)/c on valid rows, c = *divisor or the forward's valid count, written to
+ * dpl/dnl, and out[0..3] = {loss sum, count, mean loss (as rs_bce_fwd), neg-term sum}; with
+ * dpl_in/dnl_in given (autograd) those are used.  Then df = dpl E[pos] + dnl E[neg] and
+ * dx = LN'(x, df) (bf16); lnpart[b][2][d] = LN affine partials (reduce with rs_reduce_segments).
+ * The item-table gradient of the logits is left to rs_item_grad. */
+int rs_sas_head_bwd(int64_t M, int64_t d, const float* part, const float* divisor, float* out, const float* pl,
+                    const float* nl, const float* dpl_in, const float* dnl_in, float* dpl, float* dnl,
+                    const int64_t* pos, const int64_t* neg, const void* E, const void* x, const float* ln_w,
+                    const float* mean, const float* rstd, void* dx, float* lnpart, void* stream);
+
 /* ABI version of this header/library pair. */
 int rs_abi_version(void);
 

@@ -80,11 +80,16 @@ SIGNATURES = {
     "rs_wgrad_grouped": [i32, C.POINTER(WgradProblem), i64, i64, vp, i64, i32, C.POINTER(ReduceSegment), vp],
     "rs_reduce_segments": [i32, C.POINTER(ReduceSegment), i32, vp],
     "rs_wgrad_grouped_slab_numel": [i32, C.POINTER(WgradProblem), i64, i64],
+    "rs_item_index_ws_bytes": [i32, i64, i64, i64],
+    "rs_item_index_build": [i32, vp, vp, vp, i64, i64, i64, vp, i64, vp],
+    "rs_sas_head_fwd": [i64, i64, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
+    "rs_sas_head_bwd": [i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
+    "rs_item_grad": [vp, i32, i64, i64, i64, vp, f32, f32, u64, vp, vp, vp, vp, vp, vp],
     "rs_transpose_bf16": [i64, vp, i64, vp, vp, vp],
     "rs_abi_version": [],
 }
 
-RESTYPES = {"rs_wgrad_grouped_slab_numel": C.c_int64}
+RESTYPES = {"rs_wgrad_grouped_slab_numel": C.c_int64, "rs_item_index_ws_bytes": C.c_int64}
 
 _lib = None
 

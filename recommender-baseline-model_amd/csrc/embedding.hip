@@ -164,6 +164,7 @@ __global__ __launch_bounds__(256) void sampled_logits_bwd_kernel(const T* __rest
     float g = gp * to_f(ep[c]) + gn * to_f(en[c]);
     if (accumulate) g += to_f(dfr[c]);
     dfr[c] = from_f<T>(g);
+    if (dE == nullptr) continue;   // table gradient by rs_item_grad instead
     if (ip != 0 && gp != 0.f) atomicAdd(dE + ip * d + c, gp * x);
     if (in != 0 && gn != 0.f) atomicAdd(dE + in * d + c, gn * x);
   }

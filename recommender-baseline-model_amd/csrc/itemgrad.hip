@@ -1,0 +1,463 @@
+// Item-embedding gradient by inverted index (deterministic, no float atomics).
+//
+// The item table receives, per training step, one gradient row per token of the input sequence
+// (the embedding lookup, sas.py:59-66: scale * dropout-mask * dx[m]) and one per positive and
+// negative logit (sas.py:91-98: dpl[m] * f[m], dnl[m] * f[m]), keyed by the item id -- Zipf
+// distributed, so a handful of ids own thousands of rows.  Float atomics into the table run at
+// the memory-side atomic rate and serialise on the hot rows.  Instead:
+//
+//   rs_item_index_build: keys (ids | pos | neg) -> stable counting sort of the entries by key:
+//                        per-1024-entry-block key histograms (LDS), per-key exclusive prefix over
+//                        blocks, a scan over keys, then each block places its entries with a
+//                        block radix sort for the in-block rank.  Tables with more than 32768
+//                        rows use a device radix sort (rocPRIM) instead.  -> start[v] for v <= V
+//   rs_item_grad:        chunks of 64 sorted entries: contribution rows summed per key run in
+//                        LDS; a key wholly inside one chunk is written by that chunk (+=); a
+//                        key spanning chunks leaves per-chunk partials that the chunk holding
+//                        its first entry sums in chunk order (second kernel).
+//
+// Every destination row has exactly one writer and a fixed summation order: bitwise
+// reproducible.  Rows with key 0 (padding_idx) are skipped.
+#include <hipcub/hipcub.hpp>
+
+#include "common.h"
+#include "../../include/recsys_hip.h"
+
+namespace ig {
+
+constexpr int CH = 64;          // sorted entries per gradient chunk
+constexpr int BE = 1024;        // entries per counting-sort block
+constexpr int VMAX_CS = 32768;  // largest table for the counting sort (LDS histogram)
+
+struct Layout {
+  int64_t n, nchunks, nb, V;
+  bool cs;
+  size_t sk, sv, start, part, H, total, keys_in, vals_in, temp, temp_bytes, total_bytes;
+};
+
+static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static int key_bits(int64_t table_rows) {
+  int b = 1;
+  while (b < 32 && ((int64_t)1 << b) < table_rows) ++b;
+  return b;
+}
+
+static hipError_t layout(int nsrc, int64_t rows, int64_t table_rows, int64_t d, Layout& L) {
+  L.n = nsrc * rows;
+  L.nchunks = cdiv(L.n, CH);
+  L.nb = cdiv(L.n, BE);
+  L.V = table_rows;
+  L.cs = table_rows <= VMAX_CS;
+  size_t o = 0;
+  L.sk = o; o = al256(o + L.n * 4);
+  L.sv = o; o = al256(o + L.n * 4);
+  L.start = o; o = al256(o + (table_rows + 1) * 4);
+  L.part = o; o = al256(o + L.nchunks * 2 * d * 4);
+  L.temp_bytes = 0;
+  if (L.cs) {
+    L.H = o; o = al256(o + L.nb * table_rows * 4);
+    L.total = o; o = al256(o + table_rows * 4);
+    L.keys_in = L.vals_in = L.temp = 0;
+  } else {
+    L.H = L.total = 0;
+    L.keys_in = o; o = al256(o + L.n * 4);
+    L.vals_in = o; o = al256(o + L.n * 4);
+    L.temp = o;
+    size_t tb = 0;
+    const hipError_t e = hipcub::DeviceRadixSort::SortPairs(
+        nullptr, tb, (const uint32_t*)nullptr, (uint32_t*)nullptr, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+        (int)L.n, 0, key_bits(table_rows), (hipStream_t)0);
+    if (e != hipSuccess) return e;
+    L.temp_bytes = tb;
+    o = al256(o + tb);
+  }
+  L.total_bytes = o;
+  return hipSuccess;
+}
+
+struct Keys {
+  const int64_t* k[3];
+  int64_t rows, n, V;
+  __device__ __forceinline__ uint32_t get(int64_t e) const {
+    const int src = (int)(e / rows);
+    const int64_t r = e - src * rows;
+    int64_t v = k[src][r];
+    return (v < 0 || v >= V) ? 0u : (uint32_t)v;
+  }
+};
+
+// ---- counting sort ------------------------------------------------------------------------
+// H[b][v] = number of entries of block b with key v
+__global__ __launch_bounds__(256) void hist_kernel(Keys K, int* __restrict__ H) {
+  __shared__ int hist[VMAX_CS];
+  const int tid = threadIdx.x;
+  const int V = (int)K.V;
+  for (int v = tid; v < V; v += 256) hist[v] = 0;
+  __syncthreads();
+  const int64_t e0 = (int64_t)blockIdx.x * BE;
+  uint32_t key[BE / 256];
+#pragma unroll
+  for (int i = 0; i < BE / 256; ++i) {
+    const int64_t e = e0 + tid + i * 256;
+    key[i] = e < K.n ? K.get(e) : 0xffffffffu;
+  }
+#pragma unroll
+  for (int i = 0; i < BE / 256; ++i)
+    if (key[i] != 0xffffffffu) atomicAdd(&hist[key[i]], 1);
+  __syncthreads();
+  int* h = H + (int64_t)blockIdx.x * V;
+  for (int v = tid; v < V; v += 256) h[v] = hist[v];
+}
+
+// H[b][v] <- sum_{b' < b} H[b'][v];  total[v] = sum_b H[b][v].  Workgroup = 64 keys (lanes) x 4
+// waves, wave w owning a contiguous quarter of the block range; quarters combined through LDS.
+__global__ __launch_bounds__(256) void prefix_blocks_kernel(int* __restrict__ H, int64_t nb, int64_t V,
+                                                            int* __restrict__ total) {
+  __shared__ int part[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t v = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t q = cdiv(nb, 4), b0 = w * q, b1 = min(nb, b0 + q);
+  constexpr int U = 8;
+  int h[U];
+  int acc = 0;
+  if (v < V) {
+    for (int64_t b = b0; b < b1; b += U) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) h[u] = b + u < b1 ? H[(b + u) * V + v] : 0;
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc += h[u];
+    }
+  }
+  part[w][lane] = acc;
+  __syncthreads();
+  int off = 0;
+  for (int x = 0; x < w; ++x) off += part[x][lane];
+  if (v >= V) return;
+  if (w == 3) total[v] = off + acc;
+  for (int64_t b = b0; b < b1; b += U) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) h[u] = b + u < b1 ? H[(b + u) * V + v] : 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (b + u < b1) H[(b + u) * V + v] = off;
+      off += h[u];
+    }
+  }
+}
+
+// start[v] = sum_{v' < v} total[v'] (v <= V): one workgroup
+__global__ __launch_bounds__(1024) void scan_keys_kernel(const int* __restrict__ total, int64_t V,
+                                                         int* __restrict__ start) {
+  typedef hipcub::BlockScan<int, 1024> BS;
+  __shared__ typename BS::TempStorage tmp;
+  const int tid = threadIdx.x;
+  const int64_t per = cdiv(V, 1024);
+  const int64_t v0 = tid * per;
+  int s = 0;
+  for (int64_t v = v0; v < min(V, v0 + per); ++v) s += total[v];
+  int ex, agg;
+  BS(tmp).ExclusiveSum(s, ex, agg);
+  for (int64_t v = v0; v < min(V, v0 + per); ++v) {
+    start[v] = ex;
+    ex += total[v];
+  }
+  if (tid == 0) start[V] = agg;
+}
+
+// each block places its entries: rank inside the block by a stable block radix sort
+__global__ __launch_bounds__(256) void place_kernel(Keys K, const int* __restrict__ H, const int* __restrict__ start,
+                                                    int bits, uint32_t* __restrict__ sk, uint32_t* __restrict__ sv) {
+  typedef hipcub::BlockRadixSort<uint32_t, 256, BE / 256, uint32_t> BRS;
+  __shared__ typename BRS::TempStorage tmp;
+  __shared__ uint32_t sorted[BE];
+  const int tid = threadIdx.x;
+  const int64_t e0 = (int64_t)blockIdx.x * BE;
+  const int cnt = (int)min((int64_t)BE, K.n - e0);
+  uint32_t key[BE / 256], idx[BE / 256];
+#pragma unroll
+  for (int i = 0; i < BE / 256; ++i) {
+    const int l = tid * (BE / 256) + i;
+    idx[i] = (uint32_t)l;
+    key[i] = l < cnt ? K.get(e0 + l) : 0xffffffffu;
+  }
+  BRS(tmp).Sort(key, idx, 0, bits);
+#pragma unroll
+  for (int i = 0; i < BE / 256; ++i) sorted[tid * (BE / 256) + i] = key[i];
+  __syncthreads();
+  const int* h = H + (int64_t)blockIdx.x * K.V;
+#pragma unroll
+  for (int i = 0; i < BE / 256; ++i) {
+    const int j = tid * (BE / 256) + i;
+    if ((int)idx[i] >= cnt) continue;
+    const uint32_t k = key[i];
+    int lo = 0, hi = j;                       // first position of k in the sorted block
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (sorted[mid] < k) lo = mid + 1;
+      else hi = mid;
+    }
+    const int64_t pos = (int64_t)start[k] + h[k] + (j - lo);
+    sk[pos] = k;
+    sv[pos] = (uint32_t)(e0 + idx[i]);
+  }
+}
+
+// ---- device radix sort path (large tables) --------------------------------------------------
+__global__ __launch_bounds__(256) void make_keys_kernel(Keys K, uint32_t* __restrict__ keys,
+                                                        uint32_t* __restrict__ vals) {
+  const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (e >= K.n) return;
+  keys[e] = K.get(e);
+  vals[e] = (uint32_t)e;
+}
+
+// start[v] = first sorted position with key >= v, for v <= V
+__global__ __launch_bounds__(256) void lower_bounds_kernel(const uint32_t* __restrict__ sk, int64_t n, int64_t V,
+                                                           int* __restrict__ start) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i > n) return;
+  const int64_t lo = i == 0 ? -1 : (int64_t)sk[i - 1];
+  const int64_t hi = i == n ? V : (int64_t)sk[i];
+  for (int64_t v = lo + 1; v <= hi; ++v) start[v] = (int)i;
+}
+
+// ---- gradient ---------------------------------------------------------------------------------
+struct GradArgs {
+  const uint32_t* sk;
+  const uint32_t* sv;
+  const int* start;      // [V + 1]
+  float* part;
+  int64_t n, rows;
+  const __bf16* dx;      // source 0 rows: scale * drop(m*d + c) * dx[m]
+  float scale, drop_p;
+  uint64_t salt;
+  const uint64_t* seed_base;
+  const __bf16* f;       // sources 1, 2 rows: w1[m] * f[m], w2[m] * f[m]
+  const float* w1;
+  const float* w2;
+  float* dtable;
+};
+
+// one block per chunk of CH sorted entries
+template <int D>
+__global__ __launch_bounds__(256) void item_chunk_kernel(GradArgs a) {
+  constexpr int TPE = D / 8, EPP = 256 / TPE;   // threads per entry row, entry rows per pass
+  __shared__ __attribute__((aligned(16))) float rowsum[CH][D];
+  __shared__ uint32_t skey[CH], sent[CH];
+  __shared__ int kst[CH], ken[CH];
+  const int tid = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * CH;
+  const int cnt = (int)min((int64_t)CH, a.n - base);
+  const bool drop = a.drop_p > 0.f;
+  const uint32_t s32 = drop ? seed32(eff_seed(a.salt, a.seed_base)) : 0u;
+  if (tid < CH) {
+    const uint32_t k = tid < cnt ? a.sk[base + tid] : 0xffffffffu;
+    const uint32_t e = tid < cnt ? a.sv[base + tid] : 0u;
+    skey[tid] = k;
+    sent[tid] = e;
+    kst[tid] = tid < cnt ? a.start[k] : 0;
+    ken[tid] = tid < cnt ? a.start[k + 1] : 0;
+  }
+  __syncthreads();
+  // contribution rows (all loads of a pass issued before use)
+#pragma unroll
+  for (int p0 = 0; p0 < CH; p0 += EPP) {
+    const int j = p0 + tid / TPE, c0 = (tid % TPE) * 8;
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = 0.f;
+    if (j < cnt) {
+      const uint32_t e = sent[j];
+      const uint32_t key = skey[j];
+      const int src = (int)(e / (uint32_t)a.rows);
+      const int64_t m = (int64_t)e - (int64_t)src * a.rows;
+      if (key != 0) {
+        if (src == 0) {
+          load_chunk<__bf16>(v, a.dx + m * D + c0);
+          float dm[8];
+#pragma unroll
+          for (int q = 0; q < 8; q += 2) {
+            if (drop) drop_mul2(a.drop_p, s32, (uint64_t)(m * D + c0 + q), dm[q], dm[q + 1]);
+            else dm[q] = dm[q + 1] = 1.f;
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] = v[q] * a.scale * dm[q];
+        } else {
+          const float w = src == 1 ? a.w1[m] : a.w2[m];
+          load_chunk<__bf16>(v, a.f + m * D + c0);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] *= w;
+        }
+      }
+    }
+    *reinterpret_cast<float4*>(&rowsum[j][c0]) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(&rowsum[j][c0 + 4]) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+  __syncthreads();
+  // per-column run sums in entry order, stored at the run's first row
+  if (tid < D) {
+    const int c = tid;
+    float acc = 0.f;
+    int rs = 0;
+    for (int j = 0; j < cnt; ++j) {
+      acc += rowsum[j][c];
+      if (j + 1 < cnt && skey[j + 1] == skey[j]) continue;
+      rowsum[rs][c] = acc;
+      acc = 0.f;
+      rs = j + 1;
+    }
+  }
+  __syncthreads();
+  // emit: whole key in this chunk -> table row (sole writer); else the chunk's partial
+#pragma unroll
+  for (int p0 = 0; p0 < CH; p0 += EPP) {
+    const int j = p0 + tid / TPE, c0 = (tid % TPE) * 8;
+    if (j >= cnt || (j > 0 && skey[j - 1] == skey[j]) || skey[j] == 0) continue;
+    const uint32_t k = skey[j];
+    const float4 r0 = *reinterpret_cast<const float4*>(&rowsum[j][c0]);
+    const float4 r1 = *reinterpret_cast<const float4*>(&rowsum[j][c0 + 4]);
+    if (kst[j] >= base && ken[j] <= base + cnt) {
+      float4* t = reinterpret_cast<float4*>(a.dtable + (int64_t)k * D + c0);
+      float4 t0 = t[0], t1 = t[1];
+      t0.x += r0.x; t0.y += r0.y; t0.z += r0.z; t0.w += r0.w;
+      t1.x += r1.x; t1.y += r1.y; t1.z += r1.z; t1.w += r1.w;
+      t[0] = t0;
+      t[1] = t1;
+    } else {
+      float4* o = reinterpret_cast<float4*>(a.part + ((int64_t)blockIdx.x * 2 + (j == 0 ? 0 : 1)) * D + c0);
+      o[0] = r0;
+      o[1] = r1;
+    }
+  }
+}
+
+// one wave per chunk: the chunk holding the first entry of a key that continues past the chunk
+// sums that key's partials in chunk order and writes the table row
+template <int D>
+__global__ __launch_bounds__(256) void item_span_kernel(GradArgs a, int64_t nchunks) {
+  constexpr int CPL = D / 64 > 0 ? D / 64 : 1;    // columns per lane
+  const int lane = threadIdx.x & 63;
+  const int64_t ch = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (ch >= nchunks) return;
+  const int64_t base = ch * CH;
+  const int64_t last = min(a.n, base + CH) - 1;
+  const uint32_t k = a.sk[last];
+  if (k == 0) return;
+  const int64_t ks = a.start[k], ke = a.start[k + 1];
+  if (ke <= last + 1 || ks < base) return;               // key ends here, or owned by an earlier chunk
+  const int64_t cl = (ke - 1) / CH;                      // chunk of the key's last entry
+  const int own_slot = ks == base ? 0 : 1;
+  float acc[CPL];
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) {
+    const int c = lane + 64 * q;
+    acc[q] = c < D ? a.part[(ch * 2 + own_slot) * D + c] : 0.f;
+  }
+  int64_t cc = ch + 1;
+  for (; cc + 7 <= cl; cc += 8) {
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) {
+      const int c = lane + 64 * q;
+      if (c < D) {
+        float u[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) u[t] = a.part[((cc + t) * 2) * D + c];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[q] += u[t];
+      }
+    }
+  }
+  for (; cc <= cl; ++cc) {
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) {
+      const int c = lane + 64 * q;
+      if (c < D) acc[q] += a.part[(cc * 2) * D + c];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) {
+    const int c = lane + 64 * q;
+    if (c < D) a.dtable[(int64_t)k * D + c] += acc[q];
+  }
+}
+
+}  // namespace ig
+
+extern "C" {
+
+int64_t rs_item_index_ws_bytes(int nsrc, int64_t rows, int64_t table_rows, int64_t d) {
+  if (nsrc < 1 || nsrc > 3 || rows <= 0 || table_rows <= 0 || d <= 0) return -1;
+  ig::Layout L;
+  if (ig::layout(nsrc, rows, table_rows, d, L) != hipSuccess) return -1;
+  return (int64_t)L.total_bytes;
+}
+
+int rs_item_index_build(int nsrc, const int64_t* keys0, const int64_t* keys1, const int64_t* keys2, int64_t rows,
+                        int64_t table_rows, int64_t d, void* ws, int64_t ws_bytes, void* stream) {
+  if (nsrc < 1 || nsrc > 3 || rows <= 0 || table_rows <= 0 || !ws || !keys0 || (nsrc > 1 && !keys1) ||
+      (nsrc > 2 && !keys2) || nsrc * rows >= ((int64_t)1 << 31))
+    return RS_ERR_ARG;
+  ig::Layout L;
+  hipError_t e = ig::layout(nsrc, rows, table_rows, d, L);
+  if (e != hipSuccess) return (int)e;
+  if ((int64_t)L.total_bytes > ws_bytes) return RS_ERR_ARG;
+  char* w = (char*)ws;
+  hipStream_t s = (hipStream_t)stream;
+  const ig::Keys K = {{keys0, keys1, keys2}, rows, L.n, table_rows};
+  uint32_t* sk = (uint32_t*)(w + L.sk);
+  uint32_t* sv = (uint32_t*)(w + L.sv);
+  int* start = (int*)(w + L.start);
+  const int bits = ig::key_bits(table_rows);
+  if (L.cs) {
+    int* H = (int*)(w + L.H);
+    int* total = (int*)(w + L.total);
+    hipLaunchKernelGGL(ig::hist_kernel, dim3((unsigned)L.nb), dim3(256), 0, s, K, H);
+    hipLaunchKernelGGL(ig::prefix_blocks_kernel, dim3((unsigned)cdiv(table_rows, 64)), dim3(256), 0, s, H, L.nb,
+                       table_rows, total);
+    hipLaunchKernelGGL(ig::scan_keys_kernel, dim3(1), dim3(1024), 0, s, total, table_rows, start);
+    hipLaunchKernelGGL(ig::place_kernel, dim3((unsigned)L.nb), dim3(256), 0, s, K, H, start, bits, sk, sv);
+    return (int)hipGetLastError();
+  }
+  uint32_t* kin = (uint32_t*)(w + L.keys_in);
+  uint32_t* vin = (uint32_t*)(w + L.vals_in);
+  hipLaunchKernelGGL(ig::make_keys_kernel, dim3((unsigned)cdiv(L.n, 256)), dim3(256), 0, s, K, kin, vin);
+  if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+  size_t tb = L.temp_bytes;
+  e = hipcub::DeviceRadixSort::SortPairs((void*)(w + L.temp), tb, kin, sk, vin, sv, (int)L.n, 0, bits, s);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(ig::lower_bounds_kernel, dim3((unsigned)cdiv(L.n + 1, 256)), dim3(256), 0, s, sk, L.n,
+                     table_rows, start);
+  return (int)hipGetLastError();
+}
+
+int rs_item_grad(const void* ws, int nsrc, int64_t rows, int64_t table_rows, int64_t d, const void* dx, float scale,
+                 float drop_p, uint64_t salt, const uint64_t* seed_base, const void* f, const float* w1,
+                 const float* w2, float* dtable, void* stream) {
+  if (nsrc < 1 || nsrc > 3 || rows <= 0 || !ws || !dtable || !dx || (nsrc > 1 && (!f || !w1)) || (nsrc > 2 && !w2))
+    return RS_ERR_ARG;
+  ig::Layout L;
+  hipError_t e = ig::layout(nsrc, rows, table_rows, d, L);
+  if (e != hipSuccess) return (int)e;
+  const char* w = (const char*)ws;
+  ig::GradArgs a = {(const uint32_t*)(w + L.sk), (const uint32_t*)(w + L.sv), (const int*)(w + L.start),
+                    (float*)(w + L.part), L.n, rows, (const __bf16*)dx, scale, drop_p, salt, seed_base,
+                    (const __bf16*)f, w1, w2, dtable};
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 g1((unsigned)L.nchunks), g2((unsigned)cdiv(L.nchunks, 4));
+  if (d == 64) {
+    hipLaunchKernelGGL(ig::item_chunk_kernel<64>, g1, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(ig::item_span_kernel<64>, g2, dim3(256), 0, s, a, L.nchunks);
+  } else if (d == 128) {
+    hipLaunchKernelGGL(ig::item_chunk_kernel<128>, g1, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(ig::item_span_kernel<128>, g2, dim3(256), 0, s, a, L.nchunks);
+  } else if (d == 256) {
+    hipLaunchKernelGGL(ig::item_chunk_kernel<256>, g1, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(ig::item_span_kernel<256>, g2, dim3(256), 0, s, a, L.nchunks);
+  } else {
+    return RS_ERR_UNSUPPORTED;
+  }
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

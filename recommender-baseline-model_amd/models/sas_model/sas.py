@@ -184,10 +184,12 @@ class SASEngine:
         s = {"B": B, "T": T, "p": p, "ids": ids, "pos": pos, "neg": neg, "sb": sb,
              "x": [], "Q": [], "mu1": [], "r1": [], "q": [], "kv": [], "o": [], "lse": [],
              "x1": [], "z": [], "mu2": [], "r2": [], "h1": []}
+        fused = ops.sas_block_fused_ok(d, self.dt)
+        if fused and training and pos is not None:
+            s["side"] = self._side_prologue(ids, pos, neg)
         x = e("x0", (M, d))
         ops.embed_fwd(0, ids, T, self.W("item_emb.weight"), self.W("pos_emb.weight"), math.sqrt(d), p,
                       self.salt["emb"], sb, x)
-        fused = ops.sas_block_fused_ok(d, self.dt)
         for i in range(L):
             pre = f"attention_layers.{i}."
             Q, mu1, r1 = e("Q", (M, d)), e("mu", (M,), torch.float32), e("r", (M,), torch.float32)
@@ -230,17 +232,32 @@ class SASEngine:
                 s[k_].append(v_)
             x = xn
         f, muf, rf = e("f", (M, d)), e("mu", (M,), torch.float32), e("r", (M,), torch.float32)
-        ops.layernorm_fwd(x, self.Wf("last_layernorm.weight"), self.Wf("last_layernorm.bias"), LN_EPS, f, muf, rf, 0)
         s.update(xL=x, f=f, muf=muf, rf=rf)
+        if fused and need_logits:
+            # last LayerNorm + tied sampled logits + BCE partial sums in one kernel (head.hip)
+            pl, nl = e("pl", (B, T), torch.float32), e("nl", (B, T), torch.float32)
+            headp = e("headp", (3 * (-(-M // 64)),), torch.float32)
+            ops.sas_head_fwd(x, self.Wf("last_layernorm.weight"), self.Wf("last_layernorm.bias"), LN_EPS, f, muf, rf,
+                             self.W("item_emb.weight"), pos, neg, pl, nl, headp)
+            s.update(pl=pl, nl=nl, headp=headp)
+            return pl, nl, s
+        ops.layernorm_fwd(x, self.Wf("last_layernorm.weight"), self.Wf("last_layernorm.bias"), LN_EPS, f, muf, rf, 0)
         if not need_logits:
             return None, None, s
         pl, nl = e("pl", (B, T), torch.float32), e("nl", (B, T), torch.float32)
         ops.sampled_logits_fwd(f, self.W("item_emb.weight"), pos, neg, pl, nl)
         return pl, nl, s
 
+    @property
+    def fused_head(self):
+        """True when forward/backward take the fused bf16 path (head.hip, rowfused.hip, itemgrad.hip)."""
+        return ops.sas_block_fused_ok(self.d, self.dt)
+
     # ---- backward ------------------------------------------------------------------
-    def backward(self, s, dpl, dnl, grad):
-        """Accumulates every parameter gradient into the flat fp32 buffer ``grad``."""
+    def backward(self, s, dpl, dnl, grad, loss_out=None, divisor=None):
+        """Accumulates every parameter gradient into the flat fp32 buffer ``grad``.  dpl/dnl: the
+        logits' gradients; None (fused path only) = form the BCE gradient of the forward's logits here,
+        writing the loss statistics to loss_out (divisor: device count, None = this batch's)."""
         B, T, p, ids = s["B"], s["T"], s["p"], s["ids"]
         M, d, H, Dh, L = B * T, self.d, self.H, self.Dh, self.L
         sb = s["sb"]
@@ -250,15 +267,34 @@ class SASEngine:
         wln = self.ws.get("ln", (2 * 512 * d,), torch.float32)
         wat = self.ws.get("attn", (B * H * T,), torch.float32)
 
+        fused = ops.sas_block_fused_ok(d, self.dt)
+        if fused:
+            # the side-stream prologue of forward built the item index and the transposed weights
+            ev, iws = s["side"] if "side" in s else self._side_prologue(ids, s["pos"], s["neg"])
+            torch.cuda.current_stream().wait_event(ev)
+        if fused:
+            dx = e("dx", (M, d))
+            lnh = self.ws.get("lnh", (2 * d * (-(-M // 64)),), torch.float32)
+            E, gl = self.W("item_emb.weight"), self.Wf("last_layernorm.weight")
+            if dpl is None:
+                dpl, dnl = e("dpl", (B, T), torch.float32), e("dnl", (B, T), torch.float32)
+                ops.sas_head_bwd(s["headp"], divisor, loss_out, s["pl"], s["nl"], None, None, dpl, dnl, s["pos"],
+                                 s["neg"], E, s["xL"], gl, s["muf"], s["rf"], dx, lnh)
+            else:
+                ops.sas_head_bwd(None, None, None, None, None, dpl, dnl, None, None, s["pos"], s["neg"], E, s["xL"],
+                                 gl, s["muf"], s["rf"], dx, lnh)
+            segs = ops.ln_partial_segments(lnh, M, d, G("last_layernorm.weight"), G("last_layernorm.bias"))
+            dx = self._backward_blocks_fused(s, dx, grad, segs)
+            ops.embed_bwd(0, ids, T, dx, math.sqrt(d), p, self.salt["emb"], sb, None, G("pos_emb.weight"))
+            ops.item_grad(iws, 3, M, dx, math.sqrt(d), p, self.salt["emb"], sb, s["f"], dpl, dnl,
+                          G("item_emb.weight"))
+            return
         df = e("df", (M, d))
         ops.sampled_logits_bwd(s["f"], self.W("item_emb.weight"), s["pos"], s["neg"], dpl, dnl, df,
                                G("item_emb.weight"))
         dx = e("dx", (M, d))
         ops.layernorm_bwd(s["xL"], df, self.Wf("last_layernorm.weight"), s["muf"], s["rf"], LN_EPS, dx,
                           G("last_layernorm.weight"), G("last_layernorm.bias"), wln, 0)
-        if ops.sas_block_fused_ok(d, self.dt):
-            self._backward_blocks_fused(s, dx, grad, slab)
-            return
         for i in reversed(range(L)):
             pre = f"attention_layers.{i}."
             fw = f"forward_layers.{i}."
@@ -299,6 +335,25 @@ class SASEngine:
         ops.embed_bwd(0, ids, T, dx, math.sqrt(d), p, self.salt["emb"], sb, G("item_emb.weight"),
                       G("pos_emb.weight"))
 
+    def _side_prologue(self, ids, pos, neg):
+        """Work of the fused backward that depends only on the batch's keys and the weights, issued on a
+        side stream so it overlaps the forward pass: the item-gradient index (rs_item_index_build) and
+        the transposed block weights (rs_transpose_bf16).  Returns (event, index workspace)."""
+        cur = torch.cuda.current_stream()
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(device=self.dev)
+        self._side.wait_stream(cur)
+        B, T = ids.shape
+        M, d = B * T, self.d
+        V1 = self.flat.shapes["item_emb.weight"][0]
+        with torch.cuda.stream(self._side):
+            iws = self.ws.get("itemidx", (ops.item_index_ws_bytes(3, M, V1, d),), torch.uint8)
+            ops.item_index_build([ids, pos, neg], V1, d, iws)
+            self._refresh_transposed()
+            ev = torch.cuda.Event()
+            ev.record(self._side)
+        return ev, iws
+
     def _refresh_transposed(self):
         """bf16 [in][out] copies of the block weights for the fused backward's input-gradient
         GEMMs (rs_transpose_bf16, one launch); per layer: in_proj^T [d][3d], out_proj^T, conv1^T,
@@ -318,19 +373,20 @@ class SASEngine:
         ops.transpose_bf16(self._wT_desc, self._wT_tiles, self.flat.bf16, self._wT)
         return self._wT
 
-    def _backward_blocks_fused(self, s, dx, grad, slab):
+    def _backward_blocks_fused(self, s, dx, grad, extra_segs=()):
         """SAS blocks' backward with rs_sas_block_out_bwd / rs_sas_block_in_bwd (rowfused.hip) for the
         row-local chains; then ALL ten weight gradients and the four LayerNorm affine partial sets in
-        one grouped GEMM launch + one grouped reduction (rs_wgrad_grouped, wgrad.hip)."""
+        one grouped GEMM launch + one grouped reduction (rs_wgrad_grouped, wgrad.hip).  Returns the
+        gradient at the embedding output."""
         B, T, p, ids, sb = s["B"], s["T"], s["p"], s["ids"], s["sb"]
         M, d, H, Dh, L = B * T, self.d, self.H, self.Dh, self.L
         e = self._buf
         G = lambda n: self.flat.view(n, grad)  # noqa: E731
-        wT = self._refresh_transposed().view(L, 6, d, d)
+        wT = self._wT.view(L, 6, d, d)              # refreshed by _side_prologue
         nb = -(-M // 64)
         lnp = self.ws.get("lnp", (L, 2, 2 * d * nb), torch.float32)
         wat = self.ws.get("attn", (B * H * T,), torch.float32)
-        probs, segs = [], []
+        probs, segs = [], list(extra_segs)
         for i in reversed(range(L)):
             pre, fw = f"attention_layers.{i}.", f"forward_layers.{i}."
             inT = wT[i, 0:3].reshape(d, 3 * d)
@@ -360,8 +416,7 @@ class SASEngine:
         wslab = self.ws.get("wslab", (ops.wgrad_grouped_slab_numel([(d, d)] * 4 * L + [(2 * d, d)] * L, M, rows),),
                             torch.float32)
         ops.wgrad_grouped(probs, M, rows, wslab, extra=segs)
-        ops.embed_bwd(0, ids, T, dx, math.sqrt(d), p, self.salt["emb"], sb, G("item_emb.weight"),
-                      G("pos_emb.weight"))
+        return dx
 
     @staticmethod
     def _wgrad_rows(M, tiles):

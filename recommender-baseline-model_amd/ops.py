@@ -297,3 +297,39 @@ def reduce_segments(segs, accumulate=True):
 def transpose_bf16(desc, max_tiles, src, dst):
     """desc: int64 device tensor [nmat][6] (rows, cols, src_off, lds, dst_off, ldd)."""
     call("rs_transpose_bf16", desc.shape[0], ptr(desc), max_tiles, ptr(src), ptr(dst), stream())
+
+
+# ---- item-table gradient by inverted index (itemgrad.hip) ----------------------------------
+def item_index_ws_bytes(nsrc, rows, table_rows, d):
+    n = _lib.lib().rs_item_index_ws_bytes(nsrc, rows, table_rows, d)
+    if n < 0:
+        raise RuntimeError("rs_item_index_ws_bytes: bad arguments")
+    return n
+
+
+def item_index_build(keys, table_rows, d, ws):
+    """keys: 1-3 int64 device tensors of the same numel (ids, pos, neg)."""
+    rows = keys[0].numel()
+    kp = [ptr(k) for k in keys] + [None] * (3 - len(keys))
+    call("rs_item_index_build", len(keys), kp[0], kp[1], kp[2], rows, table_rows, d, ptr(ws), ws.numel(), stream())
+
+
+def item_grad(ws, nsrc, rows, dx, scale, drop_p, salt, seed_base, f, w1, w2, dtable):
+    table_rows, d = dtable.shape
+    call("rs_item_grad", ptr(ws), nsrc, rows, table_rows, d, ptr(dx), scale, drop_p, salt, ptr(seed_base),
+         ptr(f) if f is not None else None, ptr(w1) if w1 is not None else None,
+         ptr(w2) if w2 is not None else None, ptr(dtable), stream())
+
+
+# ---- fused SAS output head (head.hip) --------------------------------------------------------
+def sas_head_fwd(x, ln_w, ln_b, eps, f, mean, rstd, E, pos, neg, pl, nl, part):
+    M, d = x.shape
+    call("rs_sas_head_fwd", M, d, ptr(x), ptr(ln_w), ptr(ln_b), eps, ptr(f), ptr(mean), ptr(rstd), ptr(E), ptr(pos),
+         ptr(neg), ptr(pl), ptr(nl), ptr(part), stream())
+
+
+def sas_head_bwd(part, divisor, out, pl, nl, dpl_in, dnl_in, dpl, dnl, pos, neg, E, x, ln_w, mean, rstd, dx, lnpart):
+    M, d = x.shape
+    call("rs_sas_head_bwd", M, d, ptr(part), ptr(divisor), ptr(out), ptr(pl), ptr(nl), ptr(dpl_in), ptr(dnl_in),
+         ptr(dpl), ptr(dnl), ptr(pos), ptr(neg), ptr(E), ptr(x), ptr(ln_w), ptr(mean), ptr(rstd), ptr(dx),
+         ptr(lnpart), stream())

@@ -83,6 +83,13 @@ class FusedTrainStep:
         if self.kind == "sas":
             seq, pos, neg = batch
             pl, nl, saved = eng.forward(seq, pos, neg, True, clone_seed=False)
+            if eng.fused_head:
+                # BCE forward/backward inside the fused head kernels (head.hip)
+                eng.backward(saved, None, None, self.flat.grad, loss_out=self.loss_out,
+                             divisor=self.one if self.dp else None)
+                if self.dp:
+                    self.flat.aux[dpx.LOSS_SUM:dpx.COUNT + 1].copy_(self.loss_out[0:2])
+                return
             ws = eng.ws.get("bce", (3 * 256,), torch.float32)
             ops.bce_fwd(pl, nl, pos, ws, self.loss_out)
             div = self._divisor(self.loss_out[1:2])

@@ -146,7 +146,7 @@ def test_sas_all_padding_rows_and_zero_negatives():
 @pytest.mark.parametrize("V,T,d,L,h,B", [(500, 37, 64, 2, 2, 3), (400, 200, 128, 2, 1, 5), (300, 50, 128, 1, 4, 2)])
 def test_sas_fused_block_matches_unfused(V, T, d, L, h, B, monkeypatch):
     """rowfused.hip (rs_sas_block_in/out and their backward) against the unfused kernel sequence: same saved
-    tensors, dropout masks and logits (training mode, p=0.2, ragged last row block); gradients within 5e-3."""
+    tensors, dropout masks and logits (training mode, p=0.2, ragged last row block); gradients within 1e-2."""
     import rbm_amd  # noqa: F401
     import rbm_amd.data as synth
     from rbm_amd import ops
@@ -174,8 +174,12 @@ def test_sas_fused_block_matches_unfused(V, T, d, L, h, B, monkeypatch):
     bad = [(k, i, int((u != v).sum().item()), (u.float() - v.float()).abs().max().item())
            for k in sa for i, (u, v) in enumerate(zip(sa[k], sb[k])) if not torch.equal(u, v)]
     assert not bad, bad
-    assert torch.equal(xa, xb) and torch.equal(pa, pb) and torch.equal(na, nb)
-    # backward: fused LN reductions / bf16 roundings differ in order from the unfused kernels
+    assert torch.equal(xa, xb)
+    # the fused head's dot products sum in another order than rs_sampled_logits_fwd
+    assert rel(pa.cpu().numpy(), pb.cpu().numpy()) < 1e-5 and rel(na.cpu().numpy(), nb.cpu().numpy()) < 1e-5
+    # backward: fused LN reductions / bf16 roundings differ in order from the unfused kernels, and the
+    # fused head keeps df in fp32 where the unfused path rounds it to bf16 (accuracy vs the reference:
+    # test_sas_bf16_matches_reference, test_hr_gpu, test_curves_gpu)
     fl = eng.flat
     gfa = {n: fl.view(n, ga).cpu().numpy() for n in fl.names}
     gfb = {n: fl.view(n, gb).cpu().numpy() for n in fl.names}
@@ -183,5 +187,5 @@ def test_sas_fused_block_matches_unfused(V, T, d, L, h, B, monkeypatch):
         u, v = gfa[n], gfb[n]
         if n.endswith("in_proj_bias"):      # key-bias gradient: analytically zero, bf16 noise in both
             u, v = np.concatenate([u[:d], u[2 * d:]]), np.concatenate([v[:d], v[2 * d:]])
-        assert rel(u, v) < 5e-3, (n, rel(u, v))
+        assert rel(u, v) < 1e-2, (n, rel(u, v))
     assert (sa["h1"][0] == 0).float().mean().item() > 0.5 * 0.2   # relu + dropout zeros present
