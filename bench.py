@@ -253,7 +253,8 @@ def main():
         run = trainer.step
     else:
         trainer.capture(*batches[0])
-        run = trainer.replay
+        batches = [(torch.stack(b),) for b in batches]     # one device copy per replay (replay_packed)
+        run = trainer.replay_packed
     for i in range(args.warmup):
         loss = run(*batches[i % len(batches)])
     torch.cuda.synchronize()

@@ -186,10 +186,13 @@ int rs_scatter_rows(int dtype, const void* src, int64_t lds, int64_t d, const in
  * data-parallel step all-reduces UNnormalised gradients plus the valid-position count and
  * divides here, so the summed gradient equals the single-device mean's).  rs_adam_step then
  * updates (grad scaled by state[3])
- * p, m, v (and writes the bf16 copy of p to p_bf16 when non-null). */
-int rs_adam_prepare(double* state, const float* hyper, const float* grad_divisor, void* stream);
-int rs_adam_step(int64_t n, float* p, const float* g, float* m, float* v, void* p_bf16,
-                 const double* state, const float* hyper, void* stream);
+ * p, m, v (and writes the bf16 copy of p to p_bf16 when non-null); zero_grad != 0 also clears g
+ * (the next step's accumulation starts from zero without a separate fill).  rs_adam_prepare
+ * also advances *seed_base when non-null (the next step's dropout masks, as rs_seed_advance). */
+int rs_adam_prepare(double* state, const float* hyper, const float* grad_divisor, uint64_t* seed_base,
+                    void* stream);
+int rs_adam_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16,
+                 const double* state, const float* hyper, int zero_grad, void* stream);
 
 /* dst_bf16[i] = bf16(src[i]) */
 int rs_cast_bf16(int64_t n, const float* src, void* dst, void* stream);

@@ -93,16 +93,31 @@ __global__ __launch_bounds__(256) void embed_bwd_pos_v_kernel(const int64_t* __r
 #pragma unroll
   for (int j = 0; j < V; ++j) acc[j] = 0.f;
   if (cc * V < d) {
-    for (int64_t b = rg; b < nb; b += RG) {
-      const int64_t r = b * T_ + t;
-      if (mode == 0 && ids[r] == 0) continue;
-      float g[V];
-      load_chunk<T>(g, dx + r * d + cc * V);
+    // U rows per iteration, every load issued before any use (a branch around a load on the
+    // row's id would make hipcc wait for each load in turn)
+    constexpr int U = 8;
+    const uint32_t s32 = seed32(seed);
+    for (int64_t b0 = rg; b0 < nb; b0 += (int64_t)RG * U) {
+      float g[U][V];
+      bool keep[U];
 #pragma unroll
-      for (int j = 0; j < V; ++j) {
-        float x = g[j];
-        if (drop_p > 0.f) x *= drop_mul(drop_p, seed, (uint64_t)(r * d + cc * V + j));
-        acc[j] += x;
+      for (int u = 0; u < U; ++u) {
+        const int64_t b = b0 + (int64_t)u * RG;
+        const int64_t r = (b < nb ? b : nb - 1) * T_ + t;
+        keep[u] = b < nb && (mode != 0 || ids[r] != 0);
+        load_chunk<T>(g[u], dx + r * d + cc * V);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t r = (b0 + (int64_t)u * RG) * T_ + t;
+        float dm[V];
+#pragma unroll
+        for (int j = 0; j < V; j += 2) {
+          if (drop_p > 0.f) drop_mul2(drop_p, s32, (uint64_t)(r * d + cc * V + j), dm[j], dm[j + 1]);
+          else dm[j] = dm[j + 1] = 1.f;
+        }
+#pragma unroll
+        for (int j = 0; j < V; ++j) acc[j] += keep[u] ? g[u][j] * dm[j] : 0.f;
       }
     }
   }

@@ -239,12 +239,13 @@ struct GradArgs {
   float* dtable;
 };
 
-// one block per chunk of CH sorted entries
+// one block per chunk of CH sorted entries.  Dependent global round trips: (keys, entries) ->
+// (contribution rows, key bounds, the table rows of run heads) -> stores.
 template <int D>
 __global__ __launch_bounds__(256) void item_chunk_kernel(GradArgs a) {
-  constexpr int TPE = D / 8, EPP = 256 / TPE;   // threads per entry row, entry rows per pass
-  __shared__ __attribute__((aligned(16))) float rowsum[CH][D];
-  __shared__ uint32_t skey[CH], sent[CH];
+  constexpr int TPE = D / 8, EPP = 256 / TPE, NPASS = CH / EPP;   // threads per entry row, rows per pass
+  __shared__ __attribute__((aligned(16))) float rowsum[CH][D + 4];   // +4: rows start on different banks
+  __shared__ uint32_t skey[CH + 1], sent[CH];
   __shared__ int kst[CH], ken[CH];
   const int tid = threadIdx.x;
   const int64_t base = (int64_t)blockIdx.x * CH;
@@ -252,43 +253,50 @@ __global__ __launch_bounds__(256) void item_chunk_kernel(GradArgs a) {
   const bool drop = a.drop_p > 0.f;
   const uint32_t s32 = drop ? seed32(eff_seed(a.salt, a.seed_base)) : 0u;
   if (tid < CH) {
-    const uint32_t k = tid < cnt ? a.sk[base + tid] : 0xffffffffu;
-    const uint32_t e = tid < cnt ? a.sv[base + tid] : 0u;
-    skey[tid] = k;
-    sent[tid] = e;
-    kst[tid] = tid < cnt ? a.start[k] : 0;
-    ken[tid] = tid < cnt ? a.start[k + 1] : 0;
+    skey[tid + 1] = tid < cnt ? a.sk[base + tid] : 0xffffffffu;
+    sent[tid] = tid < cnt ? a.sv[base + tid] : 0u;
   }
+  if (tid == 0) skey[0] = 0xfffffffeu;   // sentinel: entry 0 always starts a run
   __syncthreads();
-  // contribution rows (all loads of a pass issued before use)
+  if (tid < cnt) {                        // key bounds, consumed only by the emit pass
+    const uint32_t k = skey[tid + 1];
+    kst[tid] = a.start[k];
+    ken[tid] = a.start[k + 1];
+  }
+  // contribution rows + the current table rows of run heads (prefetched for the emit pass)
+  float4 tab[NPASS][2];
 #pragma unroll
-  for (int p0 = 0; p0 < CH; p0 += EPP) {
-    const int j = p0 + tid / TPE, c0 = (tid % TPE) * 8;
+  for (int ps = 0; ps < NPASS; ++ps) {
+    const int j = ps * EPP + tid / TPE, c0 = (tid % TPE) * 8;
     float v[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) v[q] = 0.f;
-    if (j < cnt) {
+    tab[ps][0] = tab[ps][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const uint32_t key = skey[j + 1];
+    if (j < cnt && key != 0) {
       const uint32_t e = sent[j];
-      const uint32_t key = skey[j];
       const int src = (int)(e / (uint32_t)a.rows);
       const int64_t m = (int64_t)e - (int64_t)src * a.rows;
-      if (key != 0) {
-        if (src == 0) {
-          load_chunk<__bf16>(v, a.dx + m * D + c0);
-          float dm[8];
+      if (src == 0) {
+        load_chunk<__bf16>(v, a.dx + m * D + c0);
+        float dm[8];
 #pragma unroll
-          for (int q = 0; q < 8; q += 2) {
-            if (drop) drop_mul2(a.drop_p, s32, (uint64_t)(m * D + c0 + q), dm[q], dm[q + 1]);
-            else dm[q] = dm[q + 1] = 1.f;
-          }
-#pragma unroll
-          for (int q = 0; q < 8; ++q) v[q] = v[q] * a.scale * dm[q];
-        } else {
-          const float w = src == 1 ? a.w1[m] : a.w2[m];
-          load_chunk<__bf16>(v, a.f + m * D + c0);
-#pragma unroll
-          for (int q = 0; q < 8; ++q) v[q] *= w;
+        for (int q = 0; q < 8; q += 2) {
+          if (drop) drop_mul2(a.drop_p, s32, (uint64_t)(m * D + c0 + q), dm[q], dm[q + 1]);
+          else dm[q] = dm[q + 1] = 1.f;
         }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = v[q] * a.scale * dm[q];
+      } else {
+        const float w = src == 1 ? a.w1[m] : a.w2[m];
+        load_chunk<__bf16>(v, a.f + m * D + c0);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] *= w;
+      }
+      if (skey[j] != key) {
+        const float4* t = reinterpret_cast<const float4*>(a.dtable + (int64_t)key * D + c0);
+        tab[ps][0] = t[0];
+        tab[ps][1] = t[1];
       }
     }
     *reinterpret_cast<float4*>(&rowsum[j][c0]) = make_float4(v[0], v[1], v[2], v[3]);
@@ -297,29 +305,38 @@ __global__ __launch_bounds__(256) void item_chunk_kernel(GradArgs a) {
   __syncthreads();
   // per-column run sums in entry order, stored at the run's first row
   if (tid < D) {
+    // the column's CH values into registers first (the run-total stores below alias rowsum, so
+    // loads interleaved with them would be issued one at a time)
     const int c = tid;
+    float col[CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) col[j] = rowsum[j][c];
     float acc = 0.f;
     int rs = 0;
-    for (int j = 0; j < cnt; ++j) {
-      acc += rowsum[j][c];
-      if (j + 1 < cnt && skey[j + 1] == skey[j]) continue;
-      rowsum[rs][c] = acc;
-      acc = 0.f;
-      rs = j + 1;
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      if (j < cnt) {
+        acc += col[j];
+        if (j + 1 == cnt || skey[j + 2] != skey[j + 1]) {
+          rowsum[rs][c] = acc;
+          acc = 0.f;
+          rs = j + 1;
+        }
+      }
     }
   }
   __syncthreads();
   // emit: whole key in this chunk -> table row (sole writer); else the chunk's partial
 #pragma unroll
-  for (int p0 = 0; p0 < CH; p0 += EPP) {
-    const int j = p0 + tid / TPE, c0 = (tid % TPE) * 8;
-    if (j >= cnt || (j > 0 && skey[j - 1] == skey[j]) || skey[j] == 0) continue;
-    const uint32_t k = skey[j];
+  for (int ps = 0; ps < NPASS; ++ps) {
+    const int j = ps * EPP + tid / TPE, c0 = (tid % TPE) * 8;
+    const uint32_t k = skey[j + 1];
+    if (j >= cnt || skey[j] == k || k == 0) continue;
     const float4 r0 = *reinterpret_cast<const float4*>(&rowsum[j][c0]);
     const float4 r1 = *reinterpret_cast<const float4*>(&rowsum[j][c0 + 4]);
     if (kst[j] >= base && ken[j] <= base + cnt) {
       float4* t = reinterpret_cast<float4*>(a.dtable + (int64_t)k * D + c0);
-      float4 t0 = t[0], t1 = t[1];
+      float4 t0 = tab[ps][0], t1 = tab[ps][1];
       t0.x += r0.x; t0.y += r0.y; t0.z += r0.z; t0.w += r0.w;
       t1.x += r1.x; t1.y += r1.y; t1.z += r1.z; t1.w += r1.w;
       t[0] = t0;

@@ -10,8 +10,9 @@
 #include "common.h"
 #include "../../include/recsys_hip.h"
 
-__global__ void adam_prepare_kernel(double* state, const float* hyper, const float* divisor) {
+__global__ void adam_prepare_kernel(double* state, const float* hyper, const float* divisor, uint64_t* seed_base) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  if (seed_base) *seed_base += 1;   // next step's dropout masks (rs_seed_advance folded in)
   state[3] = divisor ? 1.0 / (double)divisor[0] : 1.0;
   const double step = state[0] + 1.0;
   state[0] = step;
@@ -23,10 +24,10 @@ __global__ void adam_prepare_kernel(double* state, const float* hyper, const flo
 }
 
 template <bool BF16OUT>
-__global__ __launch_bounds__(256) void adam_step_kernel(int64_t n, float* __restrict__ p, const float* __restrict__ g,
+__global__ __launch_bounds__(256) void adam_step_kernel(int64_t n, float* __restrict__ p, float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v,
                                                         __bf16* __restrict__ pb, const double* __restrict__ state,
-                                                        const float* __restrict__ hyper) {
+                                                        const float* __restrict__ hyper, int zero_grad) {
   const float b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
   const float step_size = (float)state[1];
   const float bc2s = (float)state[2];
@@ -50,6 +51,7 @@ __global__ __launch_bounds__(256) void adam_step_kernel(int64_t n, float* __rest
     reinterpret_cast<float4*>(p)[i] = pp;
     reinterpret_cast<float4*>(m)[i] = mm;
     reinterpret_cast<float4*>(v)[i] = vv;
+    if (zero_grad) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (BF16OUT) {
       bf16x4 o;
       o[0] = (__bf16)P[0]; o[1] = (__bf16)P[1]; o[2] = (__bf16)P[2]; o[3] = (__bf16)P[3];
@@ -66,6 +68,7 @@ __global__ __launch_bounds__(256) void adam_step_kernel(int64_t n, float* __rest
     const float denom = sqrtf(v[j]) / bc2s + eps;
     p[j] = p[j] - step_size * (m[j] / denom);
     if (BF16OUT) pb[j] = (__bf16)p[j];
+    if (zero_grad) g[j] = 0.f;
   }
 }
 
@@ -153,22 +156,24 @@ __global__ __launch_bounds__(256) void dropout_rowmask_kernel(const T* __restric
 
 extern "C" {
 
-int rs_adam_prepare(double* state, const float* hyper, const float* grad_divisor, void* stream) {
-  hipLaunchKernelGGL(adam_prepare_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, state, hyper, grad_divisor);
+int rs_adam_prepare(double* state, const float* hyper, const float* grad_divisor, uint64_t* seed_base,
+                    void* stream) {
+  hipLaunchKernelGGL(adam_prepare_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, state, hyper, grad_divisor,
+                     seed_base);
   return (int)hipGetLastError();
 }
 
-int rs_adam_step(int64_t n, float* p, const float* g, float* m, float* v, void* p_bf16, const double* state,
-                 const float* hyper, void* stream) {
+int rs_adam_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, const double* state,
+                 const float* hyper, int zero_grad, void* stream) {
   if (n <= 0 || ((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16) return RS_ERR_ARG;
   const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(cdiv(n / 4, 256), 8192));
   hipStream_t s = (hipStream_t)stream;
   if (p_bf16)
     hipLaunchKernelGGL((adam_step_kernel<true>), dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
-                       (__bf16*)p_bf16, state, hyper);
+                       (__bf16*)p_bf16, state, hyper, zero_grad);
   else
     hipLaunchKernelGGL((adam_step_kernel<false>), dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
-                       (__bf16*)nullptr, state, hyper);
+                       (__bf16*)nullptr, state, hyper, zero_grad);
   return (int)hipGetLastError();
 }
 

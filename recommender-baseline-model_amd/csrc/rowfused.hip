@@ -104,28 +104,43 @@ __device__ __forceinline__ void tile_ln(const bf16* in, bf16* out, const float* 
   }
 }
 
+// B fragments of a wave's output columns [c0w, c0w + 16 FN) for the whole K: rows of the torch
+// [N][K] weight, 16 bytes per lane per fragment, straight from L2.  Loaded ahead of the GEMM that
+// uses them (the kernels below issue the next GEMM's fragments under the current phase).
+template <int K, int FN>
+struct BFr {
+  bf16x8 b[K / 32][FN];
+  __device__ __forceinline__ void load(const bf16* __restrict__ W, int64_t ldw, int c0w, int lane) {
+    const int g = lane >> 4, cl = lane & 15;
+#pragma unroll
+    for (int ks = 0; ks < K / 32; ++ks)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        b[ks][j] = *reinterpret_cast<const bf16x8*>(W + (int64_t)(c0w + 16 * j + cl) * ldw + 32 * ks + 8 * g);
+  }
+};
+
 // acc[i][j] (rows 16i + 4g + r, columns c0w + 16j + cl) += A_tile[64 x K] . W[n][k]^T
 template <int K, int FN>
-__device__ __forceinline__ void tile_mm(const bf16* A, int lda, const bf16* __restrict__ W, int64_t ldw, int c0w,
-                                        f32x4 (&acc)[4][FN], int lane) {
+__device__ __forceinline__ void tile_mm_b(const bf16* A, int lda, const BFr<K, FN>& B, f32x4 (&acc)[4][FN],
+                                          int lane) {
   const int g = lane >> 4, cl = lane & 15;
-  constexpr int KS = K / 32;
-  bf16x8 b[KS][FN];
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-      b[ks][j] = *reinterpret_cast<const bf16x8*>(W + (int64_t)(c0w + 16 * j + cl) * ldw + 32 * ks + 8 * g);
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
+  for (int ks = 0; ks < K / 32; ++ks) {
     bf16x8 a[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const bf16x8*>(A + (16 * i + cl) * lda + 32 * ks + 8 * g);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[ks][j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], B.b[ks][j], acc[i][j], 0, 0, 0);
   }
+}
+
+template <int FN>
+__device__ __forceinline__ void load_bias(float (&bv)[FN], const float* __restrict__ bias, int c0w, int lane) {
+#pragma unroll
+  for (int j = 0; j < FN; ++j) bv[j] = bias[c0w + 16 * j + (lane & 15)];
 }
 
 // drop_mul (common.h) with the site seed already folded to 32 bits
@@ -162,22 +177,31 @@ __global__ __launch_bounds__(256) void sas_block_in_kernel(InArgs a) {
   bf16* S = smem + 2 * Tile<D>::ELEMS;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
   const int64_t row0 = (int64_t)blockIdx.x * BMR;
+  constexpr int FQ = D / 64, FKV = 2 * D / 64;
+  BFr<D, FQ> wq;
+  float bqv[FQ];
+  wq.load(a.Wq, D, wave * (D / 4), lane);
+  load_bias(bqv, a.bq, wave * (D / 4), lane);
   tile_load<D>(X, a.x, a.ldx, row0, a.M, tid);
   __syncthreads();
   tile_ln<D>(X, Qt, a.ln_w, a.ln_b, a.eps, a.mean, a.rstd, row0, a.M, tid);
   __syncthreads();
   tile_store<D>(Qt, a.Q, D, row0, a.M, tid);
+  BFr<D, FKV> wkv;
+  float bkvv[FKV];
   // q = Q Wq^T + bq     (wave w: columns [wD/4, (w+1)D/4))
   {
-    constexpr int FN = D / 64;
+    constexpr int FN = FQ;
     f32x4 acc[4][FN];
     acc_zero(acc);
     const int c0w = wave * (D / 4);
-    tile_mm<D, FN>(Qt, LD, a.Wq, D, c0w, acc, lane);
+    tile_mm_b<D, FN>(Qt, LD, wq, acc, lane);
+    wkv.load(a.Wkv, D, wave * (2 * D / 4), lane);     // next GEMM's weights, under this epilogue
+    load_bias(bkvv, a.bkv, wave * (2 * D / 4), lane);
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int c = c0w + 16 * j + cl;
-      const float bb = a.bq[c];
+      const float bb = bqv[j];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -192,14 +216,14 @@ __global__ __launch_bounds__(256) void sas_block_in_kernel(InArgs a) {
     f32x4 acc[4][FN];
     acc_zero(acc);
     const int c0w = wave * (2 * D / 4);
-    tile_mm<D, FN>(X, LD, a.Wkv, D, c0w, acc, lane);
+    tile_mm_b<D, FN>(X, LD, wkv, acc, lane);
     __syncthreads();   // X and S are free once every wave is past its MFMAs and the q store
     bf16* dst = wave < 2 ? S : X;
     const int cb = wave < 2 ? 0 : D;
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int c = c0w + 16 * j + cl;
-      const float bb = a.bkv[c];
+      const float bb = bkvv[j];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -236,17 +260,29 @@ __global__ __launch_bounds__(256) void sas_block_out_kernel(OutArgs a) {
   const bool drop = a.drop_p > 0.f;
   const uint32_t s1 = drop ? seed32(eff_seed(a.salt1, a.seed_base)) : 0u;
   const uint32_t s2 = drop ? seed32(eff_seed(a.salt2, a.seed_base)) : 0u;
+  __shared__ bool keep_s[BMR];
+  // everything the block reads besides its two input tiles is requested up front: the first two
+  // GEMMs' weight fragments, the biases, the timeline-mask ids
+  BFr<D, FN> wo, w1, w2;
+  float bov[FN], b1v[FN], b2v[FN];
+  wo.load(a.Wo, D, c0w, lane);
+  w1.load(a.W1, D, c0w, lane);
+  load_bias(bov, a.bo, c0w, lane);
+  load_bias(b1v, a.b1, c0w, lane);
+  load_bias(b2v, a.b2, c0w, lane);
+  if (tid < BMR) keep_s[tid] = row0 + tid < a.M && a.ids[row0 + tid < a.M ? row0 + tid : 0] != 0;
   tile_load<D>(T0, a.o, D, row0, a.M, tid);
   tile_load<D>(T1, a.Q, D, row0, a.M, tid);
   __syncthreads();
   f32x4 acc[4][FN];
   // x1 = Q + o Wo^T + bo  -> T2
   acc_zero(acc);
-  tile_mm<D, FN>(T0, LD, a.Wo, D, c0w, acc, lane);
+  tile_mm_b<D, FN>(T0, LD, wo, acc, lane);
+  w2.load(a.W2, D, c0w, lane);
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int c = c0w + 16 * j + cl;
-    const float bb = a.bo[c];
+    const float bb = bov[j];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -263,11 +299,11 @@ __global__ __launch_bounds__(256) void sas_block_out_kernel(OutArgs a) {
   tile_store<D>(T0, a.z, D, row0, a.M, tid);
   // h1 = relu(drop(z W1^T + b1)) -> T1
   acc_zero(acc);
-  tile_mm<D, FN>(T0, LD, a.W1, D, c0w, acc, lane);
+  tile_mm_b<D, FN>(T0, LD, w1, acc, lane);
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int c = c0w + 16 * j + cl;
-    const float bb = a.b1[c];
+    const float bb = b1v[j];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -282,20 +318,20 @@ __global__ __launch_bounds__(256) void sas_block_out_kernel(OutArgs a) {
   tile_store<D>(T1, a.h1, D, row0, a.M, tid);
   // x' = (drop(h1 W2^T + b2) + z) * (ids != 0) -> T2
   acc_zero(acc);
-  tile_mm<D, FN>(T1, LD, a.W2, D, c0w, acc, lane);
+  tile_mm_b<D, FN>(T1, LD, w2, acc, lane);
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int rr = 16 * i + 4 * g + r;
       const int64_t m = row0 + rr;
-      const bool keep = m < a.M && a.ids[m < a.M ? m : 0] != 0;
+      const bool keep = keep_s[rr];
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int c = c0w + 16 * j + cl;
         const float dm = drop ? drop_mul32(a.drop_p, s2, (uint64_t)(m * D + c)) : 1.0f;
         // fma as rs_gemm's epilogue (explicit there too): one rounding of drop(v) + z
-        const float v = __builtin_fmaf(acc[i][j][r] + a.b2[c], dm, (float)T0[rr * LD + c]);
+        const float v = __builtin_fmaf(acc[i][j][r] + b2v[j], dm, (float)T0[rr * LD + c]);
         T2[rr * LD + c] = (bf16)(keep ? v : 0.f);
       }
     }
@@ -402,6 +438,9 @@ __global__ __launch_bounds__(256) void sas_block_out_bwd_kernel(OutBwdArgs a) {
   const bool drop = a.drop_p > 0.f;
   const uint32_t s1 = drop ? seed32(eff_seed(a.salt1, a.seed_base)) : 0u;
   const uint32_t s2 = drop ? seed32(eff_seed(a.salt2, a.seed_base)) : 0u;
+  BFr<D, FN> w2t, w1t, wot;
+  w2t.load(a.W2T, D, c0w, lane);
+  w1t.load(a.W1T, D, c0w, lane);
   // 1. dzres = dxn * mask -> T0; dy2 = drop2(dzres) -> T1 (+ global); h1 -> T2
   {
     bf16x8 v[PT], hv[PT];
@@ -439,7 +478,8 @@ __global__ __launch_bounds__(256) void sas_block_out_bwd_kernel(OutBwdArgs a) {
   f32x4 acc[4][FN];
   // 2. da1 = relu'(h1) * drop1(dy2 W2) -> T2 in place of h1
   acc_zero(acc);
-  tile_mm<D, FN>(T1, LD, a.W2T, D, c0w, acc, lane);
+  tile_mm_b<D, FN>(T1, LD, w2t, acc, lane);
+  wot.load(a.WoT, D, c0w, lane);
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int c = c0w + 16 * j + cl;
@@ -464,7 +504,7 @@ __global__ __launch_bounds__(256) void sas_block_out_bwd_kernel(OutBwdArgs a) {
     xv[i] = *reinterpret_cast<const bf16x8*>(a.x1 + m * D + c);
   }
   acc_zero(acc);
-  tile_mm<D, FN>(T2, LD, a.W1T, D, c0w, acc, lane);
+  tile_mm_b<D, FN>(T2, LD, w1t, acc, lane);
 #pragma unroll
   for (int i = 0; i < PT; ++i) {
     const int ch = tid + i * 256, r = ch / CPR, c = (ch % CPR) * 8;
@@ -500,7 +540,7 @@ __global__ __launch_bounds__(256) void sas_block_out_bwd_kernel(OutBwdArgs a) {
   tile_store<D>(T2, a.dx1, D, row0, a.M, tid);
   // 5. dout = dx1 Wo
   acc_zero(acc);
-  tile_mm<D, FN>(T2, LD, a.WoT, D, c0w, acc, lane);
+  tile_mm_b<D, FN>(T2, LD, wot, acc, lane);
   __syncthreads();   // T0 (partials scratch) free
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
@@ -533,6 +573,9 @@ __global__ __launch_bounds__(256) void sas_block_in_bwd_kernel(InBwdArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
   const int64_t row0 = (int64_t)blockIdx.x * BMR;
   const int c0w = wave * (D / 4);
+  BFr<D, FN> wk, wv, wq;
+  wk.load(a.WinT + D, a.ldwt, c0w, lane);
+  wv.load(a.WinT + 2 * D, a.ldwt, c0w, lane);
   // 1. dx_kv = dk Wk + dv Wv -> T2
   tile_load<D>(T0, a.dkv, 2 * D, row0, a.M, tid);
   tile_load<D>(T1, a.dkv + D, 2 * D, row0, a.M, tid);
@@ -552,8 +595,9 @@ __global__ __launch_bounds__(256) void sas_block_in_bwd_kernel(InBwdArgs a) {
   }
   f32x4 acc[4][FN];
   acc_zero(acc);
-  tile_mm<D, FN>(T0, LD, a.WinT + D, a.ldwt, c0w, acc, lane);
-  tile_mm<D, FN>(T1, LD, a.WinT + 2 * D, a.ldwt, c0w, acc, lane);
+  tile_mm_b<D, FN>(T0, LD, wk, acc, lane);
+  tile_mm_b<D, FN>(T1, LD, wv, acc, lane);
+  wq.load(a.WinT, a.ldwt, c0w, lane);
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int c = c0w + 16 * j + cl;
@@ -579,7 +623,7 @@ __global__ __launch_bounds__(256) void sas_block_in_bwd_kernel(InBwdArgs a) {
     xv[i] = *reinterpret_cast<const bf16x8*>(a.x + m * D + c);
   }
   acc_zero(acc);
-  tile_mm<D, FN>(T0, LD, a.WinT, a.ldwt, c0w, acc, lane);
+  tile_mm_b<D, FN>(T0, LD, wq, acc, lane);
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int c = c0w + 16 * j + cl;

@@ -156,6 +156,7 @@ class BERTEngine:
             flat.enable_bf16()
         self.ws = Workspace(self.dev)
         self.seed_base = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self.external_seed = False    # True: the fused train step's optimizer advances seed_base
         salt0 = int(torch.randint(0, 2 ** 62, (1,)).item())
         self.salt = {"emb": site_salt(salt0, 0)}
         for i in range(self.L):
@@ -198,7 +199,7 @@ class BERTEngine:
         M, d, H, Dh, L, Fd = B * T, self.d, self.H, self.Dh, self.L, self.F
         p = self.p if training else 0.0
         hp = self.hp if training else 0.0
-        if p > 0 or hp > 0:
+        if (p > 0 or hp > 0) and not self.external_seed:
             ops.seed_advance(self.seed_base)
         sb = self.seed_base.clone() if clone_seed else self.seed_base
         e = self._buf

@@ -149,6 +149,7 @@ class SASEngine:
             flat.enable_bf16()
         self.ws = Workspace(self.dev)
         self.seed_base = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self.external_seed = False    # True: the fused train step's optimizer advances seed_base
         salt0 = int(torch.randint(0, 2 ** 62, (1,)).item())
         self.salt = {"emb": site_salt(salt0, 0)}
         for i in range(self.L):
@@ -175,7 +176,7 @@ class SASEngine:
         B, T = ids.shape
         M, d, H, Dh, L = B * T, self.d, self.H, self.Dh, self.L
         p = self.p if training else 0.0
-        if p > 0:
+        if p > 0 and not self.external_seed:
             ops.seed_advance(self.seed_base)
         # this step's masks, replayed by backward (the fused step runs backward before the next
         # advance, so it reads the live word; the autograd API may interleave forwards: snapshot)
@@ -420,11 +421,12 @@ class SASEngine:
 
     @staticmethod
     def _wgrad_rows(M, tiles):
-        """rows per split of the grouped weight-gradient launch: ~480 workgroups (2 per CU)."""
+        """rows per split of the grouped weight-gradient launch: ~256 workgroups (the 128x128-tile kernel
+        runs one per CU), fewer splits also shrink the partial slab the reduction reads."""
         env = os.environ.get("RS_WGRAD_ROWS")
         if env:
             return int(env)
-        splits = max(1, 480 // tiles)
+        splits = max(1, 256 // tiles)
         return max(64, -(-(-(-M // splits)) // 64) * 64)
 
     # ---- eval ----------------------------------------------------------------------

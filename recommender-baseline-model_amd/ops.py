@@ -201,12 +201,13 @@ def scatter_rows(src, rank, dst):
     call("rs_scatter_rows", dtype_code(src), ptr(src), ld(src), d, ptr(rank), n, ptr(dst), ld(dst), stream())
 
 
-def adam_prepare(state, hyper, grad_divisor=None):
-    call("rs_adam_prepare", ptr(state), ptr(hyper), ptr(grad_divisor), stream())
+def adam_prepare(state, hyper, grad_divisor=None, seed_base=None):
+    call("rs_adam_prepare", ptr(state), ptr(hyper), ptr(grad_divisor), ptr(seed_base), stream())
 
 
-def adam_step(p, g, m, v, p_bf16, state, hyper):
-    call("rs_adam_step", p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), ptr(p_bf16), ptr(state), ptr(hyper), stream())
+def adam_step(p, g, m, v, p_bf16, state, hyper, zero_grad=False):
+    call("rs_adam_step", p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), ptr(p_bf16), ptr(state), ptr(hyper),
+         int(zero_grad), stream())
 
 
 def cast_bf16(src, dst):

@@ -41,9 +41,12 @@ class FusedAdam:
         """StepLR hook (BS/trainers/base.py:40,87): lives on the device, so graph replays see it."""
         self.hyper[0] = lr
 
-    def step(self, grad_divisor=None):
-        ops.adam_prepare(self.state, self.hyper, grad_divisor)
-        ops.adam_step(self.flat.data, self.flat.grad, self.m, self.v, self.flat.bf16, self.state, self.hyper)
+    def step(self, grad_divisor=None, seed_base=None):
+        """One Adam update; also clears the gradient buffer (the next step accumulates from zero) and
+        advances the dropout step seed when given."""
+        ops.adam_prepare(self.state, self.hyper, grad_divisor, seed_base)
+        ops.adam_step(self.flat.data, self.flat.grad, self.m, self.v, self.flat.bf16, self.state, self.hyper,
+                      zero_grad=True)
 
 
 class FusedTrainStep:
@@ -58,6 +61,8 @@ class FusedTrainStep:
         self.engine = model.sas.engine() if self.kind == "sas" else model.engine()
         self.flat = self.engine.flat
         self.engine.sync_compute_weights()
+        self.engine.external_seed = True       # advanced by the optimizer kernel at the end of each step
+        self.flat.grad.zero_()                 # then kept zero by the optimizer (zero_grad)
         self.opt = FusedAdam(self.flat, lr=lr, weight_decay=weight_decay)
         self.pg = process_group
         self.dp = dpx.world() > 1 if dp is None else bool(dp)
@@ -78,7 +83,6 @@ class FusedTrainStep:
         return self.one if self.dp else local_count
 
     def _compute(self, *batch):
-        self.flat.grad.zero_()
         eng = self.engine
         if self.kind == "sas":
             seq, pos, neg = batch
@@ -108,12 +112,13 @@ class FusedTrainStep:
             dpx.allreduce_grads(self.flat.grad, self.pg, self.bucket_numel)
 
     def _update(self):
+        sb = self.engine.seed_base
         if self.dp:
-            self.opt.step(grad_divisor=self.flat.aux[dpx.COUNT:dpx.COUNT + 1])
             torch.div(self.flat.aux[dpx.LOSS_SUM:dpx.LOSS_SUM + 1], self.flat.aux[dpx.COUNT:dpx.COUNT + 1],
                       out=self.loss_val)
+            self.opt.step(grad_divisor=self.flat.aux[dpx.COUNT:dpx.COUNT + 1], seed_base=sb)
         else:
-            self.opt.step()
+            self.opt.step(seed_base=sb)
 
     # ---------------------------------------------------------------- one step
     def step(self, *batch):
@@ -127,7 +132,15 @@ class FusedTrainStep:
     # ---------------------------------------------------------------- HIP graphs
     def capture(self, *example_batch, warmup=2):
         """Capture the step into HIP graphs; example_batch fixes the shapes."""
-        self.static = [t.clone() for t in example_batch]
+        # one packed static buffer when the inputs share shape and dtype: replay_packed() then refills
+        # all of them with ONE device copy (the bench stacks its batches the same way)
+        same = all(t.shape == example_batch[0].shape and t.dtype == example_batch[0].dtype for t in example_batch)
+        if same:
+            self.packed = torch.stack([t for t in example_batch]).contiguous()
+            self.static = list(self.packed.unbind(0))
+        else:
+            self.packed = None
+            self.static = [t.clone() for t in example_batch]
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -149,6 +162,17 @@ class FusedTrainStep:
                 self._update()
             self.graphs = (g,)
         return self
+
+    def replay_packed(self, packed):
+        """replay() for a batch already stacked as one tensor [n_inputs, ...] (see capture)."""
+        if self.packed is None:
+            return self.replay(*packed.unbind(0))
+        self.packed.copy_(packed, non_blocking=True)
+        self.graphs[0].replay()
+        if self.dp:
+            self._exchange()
+            self.graphs[1].replay()
+        return self.loss_val if self.dp else self.loss_out[2:3]
 
     def replay(self, *batch):
         for dst, src in zip(self.static, batch):

@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--only", default="", help="time only the ops whose name contains this")
     a = ap.parse_args()
     c = SHAPES[a.config]
     B, T, d, V, H, ff = c["B"], c["T"], c["d"], c["V"], c["H"], c["ff"]
@@ -64,59 +65,60 @@ def main():
     sb = torch.zeros(1, dtype=torch.int64, device=dev)
     rows = []
 
-    def rec(name, us, nbytes, flops=0.0):
+    def run(name, fn, nbytes, flops=0.0):
+        if a.only and a.only not in name:
+            return
+        us = timeit(fn, a.reps)
         rows.append((name, us, nbytes / (us * 1e-6) / 1e9, flops / (us * 1e-6) / 1e12))
 
     mb = M * d * es
-    rec("linear_fwd d->d +bias", timeit(lambda: ops.linear_fwd(x, W, y, bias=bias), a.reps), 2 * mb, 2 * M * d * d)
-    rec("linear_fwd d->ff +bias+relu+drop", timeit(lambda: ops.linear_fwd(
-        x, Wff, yff, bias=bff, act=ops.ACT_RELU, drop_p=0.2, drop_seed=7, seed_base=sb, drop_ld=ff), a.reps),
+    run("linear_fwd d->d +bias",lambda: ops.linear_fwd(x, W, y, bias=bias), 2 * mb, 2 * M * d * d)
+    run("linear_fwd d->ff +bias+relu+drop",lambda: ops.linear_fwd(
+        x, Wff, yff, bias=bff, act=ops.ACT_RELU, drop_p=0.2, drop_seed=7, seed_base=sb, drop_ld=ff),
         mb + M * ff * es, 2 * M * d * ff)
-    rec("linear_fwd d->d +bias+drop+resid+rowmask", timeit(lambda: ops.linear_fwd(
-        x, W, y, bias=bias, drop_p=0.2, drop_seed=7, seed_base=sb, drop_ld=d, resid=z, rowmask_ids=ids), a.reps),
+    run("linear_fwd d->d +bias+drop+resid+rowmask",lambda: ops.linear_fwd(
+        x, W, y, bias=bias, drop_p=0.2, drop_seed=7, seed_base=sb, drop_ld=d, resid=z, rowmask_ids=ids),
         3 * mb, 2 * M * d * d)
-    rec("linear_dgrad d<-d", timeit(lambda: ops.linear_dgrad(y, W, z), a.reps), 2 * mb, 2 * M * d * d)
+    run("linear_dgrad d<-d",lambda: ops.linear_dgrad(y, W, z), 2 * mb, 2 * M * d * d)
     dW = torch.zeros(d, d, device=dev)
     db = torch.zeros(d, device=dev)
     for sk in (None, 16, 32, 64, 128):
         s = sk or ops.split_for(M, d, d)
         slab = torch.empty(s * (d * d + d), device=dev)
-        rec(f"linear_wgrad+bias split={s}", timeit(lambda: ops.linear_wgrad(y, x, dW, slab, db=db, split_k=s),
-                                                   a.reps), 2 * mb, 2 * M * d * d)
+        run(f"linear_wgrad+bias split={s}",lambda: ops.linear_wgrad(y, x, dW, slab, db=db, split_k=s), 2 * mb, 2 * M * d * d)
     gam, bet = torch.ones(d, device=dev), torch.zeros(d, device=dev)
     mu, ri = torch.empty(M, device=dev), torch.empty(M, device=dev)
-    rec("layernorm_fwd", timeit(lambda: ops.layernorm_fwd(x, gam, bet, 1e-8, y, mu, ri, 0), a.reps), 2 * mb)
+    run("layernorm_fwd",lambda: ops.layernorm_fwd(x, gam, bet, 1e-8, y, mu, ri, 0), 2 * mb)
     ws = torch.empty(2 * 512 * d, device=dev)
     dg, dbt = torch.zeros(d, device=dev), torch.zeros(d, device=dev)
-    rec("layernorm_bwd", timeit(lambda: ops.layernorm_bwd(x, y, gam, mu, ri, 1e-8, z, dg, dbt, ws, 0), a.reps),
+    run("layernorm_bwd",lambda: ops.layernorm_bwd(x, y, gam, mu, ri, 1e-8, z, dg, dbt, ws, 0),
         3 * mb)
     wsc = torch.empty(64 * d, device=dev)
-    rec("colsum", timeit(lambda: ops.colsum(y, db, wsc), a.reps), mb)
+    run("colsum",lambda: ops.colsum(y, db, wsc), mb)
     table = rn(V + 1, d)
     pe = rn(T, d)
-    rec("embed_fwd", timeit(lambda: ops.embed_fwd(0, ids, T, table, pe, math.sqrt(d), 0.2, 5, sb, x), a.reps), 2 * mb)
+    run("embed_fwd",lambda: ops.embed_fwd(0, ids, T, table, pe, math.sqrt(d), 0.2, 5, sb, x), 2 * mb)
     dtab = torch.zeros(V + 1, d, device=dev)
     dpos = torch.zeros(T, d, device=dev)
-    rec("embed_bwd (table atomics + pos)", timeit(lambda: ops.embed_bwd(0, ids, T, y, math.sqrt(d), 0.2, 5, sb, dtab,
-                                                                      dpos), a.reps), mb + M * d * 4)
-    rec("embed_bwd pos only", timeit(lambda: ops.embed_bwd(0, ids, T, y, math.sqrt(d), 0.2, 5, sb, None, dpos),
-                                     a.reps), mb)
+    run("embed_bwd (table atomics + pos)",lambda: ops.embed_bwd(0, ids, T, y, math.sqrt(d), 0.2, 5, sb, dtab,
+                                                                      dpos), mb + M * d * 4)
+    run("embed_bwd pos only",lambda: ops.embed_bwd(0, ids, T, y, math.sqrt(d), 0.2, 5, sb, None, dpos), mb)
     pl, nl = torch.empty(M, device=dev), torch.empty(M, device=dev)
-    rec("sampled_logits_fwd", timeit(lambda: ops.sampled_logits_fwd(x, table, pos, neg, pl, nl), a.reps), 3 * mb)
-    rec("sampled_logits_bwd", timeit(lambda: ops.sampled_logits_bwd(x, table, pos, neg, pl, nl, y, dtab), a.reps),
+    run("sampled_logits_fwd",lambda: ops.sampled_logits_fwd(x, table, pos, neg, pl, nl), 3 * mb)
+    run("sampled_logits_bwd",lambda: ops.sampled_logits_bwd(x, table, pos, neg, pl, nl, y, dtab),
         4 * mb + 2 * M * d * 4)
     Dh = d // H
     q, kv, o = rn(M, d), rn(M, 2 * d), rn(M, d)
     lse = torch.empty(B * H * T, device=dev)
     aflops = 2.0 * T * (T + 1) * Dh * B * H
-    rec("attn_fwd causal drop", timeit(lambda: ops.attn_fwd(B, T, H, Dh, q, kv[:, :d], kv[:, d:], o, lse,
-                                                            1 / math.sqrt(Dh), 0, ids, 0.2, 9, sb), a.reps),
+    run("attn_fwd causal drop",lambda: ops.attn_fwd(B, T, H, Dh, q, kv[:, :d], kv[:, d:], o, lse,
+                                                            1 / math.sqrt(Dh), 0, ids, 0.2, 9, sb),
         4 * mb, aflops)
     dq, dkv = rn(M, d), rn(M, 2 * d)
     wat = torch.empty(B * H * T, device=dev)
-    rec("attn_bwd causal drop", timeit(lambda: ops.attn_bwd(B, T, H, Dh, q, kv[:, :d], kv[:, d:], o, y, lse, dq,
+    run("attn_bwd causal drop",lambda: ops.attn_bwd(B, T, H, Dh, q, kv[:, :d], kv[:, d:], o, y, lse, dq,
                                                             dkv[:, :d], dkv[:, d:], 1 / math.sqrt(Dh), 0, ids, 0.2,
-                                                            9, sb, wat), a.reps), 8 * mb, 2.5 * aflops)
+                                                            9, sb, wat), 8 * mb, 2.5 * aflops)
     if a.config in ("cfg3", "cfg5"):
         V1 = V + 1
         R = 1792
@@ -125,23 +127,67 @@ def main():
         Wo = (0.05 * torch.randn(V1, d, device=dev, generator=g)).to(dt)
         bo = torch.zeros(V1, device=dev)
         lg = torch.empty(R, V1p, device=dev)[:, :V1]
-        rec("vocab logits fwd (fp32 out)", timeit(lambda: ops.linear_fwd(h, Wo, lg, bias=bo), a.reps),
+        run("vocab logits fwd (fp32 out)",lambda: ops.linear_fwd(h, Wo, lg, bias=bo),
             R * V1 * 4 + V1 * d * es, 2 * R * V1 * d)
         dl = torch.randn(R, V1p, device=dev, generator=g).to(dt)[:, :V1]
         dh = rn(R, d)
-        rec("vocab dgrad", timeit(lambda: ops.linear_dgrad(dl, Wo, dh), a.reps), R * V1 * es + V1 * d * es,
+        run("vocab dgrad",lambda: ops.linear_dgrad(dl, Wo, dh), R * V1 * es + V1 * d * es,
             2 * R * V1 * d)
         dWo = torch.zeros(V1, d, device=dev)
         slab_o = torch.empty(ops.wgrad_slab_numel(R, V1, d), device=dev)
-        rec("vocab wgrad+bias", timeit(lambda: ops.linear_wgrad(dl, h, dWo, slab_o, db=bo), a.reps),
+        run("vocab wgrad+bias",lambda: ops.linear_wgrad(dl, h, dWo, slab_o, db=bo),
             R * V1 * es + V1 * d * 4, 2 * R * V1 * d)
+    if d in (64, 128) and dt == torch.bfloat16:
+        # fused SAS row-block kernels, grouped weight gradients, item-table gradient, fused head
+        Win, bin_ = rn(3 * d, d), torch.randn(3 * d, device=dev)
+        Q, qq, kvb, oo = rn(M, d), rn(M, d), rn(M, 2 * d), rn(M, d)
+        x1, zz, h1, xn = rn(M, d), rn(M, d), rn(M, d), rn(M, d)
+        m1_, r1_ = torch.zeros(M, device=dev), torch.ones(M, device=dev)
+        run("fused block_in", lambda: ops.sas_block_in(x, gam, bet, 1e-8, Q, m1_, r1_, Win[:d], bin_[:d], qq, Win[d:],
+                                                        bin_[d:], kvb), 6 * mb)
+        run("fused block_out", lambda: ops.sas_block_out(oo, Q, W, bias, x1, gam, bet, 1e-8, zz, m1_, r1_, W, bias, h1,
+                                                          W, bias, xn, ids, 0.2, 3, 4, sb), 6 * mb)
+        WT, WinT = rn(d, d), rn(d, 3 * d)
+        dy2, da1, dx1, do_ = rn(M, d), rn(M, d), rn(M, d), rn(M, d)
+        part = torch.empty(2 * d * (-(-M // 64)), device=dev)
+        run("fused block_out_bwd", lambda: ops.sas_block_out_bwd(y, ids, h1, x1, m1_, r1_, gam, WT, WT, WT, dy2, da1,
+                                                                  dx1, do_, part, 0.2, 3, 4, sb), 8 * mb)
+        dqkv = rn(M, 2 * d)
+        run("fused block_in_bwd", lambda: ops.sas_block_in_bwd(qq, dqkv, dx1, x, m1_, r1_, gam, WinT, z, part),
+            6 * mb)
+        probs = []
+        for _ in range(2):
+            probs += [(dy2, h1, torch.zeros(d, d, device=dev), torch.zeros(d, device=dev)),
+                      (da1, zz, torch.zeros(d, d, device=dev), torch.zeros(d, device=dev)),
+                      (dx1, oo, torch.zeros(d, d, device=dev), torch.zeros(d, device=dev)),
+                      (qq, Q, torch.zeros(d, d, device=dev), torch.zeros(d, device=dev)),
+                      (dqkv, x, torch.zeros(2 * d, d, device=dev), torch.zeros(2 * d, device=dev))]
+        for rows_ in (640, 1280, 2560):
+            wsl = torch.empty(ops.wgrad_grouped_slab_numel([(d, d)] * 8 + [(2 * d, d)] * 2, M, rows_), device=dev)
+            run(f"wgrad_grouped 10 problems rows={rows_}", lambda: ops.wgrad_grouped(probs, M, rows_, wsl),
+                24 * mb, 2 * M * d * d * 12)
+        zw = 1.0 / torch.arange(1, V + 1, dtype=torch.float64) ** 1.1
+        kk = [torch.multinomial(zw, M, replacement=True, generator=torch.Generator().manual_seed(5 + i)).add(1)
+              .view(B, T).to(dev) for i in range(3)]
+        iws = torch.empty(ops.item_index_ws_bytes(3, M, V + 1, d), dtype=torch.uint8, device=dev)
+        run("item_index_build (zipf)", lambda: ops.item_index_build(kk, V + 1, d, iws), 3 * M * 8)
+        ops.item_index_build(kk, V + 1, d, iws)
+        dtab2 = torch.zeros(V + 1, d, device=dev)
+        run("item_grad (zipf)", lambda: ops.item_grad(iws, 3, M, y, math.sqrt(d), 0.2, 5, sb, x, pl, nl, dtab2),
+            3 * mb)
+        hp = torch.empty(3 * (-(-M // 64)), device=dev)
+        run("head_fwd", lambda: ops.sas_head_fwd(x, gam, bet, 1e-8, y, mu, ri, table, pos, neg, pl, nl, hp), 4 * mb)
+        lout = torch.empty(4, device=dev)
+        dpl_, dnl_ = torch.empty(M, device=dev), torch.empty(M, device=dev)
+        run("head_bwd", lambda: ops.sas_head_bwd(hp, None, lout, pl, nl, None, None, dpl_, dnl_, pos, neg, table, x,
+                                                 gam, mu, ri, z, part), 4 * mb)
     n = 662400
     p, gg, m1, v1 = (torch.randn(n, device=dev) for _ in range(4))
     v1.abs_()
     pbf = torch.empty(n, dtype=torch.bfloat16, device=dev)
     st = torch.tensor([1.0, 0.001, 1.0, 1.0], dtype=torch.float64, device=dev)
     hy = torch.tensor([1e-3, 0.9, 0.999, 1e-8, 0.0], device=dev)
-    rec("adam_step (662k params)", timeit(lambda: ops.adam_step(p, gg, m1, v1, pbf, st, hy), a.reps), n * 4 * 7 + n * 2)
+    run("adam_step (662k params)",lambda: ops.adam_step(p, gg, m1, v1, pbf, st, hy, zero_grad=True), n * 4 * 7 + n * 2)
     print(f"{'op':45s} {'us':>9s} {'GB/s':>9s} {'TFLOP/s':>8s}")
     for name, us, gbs, tf in rows:
         print(f"{name:45s} {us:9.2f} {gbs:9.1f} {tf:8.2f}")
