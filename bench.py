@@ -100,6 +100,8 @@ def make_batches(cfg, B, n, seed):
     return out
 
 
+CFG_NAME = "cfg2"
+
 # ------------------------------------------------------------------------------------ roofline
 def _time_on_stream(fn, reps, stream):
     with torch.cuda.stream(stream):
@@ -120,8 +122,8 @@ def _roof(kernel, us, flops, nbytes, dtype, note):
     ridge = peak_f * 1e12 / (MI355X_HBM_GBS * 1e9)
     traffic = None
     tpath = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tpath):
-        traffic = json.load(open(tpath)).get(kernel)
+    if os.path.exists(tpath):   # measured HBM bytes per launch at this config (tools/make_traffic.py)
+        traffic = json.load(open(tpath)).get(CFG_NAME, {}).get(kernel)
     if ai < ridge:
         ach = nbytes / (us * 1e-6) / 1e9
         return {"kernel": kernel, "bound": "hbm", "achieved": round(ach, 1), "peak": MI355X_HBM_GBS, "unit": "GB/s",
@@ -231,6 +233,8 @@ def main():
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    global CFG_NAME
+    CFG_NAME = args.config
     cfg = dict(CONFIGS[args.config])
     B = args.batch or cfg["B"]
     torch.manual_seed(1234)               # identical initial weights on every rank

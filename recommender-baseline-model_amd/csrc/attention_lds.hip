@@ -139,6 +139,23 @@ __device__ __forceinline__ float masked(const AttnLdsArgs& a, const float* km, i
   return apply_mask(mask_state(a, km, q, key), s);
 }
 
+// (sequence-head, split) of this workgroup.  Workgroups are dealt to the 8 XCDs round-robin in
+// dispatch order; the nsplit workgroups of one sequence stage the same K/V (or Q/dO) rows, so they
+// are given dispatch slots on ONE XCD and the second staging reads hit that XCD's L2.
+__device__ __forceinline__ void block_coords(const AttnLdsArgs& a, int64_t& bh, int& split) {
+  const int ns = a.nsplit;
+  const int64_t BH = a.B * a.H;
+  if (ns > 1 && BH % 8 == 0) {
+    const int64_t lin = blockIdx.x + (int64_t)ns * blockIdx.y;
+    const int64_t xcd = lin & 7, slot = lin >> 3;
+    bh = (slot / ns) * 8 + xcd;
+    split = (int)(slot % ns);
+  } else {
+    bh = blockIdx.y;
+    split = blockIdx.x;
+  }
+}
+
 // tiles of 16 queries handled by this workgroup: split, split+nsplit, ...
 __device__ __forceinline__ int last_tile_of_split(int nq, int split, int nsplit) {
   return split + ((nq - 1 - split) / nsplit) * nsplit;
@@ -150,8 +167,11 @@ __global__ __launch_bounds__(NT) void attn_fwd_lds_kernel(AttnLdsArgs a) {
   constexpr int LD = Img<DH>::LD, KC = DH / 32, DT = DH / 16, NKT = 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
-  const int64_t bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
-  const int split = blockIdx.x, T = (int)a.T;
+  int64_t bh;
+  int split;
+  block_coords(a, bh, split);
+  const int64_t b = bh / a.H, h = bh % a.H;
+  const int T = (int)a.T;
   const int nq = (T + 15) / 16;
   if (split >= nq) return;
   const int lastq = last_tile_of_split(nq, split, a.nsplit);
@@ -269,8 +289,11 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_lds_kernel(AttnLdsArgs a) {
   constexpr int LD = Img<DH>::LD, KC = DH / 32, DT = DH / 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
-  const int64_t bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
-  const int split = blockIdx.x, T = (int)a.T;
+  int64_t bh;
+  int split;
+  block_coords(a, bh, split);
+  const int64_t b = bh / a.H, h = bh % a.H;
+  const int T = (int)a.T;
   const int nq = (T + 15) / 16;
   if (split >= nq) return;
   const int lastq = last_tile_of_split(nq, split, a.nsplit);
@@ -368,8 +391,11 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkv_lds_kernel(AttnLdsArgs a) {
   constexpr int LD = Img<DH>::LD, KC = DH / 32, DT = DH / 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
-  const int64_t bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
-  const int split = blockIdx.x, T = (int)a.T;
+  int64_t bh;
+  int split;
+  block_coords(a, bh, split);
+  const int64_t b = bh / a.H, h = bh % a.H;
+  const int T = (int)a.T;
   const int nk = (T + 15) / 16;  // key tiles
   if (split >= nk) return;
   // queries needed: causal -> from the first key tile of this split on (all queries of the

@@ -9,8 +9,9 @@
 //   rs_item_index_build: keys (ids | pos | neg) -> stable counting sort of the entries by key:
 //                        per-1024-entry-block key histograms (LDS), per-key exclusive prefix over
 //                        blocks, a scan over keys, then each block places its entries with a
-//                        block radix sort for the in-block rank.  Tables with more than 32768
-//                        rows use a device radix sort (rocPRIM) instead.  -> start[v] for v <= V
+//                        block radix sort for the in-block rank.  When the per-block histogram
+//                        table would exceed 2^26 ints a device radix sort (rocPRIM) is used
+//                        instead.  -> start[v] for v <= V
 //   rs_item_grad:        chunks of 64 sorted entries: contribution rows summed per key run in
 //                        LDS; a key wholly inside one chunk is written by that chunk (+=); a
 //                        key spanning chunks leaves per-chunk partials that the chunk holding
@@ -27,7 +28,8 @@ namespace ig {
 
 constexpr int CH = 64;          // sorted entries per gradient chunk
 constexpr int BE = 1024;        // entries per counting-sort block
-constexpr int VMAX_CS = 32768;  // largest table for the counting sort (LDS histogram)
+constexpr int VMAX_LDS = 32768;            // largest table for the LDS histogram
+constexpr int64_t HMAX = (int64_t)1 << 26;  // largest per-block histogram table (ints) for the counting sort
 
 struct Layout {
   int64_t n, nchunks, nb, V;
@@ -48,7 +50,7 @@ static hipError_t layout(int nsrc, int64_t rows, int64_t table_rows, int64_t d, 
   L.nchunks = cdiv(L.n, CH);
   L.nb = cdiv(L.n, BE);
   L.V = table_rows;
-  L.cs = table_rows <= VMAX_CS;
+  L.cs = L.nb * table_rows <= HMAX;
   size_t o = 0;
   L.sk = o; o = al256(o + L.n * 4);
   L.sv = o; o = al256(o + L.n * 4);
@@ -90,7 +92,7 @@ struct Keys {
 // ---- counting sort ------------------------------------------------------------------------
 // H[b][v] = number of entries of block b with key v
 __global__ __launch_bounds__(256) void hist_kernel(Keys K, int* __restrict__ H) {
-  __shared__ int hist[VMAX_CS];
+  __shared__ int hist[VMAX_LDS];
   const int tid = threadIdx.x;
   const int V = (int)K.V;
   for (int v = tid; v < V; v += 256) hist[v] = 0;
@@ -108,6 +110,17 @@ __global__ __launch_bounds__(256) void hist_kernel(Keys K, int* __restrict__ H) 
   __syncthreads();
   int* h = H + (int64_t)blockIdx.x * V;
   for (int v = tid; v < V; v += 256) h[v] = hist[v];
+}
+
+// larger tables: the same counts with integer atomics straight into the (zeroed) row of block b
+__global__ __launch_bounds__(256) void hist_global_kernel(Keys K, int* __restrict__ H) {
+  const int64_t e0 = (int64_t)blockIdx.x * BE;
+  int* h = H + (int64_t)blockIdx.x * K.V;
+#pragma unroll
+  for (int i = 0; i < BE / 256; ++i) {
+    const int64_t e = e0 + threadIdx.x + i * 256;
+    if (e < K.n) atomicAdd(&h[K.get(e)], 1);
+  }
 }
 
 // H[b][v] <- sum_{b' < b} H[b'][v];  total[v] = sum_b H[b][v].  Workgroup = 64 keys (lanes) x 4
@@ -429,7 +442,12 @@ int rs_item_index_build(int nsrc, const int64_t* keys0, const int64_t* keys1, co
   if (L.cs) {
     int* H = (int*)(w + L.H);
     int* total = (int*)(w + L.total);
-    hipLaunchKernelGGL(ig::hist_kernel, dim3((unsigned)L.nb), dim3(256), 0, s, K, H);
+    if (table_rows <= ig::VMAX_LDS) {
+      hipLaunchKernelGGL(ig::hist_kernel, dim3((unsigned)L.nb), dim3(256), 0, s, K, H);
+    } else {
+      if ((e = hipMemsetAsync(H, 0, (size_t)L.nb * table_rows * 4, s)) != hipSuccess) return (int)e;
+      hipLaunchKernelGGL(ig::hist_global_kernel, dim3((unsigned)L.nb), dim3(256), 0, s, K, H);
+    }
     hipLaunchKernelGGL(ig::prefix_blocks_kernel, dim3((unsigned)cdiv(table_rows, 64)), dim3(256), 0, s, H, L.nb,
                        table_rows, total);
     hipLaunchKernelGGL(ig::scan_keys_kernel, dim3(1), dim3(1024), 0, s, total, table_rows, start);
