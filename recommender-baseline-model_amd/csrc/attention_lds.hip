@@ -58,6 +58,21 @@ struct AttnLdsArgs {
 #define MASK2 (-1e9f * LOG2E)
 __device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// phase timestamps for tools/micro/attn_phase.hip (compiled out of the library)
+#ifdef ATTN_PROF
+__device__ unsigned long long g_attn_prof[8192 * NW * 10];
+#define APROF(slot)                                                                          \
+  do {                                                                                       \
+    if ((threadIdx.x & 63) == 0)                                                             \
+      g_attn_prof[((blockIdx.x + gridDim.x * blockIdx.y) * NW + (threadIdx.x >> 6)) * 10 + (slot)] = \
+          wall_clock64();                                                                    \
+  } while (0)
+#else
+#define APROF(slot) \
+  do {              \
+  } while (0)
+#endif
+
 template <int DH> struct Img { static constexpr int LD = DH + 16; };  // row stride (elements), +32 B pad
 
 __device__ __forceinline__ bf16x8 cat8(bf4 a, bf4 b) {
@@ -122,6 +137,32 @@ __device__ __forceinline__ void stage(bf16* img, const bf16* src, int64_t ld, in
   }
 }
 
+// two images at once: every load of both is issued before the first LDS store (one dependent HBM
+// round trip for both operands instead of one each)
+template <int DH>
+__device__ __forceinline__ void stage2(bf16* imgA, const bf16* srcA, int64_t ldA, bf16* imgB, const bf16* srcB,
+                                       int64_t ldB, int64_t T, int rows, int tid) {
+  constexpr int CPR = DH / 8, LD = Img<DH>::LD, U = 8;
+  const int n = rows * CPR;
+  for (int i0 = tid; i0 < n; i0 += NT * U) {
+    bf16x8 va[U], vb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = min(i0 + u * NT, n - 1);
+      va[u] = gload8(srcA, ldA, i / CPR, T, (i % CPR) * 8);
+      vb[u] = gload8(srcB, ldB, i / CPR, T, (i % CPR) * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * NT;
+      if (i < n) {
+        *reinterpret_cast<bf16x8*>(imgA + (i / CPR) * LD + (i % CPR) * 8) = va[u];
+        *reinterpret_cast<bf16x8*>(imgB + (i / CPR) * LD + (i % CPR) * 8) = vb[u];
+      }
+    }
+  }
+}
+
 // 1.0 where the key is masked by key padding (mask_kind 1), else 0; keys >= T are handled separately
 __device__ __forceinline__ void stage_keymask(float* km, const AttnLdsArgs& a, int64_t b, int rows, int tid) {
   for (int i = tid; i < rows; i += NT)
@@ -166,7 +207,8 @@ template <int DH>
 __global__ __launch_bounds__(NT) void attn_fwd_lds_kernel(AttnLdsArgs a) {
   constexpr int LD = Img<DH>::LD, KC = DH / 32, DT = DH / 16, NKT = 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
+  APROF(0);
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4, cl = lane & 15;
   int64_t bh;
   int split;
   block_coords(a, bh, split);
@@ -183,18 +225,26 @@ __global__ __launch_bounds__(NT) void attn_fwd_lds_kernel(AttnLdsArgs a) {
   const bf16* Kg = a.k + b * a.T * a.ldk + h * DH;
   const bf16* Vg = a.v + b * a.T * a.ldv + h * DH;
   const bf16* Qg = a.q + b * a.T * a.ldq + h * DH;
-  stage<DH>(Ks, Kg, a.ldk, a.T, rows, tid);
-  stage<DH>(Vs, Vg, a.ldv, a.T, rows, tid);
+  // the first query tile's operands are requested before (and so arrive with) the K/V staging
+  bf16x8 qf[KC];
+  {
+    const int64_t qrow0 = (split + wave * a.nsplit) * 16 + cl;
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) qf[kc] = gload8(Qg, a.ldq, qrow0, a.T, kc * 32 + 8 * g);
+  }
+  stage2<DH>(Ks, Kg, a.ldk, Vs, Vg, a.ldv, a.T, rows, tid);
   stage_keymask(km, a, b, rows, tid);
   __syncthreads();
+  APROF(1);
   const uint64_t seed = eff_seed(a.seed, a.seed_base);
 
   for (int qt = split + wave * a.nsplit; qt < nq; qt += NW * a.nsplit) {
     const int q0 = qt * 16;
     const int64_t qrow = q0 + cl;  // this lane's query
-    bf16x8 qf[KC];
+    if (qt != split + wave * a.nsplit) {
 #pragma unroll
-    for (int kc = 0; kc < KC; ++kc) qf[kc] = gload8(Qg, a.ldq, qrow, a.T, kc * 32 + 8 * g);
+      for (int kc = 0; kc < KC; ++kc) qf[kc] = gload8(Qg, a.ldq, qrow, a.T, kc * 32 + 8 * g);
+    }
     const int nkt = a.mask_kind == 0 ? qt + 1 : nq;
     const float sl2 = a.scale * LOG2E;
     const int qi = q0 + cl;
@@ -281,6 +331,7 @@ __global__ __launch_bounds__(NT) void attn_fwd_lds_kernel(AttnLdsArgs a) {
       }
     }
   }
+  APROF(2);
 }
 
 // ------------------------------------------------------------------ backward: delta + dQ
@@ -288,7 +339,7 @@ template <int DH>
 __global__ __launch_bounds__(NT) void attn_bwd_dq_lds_kernel(AttnLdsArgs a) {
   constexpr int LD = Img<DH>::LD, KC = DH / 32, DT = DH / 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4, cl = lane & 15;
   int64_t bh;
   int split;
   block_coords(a, bh, split);
@@ -302,27 +353,41 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_lds_kernel(AttnLdsArgs a) {
   bf16* Ks = reinterpret_cast<bf16*>(smem);
   bf16* Vs = Ks + rows * LD;
   float* km = reinterpret_cast<float*>(Vs + rows * LD);
-  stage<DH>(Ks, a.k + b * a.T * a.ldk + h * DH, a.ldk, a.T, rows, tid);
-  stage<DH>(Vs, a.v + b * a.T * a.ldv + h * DH, a.ldv, a.T, rows, tid);
-  stage_keymask(km, a, b, rows, tid);
-  __syncthreads();
-  const uint64_t seed = eff_seed(a.seed, a.seed_base);
   const bf16* Qg = a.q + b * a.T * a.ldq + h * DH;
   const bf16* Og = a.o + b * a.T * a.ldo + h * DH;
   const bf16* dOg = a.dout + b * a.T * a.lddo + h * DH;
+  // the first query tile's q, dO, O rows are requested before (and arrive with) the K/V staging
+  bf16x8 qf[KC], df[KC], of[KC];
+  {
+    const int64_t qrow0 = (split + wave * a.nsplit) * 16 + cl;
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      qf[kc] = gload8(Qg, a.ldq, qrow0, a.T, kc * 32 + 8 * g);
+      df[kc] = gload8(dOg, a.lddo, qrow0, a.T, kc * 32 + 8 * g);
+      of[kc] = gload8(Og, a.ldo, qrow0, a.T, kc * 32 + 8 * g);
+    }
+  }
+  stage2<DH>(Ks, a.k + b * a.T * a.ldk + h * DH, a.ldk, Vs, a.v + b * a.T * a.ldv + h * DH, a.ldv, a.T, rows, tid);
+  stage_keymask(km, a, b, rows, tid);
+  __syncthreads();
+  const uint64_t seed = eff_seed(a.seed, a.seed_base);
 
   for (int qt = split + wave * a.nsplit; qt < nq; qt += NW * a.nsplit) {
     const int q0 = qt * 16;
     const int64_t qrow = q0 + cl;
-    bf16x8 qf[KC], df[KC];
+    if (qt != split + wave * a.nsplit) {
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) {
+        qf[kc] = gload8(Qg, a.ldq, qrow, a.T, kc * 32 + 8 * g);
+        df[kc] = gload8(dOg, a.lddo, qrow, a.T, kc * 32 + 8 * g);
+        of[kc] = gload8(Og, a.ldo, qrow, a.T, kc * 32 + 8 * g);
+      }
+    }
     float dl = 0.f;
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
-      qf[kc] = gload8(Qg, a.ldq, qrow, a.T, kc * 32 + 8 * g);
-      df[kc] = gload8(dOg, a.lddo, qrow, a.T, kc * 32 + 8 * g);
-      const bf16x8 of = gload8(Og, a.ldo, qrow, a.T, kc * 32 + 8 * g);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) dl += (float)df[kc][j] * (float)of[j];
+      for (int j = 0; j < 8; ++j) dl += (float)df[kc][j] * (float)of[kc][j];
     }
     dl += __shfl_xor(dl, 16, 64);
     dl += __shfl_xor(dl, 32, 64);  // delta = rowsum(dO * O) for query qrow
@@ -390,7 +455,7 @@ template <int DH>
 __global__ __launch_bounds__(NT) void attn_bwd_dkv_lds_kernel(AttnLdsArgs a) {
   constexpr int LD = Img<DH>::LD, KC = DH / 32, DT = DH / 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4, cl = lane & 15;
   int64_t bh;
   int split;
   block_coords(a, bh, split);
@@ -406,28 +471,43 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkv_lds_kernel(AttnLdsArgs a) {
   float* lse_s = reinterpret_cast<float*>(dOs + rows * LD);
   float* dl_s = lse_s + rows;
   float* km = dl_s + rows;
-  stage<DH>(Qs, a.q + b * a.T * a.ldq + h * DH, a.ldq, a.T, rows, tid);
-  stage<DH>(dOs, a.dout + b * a.T * a.lddo + h * DH, a.lddo, a.T, rows, tid);
-  for (int i = tid; i < rows; i += NT) {
-    lse_s[i] = i < T ? a.lse[bh * a.T + i] * LOG2E : 0.f;
-    dl_s[i] = i < T ? a.delta[bh * a.T + i] : 0.f;
+  const bf16* Kg = a.k + b * a.T * a.ldk + h * DH;
+  const bf16* Vg = a.v + b * a.T * a.ldv + h * DH;
+  // everything this workgroup reads before its first MFMA is requested in one batch: the first key
+  // tile's k/v rows, the per-query lse/delta (rows <= 256 <= NT: one per thread), the Q/dO images
+  bf16x8 kf[KC], vf[KC];
+  {
+    const int64_t key0 = (split + wave * a.nsplit) * 16 + cl;
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      kf[kc] = gload8(Kg, a.ldk, key0, a.T, kc * 32 + 8 * g);
+      vf[kc] = gload8(Vg, a.ldv, key0, a.T, kc * 32 + 8 * g);
+    }
+  }
+  const int ti = min(tid, T - 1);            // branch-free: clamped load, masked value
+  float lse_v = a.lse[bh * a.T + ti] * LOG2E, dl_v = a.delta[bh * a.T + ti];
+  if (tid >= T) lse_v = dl_v = 0.f;
+  stage2<DH>(Qs, a.q + b * a.T * a.ldq + h * DH, a.ldq, dOs, a.dout + b * a.T * a.lddo + h * DH, a.lddo, a.T, rows,
+             tid);
+  if (tid < rows) {
+    lse_s[tid] = lse_v;
+    dl_s[tid] = dl_v;
   }
   stage_keymask(km, a, b, rows, tid);
   __syncthreads();
   const uint64_t seed = eff_seed(a.seed, a.seed_base);
-  const bf16* Kg = a.k + b * a.T * a.ldk + h * DH;
-  const bf16* Vg = a.v + b * a.T * a.ldv + h * DH;
   const int nqc = (T + 31) / 32;  // 32-query chunks
 
   const float sl2 = a.scale * LOG2E;
   for (int kt = split + wave * a.nsplit; kt < nk; kt += NW * a.nsplit) {
     const int64_t key = kt * 16 + cl;  // this lane's key
     const int ki = kt * 16 + cl;
-    bf16x8 kf[KC], vf[KC];
+    if (kt != split + wave * a.nsplit) {
 #pragma unroll
-    for (int kc = 0; kc < KC; ++kc) {
-      kf[kc] = gload8(Kg, a.ldk, key, a.T, kc * 32 + 8 * g);
-      vf[kc] = gload8(Vg, a.ldv, key, a.T, kc * 32 + 8 * g);
+      for (int kc = 0; kc < KC; ++kc) {
+        kf[kc] = gload8(Kg, a.ldk, key, a.T, kc * 32 + 8 * g);
+        vf[kc] = gload8(Vg, a.ldv, key, a.T, kc * 32 + 8 * g);
+      }
     }
     f32x4 dk[DT], dv[DT];
 #pragma unroll

@@ -106,7 +106,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
   T* As = lds;
   T* Bs = lds + LA::LDS_ELEMS;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   constexpr int FM = BM / 32, FN = BN / 32;  // 16x16 fragments per wave per dim
 

@@ -273,7 +273,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
   __bf16* stage0 = reinterpret_cast<__bf16*>(smem);
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   constexpr int FM = BM / 32, FN = BN / 32;
 

@@ -175,7 +175,7 @@ __global__ __launch_bounds__(256) void sas_block_in_kernel(InArgs a) {
   bf16* X = smem;
   bf16* Qt = smem + Tile<D>::ELEMS;
   bf16* S = smem + 2 * Tile<D>::ELEMS;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4, cl = lane & 15;
   const int64_t row0 = (int64_t)blockIdx.x * BMR;
   constexpr int FQ = D / 64, FKV = 2 * D / 64;
   BFr<D, FQ> wq;
@@ -254,7 +254,7 @@ __global__ __launch_bounds__(256) void sas_block_out_kernel(OutArgs a) {
   bf16* T0 = smem;
   bf16* T1 = smem + Tile<D>::ELEMS;
   bf16* T2 = smem + 2 * Tile<D>::ELEMS;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4, cl = lane & 15;
   const int64_t row0 = (int64_t)blockIdx.x * BMR;
   const int c0w = wave * (D / 4);
   const bool drop = a.drop_p > 0.f;
@@ -432,7 +432,7 @@ __global__ __launch_bounds__(256) void sas_block_out_bwd_kernel(OutBwdArgs a) {
   bf16* T0 = smem;
   bf16* T1 = smem + Tile<D>::ELEMS;
   bf16* T2 = smem + 2 * Tile<D>::ELEMS;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4, cl = lane & 15;
   const int64_t row0 = (int64_t)blockIdx.x * BMR;
   const int c0w = wave * (D / 4);
   const bool drop = a.drop_p > 0.f;
@@ -570,7 +570,7 @@ __global__ __launch_bounds__(256) void sas_block_in_bwd_kernel(InBwdArgs a) {
   bf16* T0 = smem;
   bf16* T1 = smem + Tile<D>::ELEMS;
   bf16* T2 = smem + 2 * Tile<D>::ELEMS;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4, cl = lane & 15;
   const int64_t row0 = (int64_t)blockIdx.x * BMR;
   const int c0w = wave * (D / 4);
   BFr<D, FN> wk, wv, wq;

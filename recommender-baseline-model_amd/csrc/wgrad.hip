@@ -40,7 +40,7 @@ __global__ __launch_bounds__(256) void wgrad_group_kernel(Args a) {
   constexpr int STAGE = 2 * I::ELEMS;
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * STAGE];
   constexpr int BKT = gbf::BKT;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), wm = wave >> 1, wn = wave & 1;
   constexpr int FM = T / 32, FN = T / 32;
 
   const int t = (int)(blockIdx.x % (unsigned)a.ntiles);
