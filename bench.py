@@ -65,6 +65,9 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--nbatches", type=int, default=8, help="distinct synthetic batches cycled through")
+    ap.add_argument("--sampler", default="host", choices=["host", "device"],
+                    help="SAS: 'device' = batches drawn each step by the on-device WarpSampler "
+                         "(rs_sas_sample) inside the step's graph, from synthetic user histories")
     return ap.parse_args()
 
 
@@ -253,7 +256,16 @@ def main():
     from rbm_amd.train_step import FusedTrainStep
     trainer = FusedTrainStep(model, lr=1e-3, max_labelled=max_lab)
 
-    if args.no_graph:
+    if args.sampler == "device" and cfg["model"] == "sas":
+        import rbm_amd.data as synth
+        from rbm_amd.dataloaders import DeviceWarpSampler
+        users = synth.user_histories(np.random.default_rng(77 + rank), cfg.get("users", 6040), cfg["T"], cfg["V"],
+                                     shape=cfg["shape"])
+        sampler = DeviceWarpSampler(users, cfg["V"], B, cfg["T"], seed=5 + rank)
+        trainer.capture_sampled(sampler)
+        batches = [()]
+        run = trainer.replay_sampled
+    elif args.no_graph:
         run = trainer.step
     else:
         trainer.capture(*batches[0])
@@ -299,7 +311,8 @@ def main():
             "config": {"workload": cfg["name"], "model": "SASRec" if cfg["model"] == "sas" else "BERT4Rec",
                        "global_batch": world * B, "per_gpu_batch": B, "seq_len": cfg["T"], "hidden": cfg["d"],
                        "blocks": cfg["L"], "heads": cfg["h"], "num_items": cfg["V"], "parallelism": f"dp{world}",
-                       "hip_graph": not args.no_graph, "bench_config": args.config},
+                       "hip_graph": not args.no_graph, "bench_config": args.config,
+                       "sampler": args.sampler},
             "final_loss": round(final_loss, 5),
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -204,6 +204,13 @@ int rs_dropout_rowmask(int dtype, const void* x, int64_t M, int64_t N, int64_t l
                        uint64_t seed, const uint64_t* seed_base, int64_t drop_ld, const int64_t* rowmask_ids,
                        void* out, void* out_masked, void* stream);
 
+/* Two stacked dropout sites' backward in one pass (bert.py encode_backward: block-output then
+ * residual dropout of BERT4Rec's SublayerConnection/TransformerBlock, BS/models/bert_modules/
+ * transformer.py:32, utils/sublayer.py:18): out1 = x * keep(salt1)/(1-p),
+ * out2 = out1 * keep(salt2)/(1-p), each rounded to the dtype.  N, ld multiples of 8. */
+int rs_dropout2(int dtype, const void* x, int64_t M, int64_t N, int64_t ld, float drop_p, uint64_t salt1,
+                uint64_t salt2, const uint64_t* seed_base, int64_t drop_ld, void* out1, void* out2, void* stream);
+
 /* *seed_base += 1 on the stream (advances every dropout mask; capturable). */
 int rs_seed_advance(uint64_t* seed_base, void* stream);
 
@@ -311,6 +318,22 @@ int rs_sas_head_bwd(int64_t M, int64_t d, const float* part, const float* diviso
                     const float* nl, const float* dpl_in, const float* dnl_in, float* dpl, float* dnl,
                     const int64_t* pos, const int64_t* neg, const void* E, const void* x, const float* ln_w,
                     const float* mean, const float* rstd, void* dx, float* lnpart, void* stream);
+
+/* ---- on-device SAS sampler and ranking metrics (sampler.hip) ----------------------------------
+ * rs_sas_sample: one training batch as WarpSampler's workers build it (BS/dataloaders/sas.py:65-91):
+ * per row a uniform user, its last max_len items, seq/pos = the window shifted by one, left padded
+ * with 0, neg = uniform draws over {0..item_num} minus the window's items.  Histories are a CSR pair
+ * (user_offsets[n_users+1], user_items).  *seed_base is advanced first (device counter; graph-
+ * capturable); salt separates samplers.  seq/pos/neg: int64 [batch][max_len]; max_len <= 512. */
+int rs_sas_sample(const int64_t* user_offsets, const int64_t* user_items, int64_t n_users, int64_t item_num,
+                  int64_t batch, int64_t max_len, uint64_t* seed_base, uint64_t salt, int64_t* seq, int64_t* pos,
+                  int64_t* neg, void* stream);
+/* rs_rank_metrics: recalls_ndcgs_and_mrr_for_ks (BS/trainers/utils.py:28-57) over scores/labels
+ * fp32 [rows][cands] (labels 0/1 weights), ks: device int[nk] (nk <= 8).  out[3*q + {0,1,2}] =
+ * mean Recall@k, NDCG@k, MRR@k for ks[q]; ws >= 3*nk*rows floats.  Ranks follow a stable
+ * descending sort (ties by candidate index). */
+int rs_rank_metrics(const float* scores, const float* labels, int64_t rows, int64_t cands, int nk, const int* ks,
+                    float* ws, float* out, void* stream);
 
 /* ABI version of this header/library pair. */
 int rs_abi_version(void);

@@ -70,6 +70,7 @@ SIGNATURES = {
     "rs_adam_step": [i64, vp, vp, vp, vp, vp, vp, vp, i32, vp],
     "rs_cast_bf16": [i64, vp, vp, vp],
     "rs_dropout_rowmask": [i32, vp, i64, i64, i64, f32, u64, vp, i64, vp, vp, vp, vp],
+    "rs_dropout2": [i32, vp, i64, i64, i64, f32, u64, u64, vp, i64, vp, vp, vp],
     "rs_seed_advance": [vp, vp],
     "rs_sas_block_in": [i64, i64, vp, i64, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "rs_sas_block_out": [i64, i64, vp, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32,
@@ -86,6 +87,8 @@ SIGNATURES = {
     "rs_sas_head_bwd": [i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "rs_item_grad": [vp, i32, i64, i64, i64, vp, f32, f32, u64, vp, vp, vp, vp, vp, vp],
     "rs_transpose_bf16": [i64, vp, i64, vp, vp, vp],
+    "rs_sas_sample": [vp, vp, i64, i64, i64, i64, vp, u64, vp, vp, vp, vp],
+    "rs_rank_metrics": [vp, vp, i64, i64, i32, vp, vp, vp, vp],
     "rs_abi_version": [],
 }
 

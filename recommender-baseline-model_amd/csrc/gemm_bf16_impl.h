@@ -145,9 +145,9 @@ __device__ __forceinline__ void epi8(const GemmArgs& a, int64_t m, int64_t n, fl
     if (e.bias) x += bias[j];
     pre[j] = x;
     if (e.act == 1) x = fmaxf(x, 0.f);
-    else if (e.act == 2) x = gelu_tanh(x);
+    else if (e.act == 2) x = gelu_tanh_fast(x);
     else if (e.act == 3) x = auxv[j] > 0.f ? x : 0.f;
-    else if (e.act == 4) x *= gelu_tanh_grad(auxv[j]);
+    else if (e.act == 4) x *= gelu_tanh_grad_fast(auxv[j]);
     const float dmj = e.drop_p > 0.f ? drop_mul(e.drop_p, s1, (uint64_t)(m * e.drop_ld + n + j)) : 1.0f;
     x = res ? __builtin_fmaf(x, dmj, resv[j]) : x * dmj;
     if (!rowkeep) x = 0.f;
@@ -227,9 +227,9 @@ __device__ __forceinline__ void epi8_t(const GemmArgs& a, int64_t m, int64_t n, 
     if constexpr ((EC & EB) != 0) x += bias[j];
     pre[j] = x;
     if constexpr (ACT == 1) x = fmaxf(x, 0.f);
-    if constexpr (ACT == 2) x = gelu_tanh(x);
+    if constexpr (ACT == 2) x = gelu_tanh_fast(x);
     if constexpr (ACT == 3) x = auxv[j] > 0.f ? x : 0.f;
-    if constexpr (ACT == 4) x *= gelu_tanh_grad(auxv[j]);
+    if constexpr (ACT == 4) x *= gelu_tanh_grad_fast(auxv[j]);
     if constexpr ((EC & ED) != 0 && (EC & ER) != 0) x = __builtin_fmaf(x, dm[j], resv[j]);  // one rounding
     else if constexpr ((EC & ED) != 0) x *= dm[j];
     else if constexpr ((EC & ER) != 0) x += resv[j];
@@ -260,6 +260,105 @@ __device__ __forceinline__ void epi8_t(const GemmArgs& a, int64_t m, int64_t n, 
       for (int j = 0; j < 8; ++j) v[j] += old[j];
     }
     store_chunk<__bf16>(C, v);
+  }
+}
+
+__device__ __forceinline__ void bf8_to_f(const bf16x8& x, float* o) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (float)x[j];
+}
+
+// Whole-tile epilogue of a compile-time class, columns n..n+7 in range: every global operand of the
+// thread's NP rows (pre-activation, residual, row-mask id, old C) is loaded before any row is
+// finished, so the tile pays one memory round trip instead of one per row.
+template <int EC, int NP, int RPP, int LDC>
+__device__ __forceinline__ void epi_rows(const GemmArgs& a, const float* Cs, int row0, int c8, int64_t m0, int64_t Mb,
+                                         int64_t n, uint32_t s1, uint32_t s2) {
+  constexpr int ACT = ec_act(EC);
+  const rs_epilogue& e = a.epi;
+  float bias[8];
+  if constexpr ((EC & EB) != 0) {
+    load_chunk<float>(bias, e.bias + n);
+    load_chunk<float>(bias + 4, e.bias + n + 4);
+  }
+  bf16x8 auxr[NP], resr[NP], oldr[NP];
+  int64_t idr[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int64_t m = m0 + row0 + p * RPP;
+    if (m < Mb) {
+      if constexpr (ACT >= 3) auxr[p] = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const __bf16*>(e.aux) + m * e.ldaux + n);
+      if constexpr ((EC & ER) != 0) resr[p] = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const __bf16*>(e.resid) + m * e.ldres + n);
+      if constexpr ((EC & EM) != 0) idr[p] = e.rowmask_ids[m];
+      if constexpr ((EC & EA) != 0 && (EC & EF) == 0) oldr[p] = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const __bf16*>(a.C) + m * a.ldc + n);
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int row = row0 + p * RPP;
+    const int64_t m = m0 + row;
+    if (m >= Mb) break;
+    float v[8];
+    {
+      const float4 v0 = *reinterpret_cast<const float4*>(Cs + row * LDC + c8);
+      const float4 v1 = *reinterpret_cast<const float4*>(Cs + row * LDC + c8 + 4);
+      v[0] = v0.x; v[1] = v0.y; v[2] = v0.z; v[3] = v0.w; v[4] = v1.x; v[5] = v1.y; v[6] = v1.z; v[7] = v1.w;
+    }
+    float auxv[8], resv[8], dm[8], pm[8];
+    if constexpr (ACT >= 3) bf8_to_f(auxr[p], auxv);
+    if constexpr ((EC & ER) != 0) bf8_to_f(resr[p], resv);
+    if constexpr ((EC & ED) != 0) {
+      const uint64_t base = (uint64_t)(m * e.drop_ld + n);
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) drop_mul2(e.drop_p, s1, base + j, dm[j], dm[j + 1]);
+    }
+    if constexpr ((EC & EP) != 0) {
+      const uint64_t base = (uint64_t)(m * e.drop_ld + n);
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) drop_mul2(e.post_drop_p, s2, base + j, pm[j], pm[j + 1]);
+    }
+    bool keep = true;
+    if constexpr ((EC & EM) != 0) keep = idr[p] != 0;
+    float pre[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float x = v[j];
+      if constexpr ((EC & EB) != 0) x += bias[j];
+      pre[j] = x;
+      if constexpr (ACT == 1) x = fmaxf(x, 0.f);
+      if constexpr (ACT == 2) x = gelu_tanh_fast(x);
+      if constexpr (ACT == 3) x = auxv[j] > 0.f ? x : 0.f;
+      if constexpr (ACT == 4) x *= gelu_tanh_grad_fast(auxv[j]);
+      if constexpr ((EC & ED) != 0 && (EC & ER) != 0) x = __builtin_fmaf(x, dm[j], resv[j]);  // one rounding
+      else if constexpr ((EC & ED) != 0) x *= dm[j];
+      else if constexpr ((EC & ER) != 0) x += resv[j];
+      if constexpr ((EC & EM) != 0) x = keep ? x : 0.f;
+      if constexpr ((EC & EP) != 0) x *= pm[j];
+      v[j] = x;
+    }
+    if constexpr (ACT == 1 || ACT == 2) {
+      if (e.aux_out) store_chunk<__bf16>(reinterpret_cast<__bf16*>(e.aux_out) + m * e.ldaux + n, pre);
+    }
+    if constexpr ((EC & EF) != 0) {
+      float* C = reinterpret_cast<float*>(a.C) + m * a.ldc + n;
+      if constexpr ((EC & EA) != 0) {
+        float old[8];
+        load_chunk<float>(old, C);
+        load_chunk<float>(old + 4, C + 4);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += old[j];
+      }
+      store_chunk<float>(C, v);
+      store_chunk<float>(C + 4, v + 4);
+    } else {
+      if constexpr ((EC & EA) != 0) {
+        float old[8];
+        bf8_to_f(oldr[p], old);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += old[j];
+      }
+      store_chunk<__bf16>(reinterpret_cast<__bf16*>(a.C) + m * a.ldc + n, v);
+    }
   }
 }
 
@@ -408,6 +507,10 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs a) {
   if constexpr (EC >= 0) {
     if constexpr ((EC & ED) != 0) s1 = seed32(eff_seed(a.epi.drop_seed, a.epi.seed_base));
     if constexpr ((EC & EP) != 0) s2 = seed32(eff_seed(a.epi.post_drop_seed, a.epi.seed_base));
+    if (n + 8 <= a.N) {
+      epi_rows<EC, BM / RPP, RPP, LDC>(a, Cs, tid / TPR, c8, m0, Mb, n, s1, s2);
+      return;
+    }
   }
   for (int row = tid / TPR; row < BM; row += RPP) {
     const int64_t m = m0 + row;

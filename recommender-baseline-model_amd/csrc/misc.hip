@@ -154,6 +154,67 @@ __global__ __launch_bounds__(256) void dropout_rowmask_kernel(const T* __restric
   out[m * ld + c] = from_f<T>(v);
 }
 
+
+// 8 columns per thread (N, ld, drop_ld multiples of 8; 16-B aligned rows): the same masks as
+// dropout_rowmask_kernel (element m*drop_ld+c, drop_mul2 pairs = drop_mul).  TWO: the chained
+// backward of two stacked dropouts, out = round(x * m1) and out2 = round(out * m2) in one pass
+// (BERT's block-output and residual dropouts, bert.py encode_backward).
+template <typename T, bool TWO>
+__global__ __launch_bounds__(256) void dropout_v8_kernel(const T* __restrict__ x, int64_t M, int64_t N, int64_t ld,
+                                                         float p, uint64_t salt, uint64_t salt2,
+                                                         const uint64_t* seed_base, int64_t drop_ld,
+                                                         const int64_t* __restrict__ ids, T* __restrict__ out,
+                                                         T* __restrict__ out2) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t n8 = N >> 3;
+  if (i >= M * n8) return;
+  const int64_t m = i / n8, c = (i - m * n8) * 8;
+  const bool keep = !ids || ids[m] != 0;
+  float v[8];
+  if (sizeof(T) == 2) {
+    load_chunk<__bf16>(v, reinterpret_cast<const __bf16*>(x) + m * ld + c);
+  } else {
+    load_chunk<float>(v, reinterpret_cast<const float*>(x) + m * ld + c);
+    load_chunk<float>(v + 4, reinterpret_cast<const float*>(x) + m * ld + c + 4);
+  }
+  auto put = [&](T* dst, const float* w) {
+    if (sizeof(T) == 2) {
+      store_chunk<__bf16>(reinterpret_cast<__bf16*>(dst) + m * ld + c, w);
+    } else {
+      store_chunk<float>(reinterpret_cast<float*>(dst) + m * ld + c, w);
+      store_chunk<float>(reinterpret_cast<float*>(dst) + m * ld + c + 4, w + 4);
+    }
+  };
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = keep ? v[j] : 0.f;
+  if (!TWO && out2) put(out2, v);   // the single-mask form's out_masked
+  const uint64_t base = (uint64_t)(m * drop_ld + c);
+  if (p > 0.f) {
+    const uint32_t s1 = seed32(eff_seed(salt, seed_base));
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      float a, b;
+      drop_mul2(p, s1, base + j, a, b);
+      v[j] = to_f(from_f<T>(v[j] * a));
+      v[j + 1] = to_f(from_f<T>(v[j + 1] * b));
+    }
+  }
+  put(out, v);
+  if (TWO) {
+    if (p > 0.f) {
+      const uint32_t s2 = seed32(eff_seed(salt2, seed_base));
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        float a, b;
+        drop_mul2(p, s2, base + j, a, b);
+        v[j] *= a;
+        v[j + 1] *= b;
+      }
+    }
+    put(out2, v);
+  }
+}
+
 extern "C" {
 
 int rs_adam_prepare(double* state, const float* hyper, const float* grad_divisor, uint64_t* seed_base,
@@ -201,6 +262,17 @@ int rs_dropout_rowmask(int dtype, const void* x, int64_t M, int64_t N, int64_t l
                        void* out_masked, void* stream) {
   if (M <= 0 || N <= 0) return RS_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
+  const int es = dtype == RS_DTYPE_BF16 ? 2 : 4;
+  if (N % 8 == 0 && ld % 8 == 0 && drop_ld % 2 == 0 && ((uintptr_t)x | (uintptr_t)out | (uintptr_t)out_masked) % 16 == 0) {
+    dim3 g8((unsigned)cdiv(M * (N / 8), 256));
+    if (es == 2)
+      hipLaunchKernelGGL((dropout_v8_kernel<__bf16, false>), g8, dim3(256), 0, s, (const __bf16*)x, M, N, ld, drop_p,
+                         seed, 0ull, seed_base, drop_ld, rowmask_ids, (__bf16*)out, (__bf16*)out_masked);
+    else
+      hipLaunchKernelGGL((dropout_v8_kernel<float, false>), g8, dim3(256), 0, s, (const float*)x, M, N, ld, drop_p,
+                         seed, 0ull, seed_base, drop_ld, rowmask_ids, (float*)out, (float*)out_masked);
+    return (int)hipGetLastError();
+  }
   dim3 grid((unsigned)cdiv(M * N, 256));
   if (dtype == RS_DTYPE_BF16)
     hipLaunchKernelGGL((dropout_rowmask_kernel<__bf16>), grid, dim3(256), 0, s, (const __bf16*)x, M, N, ld, drop_p,
@@ -208,6 +280,22 @@ int rs_dropout_rowmask(int dtype, const void* x, int64_t M, int64_t N, int64_t l
   else
     hipLaunchKernelGGL((dropout_rowmask_kernel<float>), grid, dim3(256), 0, s, (const float*)x, M, N, ld, drop_p,
                        seed, seed_base, drop_ld, rowmask_ids, (float*)out, (float*)out_masked);
+  return (int)hipGetLastError();
+}
+
+int rs_dropout2(int dtype, const void* x, int64_t M, int64_t N, int64_t ld, float drop_p, uint64_t salt1,
+                uint64_t salt2, const uint64_t* seed_base, int64_t drop_ld, void* out1, void* out2, void* stream) {
+  if (M <= 0 || N <= 0 || N % 8 || ld % 8 || drop_ld % 2 || !x || !out1 || !out2 ||
+      ((uintptr_t)x | (uintptr_t)out1 | (uintptr_t)out2) % 16)
+    return RS_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 g8((unsigned)cdiv(M * (N / 8), 256));
+  if (dtype == RS_DTYPE_BF16)
+    hipLaunchKernelGGL((dropout_v8_kernel<__bf16, true>), g8, dim3(256), 0, s, (const __bf16*)x, M, N, ld, drop_p,
+                       salt1, salt2, seed_base, drop_ld, (const int64_t*)nullptr, (__bf16*)out1, (__bf16*)out2);
+  else
+    hipLaunchKernelGGL((dropout_v8_kernel<float, true>), g8, dim3(256), 0, s, (const float*)x, M, N, ld, drop_p,
+                       salt1, salt2, seed_base, drop_ld, (const int64_t*)nullptr, (float*)out1, (float*)out2);
   return (int)hipGetLastError();
 }
 

@@ -89,3 +89,11 @@ def bert_batch(rng, batch, max_len, num_items, mask_prob=0.2, shape="ml-1m", zip
         tokens[b, max_len - n:] = tok
         labels[b, max_len - n:] = lab
     return tokens, labels
+
+
+def user_histories(rng, n_users, max_len, num_items, shape="ml-1m", zipf=None):
+    """Synthetic per-user training histories (list of item-id lists, as ``data_partition`` yields
+    ``user_train``): config-shaped lengths, Zipf item ids.  Input of rbm_amd.dataloaders.DeviceWarpSampler."""
+    zipf = zipf or ZipfItems(num_items)
+    lens = history_lengths(rng, n_users, max_len, shape)
+    return [zipf.sample(rng, int(n)).tolist() for n in lens]

@@ -260,8 +260,7 @@ class BERTEngine:
             # x_out = drop_blk(x1 + drop_res2(g W2^T + b2))
             if hp > 0:
                 dx2, dy = e((M, d)), e((M, d))
-                ops.dropout_rowmask(dx, hp, self.salt[f"blk{i}"], sb, None, dx2)
-                ops.dropout_rowmask(dx2, hp, self.salt[f"res2{i}"], sb, None, dy)
+                ops.dropout2(dx, hp, self.salt[f"blk{i}"], self.salt[f"res2{i}"], sb, dx2, dy)
             else:
                 dx2, dy = dx, dx
             ops.linear_wgrad(dy, a["g"], G(pre + "feed_forward.w_2.weight"), slab, db=G(pre + "feed_forward.w_2.bias"))

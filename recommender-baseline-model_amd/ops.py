@@ -220,6 +220,13 @@ def dropout_rowmask(x, drop_p, seed, seed_base, rowmask_ids, out, out_masked=Non
          ptr(rowmask_ids), ptr(out), ptr(out_masked), stream())
 
 
+def dropout2(x, drop_p, salt1, salt2, seed_base, out1, out2):
+    """out1 = drop(x; salt1), out2 = drop(out1; salt2): two stacked dropout sites' backward, one pass."""
+    M, N = x.shape
+    call("rs_dropout2", dtype_code(x), ptr(x), M, N, ld(x), drop_p, salt1, salt2, ptr(seed_base), N, ptr(out1),
+         ptr(out2), stream())
+
+
 def seed_advance(seed_base):
     call("rs_seed_advance", ptr(seed_base), stream())
 
@@ -334,3 +341,15 @@ def sas_head_bwd(part, divisor, out, pl, nl, dpl_in, dnl_in, dpl, dnl, pos, neg,
     call("rs_sas_head_bwd", M, d, ptr(part), ptr(divisor), ptr(out), ptr(pl), ptr(nl), ptr(dpl_in), ptr(dnl_in),
          ptr(dpl), ptr(dnl), ptr(pos), ptr(neg), ptr(E), ptr(x), ptr(ln_w), ptr(mean), ptr(rstd), ptr(dx),
          ptr(lnpart), stream())
+
+
+# ---- on-device sampler and ranking metrics (sampler.hip) -----------------------------------
+def sas_sample(user_offsets, user_items, n_users, item_num, seed_base, salt, seq, pos, neg):
+    B, T = seq.shape
+    call("rs_sas_sample", ptr(user_offsets), ptr(user_items), n_users, item_num, B, T, ptr(seed_base), salt,
+         ptr(seq), ptr(pos), ptr(neg), stream())
+
+
+def rank_metrics(scores, labels, ks_dev, ws, out):
+    R, C = scores.shape
+    call("rs_rank_metrics", ptr(scores), ptr(labels), R, C, ks_dev.numel(), ptr(ks_dev), ptr(ws), ptr(out), stream())

@@ -129,6 +129,71 @@ class FusedTrainStep:
         self._update()
         return self.loss_val if self.dp else self.loss_out[2:3]
 
+    # ---------------------------------------------------------------- checkpoints
+    def _param_slices(self):
+        """(nn.Parameter, offset) of every model parameter in the reference's optimizer order
+        (model.parameters(), BS/trainers/base.py:225-228); offsets index the flat buffers."""
+        base = self.flat.data.data_ptr()
+        out = []
+        for p in self.model.parameters():
+            off = (p.data_ptr() - base) // 4
+            if not 0 <= off < self.flat.numel:
+                raise RuntimeError("parameter is not a view of the flat buffer")
+            out.append((p, off))
+        return out
+
+    def optimizer_state_dict(self):
+        """The optimizer state in torch.optim.Adam's state_dict() layout (param_groups from a real Adam over
+        the same parameters; per-parameter 'step', 'exp_avg', 'exp_avg_sq'), so the reference trainer can
+        resume from it (BS/trainers/base.py:255-259, 'optimizer_state_dict')."""
+        torch.cuda.synchronize()
+        hy = self.opt.hyper.cpu().tolist()
+        ref = torch.optim.Adam(self.model.parameters(), lr=hy[0], betas=(hy[1], hy[2]), eps=hy[3], weight_decay=hy[4])
+        sd = ref.state_dict()
+        step = float(self.opt.state[0].item())
+        if step > 0:
+            for i, (p, off) in enumerate(self._param_slices()):
+                n = p.numel()
+                sd["state"][i] = {"step": torch.tensor(step),
+                                  "exp_avg": self.opt.m[off:off + n].view(p.shape).detach().cpu().clone(),
+                                  "exp_avg_sq": self.opt.v[off:off + n].view(p.shape).detach().cpu().clone()}
+        return sd
+
+    def load_optimizer_state_dict(self, sd):
+        """Resume from a torch.optim.Adam state_dict (e.g. a reference checkpoint's 'optimizer_state_dict')."""
+        g = sd["param_groups"][0]
+        self.opt.hyper.copy_(torch.tensor([g["lr"], g["betas"][0], g["betas"][1], g["eps"], g["weight_decay"]],
+                                          dtype=torch.float32))
+        slices = self._param_slices()
+        steps = set()
+        self.opt.m.zero_()
+        self.opt.v.zero_()
+        for i, (p, off) in enumerate(slices):
+            st = sd["state"].get(i)
+            if not st:
+                continue
+            n = p.numel()
+            self.opt.m[off:off + n].copy_(st["exp_avg"].reshape(-1))
+            self.opt.v[off:off + n].copy_(st["exp_avg_sq"].reshape(-1))
+            steps.add(float(st["step"]))
+        if len(steps) > 1:
+            raise ValueError("per-parameter Adam step counts differ; the fused optimizer keeps one")
+        self.opt.state.zero_()
+        self.opt.state[0] = steps.pop() if steps else 0.0
+
+    def checkpoint(self, epoch=None):
+        """{'model_state_dict', 'optimizer_state_dict'[, 'epoch']} as the reference's loggers save it
+        (BS/trainers/base.py:255-259, BS/loggers.py:48-58)."""
+        d = {"model_state_dict": self.model.state_dict(), "optimizer_state_dict": self.optimizer_state_dict()}
+        if epoch is not None:
+            d["epoch"] = epoch
+        return d
+
+    def load_checkpoint(self, d):
+        self.model.load_state_dict(d["model_state_dict"])
+        self.engine.sync_compute_weights()
+        self.load_optimizer_state_dict(d["optimizer_state_dict"])
+
     # ---------------------------------------------------------------- HIP graphs
     def capture(self, *example_batch, warmup=2):
         """Capture the step into HIP graphs; example_batch fixes the shapes."""
@@ -162,6 +227,49 @@ class FusedTrainStep:
                 self._update()
             self.graphs = (g,)
         return self
+
+    def capture_sampled(self, sampler, warmup=2):
+        """SAS: capture sampling (rbm_amd.dataloaders.DeviceWarpSampler, into static buffers) together with
+        the step, so ``replay_sampled()`` runs a whole training iteration -- batch construction included --
+        as one graph replay (the reference's WarpSampler + train_one_epoch body, BS/trainers/base.py:114-123)."""
+        if self.kind != "sas":
+            raise ValueError("capture_sampled is for the SAS step")
+        self.sampler = sampler
+        shape = (sampler.batch_size, sampler.max_len)
+        self.packed = torch.zeros((3,) + shape, dtype=torch.int64, device=self.flat.device)
+        self.static = list(self.packed.unbind(0))
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                sampler.sample_into(*self.static)
+                self.step(*self.static)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        if self.dp:
+            g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g1):
+                sampler.sample_into(*self.static)
+                self._compute(*self.static)
+            with torch.cuda.graph(g2):
+                self._update()
+            self.graphs = (g1, g2)
+        else:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                sampler.sample_into(*self.static)
+                self._compute(*self.static)
+                self._update()
+            self.graphs = (g,)
+        return self
+
+    def replay_sampled(self):
+        """One training iteration on a freshly sampled batch (after capture_sampled)."""
+        self.graphs[0].replay()
+        if self.dp:
+            self._exchange()
+            self.graphs[1].replay()
+        return self.loss_val if self.dp else self.loss_out[2:3]
 
     def replay_packed(self, packed):
         """replay() for a batch already stacked as one tensor [n_inputs, ...] (see capture)."""

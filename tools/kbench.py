@@ -120,6 +120,24 @@ def main():
                                                             dkv[:, :d], dkv[:, d:], 1 / math.sqrt(Dh), 0, ids, 0.2,
                                                             9, sb, wat), 8 * mb, 2.5 * aflops)
     if a.config in ("cfg3", "cfg5"):
+        # BERT block GEMMs with their fused epilogues (bert.py encode / encode_backward)
+        hg, apre, gg = rn(M, d), rn(M, ff), rn(M, ff)
+        Wqkv, bqkv, qkv = rn(3 * d, d), torch.randn(3 * d, device=dev), rn(M, 3 * d)
+        W1b, W2b = rn(ff, d), rn(d, ff)
+        run("bert qkv fwd +bias", lambda: ops.linear_fwd(hg, Wqkv, qkv, bias=bqkv), 4 * mb, 6 * M * d * d)
+        run("bert out fwd +bias+drop+resid", lambda: ops.linear_fwd(
+            x, W, y, bias=bias, drop_p=0.1, drop_seed=7, seed_base=sb, drop_ld=d, resid=z), 3 * mb, 2 * M * d * d)
+        run("bert ffn1 fwd +bias+gelu+drop+aux", lambda: ops.linear_fwd(
+            hg, W1b, gg, bias=bff, act=ops.ACT_GELU, aux_out=apre, drop_p=0.1, drop_seed=7, seed_base=sb,
+            drop_ld=ff), mb + 2 * M * ff * es, 2 * M * d * ff)
+        run("bert ffn2 fwd +bias+drop+resid+post", lambda: ops.linear_fwd(
+            gg, W2b, y, bias=bias, drop_p=0.1, drop_seed=7, seed_base=sb, drop_ld=d, resid=z, post_drop_p=0.1,
+            post_drop_seed=8), M * ff * es + 2 * mb, 2 * M * d * ff)
+        run("bert ffn2 dgrad +gelu'+drop", lambda: ops.linear_dgrad(
+            y, W2b, gg, act=ops.ACT_GELU_BWD, aux=apre, drop_p=0.1, drop_seed=7, seed_base=sb, drop_ld=ff),
+            mb + 2 * M * ff * es, 2 * M * d * ff)
+        run("bert ffn1 dgrad", lambda: ops.linear_dgrad(gg, W1b, z), M * ff * es + mb, 2 * M * d * ff)
+        run("bert qkv dgrad", lambda: ops.linear_dgrad(qkv, Wqkv, z), 4 * mb, 6 * M * d * d)
         V1 = V + 1
         R = 1792
         V1p = -(-V1 // 64) * 64
