@@ -206,6 +206,42 @@ __global__ __launch_bounds__(256) void reduce_segments_kernel(RArgs a) {
   }
 }
 
+// few splits (<= 32): one float4 column per thread, all splits summed in order by that thread (4 loads
+// in flight), 1024 columns per block -- the large BERT-size segments stream at HBM rate
+__global__ __launch_bounds__(256) void reduce_cols_kernel(RArgs a) {
+  const int b = blockIdx.x;
+  int si = 0;
+#pragma unroll 1
+  for (int q = 1; q < a.nseg; ++q)
+    if (b >= a.blk0[q]) si = q;
+  const Seg& S = a.s[si];
+  const int64_t i4 = (int64_t)(b - a.blk0[si]) * 256 + threadIdx.x;
+  const int64_t n4 = S.n / 4;
+  if (i4 >= n4) return;
+  const float4* src = reinterpret_cast<const float4*>(S.src) + i4;
+  const int64_t st4 = S.stride / 4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  int z = 0;
+  for (; z + 4 <= S.splits; z += 4) {
+    const float4 u0 = src[(int64_t)z * st4], u1 = src[(int64_t)(z + 1) * st4];
+    const float4 u2 = src[(int64_t)(z + 2) * st4], u3 = src[(int64_t)(z + 3) * st4];
+    acc.x += u0.x; acc.y += u0.y; acc.z += u0.z; acc.w += u0.w;
+    acc.x += u1.x; acc.y += u1.y; acc.z += u1.z; acc.w += u1.w;
+    acc.x += u2.x; acc.y += u2.y; acc.z += u2.z; acc.w += u2.w;
+    acc.x += u3.x; acc.y += u3.y; acc.z += u3.z; acc.w += u3.w;
+  }
+  for (; z < S.splits; ++z) {
+    const float4 u = src[(int64_t)z * st4];
+    acc.x += u.x; acc.y += u.y; acc.z += u.z; acc.w += u.w;
+  }
+  float4* o = reinterpret_cast<float4*>(S.out) + i4;
+  if (a.accumulate) {
+    const float4 p = *o;
+    acc.x += p.x; acc.y += p.y; acc.z += p.z; acc.w += p.w;
+  }
+  *o = acc;
+}
+
 }  // namespace wg
 
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -216,16 +252,20 @@ static int launch_segments(int nseg, const rs_reduce_segment* segs, int accumula
     wg::RArgs ra{};
     ra.nseg = min(wg::MAXS, nseg - base);
     ra.accumulate = accumulate;
+    int64_t max_splits = 0;
+    for (int q = 0; q < ra.nseg; ++q) max_splits = max(max_splits, segs[base + q].splits);
+    const bool cols = max_splits <= 16;     // few splits: a column per thread (reduce_cols_kernel)
     int blk = 0;
     for (int q = 0; q < ra.nseg; ++q) {
       const rs_reduce_segment& g = segs[base + q];
       if (g.n <= 0 || g.n % 4 || g.stride % 4 || g.splits < 1 || !al16(g.src) || !al16(g.out)) return RS_ERR_ARG;
       ra.s[q] = {g.src, g.stride, (int)g.splits, (int)g.n, g.out};
       ra.blk0[q] = blk;
-      blk += (int)cdiv(g.n / 4, 16);
+      blk += (int)cdiv(g.n / 4, cols ? 256 : 16);
     }
     ra.blk0[ra.nseg] = blk;
-    hipLaunchKernelGGL(wg::reduce_segments_kernel, dim3((unsigned)blk), dim3(256), 0, s, ra);
+    if (cols) hipLaunchKernelGGL(wg::reduce_cols_kernel, dim3((unsigned)blk), dim3(256), 0, s, ra);
+    else hipLaunchKernelGGL(wg::reduce_segments_kernel, dim3((unsigned)blk), dim3(256), 0, s, ra);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
   }

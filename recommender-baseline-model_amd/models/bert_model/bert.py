@@ -22,6 +22,7 @@ rs_gather_rows), runs the vocabulary GEMM + CE on those rows only, and scatters
 the hidden-state gradient back (rs_scatter_rows).
 """
 import math
+import os
 import random
 
 import numpy as np
@@ -254,33 +255,46 @@ class BERTEngine:
                                         ops.wgrad_slab_numel(M, 3 * d, d)),), torch.float32)
         wln = self.ws.get("ln", (2 * 512 * d,), torch.float32)
         wat = self.ws.get("attn", (B * H * T,), torch.float32)
+        # bf16: every block weight gradient is deferred into ONE grouped launch + ONE reduction
+        # (rs_wgrad_grouped, wgrad.hip) after the last block's input gradient
+        grouped = (self.dt == torch.bfloat16 and self.qkv_fused and d % 64 == 0 and Fd % 64 == 0
+                   and os.environ.get("RS_BERT_UNGROUPED", "0") != "1")
+        probs = []
+
+        def wgrad(dY, X, dW, db):
+            if grouped:
+                probs.append((dY, X, dW, db))
+            else:
+                ops.linear_wgrad(dY, X, dW, slab, db=db)
+
         for i in reversed(range(L)):
             a = s["blocks"][i]
             pre = f"bert.transformer_blocks.{i}."
             # x_out = drop_blk(x1 + drop_res2(g W2^T + b2))
-            if hp > 0:
+            # (the deferred weight gradients need dy / dyo to outlive the in-place LayerNorm-backward
+            # accumulations into dx2: separate buffers even without dropout)
+            if hp > 0 or grouped:
                 dx2, dy = e((M, d)), e((M, d))
                 ops.dropout2(dx, hp, self.salt[f"blk{i}"], self.salt[f"res2{i}"], sb, dx2, dy)
             else:
                 dx2, dy = dx, dx
-            ops.linear_wgrad(dy, a["g"], G(pre + "feed_forward.w_2.weight"), slab, db=G(pre + "feed_forward.w_2.bias"))
+            wgrad(dy, a["g"], G(pre + "feed_forward.w_2.weight"), G(pre + "feed_forward.w_2.bias"))
             da = e((M, Fd))
             ops.linear_dgrad(dy, self.W(pre + "feed_forward.w_2.weight"), da, act=ops.ACT_GELU_BWD, aux=a["a_pre"],
                              drop_p=hp, drop_seed=self.salt[f"ffn{i}"], seed_base=sb, drop_ld=Fd)
-            ops.linear_wgrad(da, a["h2"], G(pre + "feed_forward.w_1.weight"), slab, db=G(pre + "feed_forward.w_1.bias"))
+            wgrad(da, a["h2"], G(pre + "feed_forward.w_1.weight"), G(pre + "feed_forward.w_1.bias"))
             dh2 = e((M, d))
             ops.linear_dgrad(da, self.W(pre + "feed_forward.w_1.weight"), dh2)
             ops.layernorm_bwd(a["x1"], dh2, self.Wf(pre + "output_sublayer.norm.a_2"), a["mu2"], a["r2"], LN_EPS, dx2,
                               G(pre + "output_sublayer.norm.a_2"), G(pre + "output_sublayer.norm.b_2"), wln, 1,
                               accumulate=True)
             # x1 = x + drop_res1(o Wo^T + bo)
-            if hp > 0:
+            if hp > 0 or grouped:
                 dyo = e((M, d))
                 ops.dropout_rowmask(dx2, hp, self.salt[f"res1{i}"], sb, None, dyo)
             else:
                 dyo = dx2
-            ops.linear_wgrad(dyo, a["o"], G(pre + "attention.output_linear.weight"), slab,
-                             db=G(pre + "attention.output_linear.bias"))
+            wgrad(dyo, a["o"], G(pre + "attention.output_linear.weight"), G(pre + "attention.output_linear.bias"))
             do = e((M, d))
             ops.linear_dgrad(dyo, self.W(pre + "attention.output_linear.weight"), do)
             qkv = a["qkv"]
@@ -290,7 +304,7 @@ class BERTEngine:
                          self.salt[f"attn{i}"], sb, wat)
             dh = e((M, d))
             if self.qkv_fused:
-                ops.linear_wgrad(dqkv, a["h"], self.Wqkv(i, grad), slab, db=self.bqkv(i, grad))
+                wgrad(dqkv, a["h"], self.Wqkv(i, grad), self.bqkv(i, grad))
                 ops.linear_dgrad(dqkv, self.Wqkv(i), dh)
             else:
                 for j in range(3):
@@ -304,6 +318,22 @@ class BERTEngine:
             dx = dx2
         ops.embed_bwd(1, ids, T, dx, 1.0, hp, self.salt["emb"], sb, G("bert.embedding.token.weight"),
                       G("bert.embedding.position.pe.weight"))
+        for c in range(0, len(probs), 16):              # rs_wgrad_grouped takes up to 16 problems
+            chunk = probs[c:c + 16]
+            shapes = [(p[0].shape[1], p[1].shape[1]) for p in chunk]
+            rows = self._wgrad_rows(M, sum(-(-n // 128) * -(-k // 128) for n, k in shapes))
+            wslab = self.ws.get(f"wslab{c}", (ops.wgrad_grouped_slab_numel(shapes, M, rows),), torch.float32)
+            ops.wgrad_grouped(chunk, M, rows, wslab)
+
+    @staticmethod
+    def _wgrad_rows(M, tiles):
+        """rows per split of the grouped weight-gradient launch: about three 128x128-tile workgroups per
+        CU in total (one resident at a time), so the row ranges balance over the 256 CUs."""
+        env = os.environ.get("RS_WGRAD_ROWS")
+        if env:
+            return int(env)
+        splits = max(1, round(768 / tiles))
+        return max(64, -(-(-(-M // splits)) // 64) * 64)
 
     # ---- full-vocabulary logits (the reference forward API) ---------------------------
     def logits(self, xL):

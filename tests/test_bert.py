@@ -137,3 +137,34 @@ def test_bert_fp32_matches_oracle_shapes(V, T, d, L, h, B, cap):
             assert float(g.norm()) <= 1e-5 * scale, k
             continue
         assert rel(g.numpy(), g64[k].numpy()) < GRAD_TOL_F32, (k, rel(g.numpy(), g64[k].numpy()))
+
+
+@pytest.mark.gpu
+def test_bert_grouped_wgrad_matches_per_weight(monkeypatch):
+    """bf16: the grouped weight-gradient launch (rs_wgrad_grouped) gives the per-weight GEMM gradients
+    (same bf16 operands, fp32 sums in another order) on a cfg3-like block (d=256, 4 heads x 64)."""
+    import rbm_amd  # noqa: F401
+    import rbm_amd.data as synth
+    from rbm_amd.models import model_factory
+    from rbm_amd.train_step import FusedTrainStep
+    a = argparse.Namespace(model_code="bert", num_items=2000, max_len=100, device="cuda", bert_hidden_units=256,
+                           bert_num_blocks=2, bert_num_heads=2, bert_dropout=0.1, bert_hidden_dropout=0.1,
+                           bert_mask_prob=0.2, model_init_seed=1, rs_dtype="bf16")
+    rng = np.random.default_rng(0)
+    tok, lab = (torch.from_numpy(t).cuda() for t in synth.bert_batch(rng, 8, 100, 2000, mask_prob=0.2))
+    grads = []
+    for ungrouped in ("1", "0"):
+        monkeypatch.setenv("RS_BERT_UNGROUPED", ungrouped)
+        torch.manual_seed(0)
+        m = model_factory(a)
+        tr = FusedTrainStep(m, lr=0.0)
+        tr.engine.seed_base.zero_()
+        tr.flat.grad.zero_()
+        tr.engine.train_loss_and_backward(tok, lab, tr.loss_out, tr._divisor, tr.flat.grad)
+        torch.cuda.synchronize()
+        grads.append({k: tr.flat.view(k, tr.flat.grad).cpu().numpy().copy() for k, _ in m.named_parameters()})
+    for k in grads[0]:
+        if "transformer_blocks" in k and "norm" not in k and "linear_layers.1.bias" not in k:
+            assert rel(grads[1][k], grads[0][k]) < 1e-5, (k, rel(grads[1][k], grads[0][k]))
+        else:                                       # untouched by the change (float atomics in the table)
+            assert rel(grads[1][k], grads[0][k]) < 1e-6, k

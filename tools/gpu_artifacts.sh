@@ -23,6 +23,6 @@ for c in ${CONFIGS:-cfg2 cfg3 cfg4}; do
   timeout -k 10 900 python bench.py --config $c $CB > $OUT/bench_$c.log 2>&1; rc=$?; tail -1 $OUT/bench_$c.log | cut -c1-160
   [ $rc -eq 0 ] || exit $rc
   tail -1 $OUT/bench_$c.log > $OUT/bench_$c.json
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_$c -o prof -- python3 bench.py --config $c --steps 50 --warmup 10 --cpu-baseline-seconds 0 > $OUT/rocprof_$c.log 2>&1 || { tail -20 $OUT/rocprof_$c.log; exit 1; }
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_$c -o prof --output-format csv -- python3 bench.py --config $c --steps 50 --warmup 10 --cpu-baseline-seconds 0 > $OUT/rocprof_$c.log 2>&1 || { tail -20 $OUT/rocprof_$c.log; exit 1; }
 done
 echo done
