@@ -211,6 +211,21 @@ int rs_dropout_rowmask(int dtype, const void* x, int64_t M, int64_t N, int64_t l
 int rs_dropout2(int dtype, const void* x, int64_t M, int64_t N, int64_t ld, float drop_p, uint64_t salt1,
                 uint64_t salt2, const uint64_t* seed_base, int64_t drop_ld, void* out1, void* out2, void* stream);
 
+/* ---- BERT vocabulary head + CrossEntropyLoss(ignore_index=0), logits never materialised (bf16;
+ * vocab_ce.hip).  Replaces, for the labelled rows of the fused step, rs_gemm (logits = h E^T + b,
+ * BS/models/bert.py:16) + rs_ce_fwd + rs_ce_bwd (BS/trainers/bert.py:11,36-40).
+ * h [R][d] bf16 (ldh), E [V1][d] bf16 (lde), bias [V1] fp32, labels [R] (0 = ignored), rows_dev:
+ * device row count (rows >= it are skipped; nullable).  ws: rs_vocab_ce_ws_numel floats, written by
+ * fwd and read by bwd.  fwd: out = {loss sum, labelled count, sum / (count_override or count)};
+ * bwd: dlogits [R][V1] bf16 (lddl, 16-B aligned rows) = (softmax - onehot) * (dloss or 1) / count. */
+int64_t rs_vocab_ce_ws_numel(int64_t R, int64_t V1);
+int rs_vocab_ce_fwd(int64_t R, int64_t V1, int64_t d, const void* h, int64_t ldh, const void* E, int64_t lde,
+                    const float* bias, const int64_t* labels, const int* rows_dev, const float* count_override,
+                    float* ws, float* out, void* stream);
+int rs_vocab_ce_bwd(int64_t R, int64_t V1, int64_t d, const void* h, int64_t ldh, const void* E, int64_t lde,
+                    const float* bias, const int64_t* labels, const int* rows_dev, const float* count,
+                    const float* dloss, const float* ws, void* dlogits, int64_t lddl, void* stream);
+
 /* *seed_base += 1 on the stream (advances every dropout mask; capturable). */
 int rs_seed_advance(uint64_t* seed_base, void* stream);
 

@@ -71,6 +71,9 @@ SIGNATURES = {
     "rs_cast_bf16": [i64, vp, vp, vp],
     "rs_dropout_rowmask": [i32, vp, i64, i64, i64, f32, u64, vp, i64, vp, vp, vp, vp],
     "rs_dropout2": [i32, vp, i64, i64, i64, f32, u64, u64, vp, i64, vp, vp, vp],
+    "rs_vocab_ce_ws_numel": [i64, i64],
+    "rs_vocab_ce_fwd": [i64, i64, i64, vp, i64, vp, i64, vp, vp, vp, vp, vp, vp, vp],
+    "rs_vocab_ce_bwd": [i64, i64, i64, vp, i64, vp, i64, vp, vp, vp, vp, vp, vp, vp, i64, vp],
     "rs_seed_advance": [vp, vp],
     "rs_sas_block_in": [i64, i64, vp, i64, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "rs_sas_block_out": [i64, i64, vp, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32,
@@ -92,7 +95,8 @@ SIGNATURES = {
     "rs_abi_version": [],
 }
 
-RESTYPES = {"rs_wgrad_grouped_slab_numel": C.c_int64, "rs_item_index_ws_bytes": C.c_int64}
+RESTYPES = {"rs_wgrad_grouped_slab_numel": C.c_int64, "rs_item_index_ws_bytes": C.c_int64,
+            "rs_vocab_ce_ws_numel": C.c_int64}
 
 _lib = None
 

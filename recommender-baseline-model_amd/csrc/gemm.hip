@@ -235,7 +235,7 @@ int rs_gemm(int dtype, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t
   const int vec = 16 / esz;
   if ((lda % vec) || (ldb % vec) || ((uintptr_t)A % 16) || ((uintptr_t)B % 16)) return RS_ERR_ARG;
   if (split_k > 1 && !slab) return RS_ERR_ARG;
-  GemmArgs a;
+  GemmArgs a{};
   a.M = M; a.N = N; a.K = K; a.A = A; a.lda = lda; a.B = B; a.ldb = ldb; a.C = C; a.ldc = ldc;
   a.c_f32 = c_f32; a.split_k = split_k;
   a.k_per_split = split_k > 1 ? cdiv(cdiv(K, split_k), 64) * 64 : (K > 0 ? K : 1);
@@ -260,7 +260,20 @@ int rs_linear_wgrad(int dtype, int64_t M, int64_t N, int64_t K, const void* dY, 
   const int vec = 16 / esz;
   if ((lddy % vec) || (ldx % vec) || ((uintptr_t)dY % 16) || ((uintptr_t)X % 16) || ((uintptr_t)slab % 16))
     return RS_ERR_ARG;
-  GemmArgs a;
+  GemmArgs a{};
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == RS_DTYPE_BF16 && splits == 1 && K % 8 == 0 && ((uintptr_t)dW % 16) == 0) {
+    // one split: the tiles accumulate straight into dW (and the ones-operand column sums into db)
+    a.M = N; a.N = K; a.K = M; a.A = dY; a.lda = lddy; a.B = X; a.ldb = ldx; a.C = dW; a.ldc = K;
+    a.c_f32 = 1; a.split_k = 1; a.k_per_split = M;
+    a.bias_colsum = db ? 1 : 0;
+    a.colsum_out = db;
+    a.epi = rs_epilogue{};
+    a.epi.alpha = 1.0f;
+    a.epi.accumulate = accumulate;
+    a.epi.rows_dev = rows_dev;
+    return (int)gemm_bf16_launch(1, 1, a, s);
+  }
   a.M = N; a.N = K; a.K = M; a.A = dY; a.lda = lddy; a.B = X; a.ldb = ldx; a.C = nullptr; a.ldc = 0;
   a.c_f32 = 1; a.split_k = splits;
   a.k_per_split = cdiv(cdiv(M, splits), 64) * 64;
@@ -270,7 +283,6 @@ int rs_linear_wgrad(int dtype, int64_t M, int64_t N, int64_t K, const void* dY, 
   a.epi = rs_epilogue{};
   a.epi.alpha = 1.0f;
   a.epi.rows_dev = rows_dev;
-  hipStream_t s = (hipStream_t)stream;
   hipError_t err = dtype == RS_DTYPE_BF16 ? gemm_bf16_launch(1, 1, a, s) : launch_t<float, true, true>(a, s);
   if (err != hipSuccess) return (int)err;
   // one pass over the slabs: columns [0, N*K) -> dW, [N*K, N*K+N) -> db

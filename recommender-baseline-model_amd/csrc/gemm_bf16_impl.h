@@ -193,7 +193,7 @@ __device__ __forceinline__ void epi8(const GemmArgs& a, int64_t m, int64_t n, fl
 // ---- compile-time epilogue classes: the runtime-flag epilogue (epi8) made hipcc spill SGPRs
 // into VGPR lanes and roughly tripled the per-wave instruction count of these short GEMMs
 enum : int { EB = 1, ED = 2, ER = 4, EM = 8, EP = 16, EA = 32, EF = 64 };  // bias drop resid rowmask post acc f32C
-constexpr int EC_GENERIC = -1, EC_SLAB = -2;
+constexpr int EC_GENERIC = -1, EC_SLAB = -2, EC_CE_PART = -3, EC_CE_GRAD = -4;
 constexpr int ec_act(int ec) { return (ec >> 8) & 7; }
 
 template <int EC>
@@ -362,6 +362,83 @@ __device__ __forceinline__ void epi_rows(const GemmArgs& a, const float* Cs, int
   }
 }
 
+// Vocabulary cross-entropy epilogues (vocab_ce.hip).  Columns n..n+7 of rows row0 + p*RPP (the 16
+// threads of a row hold its 128 columns; columns >= N are masked).
+//  EC_CE_PART: per (row, column tile) the online-softmax pair (max, sum exp(x - max)) of the
+//              tile's logits x = acc + bias, and the label's logit when it falls in the tile;
+//  EC_CE_GRAD: dlogits = (exp(x - lse[row]) - [col == label]) * dloss / count as bf16 (ce_bwd_kernel's
+//              arithmetic, loss.hip), so the fp32 logits are never written.
+template <int EC, int NP, int RPP, int LDC, int TPR>
+__device__ __forceinline__ void ce_rows(const GemmArgs& a, const float* Cs, int row0, int c8, int64_t m0, int64_t Mb,
+                                        int64_t n, unsigned tn) {
+  float bias[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bias[j] = (a.epi.bias && n + j < a.N) ? a.epi.bias[n + j] : 0.f;
+  int64_t lab[NP];
+  float lse[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int64_t m = m0 + row0 + p * RPP;
+    lab[p] = m < Mb ? a.ce.labels[m] : 0;
+    if constexpr (EC == EC_CE_GRAD) lse[p] = m < Mb ? a.ce.lse[m] : 0.f;
+  }
+  float sc = 0.f;
+  if constexpr (EC == EC_CE_GRAD) sc = (a.ce.dloss ? *a.ce.dloss : 1.f) / *a.ce.count;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int row = row0 + p * RPP;
+    const int64_t m = m0 + row;
+    if (m >= Mb) break;     // uniform over the TPR threads of a row
+    float v[8];
+    {
+      const float4 v0 = *reinterpret_cast<const float4*>(Cs + row * LDC + c8);
+      const float4 v1 = *reinterpret_cast<const float4*>(Cs + row * LDC + c8 + 4);
+      v[0] = v0.x; v[1] = v0.y; v[2] = v0.z; v[3] = v0.w; v[4] = v1.x; v[5] = v1.y; v[6] = v1.z; v[7] = v1.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += bias[j];
+    if constexpr (EC == EC_CE_PART) {
+      float mx = -__builtin_inff(), sm = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (n + j < a.N) mx = fmaxf(mx, v[j]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (n + j < a.N) sm += __expf(v[j] - mx);
+#pragma unroll
+      for (int o = TPR / 2; o > 0; o >>= 1) {
+        const float m2 = __shfl_xor(mx, o, TPR), s2 = __shfl_xor(sm, o, TPR);
+        const float mm = fmaxf(mx, m2);
+        sm = (mm == -__builtin_inff()) ? 0.f : sm * __expf(mx - mm) + s2 * __expf(m2 - mm);
+        mx = mm;
+      }
+      if (c8 == 0) {
+        a.ce.part[(m * a.ce.ntn + tn) * 2 + 0] = mx;
+        a.ce.part[(m * a.ce.ntn + tn) * 2 + 1] = sm;
+      }
+      const int64_t l = lab[p];
+      if (l >= n && l < n + 8 && l < a.N) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (l == n + j) a.ce.tgt[m] = v[j];
+      }
+    } else {
+      float g[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        g[j] = lab[p] != 0 ? (__expf(v[j] - lse[p]) - (n + j == lab[p] ? 1.f : 0.f)) * sc : 0.f;
+      __bf16* C = reinterpret_cast<__bf16*>(a.C) + m * a.ldc + n;
+      if (n + 8 <= a.N) {
+        store_chunk<__bf16>(C, g);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (n + j < a.N) C[j] = (__bf16)g[j];
+      }
+    }
+  }
+}
+
 template <bool AK, bool BK, int BM, int BN, int EC>
 __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs a) {
   using IA = Img<AK, BM>;
@@ -493,7 +570,10 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int64_t m = m0 + wm * (BM / 2) + 16 * i + 4 * g + r;
-          if (m < a.M) a.slab[(int64_t)z * a.slab_stride + a.M * a.N + m] = accb[i][r];
+          if (m < a.M) {
+            if (a.colsum_out) a.colsum_out[m] = (a.epi.accumulate ? a.colsum_out[m] : 0.f) + accb[i][r];
+            else a.slab[(int64_t)z * a.slab_stride + a.M * a.N + m] = accb[i][r];
+          }
         }
     }
   }
@@ -502,6 +582,10 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs a) {
   constexpr int RPP = 256 / TPR;      // rows per pass
   const int c8 = (tid % TPR) * 8;
   const int64_t n = n0 + c8;
+  if constexpr (EC == EC_CE_PART || EC == EC_CE_GRAD) {
+    ce_rows<EC, BM / RPP, RPP, LDC, TPR>(a, Cs, tid / TPR, c8, m0, Mb, n, tn);
+    return;
+  }
   if (n >= a.N) return;
   uint32_t s1 = 0, s2 = 0;
   if constexpr (EC >= 0) {

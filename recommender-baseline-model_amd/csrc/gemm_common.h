@@ -20,8 +20,20 @@ struct GemmArgs {
   float* slab;  // when non-null: write raw fp32 partials to slab[z*slab_stride + m*N + n]
   int64_t slab_stride;
   int bias_colsum;  // (AK only) also write sum_k A(m,k) of this split to slab[z*slab_stride + M*N + m]
+  float* colsum_out;  // (bf16 path, no slab) ... or add it to colsum_out[m] (epi.accumulate) / store it there
   rs_epilogue epi;
   int vec_ok;  // (bf16 path) 8-column vectorised epilogue legal for this call
+  // (bf16 path, vocabulary cross-entropy epilogues of vocab_ce.hip) row labels; per (row, column
+  // tile) (max, sum exp) partials [M][ntn][2]; label logits [M]; row log-sum-exp [M]; loss divisor
+  struct {
+    const int64_t* labels;
+    float* part;
+    float* tgt;
+    const float* lse;
+    const float* count;
+    const float* dloss;
+    int64_t ntn;
+  } ce;
 };
 
 

@@ -369,16 +369,24 @@ class BERTEngine:
         hl = self.ws.get("hl", (cap, d), self.dt)
         lab = self.ws.get("lab", (cap,), torch.int64)
         ops.gather_rows(xL, idx, cnt, cap, hl, labels, lab)
-        logits = self.ws.get("logits", (cap, self.V1p), torch.float32)[:, :self.V1]
-        ops.linear_fwd(hl, self.W("out.weight"), logits, bias=self.Wf("out.bias"), rows_dev=cnt)
-        wce = self.ws.get("wce", (3 * cap,), torch.float32)
-        ops.ce_fwd(logits, lab, wce, loss_out, None, rows_dev=cnt)
-        count = global_count(loss_out[1:2])
-        if self.dt == torch.float32:
-            dl = logits                                   # in place
-        else:
+        if self.dt == torch.bfloat16 and os.environ.get("RS_BERT_UNFUSED_CE", "0") != "1":
+            # logits never materialised: GEMM + online-softmax partials, then GEMM + dlogits (vocab_ce.hip)
+            wce = self.ws.get("vce", (ops.vocab_ce_ws_numel(cap, self.V1),), torch.float32)
+            ops.vocab_ce_fwd(hl, self.W("out.weight"), self.Wf("out.bias"), lab, wce, loss_out, rows_dev=cnt)
+            count = global_count(loss_out[1:2])
             dl = self.ws.get("dlogits", (cap, self.V1p), self.dt)[:, :self.V1]
-        ops.ce_bwd(logits, lab, count, None, wce, dl, rows_dev=cnt)
+            ops.vocab_ce_bwd(hl, self.W("out.weight"), self.Wf("out.bias"), lab, wce, count, dl, rows_dev=cnt)
+        else:
+            logits = self.ws.get("logits", (cap, self.V1p), torch.float32)[:, :self.V1]
+            ops.linear_fwd(hl, self.W("out.weight"), logits, bias=self.Wf("out.bias"), rows_dev=cnt)
+            wce = self.ws.get("wce", (3 * cap,), torch.float32)
+            ops.ce_fwd(logits, lab, wce, loss_out, None, rows_dev=cnt)
+            count = global_count(loss_out[1:2])
+            if self.dt == torch.float32:
+                dl = logits                                   # in place
+            else:
+                dl = self.ws.get("dlogits", (cap, self.V1p), self.dt)[:, :self.V1]
+            ops.ce_bwd(logits, lab, count, None, wce, dl, rows_dev=cnt)
         slab = self.ws.get("slab_out", (ops.wgrad_slab_numel(cap, self.V1, d),), torch.float32)
         ops.linear_wgrad(dl, hl, self.flat.view("out.weight", grad), slab, db=self.flat.view("out.bias", grad),
                          rows_dev=cnt)

@@ -105,7 +105,8 @@ def linear_wgrad(dY, X, dW, slab, db=None, split_k=None, accumulate=True, rows_d
     M, N = dY.shape
     K = X.shape[1]
     s = split_k or split_for(M, N, K)
-    assert slab.numel() >= s * (N * K + N), "slab workspace too small"
+    direct = s == 1 and dY.dtype == torch.bfloat16 and K % 8 == 0 and dW.data_ptr() % 16 == 0  # no slab used
+    assert direct or slab.numel() >= s * (N * K + N), "slab workspace too small"
     assert dY.dtype == X.dtype
     call("rs_linear_wgrad", dtype_code(dY), M, N, K, ptr(dY), ld(dY), ptr(X), ld(X), ptr(dW), ptr(db),
          int(accumulate), s, ptr(slab), ptr(rows_dev), stream())
@@ -225,6 +226,31 @@ def dropout2(x, drop_p, salt1, salt2, seed_base, out1, out2):
     M, N = x.shape
     call("rs_dropout2", dtype_code(x), ptr(x), M, N, ld(x), drop_p, salt1, salt2, ptr(seed_base), N, ptr(out1),
          ptr(out2), stream())
+
+
+# ---- BERT vocabulary head + cross entropy, logits not materialised (vocab_ce.hip) -----------
+def vocab_ce_ws_numel(R, V1):
+    n = _lib.lib().rs_vocab_ce_ws_numel(R, V1)
+    if n < 0:
+        raise RuntimeError("rs_vocab_ce_ws_numel: bad arguments")
+    return n
+
+
+def vocab_ce_fwd(h, E, bias, labels, ws, out, rows_dev=None, count_override=None):
+    """out[0:3] = (loss sum, labelled count, mean) of CE(h E^T + bias, labels, ignore_index=0); ws keeps
+    the row log-sum-exp for vocab_ce_bwd."""
+    R, d = h.shape
+    V1 = E.shape[0]
+    call("rs_vocab_ce_fwd", R, V1, d, ptr(h), ld(h), ptr(E), ld(E), ptr(bias), ptr(labels), ptr(rows_dev),
+         ptr(count_override), ptr(ws), ptr(out), stream())
+
+
+def vocab_ce_bwd(h, E, bias, labels, ws, count, dl, rows_dev=None, dloss=None):
+    """dl [R, V1] bf16 = (softmax(h E^T + bias) - onehot(labels)) * dloss / count."""
+    R, d = h.shape
+    V1 = E.shape[0]
+    call("rs_vocab_ce_bwd", R, V1, d, ptr(h), ld(h), ptr(E), ld(E), ptr(bias), ptr(labels), ptr(rows_dev),
+         ptr(count), ptr(dloss), ptr(ws), ptr(dl), ld(dl), stream())
 
 
 def seed_advance(seed_base):

@@ -168,3 +168,36 @@ def test_bert_grouped_wgrad_matches_per_weight(monkeypatch):
             assert rel(grads[1][k], grads[0][k]) < 1e-5, (k, rel(grads[1][k], grads[0][k]))
         else:                                       # untouched by the change (float atomics in the table)
             assert rel(grads[1][k], grads[0][k]) < 1e-6, k
+
+
+@pytest.mark.gpu
+def test_bert_fused_vocab_ce_matches_materialised(monkeypatch):
+    """bf16: the vocabulary head without materialised logits (rs_vocab_ce_fwd/bwd) gives the loss and
+    gradients of the materialised sequence (rs_gemm fp32 logits + rs_ce_fwd + rs_ce_bwd), at the cfg3
+    vocabulary (26,745 classes: a ragged last column tile)."""
+    import rbm_amd  # noqa: F401
+    import rbm_amd.data as synth
+    from rbm_amd.models import model_factory
+    from rbm_amd.train_step import FusedTrainStep
+    a = argparse.Namespace(model_code="bert", num_items=26744, max_len=50, device="cuda", bert_hidden_units=64,
+                           bert_num_blocks=1, bert_num_heads=2, bert_dropout=0.0, bert_hidden_dropout=0.0,
+                           bert_mask_prob=0.2, model_init_seed=1, rs_dtype="bf16")
+    rng = np.random.default_rng(1)
+    tok, lab = (torch.from_numpy(t).cuda() for t in synth.bert_batch(rng, 16, 50, 26744, mask_prob=0.2))
+    out = []
+    for unfused in ("1", "0"):
+        monkeypatch.setenv("RS_BERT_UNFUSED_CE", unfused)
+        torch.manual_seed(0)
+        m = model_factory(a)
+        tr = FusedTrainStep(m, lr=0.0, max_labelled=256)
+        tr.flat.grad.zero_()
+        tr.engine.train_loss_and_backward(tok, lab, tr.loss_out, tr._divisor, tr.flat.grad, max_labelled=256)
+        torch.cuda.synchronize()
+        out.append((tr.loss_out[:3].cpu().numpy().copy(),
+                    {k: tr.flat.view(k, tr.flat.grad).cpu().numpy().copy() for k, _ in m.named_parameters()}))
+    (l0, g0), (l1, g1) = out
+    assert l1[1] == l0[1] and abs(l1[0] - l0[0]) < 1e-5 * abs(l0[0]) and abs(l1[2] - l0[2]) < 1e-5 * abs(l0[2])
+    for k in g0:
+        if "linear_layers.1.bias" in k:
+            continue
+        assert rel(g1[k], g0[k]) < 2e-3, (k, rel(g1[k], g0[k]))

@@ -57,3 +57,27 @@ def test_wgrad_grouped_is_deterministic():
         ops.wgrad_grouped([(dY, X, dW, db)], M, 128, slab)
         outs.append((dW.clone(), db.clone()))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("M,N,K,acc", [(1792, 26745, 256, True), (300, 1000, 64, False), (1000, 130, 128, True)])
+def test_linear_wgrad_single_split_direct(M, N, K, acc):
+    """rs_linear_wgrad with one split accumulates straight into dW / db (no slab): the BERT vocabulary
+    weight gradient (N = |items|+1 not a multiple of 8), with a device row count below M."""
+    import rbm_amd  # noqa: F401
+    from rbm_amd import ops
+    g = torch.Generator(device="cuda").manual_seed(M + N)
+    Np = -(-N // 64) * 64                                   # row pitch: a multiple of 8 elements, as the ABI asks
+    dY = torch.randn(M, Np, device="cuda", generator=g).bfloat16()[:, :N]
+    X = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    dW0 = torch.randn(N, K, device="cuda", generator=g)
+    db0 = torch.randn(N, device="cuda", generator=g)
+    rows = M - 37
+    rows_dev = torch.tensor([rows], dtype=torch.int32, device="cuda")
+    dW, db = dW0.clone(), db0.clone()
+    slab = torch.empty(1, device="cuda")
+    ops.linear_wgrad(dY, X, dW, slab, db=db, split_k=1, accumulate=acc, rows_dev=rows_dev)
+    torch.cuda.synchronize()
+    ref_w = dY[:rows].float().t() @ X[:rows].float() + (dW0 if acc else 0)
+    ref_b = dY[:rows].float().sum(0) + (db0 if acc else 0)
+    assert rel(dW.cpu().numpy(), ref_w.cpu().numpy()) < 1e-5
+    assert rel(db.cpu().numpy(), ref_b.cpu().numpy()) < 1e-5
