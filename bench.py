@@ -143,7 +143,7 @@ def _roof(kernel, us, flops, nbytes, dtype, note):
 def roofline(cfg, B, dtype, reps=50):
     """Dominant kernel of the step (by rocprof device time), timed alone with HIP events on a
     dedicated stream.  SAS: the attention backward (rs_attn_bwd: dQ+delta and dK/dV kernels);
-    BERT: the labelled-row vocabulary-logits GEMM (rs_gemm, fp32 out)."""
+    BERT: the grouped block weight gradients (rs_wgrad_grouped)."""
     from rbm_amd import ops
     es = 2 if dtype == "bf16" else 4
     dt = torch.bfloat16 if dtype == "bf16" else torch.float32
@@ -173,18 +173,22 @@ def roofline(cfg, B, dtype, reps=50):
         nbytes = 8 * M * d * es + B * H * T * 4 * 2
         return _roof("rs_attn_bwd (attn_bwd_dq_lds + attn_bwd_dkv_lds)", us, flops, nbytes, dtype,
                      f"causal attention backward, B={B} T={T} Dh={Dh} dropout {cfg['p']}; 2 launches per call")
-    V1 = cfg["V"] + 1
-    R = int(round(B * T * 0.72 * cfg["mask"] / 64)) * 64   # ~ labelled rows per batch (ML-1M-shaped lengths)
-    V1p = -(-V1 // 64) * 64
-    h = torch.randn(R, d, device="cuda", generator=g).to(dt)
-    W = (0.05 * torch.randn(V1, d, device="cuda", generator=g)).to(dt)
-    b = torch.zeros(V1, device="cuda")
-    out = torch.empty(R, V1p, device="cuda")[:, :V1]
-    us = _time_on_stream(lambda: ops.linear_fwd(h, W, out, bias=b), reps, stream)
-    flops = 2.0 * R * V1 * d
-    nbytes = R * d * es + V1 * d * es + R * V1 * 4
-    return _roof("rs_gemm (vocab logits, labelled rows)", us, flops, nbytes, dtype,
-                 f"R={R} labelled rows x V+1={V1} x d={d}, fp32 logits out")
+    # BERT: the grouped weight-gradient launch of all block weights (rs_wgrad_grouped: GEMM + reduction),
+    # the largest single kernel of the step
+    from rbm_amd.models.bert_model.bert import BERTEngine
+    M, Fd, L = B * T, 4 * d, cfg["L"]
+    rn = lambda *s: torch.randn(*s, device="cuda", generator=g).to(dt)  # noqa: E731
+    shapes = [(d, Fd), (Fd, d), (d, d), (3 * d, d)] * L        # W2, W1, Wo, Wqkv  (N, K)
+    probs = [(rn(M, n), rn(M, k), torch.zeros(n, k, device="cuda"), torch.zeros(n, device="cuda"))
+             for n, k in shapes]
+    rows = BERTEngine._wgrad_rows(M, sum((n // 128) * (k // 128) for n, k in shapes))
+    slab = torch.empty(ops.wgrad_grouped_slab_numel(shapes, M, rows), device="cuda")
+    us = _time_on_stream(lambda: ops.wgrad_grouped(probs, M, rows, slab), reps, stream)
+    flops = sum(2.0 * M * n * k for n, k in shapes)
+    nbytes = sum(M * (n + k) * es + (n * k + n) * 4 * 2 for n, k in shapes)   # dY, X once; dW, db read+write
+    return _roof("rs_wgrad_grouped (wgrad_group_kernel + reduce_cols_kernel)", us, flops, nbytes, dtype,
+                 f"{len(shapes)} block weight gradients of M={M} token rows (d={d}, ff={Fd}, L={L}), "
+                 f"{-(-M // rows)} row splits; 2 launches per call")
 
 
 # ------------------------------------------------------------------------------------ CPU baseline
@@ -245,7 +249,7 @@ def main():
     model.train()
     host_batches = make_batches(cfg, B, args.nbatches, seed=1000 + rank)
     max_lab = None
-    if cfg["model"] == "bert":
+    if cfg["model"] == "bert" and args.sampler == "host":
         cnt = max(int((lab != 0).sum()) for _, lab in host_batches)
         if world > 1:
             t = torch.tensor([cnt], device="cuda")
@@ -262,6 +266,18 @@ def main():
         users = synth.user_histories(np.random.default_rng(77 + rank), cfg.get("users", 6040), cfg["T"], cfg["V"],
                                      shape=cfg["shape"])
         sampler = DeviceWarpSampler(users, cfg["V"], B, cfg["T"], seed=5 + rank)
+        trainer.capture_sampled(sampler)
+        batches = [()]
+        run = trainer.replay_sampled
+    elif args.sampler == "device":
+        # BERT: on-device cloze masking (rs_bert_mask) in the step graph; the labelled-row cap stays
+        # B*T (default), every vocabulary GEMM is bounded by the device-side labelled count
+        import rbm_amd.data as synth
+        from rbm_amd.dataloaders import DeviceBertMasker
+        users = synth.user_histories(np.random.default_rng(77 + rank), cfg.get("users", 6040), cfg["T"], cfg["V"],
+                                     shape=cfg["shape"])
+        sampler = DeviceBertMasker(users, cfg["V"], B, cfg["T"], cfg["mask"], seed=5 + rank)
+        sampler.new_epoch()
         trainer.capture_sampled(sampler)
         batches = [()]
         run = trainer.replay_sampled

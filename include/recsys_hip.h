@@ -178,6 +178,12 @@ int rs_gather_rows(int dtype, const void* src, int64_t lds, int64_t d, const int
 int rs_scatter_rows(int dtype, const void* src, int64_t lds, int64_t d, const int32_t* rank, int64_t n, void* dst,
                     int64_t ldd, void* stream);
 
+/* dst[r] = rank[r] >= 0 ? sum_z slab[z][rank[r]][:] : 0 (cast to dtype) for r < n: the split-K partials
+ * (slab[splits][cap][d] fp32, rs_gemm split_k of a compacted-row GEMM) reduced, cast and scattered back
+ * to the token rows in one pass (replaces rs_reduce_slabs + rs_cast_bf16 + rs_scatter_rows). */
+int rs_splitk_scatter_rows(int dtype, const float* slab, int splits, int64_t cap, int64_t d, const int32_t* rank,
+                           int64_t n, void* dst, int64_t ldd, void* stream);
+
 /* torch.optim.Adam step (BS/trainers/base.py:225-228; amsgrad=False) over a
  * flat fp32 buffer.  hyper (device fp32[5]) = {lr, beta1, beta2, eps, weight_decay}.
  * state (device double[4]): rs_adam_prepare does state[0] += 1 (the step count) and
@@ -343,6 +349,15 @@ int rs_sas_head_bwd(int64_t M, int64_t d, const float* part, const float* diviso
 int rs_sas_sample(const int64_t* user_offsets, const int64_t* user_items, int64_t n_users, int64_t item_num,
                   int64_t batch, int64_t max_len, uint64_t* seed_base, uint64_t salt, int64_t* seq, int64_t* pos,
                   int64_t* neg, void* stream);
+/* rs_bert_mask: one BERT4Rec training batch as BertTrainDataset builds it (BS/dataloaders/bert.py:77-110):
+ * row b's user = perm[(cursor*batch + b) mod n_users] (perm nullable = identity), its last max_len items
+ * cloze-masked (prob mask_prob; then 80 % [MASK] = num_items+1, 10 % a uniform item, 10 % kept;
+ * label = the item, 0 elsewhere), left padded.  state[2] = {step seed, cursor} on the device, both
+ * advanced by 1 before sampling (graph-capturable; reset state[1] to 0 at an epoch start). */
+int rs_bert_mask(const int64_t* user_offsets, const int64_t* user_items, int64_t n_users, int64_t num_items,
+                 int64_t batch, int64_t max_len, float mask_prob, const int64_t* perm, uint64_t* state, uint64_t salt,
+                 int64_t* tokens, int64_t* labels, void* stream);
+
 /* rs_rank_metrics: recalls_ndcgs_and_mrr_for_ks (BS/trainers/utils.py:28-57) over scores/labels
  * fp32 [rows][cands] (labels 0/1 weights), ks: device int[nk] (nk <= 8).  out[3*q + {0,1,2}] =
  * mean Recall@k, NDCG@k, MRR@k for ks[q]; ws >= 3*nk*rows floats.  Ranks follow a stable

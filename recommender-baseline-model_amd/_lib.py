@@ -91,6 +91,8 @@ SIGNATURES = {
     "rs_item_grad": [vp, i32, i64, i64, i64, vp, f32, f32, u64, vp, vp, vp, vp, vp, vp],
     "rs_transpose_bf16": [i64, vp, i64, vp, vp, vp],
     "rs_sas_sample": [vp, vp, i64, i64, i64, i64, vp, u64, vp, vp, vp, vp],
+    "rs_bert_mask": [vp, vp, i64, i64, i64, i64, f32, vp, vp, u64, vp, vp, vp],
+    "rs_splitk_scatter_rows": [i32, vp, i32, i64, i64, vp, i64, vp, i64, vp],
     "rs_rank_metrics": [vp, vp, i64, i64, i32, vp, vp, vp, vp],
     "rs_abi_version": [],
 }

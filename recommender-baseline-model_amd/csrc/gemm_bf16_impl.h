@@ -456,15 +456,22 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs a) {
   // block -> tile (32-bit: every block index fits); XCD-aware: blocks b and b+8 share an XCD, so
   // consecutive tiles (which share A rows / B columns) go to one XCD's L2
   const unsigned tiles_n = (unsigned)((a.N + BN - 1) / BN);
+  const int64_t Mb = (!AK && a.epi.rows_dev) ? min(a.M, (int64_t)*a.epi.rows_dev) : a.M;
   unsigned bid = blockIdx.x;
   {
-    const unsigned nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, x = bid & 7;
+    // a device row count (compacted rows) leaves only the first cdiv(Mb, BM) row tiles live: remap over
+    // those, so the live tiles spread over all XCDs instead of the first few XCDs' contiguous ranges
+    unsigned nwg = gridDim.x;
+    if (!AK && a.epi.rows_dev) {
+      nwg = (unsigned)(((Mb + BM - 1) / BM) * tiles_n);
+      if (bid >= nwg) return;
+    }
+    const unsigned q = nwg >> 3, r = nwg & 7, x = bid & 7;
     bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
   }
   const unsigned tm = bid / tiles_n, tn = bid - tm * tiles_n;
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
   const int z = blockIdx.z;
-  const int64_t Mb = (!AK && a.epi.rows_dev) ? min(a.M, (int64_t)*a.epi.rows_dev) : a.M;
   const int64_t Kb = (AK && a.epi.rows_dev) ? min(a.K, (int64_t)*a.epi.rows_dev) : a.K;
   if (m0 >= Mb) return;
   const int64_t kbeg = (int64_t)z * a.k_per_split;

@@ -162,20 +162,33 @@ __global__ __launch_bounds__(256) void prefix_blocks_kernel(int* __restrict__ H,
 // start[v] = sum_{v' < v} total[v'] (v <= V): one workgroup
 __global__ __launch_bounds__(1024) void scan_keys_kernel(const int* __restrict__ total, int64_t V,
                                                          int* __restrict__ start) {
+  // tiles of 1024 x 32 keys: every thread issues its 32 loads at once (one memory round trip per tile,
+  // not one per key), block exclusive scan of the thread sums, running carry across tiles
   typedef hipcub::BlockScan<int, 1024> BS;
   __shared__ typename BS::TempStorage tmp;
+  constexpr int IPT = 32;
   const int tid = threadIdx.x;
-  const int64_t per = cdiv(V, 1024);
-  const int64_t v0 = tid * per;
-  int s = 0;
-  for (int64_t v = v0; v < min(V, v0 + per); ++v) s += total[v];
-  int ex, agg;
-  BS(tmp).ExclusiveSum(s, ex, agg);
-  for (int64_t v = v0; v < min(V, v0 + per); ++v) {
-    start[v] = ex;
-    ex += total[v];
+  int carry = 0;
+  for (int64_t base = 0; base < V; base += 1024 * IPT) {
+    const int64_t b0 = base + (int64_t)tid * IPT;
+    int v[IPT];
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) v[j] = b0 + j < V ? total[b0 + j] : 0;
+    int s = 0;
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) s += v[j];
+    int ex, agg;
+    BS(tmp).ExclusiveSum(s, ex, agg);
+    __syncthreads();
+    ex += carry;
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+      if (b0 + j < V) start[b0 + j] = ex;
+      ex += v[j];
+    }
+    carry += agg;
   }
-  if (tid == 0) start[V] = agg;
+  if (tid == 0) start[V] = carry;
 }
 
 // each block places its entries: rank inside the block by a stable block radix sort

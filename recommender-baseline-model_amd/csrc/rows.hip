@@ -96,7 +96,46 @@ __global__ __launch_bounds__(256) void scatter_rows_kernel(const T* __restrict__
   store_chunk<T>(dst + r * ldd + c, v);
 }
 
+// dst[r] = rank[r] >= 0 ? T(sum_z slab[z][rank[r]]) : 0 over all n rows: the split-K reduction, the cast
+// and the scatter of a compacted-row GEMM output in one pass (only live rows read the slabs)
+template <typename T>
+__global__ __launch_bounds__(256) void splitk_scatter_kernel(const float* __restrict__ slab, int splits,
+                                                             int64_t slab_stride, int64_t d,
+                                                             const int32_t* __restrict__ rank, int64_t n,
+                                                             T* __restrict__ dst, int64_t ldd) {
+  const int64_t cpr = d / 4;
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n * cpr) return;
+  const int64_t r = i / cpr, c = (i % cpr) * 4;
+  const int32_t k = rank[r];
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  if (k >= 0) {
+    const float* p = slab + (int64_t)k * d + c;
+    for (int z = 0; z < splits; ++z) {
+      const float4 u = *reinterpret_cast<const float4*>(p + (int64_t)z * slab_stride);
+      v[0] += u.x; v[1] += u.y; v[2] += u.z; v[3] += u.w;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) dst[r * ldd + c + j] = from_f<T>(v[j]);
+}
+
 extern "C" {
+
+int rs_splitk_scatter_rows(int dtype, const float* slab, int splits, int64_t cap, int64_t d, const int32_t* rank,
+                           int64_t n, void* dst, int64_t ldd, void* stream) {
+  if (splits < 1 || cap <= 0 || d <= 0 || d % 4 || n <= 0 || !slab || !rank || !dst || ((uintptr_t)slab % 16))
+    return RS_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 g((unsigned)cdiv(n * (d / 4), 256));
+  if (dtype == RS_DTYPE_BF16)
+    hipLaunchKernelGGL((splitk_scatter_kernel<__bf16>), g, dim3(256), 0, s, slab, splits, cap * d, d, rank, n,
+                       (__bf16*)dst, ldd);
+  else
+    hipLaunchKernelGGL((splitk_scatter_kernel<float>), g, dim3(256), 0, s, slab, splits, cap * d, d, rank, n,
+                       (float*)dst, ldd);
+  return (int)hipGetLastError();
+}
 
 int rs_compact_rows(const int64_t* labels, int64_t n, int64_t cap, int32_t* idx, int32_t* rank, int32_t* count,
                     void* stream) {

@@ -10,6 +10,8 @@
 // device step seed, the sequence and position, the attempt): graph-capturable, reproducible.  The
 // reference's numpy stream cannot be reproduced; the distribution is the same.
 //
+// rs_bert_mask replaces BertTrainDataset's per-token Python masking (BS/dataloaders/bert.py:77-110).
+//
 // rs_rank_metrics restates recalls_ndcgs_and_mrr_for_ks (BS/trainers/utils.py:28-57) on the GPU:
 // per row the rank of every positive among the candidates (score descending, ties by index as a
 // stable sort), then Recall@k / NDCG@k / MRR@k summed over rows in a fixed order.
@@ -91,6 +93,51 @@ __global__ void seed_step_kernel(uint64_t* s) {
   if (threadIdx.x == 0) *s += 1;
 }
 
+// BERT4Rec cloze masking (BertTrainDataset.__getitem__, BS/dataloaders/bert.py:77-110): the row's user is
+// perm[(cursor * batch + b) mod n_users] (an epoch's shuffled order); every kept item (the last max_len of
+// the history) is masked with probability p -- then, with prob' = u / p, [MASK] if prob' < 0.8, a uniform
+// item of 1..num_items if prob' < 0.9, else itself -- and labelled with itself; other positions keep
+// their item with label 0; rows are left padded with 0.  state = {step seed, cursor}, advanced first.
+__global__ __launch_bounds__(256) void bert_mask_kernel(const int64_t* __restrict__ off,
+                                                        const int64_t* __restrict__ items, int64_t n_users,
+                                                        int64_t num_items, int T, float p,
+                                                        const int64_t* __restrict__ perm,
+                                                        const uint64_t* __restrict__ state, uint64_t salt,
+                                                        int64_t* __restrict__ tokens, int64_t* __restrict__ labels) {
+  const int64_t b = blockIdx.x;
+  const uint64_t seed = salt ^ (state[0] * 0xD1B54A32D192ED03ull);
+  const int64_t slot = (int64_t)(((state[1] - 1) * (uint64_t)gridDim.x + (uint64_t)b) % (uint64_t)n_users);
+  const int64_t u = perm ? perm[slot] : slot;
+  const int64_t s0 = off[u], L = off[u + 1] - s0;
+  const int64_t n = L < T ? L : T;
+  const int64_t w0 = s0 + L - n, pad = T - n;
+  const int64_t mask_token = num_items + 1;
+  for (int t = threadIdx.x; t < T; t += 256) {
+    int64_t tok = 0, lab = 0;
+    if (t >= pad) {
+      const int64_t it = items[w0 + t - pad];
+      const uint64_t h = splitmix64(seed + (((uint64_t)b * (uint64_t)T + (uint64_t)t) << 8));
+      const float prob = (float)(h >> 40) * (1.0f / 16777216.0f);      // 24-bit uniform [0, 1)
+      tok = it;
+      if (prob < p) {
+        const float q = prob / p;
+        if (q < 0.8f) tok = mask_token;
+        else if (q < 0.9f) tok = 1 + (int64_t)__umul64hi(splitmix64(h ^ 0x9E3779B97F4A7C15ull), (uint64_t)num_items);
+        lab = it;
+      }
+    }
+    tokens[b * T + t] = tok;
+    labels[b * T + t] = lab;
+  }
+}
+
+__global__ void mask_step_kernel(uint64_t* s) {
+  if (threadIdx.x == 0) {
+    s[0] += 1;
+    s[1] += 1;
+  }
+}
+
 // ---------------------------------------------------------------------------------- metrics
 constexpr int MAXK = 8;
 
@@ -170,6 +217,19 @@ int rs_sas_sample(const int64_t* user_offsets, const int64_t* user_items, int64_
   if (seed_base) hipLaunchKernelGGL(smp::seed_step_kernel, dim3(1), dim3(64), 0, s, seed_base);
   hipLaunchKernelGGL(smp::sas_sample_kernel, dim3((unsigned)batch), dim3(256), 0, s, user_offsets, user_items, n_users,
                      item_num, (int)max_len, seed_base, salt, seq, pos, neg);
+  return (int)hipGetLastError();
+}
+
+int rs_bert_mask(const int64_t* user_offsets, const int64_t* user_items, int64_t n_users, int64_t num_items,
+                 int64_t batch, int64_t max_len, float mask_prob, const int64_t* perm, uint64_t* state, uint64_t salt,
+                 int64_t* tokens, int64_t* labels, void* stream) {
+  if (n_users <= 0 || num_items <= 0 || batch <= 0 || max_len <= 0 || !(mask_prob >= 0.f && mask_prob <= 1.f) ||
+      !user_offsets || !user_items || !state || !tokens || !labels)
+    return RS_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(smp::mask_step_kernel, dim3(1), dim3(64), 0, s, state);
+  hipLaunchKernelGGL(smp::bert_mask_kernel, dim3((unsigned)batch), dim3(256), 0, s, user_offsets, user_items, n_users,
+                     num_items, (int)max_len, mask_prob, perm, state, salt, tokens, labels);
   return (int)hipGetLastError();
 }
 

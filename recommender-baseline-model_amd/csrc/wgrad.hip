@@ -35,7 +35,7 @@ struct Args {
 };
 
 template <int T>
-__global__ __launch_bounds__(256) void wgrad_group_kernel(Args a) {
+__global__ __launch_bounds__(256, 2) void wgrad_group_kernel(Args a) {
   using I = gbf::Img<true, T>;          // k-major stage image [64 rows][T + 8]
   constexpr int STAGE = 2 * I::ELEMS;
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * STAGE];

@@ -316,14 +316,46 @@ class BERTEngine:
                               G(pre + "input_sublayer.norm.a_2"), G(pre + "input_sublayer.norm.b_2"), wln, 1,
                               accumulate=True)
             dx = dx2
-        ops.embed_bwd(1, ids, T, dx, 1.0, hp, self.salt["emb"], sb, G("bert.embedding.token.weight"),
-                      G("bert.embedding.position.pe.weight"))
+        if self._det_table():
+            # token-table gradient by inverted index (rs_item_grad: sorted keys, per-row sums, no float
+            # atomics -- deterministic); the index comes from the side stream when the step issued it
+            ev, iws = s["side"] if "side" in s else self._token_index(ids, side=False)
+            if ev is not None:
+                torch.cuda.current_stream().wait_event(ev)
+            ops.embed_bwd(1, ids, T, dx, 1.0, hp, self.salt["emb"], sb, None, G("bert.embedding.position.pe.weight"))
+            ops.item_grad(iws, 1, M, dx, 1.0, hp, self.salt["emb"], sb, None, None, None,
+                          G("bert.embedding.token.weight"))
+        else:
+            ops.embed_bwd(1, ids, T, dx, 1.0, hp, self.salt["emb"], sb, G("bert.embedding.token.weight"),
+                          G("bert.embedding.position.pe.weight"))
         for c in range(0, len(probs), 16):              # rs_wgrad_grouped takes up to 16 problems
             chunk = probs[c:c + 16]
             shapes = [(p[0].shape[1], p[1].shape[1]) for p in chunk]
             rows = self._wgrad_rows(M, sum(-(-n // 128) * -(-k // 128) for n, k in shapes))
             wslab = self.ws.get(f"wslab{c}", (ops.wgrad_grouped_slab_numel(shapes, M, rows),), torch.float32)
             ops.wgrad_grouped(chunk, M, rows, wslab)
+
+    def _det_table(self):
+        return self.dt == torch.bfloat16 and self.d in (64, 128, 256) and os.environ.get("RS_BERT_ATOMIC_TABLE") != "1"
+
+    def _token_index(self, ids, side=True):
+        """rs_item_index_build over the batch's token ids (the token-table gradient's inverted index); on a
+        side stream overlapping the forward pass when ``side``.  Returns (event or None, workspace)."""
+        M = ids.numel()
+        rows = self.flat.shapes["bert.embedding.token.weight"][0]
+        iws = self.ws.get("tokidx", (ops.item_index_ws_bytes(1, M, rows, self.d),), torch.uint8)
+        if not side:
+            ops.item_index_build([ids], rows, self.d, iws)
+            return None, iws
+        cur = torch.cuda.current_stream()
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(device=self.dev)
+        self._side.wait_stream(cur)
+        with torch.cuda.stream(self._side):
+            ops.item_index_build([ids], rows, self.d, iws)
+            ev = torch.cuda.Event()
+            ev.record(self._side)
+        return ev, iws
 
     @staticmethod
     def _wgrad_rows(M, tiles):
@@ -358,7 +390,10 @@ class BERTEngine:
     def train_loss_and_backward(self, tokens, labels, loss_out, global_count, grad, max_labelled=None):
         """Forward + CE(ignore_index=0) + backward of one batch.  loss_out[0] = loss sum, [1] = local
         labelled count, [2] = local mean; ``global_count(local)`` returns the divisor (DP)."""
+        side = self._token_index(tokens) if self._det_table() else None
         xL, s = self.encode(tokens, True, clone_seed=False)
+        if side is not None:
+            s["side"] = side
         B, T = tokens.shape
         M, d = B * T, self.d
         cap = int(max_labelled or M)
@@ -390,14 +425,14 @@ class BERTEngine:
         slab = self.ws.get("slab_out", (ops.wgrad_slab_numel(cap, self.V1, d),), torch.float32)
         ops.linear_wgrad(dl, hl, self.flat.view("out.weight", grad), slab, db=self.flat.view("out.bias", grad),
                          rows_dev=cnt)
-        dhl = self.ws.get("dhl", (cap, d), self.dt)
-        # contraction over the whole vocabulary with few rows: split-K (slabs + deterministic reduce)
+        # contraction over the whole vocabulary with few rows: split-K into slabs, then ONE pass that sums
+        # the live rows' partials in a fixed order, casts and scatters them back to the token rows
         sk = int(max(1, min(64, -(-self.V1 // 2048))))
         slab_d = self.ws.get("slab_dh", (sk * cap * d,), torch.float32)
-        acc = self.ws.get("dhl_f32", (cap, d), torch.float32) if self.dt != torch.float32 else None
-        ops.linear_dgrad_splitk(dl, self.W("out.weight"), dhl, slab_d, sk, acc_f32=acc, rows_dev=cnt)
+        ops.gemm(dl, self.W("out.weight"), slab_d, cap, d, self.V1, False, True, ops.epilogue(rows_dev=cnt),
+                 split_k=sk, slab=slab_d)
         dxL = self._buf((M, d))
-        ops.scatter_rows(dhl, rank, dxL)
+        ops.splitk_scatter_rows(slab_d, sk, cap, rank, dxL)
         self.encode_backward(s, dxL, grad)
 
 

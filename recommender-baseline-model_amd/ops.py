@@ -202,6 +202,13 @@ def scatter_rows(src, rank, dst):
     call("rs_scatter_rows", dtype_code(src), ptr(src), ld(src), d, ptr(rank), n, ptr(dst), ld(dst), stream())
 
 
+def splitk_scatter_rows(slab, splits, cap, rank, dst):
+    """dst[r] = sum_z slab[z][rank[r]] (0 where rank < 0): split-K reduce + cast + scatter, one launch."""
+    n, d = dst.shape
+    call("rs_splitk_scatter_rows", dtype_code(dst), ptr(slab), splits, cap, d, ptr(rank), n, ptr(dst), ld(dst),
+         stream())
+
+
 def adam_prepare(state, hyper, grad_divisor=None, seed_base=None):
     call("rs_adam_prepare", ptr(state), ptr(hyper), ptr(grad_divisor), ptr(seed_base), stream())
 
@@ -374,6 +381,13 @@ def sas_sample(user_offsets, user_items, n_users, item_num, seed_base, salt, seq
     B, T = seq.shape
     call("rs_sas_sample", ptr(user_offsets), ptr(user_items), n_users, item_num, B, T, ptr(seed_base), salt,
          ptr(seq), ptr(pos), ptr(neg), stream())
+
+
+def bert_mask(offsets, items, n_users, num_items, mask_prob, perm, state, salt, tokens, labels):
+    """rs_bert_mask: the next (tokens, labels) batch into (batch, max_len) int64 device tensors."""
+    B, T = tokens.shape
+    call("rs_bert_mask", ptr(offsets), ptr(items), n_users, num_items, B, T, mask_prob, ptr(perm), ptr(state), salt,
+         ptr(tokens), ptr(labels), stream())
 
 
 def rank_metrics(scores, labels, ks_dev, ws, out):

@@ -229,14 +229,16 @@ class FusedTrainStep:
         return self
 
     def capture_sampled(self, sampler, warmup=2):
-        """SAS: capture sampling (rbm_amd.dataloaders.DeviceWarpSampler, into static buffers) together with
-        the step, so ``replay_sampled()`` runs a whole training iteration -- batch construction included --
-        as one graph replay (the reference's WarpSampler + train_one_epoch body, BS/trainers/base.py:114-123)."""
-        if self.kind != "sas":
-            raise ValueError("capture_sampled is for the SAS step")
+        """Capture sampling (rbm_amd.dataloaders.DeviceWarpSampler for SAS, DeviceBertMasker for BERT, into
+        static buffers) together with the step, so ``replay_sampled()`` runs a whole training iteration --
+        batch construction included -- as one graph replay (the reference's sampler / DataLoader +
+        train_one_epoch body, BS/trainers/base.py:114-123)."""
+        want = 3 if self.kind == "sas" else 2
+        if getattr(sampler, "n_outputs", None) != want:
+            raise ValueError(f"the {self.kind} step needs a sampler producing {want} tensors")
         self.sampler = sampler
         shape = (sampler.batch_size, sampler.max_len)
-        self.packed = torch.zeros((3,) + shape, dtype=torch.int64, device=self.flat.device)
+        self.packed = torch.zeros((want,) + shape, dtype=torch.int64, device=self.flat.device)
         self.static = list(self.packed.unbind(0))
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())

@@ -136,3 +136,91 @@ def test_sampled_step_graph_equals_eager():
     assert runs[0][0] == runs[1][0]
     assert torch.equal(runs[0][1], runs[1][1])
     assert all(np.isfinite(runs[0][0]))
+
+
+def _originals(tok, lab):
+    return np.where(lab != 0, lab, tok)
+
+
+def test_bert_masker_rows_and_epoch():
+    """rs_bert_mask rows follow BertTrainDataset.__getitem__ (BS/dataloaders/bert.py:77-110): a user's last
+    max_len items, left padded; labels only at masked positions and equal to the item; unmasked tokens are
+    the item itself; one epoch visits every user once (shuffled)."""
+    import rbm_amd  # noqa: F401
+    from rbm_amd.dataloaders import DeviceBertMasker
+    rng = np.random.default_rng(2)
+    V, T, B = 700, 40, 16
+    users = _histories(64, V, rng, max_hist=90)
+    windows = {tuple(h[-T:]): u for u, h in enumerate(users)}
+    m = DeviceBertMasker(users, V, B, T, 0.3, seed=3)
+    assert len(m) == 4
+    seen = []
+    for tok, lab in m:
+        tok, lab = tok.cpu().numpy(), lab.cpu().numpy()
+        orig = _originals(tok, lab)
+        for b in range(B):
+            nz = np.nonzero(orig[b])[0]
+            pad = T - len(nz)
+            assert (nz == np.arange(pad, T)).all(), "left padding"
+            w = tuple(orig[b, pad:])
+            assert w in windows, "row is not a user's window"
+            seen.append(windows[w])
+            masked = lab[b] != 0
+            assert ((tok[b][~masked] == orig[b][~masked])).all()
+            assert ((tok[b][masked] >= 1) & (tok[b][masked] <= V + 1)).all()
+    assert sorted(seen) == list(range(64)), "an epoch visits every user once"
+
+
+def test_bert_masker_rates():
+    import rbm_amd  # noqa: F401
+    from rbm_amd.dataloaders import DeviceBertMasker
+    V, T, B = 5000, 100, 128
+    users = [list(range(1 + u, 201 + u)) for u in range(256)]
+    m = DeviceBertMasker(users, V, B, T, 0.2, seed=4)
+    m.new_epoch()
+    n_tok = n_mask = n_mtok = n_keep = 0
+    for _ in range(20):
+        tok, lab = (x.cpu().numpy() for x in m.sample())
+        masked = lab != 0
+        n_tok += tok.size
+        n_mask += masked.sum()
+        n_mtok += (tok[masked] == V + 1).sum()
+        n_keep += (tok[masked] == lab[masked]).sum()
+    f = n_mask / n_tok
+    assert abs(f - 0.2) < 0.005, f
+    assert abs(n_mtok / n_mask - 0.8) < 0.01 and abs(n_keep / n_mask - 0.1) < 0.01, (n_mtok / n_mask, n_keep / n_mask)
+
+
+def test_bert_sampled_step_graph_equals_eager():
+    import argparse
+    import rbm_amd  # noqa: F401
+    from rbm_amd.dataloaders import DeviceBertMasker
+    from rbm_amd.models import model_factory
+    from rbm_amd.train_step import FusedTrainStep
+    rng = np.random.default_rng(12)
+    V, T, B = 500, 32, 16
+    users = _histories(100, V, rng, max_hist=60)
+    a = argparse.Namespace(model_code="bert", num_items=V, max_len=T, device="cuda", bert_hidden_units=64,
+                           bert_num_blocks=1, bert_num_heads=2, bert_dropout=0.1, bert_hidden_dropout=0.1,
+                           bert_mask_prob=0.2, model_init_seed=0, rs_dtype="bf16")
+    runs = []
+    for graph in (False, True):
+        torch.manual_seed(0)
+        m = model_factory(a)
+        st = FusedTrainStep(m, lr=1e-3)
+        smp = DeviceBertMasker(users, V, B, T, 0.2, seed=6)
+        smp.new_epoch()
+        losses = []
+        if graph:
+            st.capture_sampled(smp, warmup=2)
+            for _ in range(4):
+                losses.append(st.replay_sampled().item())
+        else:
+            buf = [torch.zeros(B, T, dtype=torch.int64, device="cuda") for _ in range(2)]
+            for _ in range(6):
+                smp.sample_into(*buf)
+                losses.append(st.step(*buf).item())
+            losses = losses[2:]
+        runs.append((losses, m.engine().flat.data.clone()))
+    assert runs[0][0] == runs[1][0]
+    assert torch.equal(runs[0][1], runs[1][1])

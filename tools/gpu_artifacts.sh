@@ -10,9 +10,10 @@ mkdir -p $OUT
 timeout -k 10 900 python -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1; rc=$?; tail -3 $OUT/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
 rm -f profiles/traffic.json
-for c in cfg2 cfg4; do
+for c in cfg2 cfg3 cfg4; do
+  ONLY=attn_bwd; [ "$c" = "cfg3" ] && ONLY="bert wgrad_grouped"
   for P in FETCH_SIZE WRITE_SIZE; do
-    timeout -k 10 300 rocprofv3 --kernel-trace --pmc $P -d $OUT/traffic_${c}_$P -o pmc --output-format csv -- python3 tools/kbench.py --config $c --reps 5 --only attn_bwd > $OUT/traffic_${c}_$P.log 2>&1 || { tail -5 $OUT/traffic_${c}_$P.log; exit 1; }
+    timeout -k 10 300 rocprofv3 --kernel-trace --pmc $P -d $OUT/traffic_${c}_$P -o pmc --output-format csv -- python3 tools/kbench.py --config $c --reps 5 --only "$ONLY" > $OUT/traffic_${c}_$P.log 2>&1 || { tail -5 $OUT/traffic_${c}_$P.log; exit 1; }
   done
   mkdir -p $OUT/traffic_$c && mv $OUT/traffic_${c}_FETCH_SIZE $OUT/traffic_${c}_WRITE_SIZE $OUT/traffic_$c/
   python3 tools/make_traffic.py $OUT/traffic_$c $c profiles/traffic.json > /dev/null || exit 1

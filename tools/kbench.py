@@ -138,6 +138,13 @@ def main():
             mb + 2 * M * ff * es, 2 * M * d * ff)
         run("bert ffn1 dgrad", lambda: ops.linear_dgrad(gg, W1b, z), M * ff * es + mb, 2 * M * d * ff)
         run("bert qkv dgrad", lambda: ops.linear_dgrad(qkv, Wqkv, z), 4 * mb, 6 * M * d * d)
+        from rbm_amd.models.bert_model.bert import BERTEngine
+        bshapes = [(d, ff), (ff, d), (d, d), (3 * d, d)] * 4
+        bprobs = [(rn(M, n), rn(M, k), torch.zeros(n, k, device=dev), torch.zeros(n, device=dev)) for n, k in bshapes]
+        brows = BERTEngine._wgrad_rows(M, sum((n // 128) * (k // 128) for n, k in bshapes))
+        bslab = torch.empty(ops.wgrad_grouped_slab_numel(bshapes, M, brows), device=dev)
+        run("bert wgrad_grouped 16 problems", lambda: ops.wgrad_grouped(bprobs, M, brows, bslab),
+            sum(M * (n + k) * es for n, k in bshapes), sum(2 * M * n * k for n, k in bshapes))
         V1 = V + 1
         R = 1792
         V1p = -(-V1 // 64) * 64
