@@ -59,8 +59,15 @@ static hipError_t layout(int nsrc, int64_t rows, int64_t table_rows, int64_t d, 
   L.temp_bytes = 0;
   if (L.cs) {
     L.H = o; o = al256(o + L.nb * table_rows * 4);
-    L.total = o; o = al256(o + table_rows * 4);
-    L.keys_in = L.vals_in = L.temp = 0;
+    L.total = o; o = al256(o + (table_rows + 1) * 4);   // [V] = 0: the scan's last entry is the total
+    L.keys_in = L.vals_in = 0;
+    L.temp = o;
+    size_t tb = 0;
+    const hipError_t e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const int*)nullptr, (int*)nullptr,
+                                                          (int)(table_rows + 1), (hipStream_t)0);
+    if (e != hipSuccess) return e;
+    L.temp_bytes = tb;
+    o = al256(o + tb);
   } else {
     L.H = L.total = 0;
     L.keys_in = o; o = al256(o + L.n * 4);
@@ -130,6 +137,7 @@ __global__ __launch_bounds__(256) void prefix_blocks_kernel(int* __restrict__ H,
   __shared__ int part[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t v = (int64_t)blockIdx.x * 64 + lane;
+  if (blockIdx.x == 0 && threadIdx.x == 0) total[V] = 0;
   const int64_t q = cdiv(nb, 4), b0 = w * q, b1 = min(nb, b0 + q);
   constexpr int U = 8;
   int h[U];
@@ -160,37 +168,6 @@ __global__ __launch_bounds__(256) void prefix_blocks_kernel(int* __restrict__ H,
 }
 
 // start[v] = sum_{v' < v} total[v'] (v <= V): one workgroup
-__global__ __launch_bounds__(1024) void scan_keys_kernel(const int* __restrict__ total, int64_t V,
-                                                         int* __restrict__ start) {
-  // tiles of 1024 x 32 keys: every thread issues its 32 loads at once (one memory round trip per tile,
-  // not one per key), block exclusive scan of the thread sums, running carry across tiles
-  typedef hipcub::BlockScan<int, 1024> BS;
-  __shared__ typename BS::TempStorage tmp;
-  constexpr int IPT = 32;
-  const int tid = threadIdx.x;
-  int carry = 0;
-  for (int64_t base = 0; base < V; base += 1024 * IPT) {
-    const int64_t b0 = base + (int64_t)tid * IPT;
-    int v[IPT];
-#pragma unroll
-    for (int j = 0; j < IPT; ++j) v[j] = b0 + j < V ? total[b0 + j] : 0;
-    int s = 0;
-#pragma unroll
-    for (int j = 0; j < IPT; ++j) s += v[j];
-    int ex, agg;
-    BS(tmp).ExclusiveSum(s, ex, agg);
-    __syncthreads();
-    ex += carry;
-#pragma unroll
-    for (int j = 0; j < IPT; ++j) {
-      if (b0 + j < V) start[b0 + j] = ex;
-      ex += v[j];
-    }
-    carry += agg;
-  }
-  if (tid == 0) start[V] = carry;
-}
-
 // each block places its entries: rank inside the block by a stable block radix sort
 __global__ __launch_bounds__(256) void place_kernel(Keys K, const int* __restrict__ H, const int* __restrict__ start,
                                                     int bits, uint32_t* __restrict__ sk, uint32_t* __restrict__ sv) {
@@ -463,7 +440,11 @@ int rs_item_index_build(int nsrc, const int64_t* keys0, const int64_t* keys1, co
     }
     hipLaunchKernelGGL(ig::prefix_blocks_kernel, dim3((unsigned)cdiv(table_rows, 64)), dim3(256), 0, s, H, L.nb,
                        table_rows, total);
-    hipLaunchKernelGGL(ig::scan_keys_kernel, dim3(1), dim3(1024), 0, s, total, table_rows, start);
+    // start[v] = exclusive prefix of the per-key totals (a decoupled-lookback device scan over V+1 entries)
+    size_t tb = L.temp_bytes;
+    if ((e = hipcub::DeviceScan::ExclusiveSum((void*)(w + L.temp), tb, total, start, (int)(table_rows + 1), s)) !=
+        hipSuccess)
+      return (int)e;
     hipLaunchKernelGGL(ig::place_kernel, dim3((unsigned)L.nb), dim3(256), 0, s, K, H, start, bits, sk, sv);
     return (int)hipGetLastError();
   }
