@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-all}
 mkdir -p $OUT
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1; rc=$?; tail -5 $OUT/pytest_gpu.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; rc=$?; tail -5 $OUT/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
 for c in ${CONFIGS:-cfg2}; do
   timeout -k 10 600 python bench.py --config $c ${BENCH_ARGS} > $OUT/bench_$c.log 2>&1; rc=$?; tail -1 $OUT/bench_$c.log

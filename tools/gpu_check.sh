@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-run}
 mkdir -p $OUT
 echo "== pytest -m gpu" && \
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1; rc=$?; tail -5 $OUT/pytest_gpu.log
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; rc=$?; tail -5 $OUT/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
 echo "== smoke" && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && tail -2 $OUT/smoke.log && \
 echo "== bench" && timeout -k 10 600 python bench.py ${BENCH_ARGS} > $OUT/bench.log 2>&1 && tail -1 $OUT/bench.log && \
