@@ -119,7 +119,13 @@ def _time_on_stream(fn, reps, stream):
     return e0.elapsed_time(e1) * 1e3 / reps
 
 
-def _roof(kernel, us, flops, nbytes, dtype, note):
+def _roof(kernel, us, flops, nbytes, dtype, note, live_us=None):
+    iso_us = us
+    if live_us:
+        us = sum(live_us) / len(live_us)
+        note += (f"; avg_launch_us = mean of {len(live_us)} launches timed inside the timed steps (in-kernel "
+                 f"s_memrealtime stamps: first wave in to last wave out of the launch), isolated_launch_us = the "
+                 f"same launch re-timed alone with HIP events")
     ai = flops / nbytes if nbytes else float("inf")
     peak_f = MI355X_BF16_TFLOPS if dtype == "bf16" else MI355X_F32_TFLOPS
     ridge = peak_f * 1e12 / (MI355X_HBM_GBS * 1e9)
@@ -131,19 +137,28 @@ def _roof(kernel, us, flops, nbytes, dtype, note):
         ach = nbytes / (us * 1e-6) / 1e9
         return {"kernel": kernel, "bound": "hbm", "achieved": round(ach, 1), "peak": MI355X_HBM_GBS, "unit": "GB/s",
                 "frac": round(ach / MI355X_HBM_GBS, 4), "traffic": traffic, "avg_launch_us": round(us, 2),
+                "isolated_launch_us": round(iso_us, 2), "live_samples": len(live_us or ()),
                 "algorithmic_bytes_per_launch": int(nbytes), "algorithmic_flops_per_launch": int(flops),
                 "arith_intensity": round(ai, 1), "note": note}
     ach = flops / (us * 1e-6) / 1e12
     return {"kernel": kernel, "bound": "mfma", "achieved": round(ach, 2), "peak": peak_f, "unit": "TFLOP/s",
             "frac": round(ach / peak_f, 4), "traffic": traffic, "avg_launch_us": round(us, 2),
+            "isolated_launch_us": round(iso_us, 2), "live_samples": len(live_us or ()),
             "algorithmic_bytes_per_launch": int(nbytes), "algorithmic_flops_per_launch": int(flops),
             "arith_intensity": round(ai, 1), "note": note}
 
 
-def roofline(cfg, B, dtype, reps=50):
-    """Dominant kernel of the step (by rocprof device time), timed alone with HIP events on a
-    dedicated stream.  SAS: the attention backward (rs_attn_bwd: dQ+delta and dK/dV kernels);
-    BERT: the grouped block weight gradients (rs_wgrad_grouped)."""
+MARK = {"sas": "attn_bwd", "bert": "wgrad_grouped"}   # ops wrapper of the dominant kernel per model
+
+
+def roofline(cfg, B, dtype, live_us=None, reps=50):
+    """Dominant kernel of the step (by rocprof device time).  SAS: the attention backward (rs_attn_bwd:
+    dQ+delta and dK/dV kernels); BERT: the grouped block weight gradients (rs_wgrad_grouped).
+    live_us: its launch durations measured INSIDE the timed step replays (in-kernel begin/end stamps of
+    every launch of every timed step, ops.kernel_stamps; event-record nodes in a ROCm graph add a ~6 us
+    barrier each, so HIP events inside the graph would perturb the step they time) -- `achieved` is
+    computed from their mean.  The same launch is also re-timed alone here with HIP
+    events on a dedicated stream (`isolated_launch_us`, a cross-check)."""
     from rbm_amd import ops
     es = 2 if dtype == "bf16" else 4
     dt = torch.bfloat16 if dtype == "bf16" else torch.float32
@@ -172,7 +187,8 @@ def roofline(cfg, B, dtype, reps=50):
         flops = 4 * 2.0 * (T * (T + 1) / 2) * Dh * B * H
         nbytes = 8 * M * d * es + B * H * T * 4 * 2
         return _roof("rs_attn_bwd (attn_bwd_dq_lds + attn_bwd_dkv_lds)", us, flops, nbytes, dtype,
-                     f"causal attention backward, B={B} T={T} Dh={Dh} dropout {cfg['p']}; 2 launches per call")
+                     f"causal attention backward, B={B} T={T} Dh={Dh} dropout {cfg['p']}; 2 kernels per launch",
+                     live_us)
     # BERT: the grouped weight-gradient launch of all block weights (rs_wgrad_grouped: GEMM + reduction),
     # the largest single kernel of the step
     from rbm_amd.models.bert_model.bert import BERTEngine
@@ -188,7 +204,7 @@ def roofline(cfg, B, dtype, reps=50):
     nbytes = sum(M * (n + k) * es + (n * k + n) * 4 * 2 for n, k in shapes)   # dY, X once; dW, db read+write
     return _roof("rs_wgrad_grouped (wgrad_group_kernel + reduce_cols_kernel)", us, flops, nbytes, dtype,
                  f"{len(shapes)} block weight gradients of M={M} token rows (d={d}, ff={Fd}, L={L}), "
-                 f"{-(-M // rows)} row splits; 2 launches per call")
+                 f"{-(-M // rows)} row splits; 2 kernels per launch", live_us)
 
 
 # ------------------------------------------------------------------------------------ CPU baseline
@@ -259,6 +275,13 @@ def main():
     batches = [tuple(torch.from_numpy(a).cuda() for a in b) for b in host_batches]
     from rbm_amd.train_step import FusedTrainStep
     trainer = FusedTrainStep(model, lr=1e-3, max_labelled=max_lab)
+    # the dominant kernel is timed live, inside every timed step: the step graph is captured with kernel
+    # stamps on (first wave in / last wave out s_memrealtime ticks of each stamped launch, per step)
+    from rbm_amd import ops
+    NMARK, WAVES = 8, 16384
+    sbuf = None if args.no_graph else torch.zeros(4 + args.steps * NMARK * (1 + WAVES), dtype=torch.int64,
+                                                  device="cuda")
+    stamps = None if sbuf is None else (sbuf, (MARK[cfg["model"]],))
 
     if args.sampler == "device" and cfg["model"] == "sas":
         import rbm_amd.data as synth
@@ -266,7 +289,7 @@ def main():
         users = synth.user_histories(np.random.default_rng(77 + rank), cfg.get("users", 6040), cfg["T"], cfg["V"],
                                      shape=cfg["shape"])
         sampler = DeviceWarpSampler(users, cfg["V"], B, cfg["T"], seed=5 + rank)
-        trainer.capture_sampled(sampler)
+        trainer.capture_sampled(sampler, stamps=stamps)
         batches = [()]
         run = trainer.replay_sampled
     elif args.sampler == "device":
@@ -278,13 +301,13 @@ def main():
                                      shape=cfg["shape"])
         sampler = DeviceBertMasker(users, cfg["V"], B, cfg["T"], cfg["mask"], seed=5 + rank)
         sampler.new_epoch()
-        trainer.capture_sampled(sampler)
+        trainer.capture_sampled(sampler, stamps=stamps)
         batches = [()]
         run = trainer.replay_sampled
     elif args.no_graph:
         run = trainer.step
     else:
-        trainer.capture(*batches[0])
+        trainer.capture(*batches[0], stamps=stamps)
         batches = [(torch.stack(b),) for b in batches]     # one device copy per replay (replay_packed)
         run = trainer.replay_packed
     for i in range(args.warmup):
@@ -292,6 +315,10 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    torch.cuda.synchronize()
+    if sbuf is not None:
+        sbuf.zero_()
+        sbuf[:4] = torch.tensor([int(trainer.opt.state[0].item()), args.steps, NMARK, WAVES], dtype=torch.int64)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -306,7 +333,11 @@ def main():
     elapsed = tt.item()
     final_loss = float(loss.float().sum().item())
 
-    roof = roofline(cfg, B, args.dtype) if rank == 0 else None
+    live = None
+    if sbuf is not None:
+        live = [us for _, _, us in ops.read_kernel_stamps(sbuf, ops.wall_clock_khz())]
+        del sbuf
+    roof = roofline(cfg, B, args.dtype, live_us=live) if rank == 0 else None
     if rank == 0:
         cpu = cpu_baseline(cfg, B, args.cpu_baseline_seconds) if world == 1 and args.cpu_baseline_seconds > 0 \
             else None

@@ -232,6 +232,22 @@ int rs_vocab_ce_bwd(int64_t R, int64_t V1, int64_t d, const void* h, int64_t ldh
                     const float* bias, const int64_t* labels, const int* rows_dev, const float* count,
                     const float* dloss, const float* ws, void* dlogits, int64_t lddl, void* stream);
 
+/* Kernel stamps (bench.py's in-step timing of the dominant launch; not on the reference's path).
+ * While enabled (buf != NULL), rs_attn_bwd (bf16 LDS path) and/or rs_wgrad_grouped launches (kinds in
+ * kind_mask, bit RS_STAMP_*) are stamped -- marks numbered in launch order from 0, fixed into the kernel
+ * arguments, so a captured graph keeps stamping on every replay.  buf (device u64) = {base step, steps
+ * held, marks per step, W, then per (slot = (int64)*step - base, mark) a record {begin, exit time of
+ * wave 0 .. W-1}} in s_memrealtime ticks (begin: the first dispatched workgroup's start; the launch
+ * ends at the max wave exit).  step: the optimizer's device step count (double, rs_adam_prepare's
+ * state[0]).  rs_kernel_stamps(NULL, NULL, 0) disables.  rs_kernel_stamp_count / rs_kernel_stamp_kinds:
+ * the marks handed out since the last enable and their kinds.  rs_wall_clock_khz: tick rate. */
+#define RS_STAMP_ATTN_BWD 1
+#define RS_STAMP_WGRAD_GROUPED 2
+int rs_kernel_stamps(uint64_t* buf, const double* step, int kind_mask);
+int rs_kernel_stamp_count(void);
+int rs_kernel_stamp_kinds(int* kinds, int n);
+int rs_wall_clock_khz(int* khz);
+
 /* *seed_base += 1 on the stream (advances every dropout mask; capturable). */
 int rs_seed_advance(uint64_t* seed_base, void* stream);
 

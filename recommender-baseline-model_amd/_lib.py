@@ -94,6 +94,10 @@ SIGNATURES = {
     "rs_bert_mask": [vp, vp, i64, i64, i64, i64, f32, vp, vp, u64, vp, vp, vp],
     "rs_splitk_scatter_rows": [i32, vp, i32, i64, i64, vp, i64, vp, i64, vp],
     "rs_rank_metrics": [vp, vp, i64, i64, i32, vp, vp, vp, vp],
+    "rs_kernel_stamps": [vp, vp, i32],
+    "rs_kernel_stamp_count": [],
+    "rs_kernel_stamp_kinds": [C.POINTER(i32), i32],
+    "rs_wall_clock_khz": [C.POINTER(i32)],
     "rs_abi_version": [],
 }
 

@@ -44,6 +44,7 @@ struct AttnLdsArgs {
   uint64_t seed;
   const uint64_t* seed_base;
   int nsplit;
+  KStamp ks;                     // backward: dQ kernel stamps begin, dK/dV kernel end
 };
 
 #define NEG_INF (-__builtin_inff())
@@ -339,6 +340,7 @@ template <int DH>
 __global__ __launch_bounds__(NT) void attn_bwd_dq_lds_kernel(AttnLdsArgs a) {
   constexpr int LD = Img<DH>::LD, KC = DH / 32, DT = DH / 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  KStampBegin stamp_(a.ks);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4, cl = lane & 15;
   int64_t bh;
   int split;
@@ -455,6 +457,7 @@ template <int DH>
 __global__ __launch_bounds__(NT) void attn_bwd_dkv_lds_kernel(AttnLdsArgs a) {
   constexpr int LD = Img<DH>::LD, KC = DH / 32, DT = DH / 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  KStampEnd stamp_(a.ks);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4, cl = lane & 15;
   int64_t bh;
   int split;
@@ -664,6 +667,7 @@ hipError_t attn_lds_bwd(int64_t B, int64_t T, int64_t H, int64_t Dh, const void*
   a.dq = (bf16*)dq; a.lddq = lddq; a.dk = (bf16*)dk; a.lddk = lddk; a.dv = (bf16*)dv; a.lddv = lddv;
   a.lse = const_cast<float*>(lse); a.delta = delta; a.scale = scale; a.mask_kind = mask_kind; a.ids = ids;
   a.drop_p = drop_p; a.seed = seed; a.seed_base = seed_base;
+  a.ks = kstamp_next(RS_STAMP_ATTN_BWD);
   if (Dh == 128) return bwd_t<128>(a, s);
   if (Dh == 64) return bwd_t<64>(a, s);
   return bwd_t<32>(a, s);

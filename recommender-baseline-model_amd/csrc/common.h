@@ -200,6 +200,57 @@ __device__ __forceinline__ float gelu_tanh_grad_fast(float x) {
 
 __host__ __device__ static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// ---- kernel stamps (bench.py's in-step timing of the dominant launch; misc.hip rs_kernel_stamps) ----
+// buf: [0] base step, [1] steps held, [2] marks per step, [3] W; then per (step slot, mark) a record of
+// 1 + W u64: {begin, end of wave 0 .. W-1} in s_memrealtime ticks.  begin = the start of the first
+// dispatched workgroup's wave 0 (workgroup 0 is dispatched first); each wave stores its own exit time
+// (plain stores to distinct words: same-address atomics from thousands of waves serialise and cost
+// tens of microseconds), and the reader takes the max.  Slot = the optimizer's step count (*step, a
+// device double advanced by rs_adam_prepare) - base.  buf == null: off.
+struct KStamp {
+  unsigned long long* buf;
+  const double* step;
+  int mark;
+};
+
+__device__ __forceinline__ unsigned long long* kstamp_rec(const KStamp& k) {
+  const long long slot = (long long)(*k.step) - (long long)k.buf[0];
+  if (slot < 0 || slot >= (long long)k.buf[1] || k.mark >= (int)k.buf[2]) return nullptr;
+  return k.buf + 4 + (slot * (long long)k.buf[2] + k.mark) * (1 + (long long)k.buf[3]);
+}
+
+__device__ __forceinline__ long long kstamp_wave() {
+  return ((long long)blockIdx.x + (long long)gridDim.x * ((long long)blockIdx.y + (long long)gridDim.y * blockIdx.z)) *
+             (long long)(blockDim.x >> 6) + (threadIdx.x >> 6);
+}
+
+struct KStampBegin {
+  __device__ __forceinline__ explicit KStampBegin(const KStamp& k) {
+    if (k.buf && threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) {
+      unsigned long long* p = kstamp_rec(k);
+      if (p) *p = (unsigned long long)wall_clock64();
+    }
+  }
+};
+
+// stores the wave's exit time when it leaves the kernel (any return path); the record address is formed
+// at exit from the kernel arguments, so nothing stays live in registers across the kernel body
+struct KStampEnd {
+  const KStamp& k;
+  __device__ __forceinline__ explicit KStampEnd(const KStamp& k_) : k(k_) {}
+  __device__ __forceinline__ ~KStampEnd() {
+    if (k.buf && (threadIdx.x & 63) == 0) {
+      const long long w = kstamp_wave();
+      unsigned long long* p = w < (long long)k.buf[3] ? kstamp_rec(k) : nullptr;
+      if (p) p[1 + w] = (unsigned long long)wall_clock64();
+    }
+  }
+};
+
+// host: the stamp for the next stamped launch (marks numbered in launch order since rs_kernel_stamps);
+// kind: RS_STAMP_* of the launch, reported by rs_kernel_stamp_kinds
+KStamp kstamp_next(int kind);
+
 // second pass of every two-level reduction (reduce.hip): out0[i] (+)= sum_z slab[z*n+i] for i < n0,
 // out1[i-n0] likewise for n0 <= i < n (either output may be null to drop that part).
 hipError_t launch_reduce_slabs(const float* slab, int splits, int64_t n, int64_t n0, float* out0, float* out1,

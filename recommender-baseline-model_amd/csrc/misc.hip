@@ -308,6 +308,52 @@ int rs_seed_advance(uint64_t* seed_base, void* stream) {
   return (int)hipGetLastError();
 }
 
+// ---- kernel stamps (see common.h) ------------------------------------------------------------
+static unsigned long long* g_kstamp_buf = nullptr;
+static const double* g_kstamp_step = nullptr;
+static int g_kstamp_next = 0, g_kstamp_mask = 0;
+static int g_kstamp_kind[256];
+
+}  // extern "C"
+
+KStamp kstamp_next(int kind) {
+  KStamp k{nullptr, nullptr, 0};
+  if (g_kstamp_buf && (g_kstamp_mask >> kind & 1)) {
+    k.buf = g_kstamp_buf;
+    k.step = g_kstamp_step;
+    if (g_kstamp_next < 256) g_kstamp_kind[g_kstamp_next] = kind;
+    k.mark = g_kstamp_next++;
+  }
+  return k;
+}
+
+extern "C" {
+
+int rs_kernel_stamps(uint64_t* buf, const double* step, int kind_mask) {
+  if ((buf == nullptr) != (step == nullptr)) return RS_ERR_ARG;
+  g_kstamp_buf = (unsigned long long*)buf;
+  g_kstamp_step = step;
+  g_kstamp_mask = kind_mask;
+  if (buf) g_kstamp_next = 0;      // disabling keeps the launch log of the last enabled period
+  return 0;
+}
+
+int rs_kernel_stamp_kinds(int* kinds, int n) {
+  const int m = g_kstamp_next < 256 ? g_kstamp_next : 256;
+  for (int i = 0; i < n && i < m; ++i) kinds[i] = g_kstamp_kind[i];
+  return 0;
+}
+
+int rs_kernel_stamp_count(void) { return g_kstamp_next; }
+
+int rs_wall_clock_khz(int* khz) {
+  if (!khz) return RS_ERR_ARG;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return (int)e;
+  return (int)hipDeviceGetAttribute(khz, hipDeviceAttributeWallClockRate, dev);
+}
+
 int rs_abi_version(void) { return 1; }
 
 }  // extern "C"

@@ -32,10 +32,12 @@ struct Args {
   int nprob, ntiles, splits, rows_per_split;
   int64_t M;
   float* slab;
+  KStamp ks;                   // begin stamp of a stamped rs_wgrad_grouped launch
 };
 
 template <int T>
 __global__ __launch_bounds__(256, 2) void wgrad_group_kernel(Args a) {
+  KStampBegin stamp_(a.ks);
   using I = gbf::Img<true, T>;          // k-major stage image [64 rows][T + 8]
   constexpr int STAGE = 2 * I::ELEMS;
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * STAGE];
@@ -152,11 +154,13 @@ struct RArgs {
   Seg s[MAXS];
   int blk0[MAXS + 1];
   int nseg, accumulate;
+  KStamp ks;                   // end stamp (last reduction launch of a stamped rs_wgrad_grouped)
 };
 
 // block = 16 float4 columns x 16 split groups; group g sums splits g, g+16, ... ; fixed-order
 // combine in LDS (deterministic)
 __global__ __launch_bounds__(256) void reduce_segments_kernel(RArgs a) {
+  KStampEnd stamp_(a.ks);
   constexpr int C = 16, G = 16;
   const int b = blockIdx.x;
   int si = 0;
@@ -209,6 +213,7 @@ __global__ __launch_bounds__(256) void reduce_segments_kernel(RArgs a) {
 // few splits (<= 32): one float4 column per thread, all splits summed in order by that thread (4 loads
 // in flight), 1024 columns per block -- the large BERT-size segments stream at HBM rate
 __global__ __launch_bounds__(256) void reduce_cols_kernel(RArgs a) {
+  KStampEnd stamp_(a.ks);
   const int b = blockIdx.x;
   int si = 0;
 #pragma unroll 1
@@ -246,12 +251,14 @@ __global__ __launch_bounds__(256) void reduce_cols_kernel(RArgs a) {
 
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-static int launch_segments(int nseg, const rs_reduce_segment* segs, int accumulate, hipStream_t s) {
+static int launch_segments(int nseg, const rs_reduce_segment* segs, int accumulate, hipStream_t s,
+                           KStamp end = KStamp{}) {
   if (nseg <= 0) return 0;
   for (int base = 0; base < nseg; base += wg::MAXS) {
     wg::RArgs ra{};
     ra.nseg = min(wg::MAXS, nseg - base);
     ra.accumulate = accumulate;
+    if (base + wg::MAXS >= nseg) ra.ks = end;
     int64_t max_splits = 0;
     for (int q = 0; q < ra.nseg; ++q) max_splits = max(max_splits, segs[base + q].splits);
     const bool cols = max_splits <= 16;     // few splits: a column per thread (reduce_cols_kernel)
@@ -313,6 +320,7 @@ int rs_wgrad_grouped(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_
   }
   if (off > slab_numel) return RS_ERR_ARG;
   a.ntiles = tiles;
+  a.ks = kstamp_next(RS_STAMP_WGRAD_GROUPED);
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid((unsigned)(tiles * splits));
   if (T == 128) hipLaunchKernelGGL(wg::wgrad_group_kernel<128>, grid, dim3(256), 0, s, a);
@@ -332,7 +340,7 @@ int rs_wgrad_grouped(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_
   }
   if (nextra < 0 || nextra > wg::MAXS) return RS_ERR_ARG;
   for (int q = 0; q < nextra; ++q) segs[ns++] = extra[q];
-  return launch_segments(ns, segs, 1, s);
+  return launch_segments(ns, segs, 1, s, a.ks);
 }
 
 }  // extern "C"

@@ -186,11 +186,17 @@ class SASEngine:
              "x": [], "Q": [], "mu1": [], "r1": [], "q": [], "kv": [], "o": [], "lse": [],
              "x1": [], "z": [], "mu2": [], "r2": [], "h1": []}
         fused = ops.sas_block_fused_ok(d, self.dt)
-        if fused and training and pos is not None:
-            s["side"] = self._side_prologue(ids, pos, neg)
+        side = fused and training and pos is not None
+        if side:
+            fork = torch.cuda.Event()
+            fork.record()
         x = e("x0", (M, d))
         ops.embed_fwd(0, ids, T, self.W("item_emb.weight"), self.W("pos_emb.weight"), math.sqrt(d), p,
                       self.salt["emb"], sb, x)
+        if side:
+            # issued after the first forward launch: in the captured graph the forward chain is then the
+            # first child of the step's root and keeps the launch queue; the side branch gets the second
+            s["side"] = self._side_prologue(ids, pos, neg, after=fork)
         for i in range(L):
             pre = f"attention_layers.{i}."
             Q, mu1, r1 = e("Q", (M, d)), e("mu", (M,), torch.float32), e("r", (M,), torch.float32)
@@ -270,9 +276,9 @@ class SASEngine:
 
         fused = ops.sas_block_fused_ok(d, self.dt)
         if fused:
-            # the side-stream prologue of forward built the item index and the transposed weights
+            # the side-stream prologue of forward built the item index and the transposed weights; the head
+            # backward needs neither, so the join waits until the blocks' backward
             ev, iws = s["side"] if "side" in s else self._side_prologue(ids, s["pos"], s["neg"])
-            torch.cuda.current_stream().wait_event(ev)
         if fused:
             dx = e("dx", (M, d))
             lnh = self.ws.get("lnh", (2 * d * (-(-M // 64)),), torch.float32)
@@ -285,6 +291,7 @@ class SASEngine:
                 ops.sas_head_bwd(None, None, None, None, None, dpl, dnl, None, None, s["pos"], s["neg"], E, s["xL"],
                                  gl, s["muf"], s["rf"], dx, lnh)
             segs = ops.ln_partial_segments(lnh, M, d, G("last_layernorm.weight"), G("last_layernorm.bias"))
+            torch.cuda.current_stream().wait_event(ev)
             dx = self._backward_blocks_fused(s, dx, grad, segs)
             ops.embed_bwd(0, ids, T, dx, math.sqrt(d), p, self.salt["emb"], sb, None, G("pos_emb.weight"))
             ops.item_grad(iws, 3, M, dx, math.sqrt(d), p, self.salt["emb"], sb, s["f"], dpl, dnl,
@@ -336,14 +343,17 @@ class SASEngine:
         ops.embed_bwd(0, ids, T, dx, math.sqrt(d), p, self.salt["emb"], sb, G("item_emb.weight"),
                       G("pos_emb.weight"))
 
-    def _side_prologue(self, ids, pos, neg):
+    def _side_prologue(self, ids, pos, neg, after=None):
         """Work of the fused backward that depends only on the batch's keys and the weights, issued on a
         side stream so it overlaps the forward pass: the item-gradient index (rs_item_index_build) and
         the transposed block weights (rs_transpose_bf16).  Returns (event, index workspace)."""
         cur = torch.cuda.current_stream()
         if getattr(self, "_side", None) is None:
             self._side = torch.cuda.Stream(device=self.dev)
-        self._side.wait_stream(cur)
+        if after is not None:
+            self._side.wait_event(after)
+        else:
+            self._side.wait_stream(cur)
         B, T = ids.shape
         M, d = B * T, self.d
         V1 = self.flat.shapes["item_emb.weight"][0]

@@ -16,6 +16,48 @@ ACT_NONE, ACT_RELU, ACT_GELU, ACT_RELU_BWD, ACT_GELU_BWD = (
     _lib.ACT_NONE, _lib.ACT_RELU, _lib.ACT_GELU, _lib.ACT_RELU_BWD, _lib.ACT_GELU_BWD)
 
 
+# ------------------------------------------------------------------ kernel stamps
+STAMP_KINDS = {1: "attn_bwd", 2: "wgrad_grouped"}
+
+
+def kernel_stamps(buf, step, kinds=()):
+    """Enable (buf: int64 device tensor, step: the optimizer's float64 device step count, kinds: names from
+    STAMP_KINDS) or disable (None, None) the in-kernel begin/end stamps of rs_attn_bwd / rs_wgrad_grouped
+    launches (layout in include/recsys_hip.h).  Launches captured into a graph while enabled keep stamping
+    on every replay."""
+    mask = sum(1 << k for k, n in STAMP_KINDS.items() if n in kinds)
+    call("rs_kernel_stamps", ptr(buf), ptr(step), mask)
+
+
+def read_kernel_stamps(buf, khz):
+    """[(mark, step slot, µs)] of every complete record in a stamp buffer (after the stamped work finished)."""
+    import numpy as np
+    h = buf.cpu().numpy().view(np.uint64)
+    steps, marks, W = int(h[1]), int(h[2]), int(h[3])
+    rec = h[4:4 + steps * marks * (1 + W)].reshape(steps, marks, 1 + W)
+    out = []
+    for st in range(steps):
+        for m in range(marks):
+            b, e = int(rec[st, m, 0]), int(rec[st, m, 1:].max())
+            if b and e > b:
+                out.append((m, st, (e - b) / khz * 1e3))
+    return out
+
+
+def kernel_stamp_kinds():
+    """Kind name of every mark handed out since the last kernel_stamps(buf, step), in mark order."""
+    n = _lib.lib().rs_kernel_stamp_count()
+    arr = (C.c_int * max(n, 1))()
+    call("rs_kernel_stamp_kinds", arr, n)
+    return [STAMP_KINDS.get(arr[i], "?") for i in range(n)]
+
+
+def wall_clock_khz():
+    k = C.c_int()
+    call("rs_wall_clock_khz", C.byref(k))
+    return k.value
+
+
 def dtype_code(t):
     if t.dtype == torch.float32:
         return F32

@@ -195,8 +195,11 @@ class FusedTrainStep:
         self.load_optimizer_state_dict(d["optimizer_state_dict"])
 
     # ---------------------------------------------------------------- HIP graphs
-    def capture(self, *example_batch, warmup=2):
-        """Capture the step into HIP graphs; example_batch fixes the shapes."""
+    def capture(self, *example_batch, warmup=2, stamps=None):
+        """Capture the step into HIP graphs; example_batch fixes the shapes.
+        stamps: (int64 device buffer, kind names): the compute graph is captured with kernel stamps enabled
+        for those kinds (ops.kernel_stamps against the optimizer's step count), so every replay records the
+        begin/end ticks of its rs_attn_bwd / rs_wgrad_grouped launches there (bench.py's in-step timing)."""
         # one packed static buffer when the inputs share shape and dtype: replay_packed() then refills
         # all of them with ONE device copy (the bench stacks its batches the same way)
         same = all(t.shape == example_batch[0].shape and t.dtype == example_batch[0].dtype for t in example_batch)
@@ -213,22 +216,39 @@ class FusedTrainStep:
                 self.step(*self.static)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        if self.dp:
-            g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g1):
-                self._compute(*self.static)
-            with torch.cuda.graph(g2):
-                self._update()
-            self.graphs = (g1, g2)
-        else:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._compute(*self.static)
-                self._update()
-            self.graphs = (g,)
+        self._capture_graphs(lambda: self._compute(*self.static), stamps)
         return self
 
-    def capture_sampled(self, sampler, warmup=2):
+    def _capture_graphs(self, compute, stamps=None):
+        """The compute graph (+ the optimizer in the same graph on one device; a separate optimizer graph after
+        the eager RCCL all-reduce under DP)."""
+        g = torch.cuda.CUDAGraph()
+        if stamps is not None:
+            ops.kernel_stamps(stamps[0], self.opt.state, stamps[1])
+        try:
+            with torch.cuda.graph(g):
+                compute()
+                if not self.dp:
+                    self._update()
+        finally:
+            if stamps is not None:
+                ops.kernel_stamps(None, None)
+        self.g_compute = g
+        self.g_update = None
+        if self.dp:
+            self.g_update = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g_update):
+                self._update()
+        self.graphs = (g, self.g_update) if self.dp else (g,)
+
+    def _replay_graphs(self):
+        self.g_compute.replay()
+        if self.dp:
+            self._exchange()            # RCCL all-reduce, eager, on the current stream
+            self.g_update.replay()
+        return self.loss_val if self.dp else self.loss_out[2:3]
+
+    def capture_sampled(self, sampler, warmup=2, stamps=None):
         """Capture sampling (rbm_amd.dataloaders.DeviceWarpSampler for SAS, DeviceBertMasker for BERT, into
         static buffers) together with the step, so ``replay_sampled()`` runs a whole training iteration --
         batch construction included -- as one graph replay (the reference's sampler / DataLoader +
@@ -248,47 +268,25 @@ class FusedTrainStep:
                 self.step(*self.static)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        if self.dp:
-            g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g1):
-                sampler.sample_into(*self.static)
-                self._compute(*self.static)
-            with torch.cuda.graph(g2):
-                self._update()
-            self.graphs = (g1, g2)
-        else:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                sampler.sample_into(*self.static)
-                self._compute(*self.static)
-                self._update()
-            self.graphs = (g,)
+
+        def compute():
+            sampler.sample_into(*self.static)
+            self._compute(*self.static)
+        self._capture_graphs(compute, stamps)
         return self
 
     def replay_sampled(self):
         """One training iteration on a freshly sampled batch (after capture_sampled)."""
-        self.graphs[0].replay()
-        if self.dp:
-            self._exchange()
-            self.graphs[1].replay()
-        return self.loss_val if self.dp else self.loss_out[2:3]
+        return self._replay_graphs()
 
     def replay_packed(self, packed):
         """replay() for a batch already stacked as one tensor [n_inputs, ...] (see capture)."""
         if self.packed is None:
             return self.replay(*packed.unbind(0))
         self.packed.copy_(packed, non_blocking=True)
-        self.graphs[0].replay()
-        if self.dp:
-            self._exchange()
-            self.graphs[1].replay()
-        return self.loss_val if self.dp else self.loss_out[2:3]
+        return self._replay_graphs()
 
     def replay(self, *batch):
         for dst, src in zip(self.static, batch):
             dst.copy_(src, non_blocking=True)
-        self.graphs[0].replay()
-        if self.dp:
-            self._exchange()            # RCCL all-reduce, eager, on the current stream
-            self.graphs[1].replay()
-        return self.loss_val if self.dp else self.loss_out[2:3]
+        return self._replay_graphs()

@@ -1,0 +1,23 @@
+"""Print one training step's kernel timeline from a rocprofv3 kernel trace (the Nth-from-last step,
+delimited by the optimizer kernel), with gaps between consecutive kernels.
+usage: python tools/step_timeline.py prof_kernel_trace.csv [n_from_last=3]"""
+import csv
+import sys
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+nth = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+ad = [i for i, r in enumerate(rows) if "adam_step" in r["Kernel_Name"]]
+hi, lo = ad[-nth], ad[-nth - 1]
+sel = rows[lo + 1:hi + 1]
+t0 = int(sel[0]["Start_Timestamp"])
+prev = None
+busy = 0
+for r in sel:
+    s = int(r["Start_Timestamp"]) - t0
+    e = int(r["End_Timestamp"]) - t0
+    gap = (s - prev) / 1e3 if prev is not None else 0.0
+    print(f'{s/1e3:8.1f} {e/1e3:8.1f} dur {(e-s)/1e3:6.1f} gap {gap:6.1f} q{r["Queue_Id"]} wg {int(r["Grid_Size_X"])*int(r["Grid_Size_Y"])//int(r["Workgroup_Size_X"]):6d} {r["Kernel_Name"][:60]}')
+    prev = max(prev or 0, e)
+    busy += e - s
+print(f"step span {(int(sel[-1]['End_Timestamp'])-t0)/1e3:.1f} us, kernel time {busy/1e3:.1f} us")
