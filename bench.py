@@ -148,10 +148,16 @@ def _roof(kernel, us, flops, nbytes, dtype, note, live_us=None):
             "arith_intensity": round(ai, 1), "note": note}
 
 
-MARK = {"sas": "attn_bwd", "bert": "wgrad_grouped"}   # ops wrapper of the dominant kernel per model
+# ops wrapper of the dominant kernel per config (most device time per step in the rocprof profiles):
+# SAS -> the attention backward; BERT at 27k items -> the grouped block weight gradients; BERT at 1M items ->
+# the vocabulary-logits GEMM (rs_vocab_ce_fwd; its backward twin recomputes the same product)
+def dominant(cfg):
+    if cfg["model"] == "sas":
+        return "attn_bwd"
+    return "vocab_ce_fwd" if cfg["V"] >= 100000 else "wgrad_grouped"
 
 
-def roofline(cfg, B, dtype, live_us=None, reps=50):
+def roofline(cfg, B, dtype, live_us=None, reps=50, labelled=None):
     """Dominant kernel of the step (by rocprof device time).  SAS: the attention backward (rs_attn_bwd:
     dQ+delta and dK/dV kernels); BERT: the grouped block weight gradients (rs_wgrad_grouped).
     live_us: its launch durations measured INSIDE the timed step replays (in-kernel begin/end stamps of
@@ -189,6 +195,21 @@ def roofline(cfg, B, dtype, live_us=None, reps=50):
         return _roof("rs_attn_bwd (attn_bwd_dq_lds + attn_bwd_dkv_lds)", us, flops, nbytes, dtype,
                      f"causal attention backward, B={B} T={T} Dh={Dh} dropout {cfg['p']}; 2 kernels per launch",
                      live_us)
+    if dominant(cfg) == "vocab_ce_fwd":
+        # BERT, 1M-item vocabulary: h[R,d] . E^T + b with the online-softmax partial epilogue over the labelled
+        # rows (R = the batches' mean labelled count), E = out.weight [V+1, d] bf16
+        R, V1 = int(round(labelled)), cfg["V"] + 1
+        h = torch.randn(R, d, device="cuda", generator=g).to(dt)
+        E = (0.05 * torch.randn(V1, d, device="cuda", generator=g)).to(dt)
+        bias = torch.zeros(V1, device="cuda")
+        lab = torch.randint(1, V1, (R,), device="cuda", generator=g)
+        ws = torch.empty(ops.vocab_ce_ws_numel(R, V1), device="cuda")
+        out = torch.empty(4, device="cuda")
+        us = _time_on_stream(lambda: ops.vocab_ce_fwd(h, E, bias, lab, ws, out), reps, stream)
+        flops = 2.0 * R * V1 * d
+        nbytes = (V1 * d + R * d) * es + R * -(-V1 // 128) * 2 * 4     # E, h once; (max, sum) partials
+        return _roof("rs_vocab_ce_fwd (logits GEMM + online-softmax partial epilogue)", us, flops, nbytes, dtype,
+                     f"R={R} labelled rows (batch mean) x V+1={V1} x d={d}", live_us)
     # BERT: the grouped weight-gradient launch of all block weights (rs_wgrad_grouped: GEMM + reduction),
     # the largest single kernel of the step
     from rbm_amd.models.bert_model.bert import BERTEngine
@@ -281,7 +302,7 @@ def main():
     NMARK, WAVES = 8, 16384
     sbuf = None if args.no_graph else torch.zeros(4 + args.steps * NMARK * (1 + WAVES), dtype=torch.int64,
                                                   device="cuda")
-    stamps = None if sbuf is None else (sbuf, (MARK[cfg["model"]],))
+    stamps = None if sbuf is None else (sbuf, (dominant(cfg),))
 
     if args.sampler == "device" and cfg["model"] == "sas":
         import rbm_amd.data as synth
@@ -337,7 +358,9 @@ def main():
     if sbuf is not None:
         live = [us for _, _, us in ops.read_kernel_stamps(sbuf, ops.wall_clock_khz())]
         del sbuf
-    roof = roofline(cfg, B, args.dtype, live_us=live) if rank == 0 else None
+    labelled = (sum(float((lab != 0).sum()) for _, lab in host_batches) / len(host_batches)
+                if cfg["model"] == "bert" else None)
+    roof = roofline(cfg, B, args.dtype, live_us=live, labelled=labelled) if rank == 0 else None
     if rank == 0:
         cpu = cpu_baseline(cfg, B, args.cpu_baseline_seconds) if world == 1 and args.cpu_baseline_seconds > 0 \
             else None

@@ -233,16 +233,17 @@ int rs_vocab_ce_bwd(int64_t R, int64_t V1, int64_t d, const void* h, int64_t ldh
                     const float* dloss, const float* ws, void* dlogits, int64_t lddl, void* stream);
 
 /* Kernel stamps (bench.py's in-step timing of the dominant launch; not on the reference's path).
- * While enabled (buf != NULL), rs_attn_bwd (bf16 LDS path) and/or rs_wgrad_grouped launches (kinds in
- * kind_mask, bit RS_STAMP_*) are stamped -- marks numbered in launch order from 0, fixed into the kernel
+ * While enabled (buf != NULL), rs_attn_bwd (bf16 LDS path), rs_wgrad_grouped and rs_vocab_ce_fwd (its
+ * logits GEMM) launches of the kinds in kind_mask (bit RS_STAMP_*) are stamped -- marks numbered in launch order from 0, fixed into the kernel
  * arguments, so a captured graph keeps stamping on every replay.  buf (device u64) = {base step, steps
- * held, marks per step, W, then per (slot = (int64)*step - base, mark) a record {begin, exit time of
- * wave 0 .. W-1}} in s_memrealtime ticks (begin: the first dispatched workgroup's start; the launch
- * ends at the max wave exit).  step: the optimizer's device step count (double, rs_adam_prepare's
+ * held, marks per step, W, then per (slot = (int64)*step - base, mark) a record {begin, end lanes
+ * 0 .. W-1}} in s_memrealtime ticks (begin: the first dispatched workgroup's start; each wave raises
+ * end lane (wave index mod W) to its exit time; the launch ends at the max over the lanes).  step: the optimizer's device step count (double, rs_adam_prepare's
  * state[0]).  rs_kernel_stamps(NULL, NULL, 0) disables.  rs_kernel_stamp_count / rs_kernel_stamp_kinds:
  * the marks handed out since the last enable and their kinds.  rs_wall_clock_khz: tick rate. */
 #define RS_STAMP_ATTN_BWD 1
 #define RS_STAMP_WGRAD_GROUPED 2
+#define RS_STAMP_VOCAB_CE_FWD 3   /* the logits GEMM of rs_vocab_ce_fwd */
 int rs_kernel_stamps(uint64_t* buf, const double* step, int kind_mask);
 int rs_kernel_stamp_count(void);
 int rs_kernel_stamp_kinds(int* kinds, int n);

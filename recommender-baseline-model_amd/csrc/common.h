@@ -202,11 +202,13 @@ __host__ __device__ static inline int64_t cdiv(int64_t a, int64_t b) { return (a
 
 // ---- kernel stamps (bench.py's in-step timing of the dominant launch; misc.hip rs_kernel_stamps) ----
 // buf: [0] base step, [1] steps held, [2] marks per step, [3] W; then per (step slot, mark) a record of
-// 1 + W u64: {begin, end of wave 0 .. W-1} in s_memrealtime ticks.  begin = the start of the first
-// dispatched workgroup's wave 0 (workgroup 0 is dispatched first); each wave stores its own exit time
-// (plain stores to distinct words: same-address atomics from thousands of waves serialise and cost
-// tens of microseconds), and the reader takes the max.  Slot = the optimizer's step count (*step, a
-// device double advanced by rs_adam_prepare) - base.  buf == null: off.
+// 1 + W u64: {begin, end lanes 0 .. W-1} in s_memrealtime ticks.  begin = the start of the first
+// dispatched workgroup's wave 0 (workgroup 0 is dispatched first); every wave raises end lane
+// (wave index mod W) to its exit time with a no-return atomic max -- W distinct words, so waves
+// sharing a word are W apart in dispatch order and rarely contend (same-address atomics from
+// thousands of waves serialise and cost tens of microseconds) -- and the reader takes the max over
+// the lanes.  Slot = the optimizer's step count (*step, a device double advanced by rs_adam_prepare)
+// - base.  buf == null: off.
 struct KStamp {
   unsigned long long* buf;
   const double* step;
@@ -233,16 +235,15 @@ struct KStampBegin {
   }
 };
 
-// stores the wave's exit time when it leaves the kernel (any return path); the record address is formed
+// raises its end lane when the wave leaves the kernel (any return path); the record address is formed
 // at exit from the kernel arguments, so nothing stays live in registers across the kernel body
 struct KStampEnd {
   const KStamp& k;
   __device__ __forceinline__ explicit KStampEnd(const KStamp& k_) : k(k_) {}
   __device__ __forceinline__ ~KStampEnd() {
     if (k.buf && (threadIdx.x & 63) == 0) {
-      const long long w = kstamp_wave();
-      unsigned long long* p = w < (long long)k.buf[3] ? kstamp_rec(k) : nullptr;
-      if (p) p[1 + w] = (unsigned long long)wall_clock64();
+      unsigned long long* p = kstamp_rec(k);
+      if (p) atomicMax(p + 1 + kstamp_wave() % (long long)k.buf[3], (unsigned long long)wall_clock64());
     }
   }
 };

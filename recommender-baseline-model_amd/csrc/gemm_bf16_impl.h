@@ -441,6 +441,8 @@ __device__ __forceinline__ void ce_rows(const GemmArgs& a, const float* Cs, int 
 
 template <bool AK, bool BK, int BM, int BN, int EC>
 __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs a) {
+  KStampBegin stamp_b_(a.ks);
+  KStampEnd stamp_e_(a.ks);
   using IA = Img<AK, BM>;
   using IB = Img<BK, BN>;
   constexpr int STAGE = IA::ELEMS + IB::ELEMS;
@@ -458,18 +460,30 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs a) {
   const unsigned tiles_n = (unsigned)((a.N + BN - 1) / BN);
   const int64_t Mb = (!AK && a.epi.rows_dev) ? min(a.M, (int64_t)*a.epi.rows_dev) : a.M;
   unsigned bid = blockIdx.x;
+  unsigned tiles_m = gridDim.x / tiles_n;
   {
     // a device row count (compacted rows) leaves only the first cdiv(Mb, BM) row tiles live: remap over
     // those, so the live tiles spread over all XCDs instead of the first few XCDs' contiguous ranges
     unsigned nwg = gridDim.x;
     if (!AK && a.epi.rows_dev) {
-      nwg = (unsigned)(((Mb + BM - 1) / BM) * tiles_n);
+      tiles_m = (unsigned)((Mb + BM - 1) / BM);
+      nwg = tiles_m * tiles_n;
       if (bid >= nwg) return;
     }
     const unsigned q = nwg >> 3, r = nwg & 7, x = bid & 7;
     bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
   }
-  const unsigned tm = bid / tiles_n, tn = bid - tm * tiles_n;
+  // walk the shorter tile axis fastest: an XCD's contiguous range of tiles then shares the tiles of
+  // the LONG axis's operand in its L2, and that operand streams from HBM once (the 1M-column vocabulary
+  // GEMMs: 14 row tiles x 7.8k column tiles; row-major order re-read the 512 MB weight 14 times)
+  unsigned tm, tn;
+  if (tiles_m < tiles_n) {
+    tn = bid / tiles_m;
+    tm = bid - tn * tiles_m;
+  } else {
+    tm = bid / tiles_n;
+    tn = bid - tm * tiles_n;
+  }
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
   const int z = blockIdx.z;
   const int64_t Kb = (AK && a.epi.rows_dev) ? min(a.K, (int64_t)*a.epi.rows_dev) : a.K;

@@ -34,6 +34,7 @@ struct GemmArgs {
     const float* dloss;
     int64_t ntn;
   } ce;
+  KStamp ks;  // (bf16 path) in-kernel begin/end stamps of this launch (bench.py timing), buf null = off
 };
 
 

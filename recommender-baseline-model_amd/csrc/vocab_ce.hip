@@ -119,6 +119,7 @@ int rs_vocab_ce_fwd(int64_t R, int64_t V1, int64_t d, const void* h, int64_t ldh
   GemmArgs a = vce::gemm_args(R, V1, d, h, ldh, E, lde, bias, labels, rows_dev);
   a.ce.part = w.part;
   a.ce.tgt = w.tgt;
+  a.ks = kstamp_next(RS_STAMP_VOCAB_CE_FWD);
   hipError_t e = gbf::launch_cfg<false, false, 128, vce::BN, gbf::EC_CE_PART>(a, s);
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(vce::ce_tiles_kernel, dim3((unsigned)cdiv(R, 4)), dim3(256), 0, s, w.part, a.ce.ntn, R, labels,

@@ -17,7 +17,7 @@ ACT_NONE, ACT_RELU, ACT_GELU, ACT_RELU_BWD, ACT_GELU_BWD = (
 
 
 # ------------------------------------------------------------------ kernel stamps
-STAMP_KINDS = {1: "attn_bwd", 2: "wgrad_grouped"}
+STAMP_KINDS = {1: "attn_bwd", 2: "wgrad_grouped", 3: "vocab_ce_fwd"}
 
 
 def kernel_stamps(buf, step, kinds=()):
