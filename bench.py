@@ -205,10 +205,10 @@ def roofline(cfg, B, dtype, live_us=None, reps=50, labelled=None):
         lab = torch.randint(1, V1, (R,), device="cuda", generator=g)
         ws = torch.empty(ops.vocab_ce_ws_numel(R, V1), device="cuda")
         out = torch.empty(4, device="cuda")
-        us = _time_on_stream(lambda: ops.vocab_ce_fwd(h, E, bias, lab, ws, out), reps, stream)
+        us = _time_on_stream(lambda: ops.vocab_head_fwd(h, E, bias, lab, ws, out), reps, stream)
         flops = 2.0 * R * V1 * d
         nbytes = (V1 * d + R * d) * es + R * -(-V1 // 128) * 2 * 4     # E, h once; (max, sum) partials
-        return _roof("rs_vocab_ce_fwd (logits GEMM + online-softmax partial epilogue)", us, flops, nbytes, dtype,
+        return _roof("rs_vocab_head_fwd (E-tile-stationary logits + online-softmax partials)", us, flops, nbytes, dtype,
                      f"R={R} labelled rows (batch mean) x V+1={V1} x d={d}", live_us)
     # BERT: the grouped weight-gradient launch of all block weights (rs_wgrad_grouped: GEMM + reduction),
     # the largest single kernel of the step

@@ -232,6 +232,21 @@ int rs_vocab_ce_bwd(int64_t R, int64_t V1, int64_t d, const void* h, int64_t ldh
                     const float* bias, const int64_t* labels, const int* rows_dev, const float* count,
                     const float* dloss, const float* ws, void* dlogits, int64_t lddl, void* stream);
 
+/* ---- vocabulary head, vocabulary-tile-stationary (vocab_head.hip; bf16, d in {64, 128, 256}) -----
+ * Same math and workspace layout (rs_vocab_ce_ws_numel) as rs_vocab_ce_fwd/bwd, for the same reference
+ * lines (BS/models/bert.py:10,16, BS/trainers/bert.py:11,36-40); one persistent workgroup per CU keeps a
+ * 256- (fwd) / 128-entry (bwd) tile of E in LDS and walks every 128-row tile of h against it, so E streams
+ * from HBM once and the short d-deep products run back to back instead of one cold tile at a time.
+ * rs_vocab_head_fwd: out = {loss sum, labelled count, sum / (count_override or count)}, ws keeps lse.
+ * rs_vocab_head_bwd: dlogits [R][V1] bf16 (rows < live count) = (softmax - onehot) * (dloss or 1) / count. */
+int rs_vocab_head_supported(int64_t d);
+int rs_vocab_head_fwd(int64_t R, int64_t V1, int64_t d, const void* h, int64_t ldh, const void* E, int64_t lde,
+                      const float* bias, const int64_t* labels, const int* rows_dev, const float* count_override,
+                      float* ws, float* out, void* stream);
+int rs_vocab_head_bwd(int64_t R, int64_t V1, int64_t d, const void* h, int64_t ldh, const void* E, int64_t lde,
+                      const float* bias, const int64_t* labels, const int* rows_dev, const float* count,
+                      const float* dloss, const float* ws, void* dlogits, int64_t lddl, void* stream);
+
 /* Kernel stamps (bench.py's in-step timing of the dominant launch; not on the reference's path).
  * While enabled (buf != NULL), rs_attn_bwd (bf16 LDS path), rs_wgrad_grouped and rs_vocab_ce_fwd (its
  * logits GEMM) launches of the kinds in kind_mask (bit RS_STAMP_*) are stamped -- marks numbered in launch order from 0, fixed into the kernel
@@ -243,7 +258,7 @@ int rs_vocab_ce_bwd(int64_t R, int64_t V1, int64_t d, const void* h, int64_t ldh
  * the marks handed out since the last enable and their kinds.  rs_wall_clock_khz: tick rate. */
 #define RS_STAMP_ATTN_BWD 1
 #define RS_STAMP_WGRAD_GROUPED 2
-#define RS_STAMP_VOCAB_CE_FWD 3   /* the logits GEMM of rs_vocab_ce_fwd */
+#define RS_STAMP_VOCAB_CE_FWD 3   /* the logits GEMM of rs_vocab_ce_fwd / the rs_vocab_head_fwd kernel */
 int rs_kernel_stamps(uint64_t* buf, const double* step, int kind_mask);
 int rs_kernel_stamp_count(void);
 int rs_kernel_stamp_kinds(int* kinds, int n);

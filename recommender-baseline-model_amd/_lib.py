@@ -74,6 +74,9 @@ SIGNATURES = {
     "rs_vocab_ce_ws_numel": [i64, i64],
     "rs_vocab_ce_fwd": [i64, i64, i64, vp, i64, vp, i64, vp, vp, vp, vp, vp, vp, vp],
     "rs_vocab_ce_bwd": [i64, i64, i64, vp, i64, vp, i64, vp, vp, vp, vp, vp, vp, vp, i64, vp],
+    "rs_vocab_head_supported": [i64],
+    "rs_vocab_head_fwd": [i64, i64, i64, vp, i64, vp, i64, vp, vp, vp, vp, vp, vp, vp],
+    "rs_vocab_head_bwd": [i64, i64, i64, vp, i64, vp, i64, vp, vp, vp, vp, vp, vp, vp, i64, vp],
     "rs_seed_advance": [vp, vp],
     "rs_sas_block_in": [i64, i64, vp, i64, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "rs_sas_block_out": [i64, i64, vp, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32,

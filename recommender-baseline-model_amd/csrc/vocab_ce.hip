@@ -17,10 +17,18 @@
 namespace vce {
 
 // one wave per row: combine the row's tile partials (lane-strided, then a fixed butterfly)
+// tgt: the label logits from the GEMM epilogue, or (lh != null) computed here as <h[r], E[label]> + b[label]
+struct LabelDot {
+  const __bf16* h; int64_t ldh;
+  const __bf16* E; int64_t lde;
+  const float* bias;
+  int64_t d;
+};
+
 __global__ __launch_bounds__(256) void ce_tiles_kernel(const float* __restrict__ part, int64_t ntn, int64_t R,
                                                        const int64_t* __restrict__ labels,
                                                        const float* __restrict__ tgt, const int* __restrict__ rows_dev,
-                                                       float* __restrict__ lse, float* __restrict__ rowp) {
+                                                       float* __restrict__ lse, float* __restrict__ rowp, LabelDot lh) {
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= R) return;
@@ -42,10 +50,17 @@ __global__ __launch_bounds__(256) void ce_tiles_kernel(const float* __restrict__
     sm = (mm == -__builtin_inff()) ? 0.f : sm * __expf(mx - mm) + s2 * __expf(m2 - mm);
     mx = mm;
   }
+  float t = 0.f;
+  if (lh.h) {
+    const int64_t lb = labels[r];
+    float dot = 0.f;
+    for (int64_t k = lane; k < lh.d; k += 64) dot += (float)lh.h[r * lh.ldh + k] * (float)lh.E[lb * lh.lde + k];
+    t = wave_sum(dot) + (lh.bias ? lh.bias[lb] : 0.f);
+  }
   if (lane == 0) {
     const float L = mx + __logf(sm);
     lse[r] = L;
-    rowp[2 * r] = L - tgt[r];
+    rowp[2 * r] = L - (lh.h ? t : tgt[r]);
     rowp[2 * r + 1] = 1.f;
   }
 }
@@ -103,6 +118,17 @@ GemmArgs gemm_args(int64_t R, int64_t V1, int64_t d, const void* h, int64_t ldh,
 
 }  // namespace vce
 
+hipError_t vce_finish(const float* part, int64_t ntn, int64_t R, const int64_t* labels, const float* tgt,
+                      const int* rows_dev, float* lse, float* rowp, const float* count_override, float* out,
+                      hipStream_t s, const void* h, int64_t ldh, const void* E, int64_t lde, const float* bias,
+                      int64_t d) {
+  const vce::LabelDot lh{(const __bf16*)h, ldh, (const __bf16*)E, lde, bias, d};
+  hipLaunchKernelGGL(vce::ce_tiles_kernel, dim3((unsigned)cdiv(R, 4)), dim3(256), 0, s, part, ntn, R, labels, tgt,
+                     rows_dev, lse, rowp, lh);
+  hipLaunchKernelGGL(vce::ce_sum_kernel, dim3(1), dim3(256), 0, s, rowp, R, count_override, out);
+  return hipGetLastError();
+}
+
 extern "C" {
 
 int64_t rs_vocab_ce_ws_numel(int64_t R, int64_t V1) {
@@ -122,10 +148,8 @@ int rs_vocab_ce_fwd(int64_t R, int64_t V1, int64_t d, const void* h, int64_t ldh
   a.ks = kstamp_next(RS_STAMP_VOCAB_CE_FWD);
   hipError_t e = gbf::launch_cfg<false, false, 128, vce::BN, gbf::EC_CE_PART>(a, s);
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(vce::ce_tiles_kernel, dim3((unsigned)cdiv(R, 4)), dim3(256), 0, s, w.part, a.ce.ntn, R, labels,
-                     w.tgt, rows_dev, w.lse, w.rowp);
-  hipLaunchKernelGGL(vce::ce_sum_kernel, dim3(1), dim3(256), 0, s, w.rowp, R, count_override, out);
-  return (int)hipGetLastError();
+  return (int)vce_finish(w.part, a.ce.ntn, R, labels, w.tgt, rows_dev, w.lse, w.rowp, count_override, out, s,
+                         nullptr, 0, nullptr, 0, nullptr, 0);
 }
 
 int rs_vocab_ce_bwd(int64_t R, int64_t V1, int64_t d, const void* h, int64_t ldh, const void* E, int64_t lde,

@@ -1,0 +1,413 @@
+// BERT4Rec vocabulary head on the labelled rows, vocabulary-tile-stationary (bf16, gfx950).
+//
+// Reference: BERTModel.out = Linear(d, V+1) on every position (BS/models/bert.py:10,16) and
+// CrossEntropyLoss(ignore_index=0) (BS/trainers/bert.py:11,36-40).  The fused step keeps the R
+// labelled rows h [R][d] (R ~ 1.8k at the ML-20M / 1M-item shapes) and needs, per step,
+//   fwd: per row the log-sum-exp of the logits h E^T + b and the label's logit;
+//   bwd: dlogits = (softmax - onehot) * dloss / count (operand of the input gradient dh = dlogits E),
+//        dE = dlogits^T h and db = colsum(dlogits).
+// With V+1 = 1M these are R x 1M x d products: the generic GEMM ran them as 128x128 output tiles with
+// only d / 64 = 4 k-stages each, so every workgroup paid a cold prologue and a full epilogue for 4
+// stages of MFMAs (~15 % of the MFMA peak), and dE was a third pass re-reading 3.6 GB of dlogits.
+//
+// Here one workgroup owns a 128-column vocabulary tile at a time (persistent over tiles) and walks
+// ALL row tiles of h against it:
+//   * the h row tile [128][d] sits whole in LDS (prefetched into registers during the previous row
+//     tile); E's tile streams through double-buffered 64-deep LDS stages from L2 (HBM reads it once);
+//   * S^T = E_tile . h_tile^T is accumulated transposed (vocabulary on the accumulator's row axis), so
+//     a lane holds 4 consecutive vocabulary entries of one row: per-row softmax statistics reduce in
+//     registers + 2 shuffles, and dlogits leave as 8-byte LDS writes;
+//   * bwd: dlogits go to LDS [rows][vocab] (and, 16-B coalesced, to the global dlogits operand of dh);
+//     dE_tile [128][d] += dlogits^T . h accumulates in registers over all row tiles (both operands
+//     read k-major with ds_read_b64_tr_b16), db rides on extra MFMAs against a ones operand; dE / db
+//     are written once per vocabulary tile -- no dlogits re-read for the weight gradient.
+// The fwd partials have exactly the layout of vocab_ce.hip's EC_CE_PART epilogue, so ce_tiles_kernel /
+// ce_sum_kernel finish the loss unchanged (the label logit is formed there as <h, E[label]> + b).
+//
+// Measured at R = 1750, V+1 = 1M, d = 256 (tools/vhead_bench.py): fwd 1.94 ms = 463 TFLOP/s (the GEMM-epilogue
+// form: 2.5 ms).  Where the rest goes (switching parts off): the bare MFMA loop alone runs at 917 TFLOP/s
+// (16 MFMAs per wave between barriers, both waves of a SIMD in the same phase), the softmax epilogue costs
+// ~0.5 ms (its VALU work per logit equals the MFMA work of a d = 256 product and does not overlap it), the h
+// stream ~0.3 ms, the E tiles ~0.1 ms.  The XOR-swizzled images removed all LDS bank conflicts (44 % of the
+// LDS cycles with padded rows).
+#include "common.h"
+#include "../../include/recsys_hip.h"
+#include <type_traits>
+
+typedef __attribute__((ext_vector_type(4))) __bf16 bf4;
+
+namespace vh {
+typedef __bf16 bf16;
+
+constexpr int BR = 128;   // rows per row tile
+constexpr int NTH = 512;  // 8 waves, 2 per SIMD: wave (wm, wn) = vocabulary quarter wm x row half wn
+typedef __attribute__((ext_vector_type(4))) unsigned u4;
+
+struct Args {
+  int64_t R, V1, ntn;       // ntn: 128-column partial tiles (vocab_ce.hip's ws layout)
+  const bf16* h; int64_t ldh;
+  const bf16* E; int64_t lde;
+  const float* bias;
+  const int64_t* labels;
+  const int* rows_dev;
+  float* part;        // fwd: [R][ntn][2] (max, sum exp) per 128-column tile
+  float* tgt;         // fwd: [R] label logits
+  const float* lse;   // bwd
+  const float* count;
+  const float* dloss;
+  bf16* dl; int64_t lddl;   // bwd: dlogits [R][V1] (rows >= live count untouched)
+  KStamp ks;
+};
+
+// BV vocabulary entries per workgroup tile (E tile stationary in LDS), h streamed in BK-deep stages
+template <int DK, int BV, bool BWD> struct L {
+  static constexpr int BK = BWD ? 64 : 32;
+  static constexpr int LDE = DK;                   // unpadded rows, 16-B chunks XOR-swizzled (swz)
+  static constexpr int LDH = BK;
+  static constexpr int LDD = BV + 8;
+  static constexpr int E_ELEMS = BV * LDE;
+  static constexpr int H_ELEMS = BR * LDH;
+  static constexpr int D_ELEMS = BWD ? BR * LDD : 0;
+  static constexpr int NKS = DK / BK;
+  static constexpr int HPT = BR * BK / 8 / NTH;    // 16-B chunks of an h stage per thread
+  static constexpr int EPT = BV * DK / 8 / NTH;    // ... of an E tile
+  static constexpr int FV = BV / 64;               // 16-wide vocabulary fragments per wave
+  static constexpr int PF = 3;                     // h stages in flight (register ring)
+  static constexpr int LDS = (E_ELEMS + 2 * H_ELEMS + D_ELEMS) * 2 + BR * 12 + 4 * BR * 2 * 4;
+};
+
+// XOR swizzle of the 16-B chunk index within a row of CPR chunks: the 16 lanes of every ds_read_b128 lane
+// group (rows li = lane & 15 of a fragment, chunks c0 + (lane >> 4)) then hit 16 distinct 4-bank sets
+template <int CPR>
+__device__ __forceinline__ int swz(int row) {
+  if constexpr (CPR >= 16) return row & 15;
+  else if constexpr (CPR == 8) return ((row >> 1) & 3) << 1;
+  else return ((row >> 3) & 1) << 1;
+}
+
+// MFMA operand fragment: rows row0 + (lane & 15), 16-B chunk c0 + (lane >> 4) of a swizzled image
+template <int CPR>
+__device__ __forceinline__ bf16x8 row_frag(const bf16* img, int row0, int c0, int lane) {
+  const int row = row0 + (lane & 15), c = (c0 + (lane >> 4)) ^ swz<CPR>(row);
+  return *reinterpret_cast<const bf16x8*>(img + row * (CPR * 8) + c * 8);
+}
+
+__device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void comb(float& mx, float& sm, float m2, float s2) {
+  const float mm = fmaxf(mx, m2);
+  sm = (mm == -__builtin_inff()) ? 0.f : sm * __expf(mx - mm) + s2 * __expf(m2 - mm);
+  mx = mm;
+}
+
+template <int DK, int BV, bool BWD>
+__global__ __launch_bounds__(NTH, 1) void vhead_kernel(Args a) {
+  KStampBegin stamp_b_(a.ks);
+  KStampEnd stamp_e_(a.ks);
+  using C = L<DK, BV, BWD>;
+  constexpr int BK = C::BK, FV = C::FV;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* Et = reinterpret_cast<bf16*>(smem);           // E tile [BV][LDE]
+  bf16* Hs = Et + C::E_ELEMS;                         // 2 h stages [BR][LDH]
+  bf16* Ds = Hs + 2 * C::H_ELEMS;                     // bwd: dlogits [BR][LDD]
+  int64_t* labs = reinterpret_cast<int64_t*>(Ds + C::D_ELEMS);
+  float* lses = reinterpret_cast<float*>(labs + BR);
+  float* red = lses + BR;                             // fwd: [4 quarters][BR][2]
+
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, cl = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), wm = wave >> 1, wn = wave & 1;
+  const int v0w = wm * (BV / 4);
+  const int64_t Rl = a.rows_dev ? min(a.R, (int64_t)*a.rows_dev) : a.R;
+  const int nmt = (int)((Rl + BR - 1) / BR);
+  if (nmt == 0) return;
+  const int NIT = nmt * C::NKS;
+
+  float sc = 0.f;
+  if constexpr (BWD) sc = (a.dloss ? *a.dloss : 1.f) / *a.count;
+
+  // h stage `it` (row tile it / NKS, k stage it % NKS) -> register slot (a ring of PF stages in flight, so
+  // each stage's L2 round trip hides under PF - 1 stages of MFMAs); rows >= Rl read as zero
+  constexpr int PF = C::PF;
+  bf16x8 hr[PF][C::HPT];
+  auto h_load = [&](auto slot, int it) {
+    constexpr int sl = decltype(slot)::value;
+    const int mt = it / C::NKS, ks = it - mt * C::NKS;
+#pragma unroll
+    for (int c = 0; c < C::HPT; ++c) {
+      const int ch = tid + NTH * c, r = ch / (BK / 8), k8 = (ch % (BK / 8)) * 8;
+      const int64_t row = (int64_t)mt * BR + r;
+      const int64_t rc = row < Rl ? row : Rl - 1;
+      u4 v = *reinterpret_cast<const u4*>(a.h + rc * a.ldh + ks * BK + k8);
+      v &= (row < Rl ? 0xffffffffu : 0u);
+      hr[sl][c] = __builtin_bit_cast(bf16x8, v);
+    }
+  };
+  auto h_store = [&](auto slot, int buf) {
+    constexpr int sl = decltype(slot)::value;
+#pragma unroll
+    for (int c = 0; c < C::HPT; ++c) {
+      const int ch = tid + NTH * c, r = ch / (BK / 8), k8 = (ch % (BK / 8)) * 8;
+      *reinterpret_cast<bf16x8*>(Hs + buf * C::H_ELEMS + r * C::LDH + (((k8 >> 3) ^ swz<BK / 8>(r)) << 3)) =
+          hr[sl][c];
+    }
+  };
+  // row metadata of row tile mt -> LDS (labels; lse for the backward)
+  auto meta_store = [&](int mt) {
+    if (tid < BR) {
+      const int64_t row = (int64_t)mt * BR + tid;
+      labs[tid] = row < Rl ? a.labels[row] : 0;
+      if constexpr (BWD) lses[tid] = row < Rl ? a.lse[row] : 0.f;
+    }
+  };
+
+  for (int64_t vt = blockIdx.x; vt * BV < a.V1; vt += gridDim.x) {
+    const int64_t n0 = vt * BV;
+    float bia[FV][4];
+#pragma unroll
+    for (int i = 0; i < FV; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t v = n0 + v0w + 16 * i + 4 * g + r;
+        bia[i][r] = (a.bias && v < a.V1) ? a.bias[v] : 0.f;
+      }
+    // prologue: E tile (stationary for all row tiles), h stage (0, 0), row tile 0's metadata
+    __syncthreads();                    // the previous vocabulary tile's readers are done
+    constexpr int EB = C::EPT < 8 ? C::EPT : 8;     // chunks in flight per batch
+#pragma unroll
+    for (int c0 = 0; c0 < C::EPT; c0 += EB) {
+      u4 ex[EB];
+#pragma unroll
+      for (int c = 0; c < EB; ++c) {
+        const int ch = tid + NTH * (c0 + c), r = ch / (DK / 8), k8 = (ch % (DK / 8)) * 8;
+        const int64_t v = n0 + r;
+        const int64_t vc = v < a.V1 ? v : a.V1 - 1;
+        ex[c] = *reinterpret_cast<const u4*>(a.E + vc * a.lde + k8);
+        ex[c] &= (v < a.V1 ? 0xffffffffu : 0u);
+      }
+#pragma unroll
+      for (int c = 0; c < EB; ++c) {
+        const int ch = tid + NTH * (c0 + c), r = ch / (DK / 8), k8 = (ch % (DK / 8)) * 8;
+        *reinterpret_cast<u4*>(Et + r * C::LDE + (((k8 >> 3) ^ swz<DK / 8>(r)) << 3)) = ex[c];
+      }
+    }
+    h_load(std::integral_constant<int, 0>{}, 0);
+    if (1 < NIT) h_load(std::integral_constant<int, 1 % PF>{}, 1);
+    if (2 < NIT) h_load(std::integral_constant<int, 2 % PF>{}, 2);
+    static_assert(PF == 3, "prologue loads PF - 1 stages ahead");
+    h_store(std::integral_constant<int, 0>{}, 0);
+    meta_store(0);
+    __syncthreads();
+
+    f32x4 acc[FV][4];
+    // iteration `it` (register slot u = it % PF, a compile-time constant in the unrolled ring): MFMAs on LDS
+    // stage it & 1; stage it + 1 (slot (u + 1) % PF) -> the other LDS buffer; stage it + PF -> slot u
+    auto body = [&](int it, auto U) {
+      constexpr int u = decltype(U)::value;
+      const int mt = it / C::NKS, ks = it - mt * C::NKS;
+      if (ks == 0) {
+#pragma unroll
+        for (int i = 0; i < FV; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+      const bool more = it + 1 < NIT;
+      const bf16* H = Hs + (it & 1) * C::H_ELEMS;
+#pragma unroll
+      for (int s = 0; s < BK / 32; ++s) {
+        bf16x8 fa[FV], fb[4];
+#pragma unroll
+        for (int i = 0; i < FV; ++i) fa[i] = row_frag<DK / 8>(Et, v0w + 16 * i, (ks * BK + 32 * s) / 8, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb[j] = row_frag<BK / 8>(H, wn * 64 + 16 * j, 4 * s, lane);
+#pragma unroll
+        for (int i = 0; i < FV; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma(fa[i], fb[j], acc[i][j]);
+      }
+      if (more) h_store(std::integral_constant<int, (u + 1) % PF>{}, (it + 1) & 1);
+      if (it + PF < NIT) h_load(std::integral_constant<int, u>{}, it + PF);
+      if (ks != C::NKS - 1) {
+        __syncthreads();
+        return;
+      }
+
+      // ---- row tile mt complete: acc[i][j][r] = S^T[vocab v0w+16i+4g+r][row wn*64+16j+cl] (no bias yet)
+      const int64_t m0 = (int64_t)mt * BR;
+      // vocabulary entries of this lane's accumulator rows are base + 16 i + r, base = n0 + v0w + 4g; only the
+      // last tile is ragged (lim < 16 FV): masking there only, as selects
+      const int lim = (int)min((int64_t)BV, a.V1 - n0) - v0w - 4 * g;
+      const bool ragged = n0 + BV > a.V1;
+      if constexpr (!BWD) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int rl = wn * 64 + 16 * j + cl;
+          float mx = -__builtin_inff();
+#pragma unroll
+          for (int i = 0; i < FV; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float x = acc[i][j][r] + bia[i][r];
+              if (ragged) x = 16 * i + r < lim ? x : -__builtin_inff();
+              acc[i][j][r] = x;
+              mx = fmaxf(mx, x);
+            }
+          float sm = 0.f;
+          const float mxl = mx * 1.4426950408889634f;
+#pragma unroll
+          for (int i = 0; i < FV; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)     // e^(x - mx) = 2^(x log2e - mx log2e); masked: 2^-inf = 0
+              sm += __builtin_amdgcn_exp2f(__builtin_fmaf(acc[i][j][r], 1.4426950408889634f, -mxl));
+          if (mx == -__builtin_inff()) sm = 0.f;
+#pragma unroll
+          for (int o = 16; o < 64; o <<= 1) comb(mx, sm, __shfl_xor(mx, o, 64), __shfl_xor(sm, o, 64));
+          if (g == 0) {
+            red[(wm * BR + rl) * 2 + 0] = mx;
+            red[(wm * BR + rl) * 2 + 1] = sm;
+          }
+        }
+        __syncthreads();
+        // per 128-column partial tile: quarters {0,1} (BV = 256) or all four (BV = 128)
+        constexpr int QPT = 512 / BV;          // quarters per 128-column partial tile
+        if (tid < BR * (4 / QPT) && m0 + (tid % BR) < Rl) {
+          const int rl = tid % BR, half = tid / BR;
+          float mx = red[((half * QPT) * BR + rl) * 2], sm = red[((half * QPT) * BR + rl) * 2 + 1];
+#pragma unroll
+          for (int q = 1; q < QPT; ++q)
+            comb(mx, sm, red[((half * QPT + q) * BR + rl) * 2], red[((half * QPT + q) * BR + rl) * 2 + 1]);
+          const int64_t pt = (n0 >> 7) + half;
+          if (pt < a.ntn) {
+            a.part[((m0 + rl) * a.ntn + pt) * 2 + 0] = mx;
+            a.part[((m0 + rl) * a.ntn + pt) * 2 + 1] = sm;
+          }
+        }
+      } else {
+        // dlogits of this tile -> Ds [row][vocab] (bf16, 8-byte writes of 4 vocabulary entries) -> global
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int rl = wn * 64 + 16 * j + cl;
+          const int64_t lb = labs[rl];
+          const bool live = m0 + rl < Rl && lb != 0;
+          const float Lr = lses[rl];
+          const float scr = live ? sc : 0.f;
+          const int off = (int)(lb - (n0 + v0w + 4 * g));
+#pragma unroll
+          for (int i = 0; i < FV; ++i) {
+            bf4 o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float x = acc[i][j][r] + bia[i][r];
+              float gv = (__expf(x - Lr) - (off == 16 * i + r ? 1.f : 0.f)) * scr;
+              if (ragged) gv = 16 * i + r < lim ? gv : 0.f;
+              o[r] = (bf16)gv;
+            }
+            *reinterpret_cast<bf4*>(Ds + rl * C::LDD + v0w + 16 * i + 4 * g) = o;
+          }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < BR * BV / 8 / NTH; ++c) {
+          const int ch = tid + NTH * c, r = ch / (BV / 8), c8 = (ch % (BV / 8)) * 8;
+          const int64_t row = m0 + r, v = n0 + c8;
+          if (row < Rl) {
+            const bf16x8 x = *reinterpret_cast<const bf16x8*>(Ds + r * C::LDD + c8);
+            bf16* dst = a.dl + row * a.lddl + v;
+            if (v + 8 <= a.V1) {
+              *reinterpret_cast<bf16x8*>(dst) = x;
+            } else {
+              for (int e = 0; e < 8; ++e)
+                if (v + e < a.V1) dst[e] = x[e];
+            }
+          }
+        }
+      }
+      __syncthreads();                         // labs / red / Ds readers of this row tile are done
+      if (mt + 1 < nmt) meta_store(mt + 1);    // (visible after the next stage's barrier)
+      if constexpr (C::NKS == 1) __syncthreads();
+    };
+    for (int it0 = 0; it0 < NIT; it0 += PF) {
+      body(it0, std::integral_constant<int, 0>{});
+      if (it0 + 1 < NIT) body(it0 + 1, std::integral_constant<int, 1>{});
+      if (it0 + 2 < NIT) body(it0 + 2, std::integral_constant<int, 2>{});
+    }
+  }
+}
+
+template <int DK, int BV, bool BWD>
+hipError_t launch(Args& a, hipStream_t s) {
+  using C = L<DK, BV, BWD>;
+  static_assert(C::LDS <= 163840, "LDS budget");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)vhead_kernel<DK, BV, BWD>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              C::LDS);
+    attr = true;
+  }
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int64_t grid = std::min<int64_t>(cdiv(a.V1, BV), (int64_t)cus);
+  hipLaunchKernelGGL((vhead_kernel<DK, BV, BWD>), dim3((unsigned)grid), dim3(NTH), C::LDS, s, a);
+  return hipGetLastError();
+}
+
+// fwd: 256-entry vocabulary tiles (E tile 132 KB at d = 256); bwd: 128 (room for the dlogits staging tile)
+template <bool BWD>
+hipError_t dispatch(Args& a, int64_t d, hipStream_t s) {
+  constexpr int BV = BWD ? 128 : 256;
+  if (d == 256) return launch<256, BV, BWD>(a, s);
+  if (d == 128) return launch<128, BV, BWD>(a, s);
+  return launch<64, BV, BWD>(a, s);
+}
+
+}  // namespace vh
+
+// partials -> lse / loss (vocab_ce.hip); with h != null the label logits are formed there (<h, E[label]> + b)
+hipError_t vce_finish(const float* part, int64_t ntn, int64_t R, const int64_t* labels, const float* tgt,
+                      const int* rows_dev, float* lse, float* rowp, const float* count_override, float* out,
+                      hipStream_t s, const void* h, int64_t ldh, const void* E, int64_t lde, const float* bias,
+                      int64_t d);
+
+extern "C" {
+
+int rs_vocab_head_supported(int64_t d) { return d == 64 || d == 128 || d == 256; }
+
+int rs_vocab_head_fwd(int64_t R, int64_t V1, int64_t d, const void* h, int64_t ldh, const void* E, int64_t lde,
+                      const float* bias, const int64_t* labels, const int* rows_dev, const float* count_override,
+                      float* ws, float* out, void* stream) {
+  if (!rs_vocab_head_supported(d) || R <= 0 || V1 <= 0 || ldh % 8 || lde % 8 || ((uintptr_t)h | (uintptr_t)E) % 16 ||
+      !labels || !ws || !out)
+    return RS_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  vh::Args a{};
+  a.R = R; a.V1 = V1; a.ntn = cdiv(V1, 128);
+  a.h = (const __bf16*)h; a.ldh = ldh; a.E = (const __bf16*)E; a.lde = lde;
+  a.bias = bias; a.labels = labels; a.rows_dev = rows_dev;
+  // ws layout = vocab_ce.hip's: part [R][ntn][2] | tgt [R] | lse [R] | rowp [R][2]
+  a.part = ws;
+  a.tgt = ws + R * a.ntn * 2;
+  a.ks = kstamp_next(RS_STAMP_VOCAB_CE_FWD);
+  hipError_t e = vh::dispatch<false>(a, d, s);
+  if (e != hipSuccess) return (int)e;
+  return (int)vce_finish(a.part, a.ntn, R, labels, a.tgt, rows_dev, a.tgt + R, a.tgt + 2 * R, count_override, out, s,
+                         h, ldh, E, lde, bias, d);
+}
+
+int rs_vocab_head_bwd(int64_t R, int64_t V1, int64_t d, const void* h, int64_t ldh, const void* E, int64_t lde,
+                      const float* bias, const int64_t* labels, const int* rows_dev, const float* count,
+                      const float* dloss, const float* ws, void* dlogits, int64_t lddl, void* stream) {
+  if (!rs_vocab_head_supported(d) || R <= 0 || V1 <= 0 || ldh % 8 || lde % 8 || lddl % 8 ||
+      ((uintptr_t)h | (uintptr_t)E | (uintptr_t)dlogits) % 16 || !labels || !ws || !count || !dlogits)
+    return RS_ERR_ARG;
+  vh::Args a{};
+  a.R = R; a.V1 = V1; a.ntn = cdiv(V1, 128);
+  a.h = (const __bf16*)h; a.ldh = ldh; a.E = (const __bf16*)E; a.lde = lde;
+  a.bias = bias; a.labels = labels; a.rows_dev = rows_dev;
+  a.lse = ws + R * a.ntn * 2 + R;
+  a.count = count; a.dloss = dloss;
+  a.dl = (__bf16*)dlogits; a.lddl = lddl;
+  return (int)vh::dispatch<true>(a, d, (hipStream_t)stream);
+}
+
+}  // extern "C"

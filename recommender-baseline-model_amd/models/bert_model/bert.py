@@ -404,7 +404,15 @@ class BERTEngine:
         hl = self.ws.get("hl", (cap, d), self.dt)
         lab = self.ws.get("lab", (cap,), torch.int64)
         ops.gather_rows(xL, idx, cnt, cap, hl, labels, lab)
-        if self.dt == torch.bfloat16 and os.environ.get("RS_BERT_UNFUSED_CE", "0") != "1":
+        head = os.environ.get("RS_BERT_VOCAB_HEAD", "tile")
+        if self.dt == torch.bfloat16 and head == "tile" and ops.vocab_head_supported(d):
+            # vocabulary-tile-stationary kernels (vocab_head.hip): logits never materialised
+            wce = self.ws.get("vce", (ops.vocab_ce_ws_numel(cap, self.V1),), torch.float32)
+            ops.vocab_head_fwd(hl, self.W("out.weight"), self.Wf("out.bias"), lab, wce, loss_out, rows_dev=cnt)
+            count = global_count(loss_out[1:2])
+            dl = self.ws.get("dlogits", (cap, self.V1p), self.dt)[:, :self.V1]
+            ops.vocab_head_bwd(hl, self.W("out.weight"), self.Wf("out.bias"), lab, wce, count, dl, rows_dev=cnt)
+        elif self.dt == torch.bfloat16 and head != "materialised":
             # logits never materialised: GEMM + online-softmax partials, then GEMM + dlogits (vocab_ce.hip)
             wce = self.ws.get("vce", (ops.vocab_ce_ws_numel(cap, self.V1),), torch.float32)
             ops.vocab_ce_fwd(hl, self.W("out.weight"), self.Wf("out.bias"), lab, wce, loss_out, rows_dev=cnt)

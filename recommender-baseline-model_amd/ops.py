@@ -294,6 +294,26 @@ def vocab_ce_fwd(h, E, bias, labels, ws, out, rows_dev=None, count_override=None
          ptr(count_override), ptr(ws), ptr(out), stream())
 
 
+def vocab_head_supported(d):
+    return bool(_lib.lib().rs_vocab_head_supported(d))
+
+
+def vocab_head_fwd(h, E, bias, labels, ws, out, rows_dev=None, count_override=None):
+    """vocab_ce_fwd's result from the vocabulary-tile-stationary kernel (rs_vocab_head_fwd)."""
+    R, d = h.shape
+    V1 = E.shape[0]
+    call("rs_vocab_head_fwd", R, V1, d, ptr(h), ld(h), ptr(E), ld(E), ptr(bias), ptr(labels), ptr(rows_dev),
+         ptr(count_override), ptr(ws), ptr(out), stream())
+
+
+def vocab_head_bwd(h, E, bias, labels, ws, count, dl, rows_dev=None, dloss=None):
+    """vocab_ce_bwd's dlogits from the vocabulary-tile-stationary kernel (rs_vocab_head_bwd)."""
+    R, d = h.shape
+    V1 = E.shape[0]
+    call("rs_vocab_head_bwd", R, V1, d, ptr(h), ld(h), ptr(E), ld(E), ptr(bias), ptr(labels), ptr(rows_dev),
+         ptr(count), ptr(dloss), ptr(ws), ptr(dl), ld(dl), stream())
+
+
 def vocab_ce_bwd(h, E, bias, labels, ws, count, dl, rows_dev=None, dloss=None):
     """dl [R, V1] bf16 = (softmax(h E^T + bias) - onehot(labels)) * dloss / count."""
     R, d = h.shape

@@ -171,27 +171,31 @@ def test_bert_grouped_wgrad_matches_per_weight(monkeypatch):
 
 
 @pytest.mark.gpu
-def test_bert_fused_vocab_ce_matches_materialised(monkeypatch):
-    """bf16: the vocabulary head without materialised logits (rs_vocab_ce_fwd/bwd) gives the loss and
-    gradients of the materialised sequence (rs_gemm fp32 logits + rs_ce_fwd + rs_ce_bwd), at the cfg3
-    vocabulary (26,745 classes: a ragged last column tile)."""
+@pytest.mark.parametrize("head,d,B,cap", [("gemm", 64, 16, 256), ("tile", 64, 16, 256), ("tile", 256, 40, 512),
+                                          ("tile", 128, 3, 128)])
+def test_bert_fused_vocab_ce_matches_materialised(monkeypatch, head, d, B, cap):
+    """bf16: the vocabulary head without materialised logits -- rs_vocab_ce_fwd/bwd (GEMM epilogues, 'gemm') or
+    rs_vocab_head_fwd/bwd (vocabulary-tile-stationary, dE/db in the dlogits pass, 'tile') -- gives the loss and
+    gradients of the materialised sequence (rs_gemm fp32 logits + rs_ce_fwd + rs_ce_bwd + rs_linear_wgrad), at
+    the cfg3 vocabulary (26,745 classes: a ragged last column tile) and ragged / partial row tiles."""
     import rbm_amd  # noqa: F401
     import rbm_amd.data as synth
     from rbm_amd.models import model_factory
     from rbm_amd.train_step import FusedTrainStep
-    a = argparse.Namespace(model_code="bert", num_items=26744, max_len=50, device="cuda", bert_hidden_units=64,
+    a = argparse.Namespace(model_code="bert", num_items=26744, max_len=50, device="cuda", bert_hidden_units=d,
                            bert_num_blocks=1, bert_num_heads=2, bert_dropout=0.0, bert_hidden_dropout=0.0,
                            bert_mask_prob=0.2, model_init_seed=1, rs_dtype="bf16")
     rng = np.random.default_rng(1)
-    tok, lab = (torch.from_numpy(t).cuda() for t in synth.bert_batch(rng, 16, 50, 26744, mask_prob=0.2))
+    tok, lab = (torch.from_numpy(t).cuda() for t in synth.bert_batch(rng, B, 50, 26744, mask_prob=0.2))
+    assert int((lab != 0).sum()) <= cap
     out = []
-    for unfused in ("1", "0"):
-        monkeypatch.setenv("RS_BERT_UNFUSED_CE", unfused)
+    for h in ("materialised", head):
+        monkeypatch.setenv("RS_BERT_VOCAB_HEAD", h)
         torch.manual_seed(0)
         m = model_factory(a)
-        tr = FusedTrainStep(m, lr=0.0, max_labelled=256)
+        tr = FusedTrainStep(m, lr=0.0, max_labelled=cap)
         tr.flat.grad.zero_()
-        tr.engine.train_loss_and_backward(tok, lab, tr.loss_out, tr._divisor, tr.flat.grad, max_labelled=256)
+        tr.engine.train_loss_and_backward(tok, lab, tr.loss_out, tr._divisor, tr.flat.grad, max_labelled=cap)
         torch.cuda.synchronize()
         out.append((tr.loss_out[:3].cpu().numpy().copy(),
                     {k: tr.flat.view(k, tr.flat.grad).cpu().numpy().copy() for k, _ in m.named_parameters()}))
