@@ -10,6 +10,14 @@ the global gradient sum, loss sum and count; the optimizer divides by the count
 (rs_adam_prepare's grad_divisor).  Averaging per-rank means instead is wrong whenever ranks see
 different valid counts.
 
+Overlap with backward: the flat buffer is split into buckets that become final at
+different points of the backward -- SAS: the dense block / LayerNorm weights (+ aux) after the grouped
+weight-gradient launch, then the item / positional tables; BERT: the vocabulary head (out.weight,
+out.bias, + aux) right after its weight gradient, then everything else.  BucketedExchange starts each
+bucket's all-reduce (async, on the backend's stream, ordered after the work already issued on the
+current stream) as soon as it is final, so it overlaps the rest of the backward; finish() makes the
+current stream wait for all of them before the optimizer.
+
 These helpers only move tensors; they work for any device / backend (gloo on CPU in the tests).
 """
 import torch
@@ -40,3 +48,33 @@ def allreduce_grads(flat_grad, group=None, bucket_numel=None):
 def global_mean_loss(aux):
     """Loss of the global batch from an all-reduced aux tail (a device scalar, no sync)."""
     return aux[LOSS_SUM:LOSS_SUM + 1] / aux[COUNT:COUNT + 1]
+
+
+class BucketedExchange:
+    """All-reduce(SUM) of a flat gradient buffer bucket by bucket, each launched when it is final.
+
+    buckets: {tag: (lo, hi)} disjoint slices covering the buffer.  launch(tag) issues that slice's
+    all-reduce asynchronously; finish() waits for every launched one (on the current stream for
+    NCCL/RCCL: no host block) and checks that every bucket went out exactly once."""
+
+    def __init__(self, flat_grad, buckets, group=None):
+        self.flat_grad = flat_grad
+        self.buckets = dict(buckets)
+        self.group = group
+        spans = sorted(self.buckets.values())
+        assert spans[0][0] == 0 and spans[-1][1] == flat_grad.numel(), "buckets must cover the buffer"
+        assert all(a[1] == b[0] for a, b in zip(spans, spans[1:])), "buckets must be disjoint and contiguous"
+        self.works = []
+        self.sent = []
+
+    def launch(self, tag):
+        lo, hi = self.buckets[tag]
+        self.sent.append(tag)
+        self.works.append(dist.all_reduce(self.flat_grad[lo:hi], group=self.group, async_op=True))
+
+    def finish(self):
+        assert sorted(self.sent) == sorted(self.buckets), (self.sent, list(self.buckets))
+        for w in self.works:
+            w.wait()
+        self.works, self.sent = [], []
+        return self.flat_grad

@@ -387,7 +387,7 @@ class BERTEngine:
         return dx
 
     # ---- fused training loss (labelled rows only) -------------------------------------
-    def train_loss_and_backward(self, tokens, labels, loss_out, global_count, grad, max_labelled=None):
+    def train_loss_and_backward(self, tokens, labels, loss_out, global_count, grad, max_labelled=None, split=None):
         """Forward + CE(ignore_index=0) + backward of one batch.  loss_out[0] = loss sum, [1] = local
         labelled count, [2] = local mean; ``global_count(local)`` returns the divisor (DP)."""
         side = self._token_index(tokens) if self._det_table() else None
@@ -433,6 +433,12 @@ class BERTEngine:
         slab = self.ws.get("slab_out", (ops.wgrad_slab_numel(cap, self.V1, d),), torch.float32)
         ops.linear_wgrad(dl, hl, self.flat.view("out.weight", grad), slab, db=self.flat.view("out.bias", grad),
                          rows_dev=cnt)
+        if split is not None:
+            # join the side stream's token index here: a captured graph segment must not end with forked work
+            if s.get("side") is not None and s["side"][0] is not None:
+                torch.cuda.current_stream().wait_event(s["side"][0])
+                s["side"] = (None, s["side"][1])
+            split("out")                # the vocabulary head's gradient is final (data-parallel overlap)
         # contraction over the whole vocabulary with few rows: split-K into slabs, then ONE pass that sums
         # the live rows' partials in a fixed order, casts and scatters them back to the token rows
         sk = int(max(1, min(64, -(-self.V1 // 2048))))

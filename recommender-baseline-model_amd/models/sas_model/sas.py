@@ -261,7 +261,7 @@ class SASEngine:
         return ops.sas_block_fused_ok(self.d, self.dt)
 
     # ---- backward ------------------------------------------------------------------
-    def backward(self, s, dpl, dnl, grad, loss_out=None, divisor=None):
+    def backward(self, s, dpl, dnl, grad, loss_out=None, divisor=None, split=None):
         """Accumulates every parameter gradient into the flat fp32 buffer ``grad``.  dpl/dnl: the
         logits' gradients; None (fused path only) = form the BCE gradient of the forward's logits here,
         writing the loss statistics to loss_out (divisor: device count, None = this batch's)."""
@@ -293,6 +293,8 @@ class SASEngine:
             segs = ops.ln_partial_segments(lnh, M, d, G("last_layernorm.weight"), G("last_layernorm.bias"))
             torch.cuda.current_stream().wait_event(ev)
             dx = self._backward_blocks_fused(s, dx, grad, segs)
+            if split is not None:
+                split("dense")          # every block / LayerNorm gradient is final (data-parallel overlap)
             ops.embed_bwd(0, ids, T, dx, math.sqrt(d), p, self.salt["emb"], sb, None, G("pos_emb.weight"))
             ops.item_grad(iws, 3, M, dx, math.sqrt(d), p, self.salt["emb"], sb, s["f"], dpl, dnl,
                           G("item_emb.weight"))

@@ -51,11 +51,13 @@ class FusedAdam:
 
 class FusedTrainStep:
     def __init__(self, model, lr=1e-3, weight_decay=0.0, process_group=None, dp=None, max_labelled=None,
-                 bucket_numel=None):
+                 bucket_numel=None, overlap=None):
         """model: rbm_amd SASModel or BERTModel on a CUDA device.
         dp: data-parallel mode (default: torch.distributed initialised with world size > 1).
         max_labelled (BERT): upper bound on labelled rows per batch (sizes the compacted
-        vocabulary-logit buffers; default B*T).  bucket_numel: all-reduce bucket size (floats)."""
+        vocabulary-logit buffers; default B*T).  overlap (DP, default on unless bucket_numel is given): each
+        gradient bucket's all-reduce starts as soon as the backward has finished it (dp.BucketedExchange);
+        bucket_numel: otherwise ONE all-reduce after the backward, in buckets of that many floats."""
         self.model = model
         self.kind = model.code()
         self.engine = model.sas.engine() if self.kind == "sas" else model.engine()
@@ -67,6 +69,7 @@ class FusedTrainStep:
         self.pg = process_group
         self.dp = dpx.world() > 1 if dp is None else bool(dp)
         self.bucket_numel = bucket_numel
+        self.overlap = self.dp and (bucket_numel is None if overlap is None else bool(overlap))
         self.max_labelled = max_labelled
         dev = self.flat.device
         self.loss_out = torch.zeros(4, dtype=torch.float32, device=dev)
@@ -75,6 +78,7 @@ class FusedTrainStep:
         self.loss_val = torch.zeros(1, dtype=torch.float32, device=dev)
         self.graphs = None
         self.static = None
+        self.exchange = dpx.BucketedExchange(self.flat.grad, self._buckets(), self.pg) if self.overlap else None
 
     # ---------------------------------------------------------------- pieces
     def _divisor(self, local_count):
@@ -82,15 +86,39 @@ class FusedTrainStep:
         (DP: unnormalised; the optimizer divides by the all-reduced global count)."""
         return self.one if self.dp else local_count
 
-    def _compute(self, *batch):
+    def _buckets(self):
+        """Data-parallel all-reduce buckets, {tag: (lo, hi)} of the flat gradient buffer (+ aux tail): the one
+        final first (tag named by the engine's split call) and "final" (the rest, after the backward)."""
+        f = self.flat
+        if self.kind == "sas" and self.engine.fused_head:
+            # item_emb, pos_emb lead the buffer (reference parameter order); the block weights follow
+            cut = max(f.offsets["item_emb.weight"], f.offsets["pos_emb.weight"]) + \
+                -(-f.view("pos_emb.weight").numel() // 64) * 64
+            assert cut == min(o for n, o in f.offsets.items() if n not in ("item_emb.weight", "pos_emb.weight"))
+            return {"final": (0, cut), "dense": (cut, f.grad.numel())}
+        if self.kind == "bert":
+            cut = f.offsets["out.weight"]
+            assert f.offsets["out.bias"] > cut and all(o < cut for n, o in f.offsets.items()
+                                                       if n not in ("out.weight", "out.bias"))
+            return {"final": (0, cut), "out": (cut, f.grad.numel())}
+        return {"final": (0, f.grad.numel())}
+
+    def _compute(self, *batch, split=None):
+        """Forward + loss + backward into the flat gradient.  split(tag): called by the engine when the bucket
+        `tag` is final (DP only: the aux tail -- loss sum, count -- is written before it)."""
         eng = self.engine
+        sp = None
+        if split is not None:
+            def sp(tag):
+                self.flat.aux[dpx.LOSS_SUM:dpx.COUNT + 1].copy_(self.loss_out[0:2])
+                split(tag)
         if self.kind == "sas":
             seq, pos, neg = batch
             pl, nl, saved = eng.forward(seq, pos, neg, True, clone_seed=False)
             if eng.fused_head:
                 # BCE forward/backward inside the fused head kernels (head.hip)
                 eng.backward(saved, None, None, self.flat.grad, loss_out=self.loss_out,
-                             divisor=self.one if self.dp else None)
+                             divisor=self.one if self.dp else None, split=sp)
                 if self.dp:
                     self.flat.aux[dpx.LOSS_SUM:dpx.COUNT + 1].copy_(self.loss_out[0:2])
                 return
@@ -103,7 +131,7 @@ class FusedTrainStep:
         else:
             tokens, labels = batch
             eng.train_loss_and_backward(tokens, labels, self.loss_out, self._divisor, self.flat.grad,
-                                        max_labelled=self.max_labelled)
+                                        max_labelled=self.max_labelled, split=sp)
         if self.dp:
             self.flat.aux[dpx.LOSS_SUM:dpx.COUNT + 1].copy_(self.loss_out[0:2])
 
@@ -124,8 +152,13 @@ class FusedTrainStep:
     def step(self, *batch):
         """batch: SAS (seq, pos, neg) / BERT (tokens, labels) int64 device tensors.  Returns the
         device loss (the global batch's mean loss, as the reference's calculate_loss)."""
-        self._compute(*batch)
-        self._exchange()
+        if self.overlap:
+            self._compute(*batch, split=self.exchange.launch)
+            self.exchange.launch("final")
+            self.exchange.finish()
+        else:
+            self._compute(*batch)
+            self._exchange()
         self._update()
         return self.loss_val if self.dp else self.loss_out[2:3]
 
@@ -216,32 +249,71 @@ class FusedTrainStep:
                 self.step(*self.static)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        self._capture_graphs(lambda: self._compute(*self.static), stamps)
+        self._capture_graphs(lambda split=None: self._compute(*self.static, split=split), stamps)
         return self
 
     def _capture_graphs(self, compute, stamps=None):
-        """The compute graph (+ the optimizer in the same graph on one device; a separate optimizer graph after
-        the eager RCCL all-reduce under DP)."""
-        g = torch.cuda.CUDAGraph()
+        """The compute graph (+ the optimizer in the same graph on one device).  DP: the compute graph is cut at
+        every bucket the backward finishes (overlap: segments replayed with that bucket's all-reduce launched
+        between them) or ends after the backward, and the optimizer is a separate graph after the exchange."""
         if stamps is not None:
             ops.kernel_stamps(stamps[0], self.opt.state, stamps[1])
         try:
-            with torch.cuda.graph(g):
-                compute()
-                if not self.dp:
-                    self._update()
+            if self.overlap:
+                self.g_segments = self._capture_segments(compute)
+                self.g_compute = None
+            else:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    compute()
+                    if not self.dp:
+                        self._update()
+                self.g_compute = g
+                self.g_segments = None
         finally:
             if stamps is not None:
                 ops.kernel_stamps(None, None)
-        self.g_compute = g
         self.g_update = None
         if self.dp:
             self.g_update = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g_update):
                 self._update()
-        self.graphs = (g, self.g_update) if self.dp else (g,)
+        segs = [g for g, _ in self.g_segments] if self.g_segments else [self.g_compute]
+        self.graphs = tuple(segs) + ((self.g_update,) if self.dp else ())
+
+    def _capture_segments(self, compute):
+        """Capture compute(split) as consecutive graphs, a new one begun at every split(tag): [(graph, tag)],
+        the last tagged "final".  All segments share one memory pool and one capture stream."""
+        torch.cuda.synchronize()
+        pool = torch.cuda.graph_pool_handle()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        segs, cur = [], [torch.cuda.CUDAGraph()]
+        with torch.cuda.stream(s):
+            cur[0].capture_begin(pool=pool)
+
+            def split(tag):
+                cur[0].capture_end()
+                segs.append((cur[0], tag))
+                cur[0] = torch.cuda.CUDAGraph()
+                cur[0].capture_begin(pool=pool)
+            try:
+                compute(split)
+            finally:
+                cur[0].capture_end()
+            segs.append((cur[0], "final"))
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        return segs
 
     def _replay_graphs(self):
+        if self.overlap:
+            for g, tag in self.g_segments:
+                g.replay()
+                self.exchange.launch(tag)     # RCCL all-reduce of the bucket, overlapping the next segment
+            self.exchange.finish()
+            self.g_update.replay()
+            return self.loss_val
         self.g_compute.replay()
         if self.dp:
             self._exchange()            # RCCL all-reduce, eager, on the current stream
@@ -269,9 +341,9 @@ class FusedTrainStep:
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
 
-        def compute():
+        def compute(split=None):
             sampler.sample_into(*self.static)
-            self._compute(*self.static)
+            self._compute(*self.static, split=split)
         self._capture_graphs(compute, stamps)
         return self
 

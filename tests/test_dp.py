@@ -94,6 +94,48 @@ def test_dp_two_ranks_equal_single_device(kind, bucket, tmp_path):
     assert float((r0["g"] - ref).norm() / ref.norm()) < 1e-12
 
 
+def _bucket_worker(rank, world, port, out_dir):
+    import sys
+    sys.path.insert(0, ROOT)
+    import rbm_amd  # noqa: F401
+    from rbm_amd import dp
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(rank)
+        flat = torch.randn(1000, generator=g)
+        ref = flat.clone()
+        dist.all_reduce(ref)
+        ex = dp.BucketedExchange(flat, {"final": (0, 300), "dense": (300, 1000)})
+        ex.launch("dense")                # launched as soon as final, out of buffer order
+        flat[:300] *= 1.0                 # (the rest of the backward writing the other bucket)
+        ex.launch("final")
+        ex.finish()
+        torch.save({"flat": flat, "ref": ref}, os.path.join(out_dir, f"b{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bucketed_exchange_equals_one_allreduce(tmp_path):
+    """dp.BucketedExchange (the data-parallel step's all-reduce, bucket by bucket as the backward finishes them)
+    sums exactly what one all-reduce of the whole buffer sums, on every rank."""
+    port = _free_port()
+    mp.spawn(_bucket_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        d = torch.load(tmp_path / f"b{r}.pt", weights_only=True)
+        assert torch.equal(d["flat"], d["ref"])
+
+
+def test_bucketed_exchange_rejects_bad_buckets():
+    import sys
+    sys.path.insert(0, ROOT)
+    from rbm_amd import dp
+    with pytest.raises(AssertionError):
+        dp.BucketedExchange(torch.zeros(10), {"a": (0, 4), "b": (5, 10)})     # gap
+    with pytest.raises(AssertionError):
+        dp.BucketedExchange(torch.zeros(10), {"a": (0, 4)})                    # does not cover
+
+
 def test_ranks_have_different_counts():
     """The case the global-count normalisation exists for: per-rank means would be wrong."""
     z = load_golden("sas_mid")

@@ -51,15 +51,21 @@ def _batches(kind, n):
     return out
 
 
+@pytest.mark.parametrize("overlap", [False, True])
 @pytest.mark.parametrize("graph", [False, True])
 @pytest.mark.parametrize("kind", ["sas", "bert"])
-def test_dp_step_equals_single_device_step(nccl_group, kind, graph):
+def test_dp_step_equals_single_device_step(nccl_group, kind, graph, overlap):
+    """overlap: bucket all-reduces launched between graph segments as the backward finishes them
+    (dp.BucketedExchange); else one bucketed all-reduce after the backward."""
     from rbm_amd.train_step import FusedTrainStep
     batches = _batches(kind, 4)
     res = {}
     for dp in (False, True):
         m = _model(kind, 3)
-        tr = FusedTrainStep(m, lr=1e-3, dp=dp, bucket_numel=8192 if dp else None)
+        tr = FusedTrainStep(m, lr=1e-3, dp=dp, bucket_numel=None if (overlap or not dp) else 8192,
+                            overlap=overlap if dp else None)
+        if dp and overlap and kind == "bert":
+            assert len(tr.exchange.buckets) == 2          # vocabulary head first, then the rest
         if graph:
             tr.capture(*batches[0])
             # capture() ran warm-up steps: restart from the same weights for both arms
@@ -74,3 +80,32 @@ def test_dp_step_equals_single_device_step(nccl_group, kind, graph):
     # ~0 (the attention key bias: analytically zero, numerically noise), so the parameters agree to
     # ~1e-5 relative, not to the last bit
     assert rel(p1.numpy(), p0.numpy()) < 3e-4
+
+
+@pytest.mark.parametrize("kind", ["sas", "bert"])
+def test_dp_overlap_bitwise_equals_single_allreduce_bf16(nccl_group, kind):
+    """bf16 fused steps (SAS: the dense-block bucket is cut after the grouped weight gradients): the overlapped,
+    segment-captured DP step gives bit-identical parameters to the one-all-reduce DP step."""
+    import rbm_amd  # noqa: F401
+    from rbm_amd.models import model_factory
+    from rbm_amd.train_step import FusedTrainStep
+    batches = _batches(kind, 3)
+    res = []
+    for overlap in (False, True):
+        torch.manual_seed(5)
+        if kind == "sas":
+            a = argparse.Namespace(model_code="sas", num_items=500, max_len=50, device="cuda", sas_hidden_units=128,
+                                   sas_num_blocks=2, sas_heads=1, sas_dropout=0.1, l2_emb=0.0, rs_dtype="bf16")
+        else:
+            a = argparse.Namespace(model_code="bert", num_items=500, max_len=50, device="cuda", bert_hidden_units=64,
+                                   bert_num_blocks=2, bert_num_heads=2, bert_dropout=0.1, bert_hidden_dropout=0.1,
+                                   bert_mask_prob=0.2, model_init_seed=5, rs_dtype="bf16")
+        m = model_factory(a)
+        tr = FusedTrainStep(m, lr=1e-3, dp=True, overlap=overlap, bucket_numel=None if overlap else 1 << 30)
+        assert len(tr.exchange.buckets) == 2 if overlap else tr.exchange is None
+        tr.capture(*batches[0])
+        losses = [float(tr.replay(*b).item()) for b in batches]
+        torch.cuda.synchronize()
+        res.append((losses, tr.flat.data.detach().cpu().clone()))
+    assert res[0][0] == res[1][0]
+    assert torch.equal(res[0][1], res[1][1])
