@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse the "
+                         "multi-process path with several ranks on one GPU)")
     ap.add_argument("--nbatches", type=int, default=8, help="distinct synthetic batches cycled through")
     ap.add_argument("--sampler", default="host", choices=["host", "device"],
                     help="SAS: 'device' = batches drawn each step by the on-device WarpSampler "
@@ -273,10 +276,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    dev = local % max(1, torch.cuda.device_count())     # one GPU per rank (ranks > GPUs: gloo rehearsal only)
+    torch.cuda.set_device(dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
     global CFG_NAME
     CFG_NAME = args.config
     cfg = dict(CONFIGS[args.config])
