@@ -19,6 +19,8 @@
 //    operand (the transposed image) is read with ds_read_b64_tr_b16;
 //  * softmax statistics per query live on one lane (+2 cross-group shuffles).
 #include "common.h"
+#include <algorithm>
+#include <cstring>
 #include "../../include/recsys_hip.h"
 
 typedef __attribute__((ext_vector_type(4))) __bf16 bf4;
@@ -45,7 +47,17 @@ struct AttnLdsArgs {
   const uint64_t* seed_base;
   int nsplit;
   KStamp ks;                     // backward: dQ kernel stamps begin, dK/dV kernel end
+  // backward work plan (causal): per (split, wave) up to PLAN_I items, 0 = none; unused (use_plan 0) -> one
+  // tile per wave round robin.  Item = valid << 31 | slot << 26 | role << 24 | chunk end << 16 | chunk begin
+  // << 8 | tile; chunks are 32 keys (dQ) / 32 queries (dK/dV); role 0 = whole tile, 1 = upper half (its
+  // partial goes to LDS slot `slot`), 2 = lower half (adds that slot's partial, then writes the tile)
+  int use_plan;
+  uint32_t plan[4][8][4];
 };
+#define PLAN_S 4
+#define PLAN_I 4
+#define DQ_SLOTS 4    // fp32 partial dQ tiles (8 KB each at Dh = 128)
+#define DKV_SLOTS 3   // bf16 partial (dK, dV) tiles (8 KB each at Dh = 128)
 
 #define NEG_INF (-__builtin_inff())
 // 8 waves per workgroup (2 per SIMD): with ~7 tiles per workgroup every tile gets its own wave,
@@ -341,6 +353,7 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_lds_kernel(AttnLdsArgs a) {
   constexpr int LD = Img<DH>::LD, KC = DH / 32, DT = DH / 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   KStampBegin stamp_(a.ks);
+  APROF(4);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4, cl = lane & 15;
   int64_t bh;
   int split;
@@ -355,13 +368,34 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_lds_kernel(AttnLdsArgs a) {
   bf16* Ks = reinterpret_cast<bf16*>(smem);
   bf16* Vs = Ks + rows * LD;
   float* km = reinterpret_cast<float*>(Vs + rows * LD);
+  float* slots = km + rows;                            // plan: fp32 partial dQ tiles [slot][DT*4][64]
+  int* flags = reinterpret_cast<int*>(slots + DQ_SLOTS * DT * 4 * 64);
   const bf16* Qg = a.q + b * a.T * a.ldq + h * DH;
   const bf16* Og = a.o + b * a.T * a.ldo + h * DH;
   const bf16* dOg = a.dout + b * a.T * a.lddo + h * DH;
-  // the first query tile's q, dO, O rows are requested before (and arrive with) the K/V staging
+  // this wave's work items: the plan's (tile, key-chunk range, role), else one whole tile per wave round robin
+  auto item = [&](int it, int& qt, int& cb, int& ce, int& role, int& slot) -> bool {
+    if (a.use_plan) {
+      if (it >= PLAN_I) return false;
+      const uint32_t e = a.plan[split][wave][it];
+      if (!(e >> 31)) return false;
+      qt = e & 255; cb = (e >> 8) & 255; ce = (e >> 16) & 255; role = (e >> 24) & 3; slot = (e >> 26) & 15;
+      return true;
+    }
+    qt = split + (wave + it * NW) * a.nsplit;
+    if (qt >= nq) return false;
+    cb = 0;
+    ce = ((a.mask_kind == 0 ? qt + 1 : nq) + 1) / 2;
+    role = 0; slot = 0;
+    return true;
+  };
+  if (a.use_plan && tid < DQ_SLOTS) flags[tid] = 0;
+  // the first item's q, dO, O rows are requested before (and arrive with) the K/V staging
   bf16x8 qf[KC], df[KC], of[KC];
+  int qt0 = 0, cb0, ce0, role0, slot0;
+  const bool any = item(0, qt0, cb0, ce0, role0, slot0);
   {
-    const int64_t qrow0 = (split + wave * a.nsplit) * 16 + cl;
+    const int64_t qrow0 = (any ? qt0 : 0) * 16 + cl;
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
       qf[kc] = gload8(Qg, a.ldq, qrow0, a.T, kc * 32 + 8 * g);
@@ -372,12 +406,14 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_lds_kernel(AttnLdsArgs a) {
   stage2<DH>(Ks, a.k + b * a.T * a.ldk + h * DH, a.ldk, Vs, a.v + b * a.T * a.ldv + h * DH, a.ldv, a.T, rows, tid);
   stage_keymask(km, a, b, rows, tid);
   __syncthreads();
+  APROF(5);
   const uint64_t seed = eff_seed(a.seed, a.seed_base);
 
-  for (int qt = split + wave * a.nsplit; qt < nq; qt += NW * a.nsplit) {
+  int qt, cb, ce, role, slot;
+  for (int it = 0; item(it, qt, cb, ce, role, slot); ++it) {
     const int q0 = qt * 16;
     const int64_t qrow = q0 + cl;
-    if (qt != split + wave * a.nsplit) {
+    if (it > 0) {
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc) {
         qf[kc] = gload8(Qg, a.ldq, qrow, a.T, kc * 32 + 8 * g);
@@ -393,7 +429,7 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_lds_kernel(AttnLdsArgs a) {
     }
     dl += __shfl_xor(dl, 16, 64);
     dl += __shfl_xor(dl, 32, 64);  // delta = rowsum(dO * O) for query qrow
-    if (g == 0 && qrow < a.T) a.delta[bh * a.T + qrow] = dl;
+    if (role != 1 && g == 0 && qrow < a.T) a.delta[bh * a.T + qrow] = dl;
     const float lq2 = (qrow < a.T ? a.lse[bh * a.T + qrow] : 0.f) * LOG2E;
     const float sl2 = a.scale * LOG2E;
     const int qi = q0 + cl;
@@ -404,7 +440,7 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_lds_kernel(AttnLdsArgs a) {
     f32x4 acc[DT];
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) acc[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    for (int c = 0; 2 * c < nkt; ++c) {
+    for (int c = cb; c < ce; ++c) {
       f32x4 ds2[2];
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
@@ -440,6 +476,26 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_lds_kernel(AttnLdsArgs a) {
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) acc[dt] = mfma16(tr_frag(Ks, LD, 32 * c, 16 * dt, lane), bds, acc[dt]);
     }
+    float* sl = slots + slot * (DT * 4 * 64);
+    if (role == 1) {
+      // upper key half: partial dQ -> LDS slot, then release it to the lower half's wave
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sl[(dt * 4 + r) * 64 + lane] = acc[dt][r];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_store(&flags[slot], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      continue;
+    }
+    if (role == 2) {
+      while (__hip_atomic_load(&flags[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+        __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[dt][r] += sl[(dt * 4 + r) * 64 + lane];
+    }
     if (qrow < a.T) {
       bf16* dQ = a.dq + (b * a.T + qrow) * a.lddq + h * DH;
 #pragma unroll
@@ -450,6 +506,7 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_lds_kernel(AttnLdsArgs a) {
       }
     }
   }
+  APROF(6);
 }
 
 // ------------------------------------------------------------------ backward: dK, dV
@@ -458,6 +515,7 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkv_lds_kernel(AttnLdsArgs a) {
   constexpr int LD = Img<DH>::LD, KC = DH / 32, DT = DH / 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   KStampEnd stamp_(a.ks);
+  APROF(7);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4, cl = lane & 15;
   int64_t bh;
   int split;
@@ -474,13 +532,35 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkv_lds_kernel(AttnLdsArgs a) {
   float* lse_s = reinterpret_cast<float*>(dOs + rows * LD);
   float* dl_s = lse_s + rows;
   float* km = dl_s + rows;
+  bf16* slots = reinterpret_cast<bf16*>(km + rows);     // plan: bf16 partial (dK, dV) tiles [slot][2][DT*4][64]
+  int* flags = reinterpret_cast<int*>(slots + DKV_SLOTS * 2 * DT * 4 * 64);
   const bf16* Kg = a.k + b * a.T * a.ldk + h * DH;
   const bf16* Vg = a.v + b * a.T * a.ldv + h * DH;
+  const int nqc = (T + 31) / 32;  // 32-query chunks
+  // this wave's work items: the plan's (key tile, query-chunk range, role), else one whole key tile per wave
+  auto item = [&](int it, int& kt, int& cb, int& ce, int& role, int& slot) -> bool {
+    if (a.use_plan) {
+      if (it >= PLAN_I) return false;
+      const uint32_t e = a.plan[split][wave][it];
+      if (!(e >> 31)) return false;
+      kt = e & 255; cb = (e >> 8) & 255; ce = (e >> 16) & 255; role = (e >> 24) & 3; slot = (e >> 26) & 15;
+      return true;
+    }
+    kt = split + (wave + it * NW) * a.nsplit;
+    if (kt >= nk) return false;
+    cb = a.mask_kind == 0 ? kt / 2 : 0;
+    ce = nqc;
+    role = 0; slot = 0;
+    return true;
+  };
+  if (a.use_plan && tid < DKV_SLOTS) flags[tid] = 0;
   // everything this workgroup reads before its first MFMA is requested in one batch: the first key
   // tile's k/v rows, the per-query lse/delta (rows <= 256 <= NT: one per thread), the Q/dO images
   bf16x8 kf[KC], vf[KC];
+  int kt0 = 0, cb0, ce0, role0, slot0;
+  const bool any = item(0, kt0, cb0, ce0, role0, slot0);
   {
-    const int64_t key0 = (split + wave * a.nsplit) * 16 + cl;
+    const int64_t key0 = (any ? kt0 : 0) * 16 + cl;
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
       kf[kc] = gload8(Kg, a.ldk, key0, a.T, kc * 32 + 8 * g);
@@ -498,14 +578,15 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkv_lds_kernel(AttnLdsArgs a) {
   }
   stage_keymask(km, a, b, rows, tid);
   __syncthreads();
+  APROF(8);
   const uint64_t seed = eff_seed(a.seed, a.seed_base);
-  const int nqc = (T + 31) / 32;  // 32-query chunks
 
   const float sl2 = a.scale * LOG2E;
-  for (int kt = split + wave * a.nsplit; kt < nk; kt += NW * a.nsplit) {
+  int kt, cb, ce, role, slot;
+  for (int it = 0; item(it, kt, cb, ce, role, slot); ++it) {
     const int64_t key = kt * 16 + cl;  // this lane's key
     const int ki = kt * 16 + cl;
-    if (kt != split + wave * a.nsplit) {
+    if (it > 0) {
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc) {
         kf[kc] = gload8(Kg, a.ldk, key, a.T, kc * 32 + 8 * g);
@@ -518,8 +599,7 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkv_lds_kernel(AttnLdsArgs a) {
       dk[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
       dv[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
     }
-    const int c0 = a.mask_kind == 0 ? kt / 2 : 0;
-    for (int c = c0; c < nqc; ++c) {
+    for (int c = cb; c < ce; ++c) {
       f32x4 pd2[2], ds2[2];
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
@@ -554,6 +634,32 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkv_lds_kernel(AttnLdsArgs a) {
         dk[dt] = mfma16(tr_frag(Qs, LD, 32 * c, 16 * dt, lane), bds, dk[dt]);
       }
     }
+    bf16* sl = slots + slot * (2 * DT * 4 * 64);
+    if (role == 1) {
+      // upper query half: partial (dK, dV) -> LDS slot (bf16), then release it to the lower half's wave
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          sl[(dt * 4 + r) * 64 + lane] = (bf16)dk[dt][r];
+          sl[(DT * 4 + dt * 4 + r) * 64 + lane] = (bf16)dv[dt][r];
+        }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_store(&flags[slot], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      continue;
+    }
+    if (role == 2) {
+      while (__hip_atomic_load(&flags[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+        __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          dk[dt][r] += (float)sl[(dt * 4 + r) * 64 + lane];
+          dv[dt][r] += (float)sl[(DT * 4 + dt * 4 + r) * 64 + lane];
+        }
+    }
     if (key < a.T) {
       bf16* dK = a.dk + (b * a.T + key) * a.lddk + h * DH;
       bf16* dV = a.dv + (b * a.T + key) * a.lddv + h * DH;
@@ -570,6 +676,7 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkv_lds_kernel(AttnLdsArgs a) {
       }
     }
   }
+  APROF(9);
 }
 
 // ------------------------------------------------------------------ launchers
@@ -609,14 +716,89 @@ static hipError_t fwd_t(AttnLdsArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Causal backward work plan.  Round robin gives a wave one whole tile: the dQ tile of the last queries
+// scans every key (13 key tiles at T = 200) while the mean is half that, and the workgroup waits for its
+// longest wave.  Here the longest tiles (up to `slots` of them) are cut in two halves of their chunk range
+// -- the upper half's wave leaves a partial in an LDS slot for the lower half's wave, which adds it and
+// writes the tile -- and the items are dealt longest-first to the least-loaded wave, writers first in each
+// wave's list (a reader only ever waits for a writer, so there is no cycle).  Measured at B = 128, T = 200
+// (tools/micro/attn_bwd_phase.hip): the slowest wave did ~2x the mean work; balanced, the dK/dV pass's
+// slowest wave went 14.5 -> 12.5 us, the dQ pass's barely moved -- with every wave busy the workgroup is
+// bound by the CU's LDS operand traffic (one 1 KB fragment read per MFMA), not by its longest wave.
+struct PlanItem {
+  int tile, cb, ce, role, slot;
+};
+
+static bool make_plan(AttnLdsArgs& a, int ntiles, bool dkv, int slots) {
+  const int T = (int)a.T, nqc = (T + 31) / 32;
+  if (a.nsplit > PLAN_S) return false;
+  memset(a.plan, 0, sizeof(a.plan));
+  for (int sp = 0; sp < a.nsplit; ++sp) {
+    PlanItem items[64];
+    int n = 0;
+    for (int t = sp; t < ntiles; t += a.nsplit) {
+      if (n >= 32) return false;
+      items[n++] = dkv ? PlanItem{t, t / 2, nqc, 0, 0} : PlanItem{t, 0, (t + 2) / 2, 0, 0};
+    }
+    std::sort(items, items + n, [](const PlanItem& x, const PlanItem& y) {
+      return x.ce - x.cb != y.ce - y.cb ? x.ce - x.cb > y.ce - y.cb : x.tile < y.tile;
+    });
+    const int n0 = n;
+    for (int k = 0, used = 0; k < n0 && used < slots; ++k) {
+      PlanItem& it = items[k];
+      const int w = it.ce - it.cb;
+      if (w < 2) break;
+      const int hmid = it.cb + (w + 1) / 2;
+      items[n++] = PlanItem{it.tile, hmid, it.ce, 1, used};   // upper half: writer
+      it.ce = hmid;
+      it.role = 2;                                              // lower half: reader
+      it.slot = used++;
+    }
+    std::sort(items, items + n, [](const PlanItem& x, const PlanItem& y) {
+      return x.ce - x.cb != y.ce - y.cb ? x.ce - x.cb > y.ce - y.cb : x.tile < y.tile;
+    });
+    int load[NW] = {0}, cnt[NW] = {0};
+    PlanItem lists[NW][PLAN_I];
+    for (int k = 0; k < n; ++k) {
+      int w = 0;
+      for (int j = 1; j < NW; ++j)
+        if (load[j] < load[w]) w = j;
+      if (cnt[w] == PLAN_I) return false;
+      lists[w][cnt[w]++] = items[k];
+      load[w] += items[k].ce - items[k].cb;
+    }
+    for (int w = 0; w < NW; ++w) {
+      int o = 0;
+      for (int pass = 0; pass < 3; ++pass) {     // writers, whole tiles, readers
+        const int want = pass == 0 ? 1 : pass == 1 ? 0 : 2;
+        for (int k = 0; k < cnt[w]; ++k) {
+          const PlanItem& it = lists[w][k];
+          if (it.role != want) continue;
+          a.plan[sp][w][o++] = 1u << 31 | (uint32_t)it.slot << 26 | (uint32_t)it.role << 24 |
+                               (uint32_t)it.ce << 16 | (uint32_t)it.cb << 8 | (uint32_t)it.tile;
+        }
+      }
+    }
+  }
+  return true;
+}
+
 template <int DH>
 static hipError_t bwd_t(AttnLdsArgs& a, hipStream_t s) {
   const int nq = (int)cdiv(a.T, 16);
   a.nsplit = pick_split(a.B * a.H, nq);
+  constexpr int DT = DH / 16;
+  const size_t lds_q = fwd_lds_bytes<DH>((int)a.T), lds_kv = dkv_lds_bytes<DH>((int)a.T);
+  const size_t ext_q = (size_t)DQ_SLOTS * DT * 4 * 64 * 4 + 16, ext_kv = (size_t)DKV_SLOTS * 2 * DT * 4 * 64 * 2 + 16;
+  AttnLdsArgs aq = a, akv = a;
+  // only long causal sequences: at T = 50 (4 tiles) the split halves cost more than the imbalance they remove
+  const bool want = a.mask_kind == 0 && nq >= 8;
+  aq.use_plan = want && lds_q + ext_q <= 160 * 1024 && make_plan(aq, nq, false, DQ_SLOTS);
+  akv.use_plan = want && lds_kv + ext_kv <= 160 * 1024 && make_plan(akv, nq, true, DKV_SLOTS);
   hipLaunchKernelGGL((attn_bwd_dq_lds_kernel<DH>), dim3((unsigned)a.nsplit, (unsigned)(a.B * a.H)), dim3(NT),
-                     fwd_lds_bytes<DH>((int)a.T), s, a);
+                     lds_q + (aq.use_plan ? ext_q : 0), s, aq);
   hipLaunchKernelGGL((attn_bwd_dkv_lds_kernel<DH>), dim3((unsigned)a.nsplit, (unsigned)(a.B * a.H)), dim3(NT),
-                     dkv_lds_bytes<DH>((int)a.T), s, a);
+                     lds_kv + (akv.use_plan ? ext_kv : 0), s, akv);
   return hipGetLastError();
 }
 
