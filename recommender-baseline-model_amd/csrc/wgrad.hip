@@ -45,8 +45,16 @@ __global__ __launch_bounds__(256, 2) void wgrad_group_kernel(Args a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), wm = wave >> 1, wn = wave & 1;
   constexpr int FM = T / 32, FN = T / 32;
 
-  const int t = (int)(blockIdx.x % (unsigned)a.ntiles);
-  const int s = (int)(blockIdx.x / (unsigned)a.ntiles);
+  // XCD-aware: workgroup b runs on XCD b % 8; give each XCD a contiguous range of (split, tile) pairs, so
+  // the tiles that share a row range's dY / X column slices read them through ONE XCD's L2 (round-robin
+  // dealing had every XCD fetch its own copy: ~2.5x the algorithmic HBM bytes at the BERT shapes)
+  unsigned bid = blockIdx.x;
+  {
+    const unsigned nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, x = bid & 7;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+  }
+  const int t = (int)(bid % (unsigned)a.ntiles);
+  const int s = (int)(bid / (unsigned)a.ntiles);
   int pi = 0;
 #pragma unroll 1
   for (int q = 1; q < a.nprob; ++q)
