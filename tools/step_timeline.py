@@ -7,7 +7,7 @@ import sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 nth = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-ad = [i for i, r in enumerate(rows) if "adam_step" in r["Kernel_Name"]]
+ad = [i for i, r in enumerate(rows) if "adam_step" in r["Kernel_Name"] or "adam_fused" in r["Kernel_Name"]]
 hi, lo = ad[-nth], ad[-nth - 1]
 sel = rows[lo + 1:hi + 1]
 t0 = int(sel[0]["Start_Timestamp"])
