@@ -19,11 +19,13 @@ for c in cfg2 cfg3 cfg4; do
   python3 tools/make_traffic.py $OUT/traffic_$c $c profiles/traffic.json > /dev/null || exit 1
 done
 cp profiles/traffic.json $OUT/traffic.json
-for c in ${CONFIGS:-cfg2 cfg3 cfg4}; do
+for c in ${CONFIGS:-cfg2 cfg3 cfg4 cfg5}; do
   CB=""; [ "$c" != "cfg2" ] && CB="--cpu-baseline-seconds ${CPU_SECONDS_OTHER:-10}"
-  timeout -k 10 900 python bench.py --config $c $CB > $OUT/bench_$c.log 2>&1; rc=$?; tail -1 $OUT/bench_$c.log | cut -c1-160
+  ST=""; [ "$c" = "cfg5" ] && ST="--steps 30 --warmup 5"
+  timeout -k 10 900 python bench.py --config $c $CB $ST > $OUT/bench_$c.log 2>&1; rc=$?; tail -1 $OUT/bench_$c.log | cut -c1-160
   [ $rc -eq 0 ] || exit $rc
   tail -1 $OUT/bench_$c.log > $OUT/bench_$c.json
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_$c -o prof --output-format csv -- python3 bench.py --config $c --steps 50 --warmup 10 --cpu-baseline-seconds 0 > $OUT/rocprof_$c.log 2>&1 || { tail -20 $OUT/rocprof_$c.log; exit 1; }
+  PS="--steps 50 --warmup 10"; [ "$c" = "cfg5" ] && PS="--steps 10 --warmup 3"
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_$c -o prof --output-format csv -- python3 bench.py --config $c $PS --cpu-baseline-seconds 0 > $OUT/rocprof_$c.log 2>&1 || { tail -20 $OUT/rocprof_$c.log; exit 1; }
 done
 echo done
