@@ -64,6 +64,8 @@ def parse():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--vocab-shard", default="auto", choices=["auto", "on", "off"],
+                    help="BERT, N > 1: shard out.weight over the ranks (auto: on for vocabularies >= 100k)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse the "
                          "multi-process path with several ranks on one GPU)")
@@ -302,7 +304,9 @@ def main():
         max_lab = -(-cnt // 128) * 128
     batches = [tuple(torch.from_numpy(a).cuda() for a in b) for b in host_batches]
     from rbm_amd.train_step import FusedTrainStep
-    trainer = FusedTrainStep(model, lr=1e-3, max_labelled=max_lab)
+    vshard = cfg["model"] == "bert" and world > 1 and (
+        args.vocab_shard == "on" or (args.vocab_shard == "auto" and cfg["V"] >= 100000))
+    trainer = FusedTrainStep(model, lr=1e-3, max_labelled=max_lab, vocab_shard=vshard)
     # the dominant kernel is timed live, inside every timed step: the step graph is captured with kernel
     # stamps on (first wave in / last wave out s_memrealtime ticks of each stamped launch, per step)
     from rbm_amd import ops
@@ -396,6 +400,8 @@ def main():
         }
         if max_lab is not None:
             line["config"]["labelled_rows_cap"] = max_lab
+        if vshard:
+            line["config"]["vocab_sharded_head"] = True
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

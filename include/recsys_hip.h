@@ -245,7 +245,24 @@ int rs_vocab_head_fwd(int64_t R, int64_t V1, int64_t d, const void* h, int64_t l
                       float* ws, float* out, void* stream);
 int rs_vocab_head_bwd(int64_t R, int64_t V1, int64_t d, const void* h, int64_t ldh, const void* E, int64_t lde,
                       const float* bias, const int64_t* labels, const int* rows_dev, const float* count,
-                      const float* dloss, const float* ws, void* dlogits, int64_t lddl, void* stream);
+                      const float* dloss, const float* ws, void* dlogits, int64_t lddl, int64_t voff, void* stream);
+
+/* Vocabulary-sharded head (data-parallel rank r owns rows [v0, v1) of E = out.weight and b;
+ * every rank holds the labelled rows h of ALL ranks, all-gathered).  Labels stay absolute vocabulary ids
+ * (0 = not labelled); rs_vocab_head_bwd's voff = v0 places E's rows.
+ * rs_vocab_shard_lse: per row, log-sum-exp of h E_shard^T + b_shard (0 for unlabelled rows); ws as
+ *   rs_vocab_ce_ws_numel(R, v1 - v0).
+ * rs_vocab_shard_label_logits: tgt[r] = <h[r], E[label - v0]> + b[label - v0] where this shard holds the label,
+ *   else 0 (summed over ranks: every row's label logit).
+ * rs_vocab_shard_combine: lse_parts [N][R] (every shard's lse, all-gathered) -> lse [R] over the whole
+ *   vocabulary; out = {loss sum, labelled count, mean} of CE over the labelled rows. */
+int rs_vocab_shard_lse(int64_t R, int64_t V1s, int64_t d, const void* h, int64_t ldh, const void* E, int64_t lde,
+                       const float* bias, const int64_t* labels, float* ws, float* lse, void* stream);
+int rs_vocab_shard_label_logits(int64_t R, int64_t d, const void* h, int64_t ldh, const void* E, int64_t lde,
+                                const float* bias, const int64_t* labels, int64_t v0, int64_t v1, float* tgt,
+                                void* stream);
+int rs_vocab_shard_combine(int N, int64_t R, const float* lse_parts, const float* tgt, const int64_t* labels,
+                           float* lse, float* out, void* stream);
 
 /* Kernel stamps (bench.py's in-step timing of the dominant launch; not on the reference's path).
  * While enabled (buf != NULL), rs_attn_bwd (bf16 LDS path), rs_wgrad_grouped and rs_vocab_ce_fwd (its

@@ -76,7 +76,10 @@ SIGNATURES = {
     "rs_vocab_ce_bwd": [i64, i64, i64, vp, i64, vp, i64, vp, vp, vp, vp, vp, vp, vp, i64, vp],
     "rs_vocab_head_supported": [i64],
     "rs_vocab_head_fwd": [i64, i64, i64, vp, i64, vp, i64, vp, vp, vp, vp, vp, vp, vp],
-    "rs_vocab_head_bwd": [i64, i64, i64, vp, i64, vp, i64, vp, vp, vp, vp, vp, vp, vp, i64, vp],
+    "rs_vocab_head_bwd": [i64, i64, i64, vp, i64, vp, i64, vp, vp, vp, vp, vp, vp, vp, i64, i64, vp],
+    "rs_vocab_shard_lse": [i64, i64, i64, vp, i64, vp, i64, vp, vp, vp, vp, vp],
+    "rs_vocab_shard_label_logits": [i64, i64, vp, i64, vp, i64, vp, vp, i64, i64, vp, vp],
+    "rs_vocab_shard_combine": [i32, i64, vp, vp, vp, vp, vp, vp],
     "rs_seed_advance": [vp, vp],
     "rs_sas_block_in": [i64, i64, vp, i64, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "rs_sas_block_out": [i64, i64, vp, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32,

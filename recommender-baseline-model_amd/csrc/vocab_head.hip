@@ -56,6 +56,7 @@ struct Args {
   const float* count;
   const float* dloss;
   bf16* dl; int64_t lddl;   // bwd: dlogits [R][V1] (rows >= live count untouched)
+  int64_t voff;             // vocabulary index of E's row 0 (a shard of the table; 0 = the whole table)
   KStamp ks;
 };
 
@@ -292,7 +293,8 @@ __global__ __launch_bounds__(NTH, 1) void vhead_kernel(Args a) {
           const bool live = m0 + rl < Rl && lb != 0;
           const float Lr = lses[rl];
           const float scr = live ? sc : 0.f;
-          const int off = (int)(lb - (n0 + v0w + 4 * g));
+          const int64_t offl = lb - a.voff - (n0 + v0w + 4 * g);   // label's entry in this lane's rows
+          const int off = offl < 0 || offl >= 64 ? -1 : (int)offl;
 #pragma unroll
           for (int i = 0; i < FV; ++i) {
             bf4 o;
@@ -396,7 +398,7 @@ int rs_vocab_head_fwd(int64_t R, int64_t V1, int64_t d, const void* h, int64_t l
 
 int rs_vocab_head_bwd(int64_t R, int64_t V1, int64_t d, const void* h, int64_t ldh, const void* E, int64_t lde,
                       const float* bias, const int64_t* labels, const int* rows_dev, const float* count,
-                      const float* dloss, const float* ws, void* dlogits, int64_t lddl, void* stream) {
+                      const float* dloss, const float* ws, void* dlogits, int64_t lddl, int64_t voff, void* stream) {
   if (!rs_vocab_head_supported(d) || R <= 0 || V1 <= 0 || ldh % 8 || lde % 8 || lddl % 8 ||
       ((uintptr_t)h | (uintptr_t)E | (uintptr_t)dlogits) % 16 || !labels || !ws || !count || !dlogits)
     return RS_ERR_ARG;
@@ -407,7 +409,121 @@ int rs_vocab_head_bwd(int64_t R, int64_t V1, int64_t d, const void* h, int64_t l
   a.lse = ws + R * a.ntn * 2 + R;
   a.count = count; a.dloss = dloss;
   a.dl = (__bf16*)dlogits; a.lddl = lddl;
+  a.voff = voff;
   return (int)vh::dispatch<true>(a, d, (hipStream_t)stream);
+}
+
+}  // extern "C"
+
+// ---- vocabulary-sharded head (data-parallel ranks each own a slice of E = out.weight) ---------------
+namespace vh {
+
+// one wave per row: log-sum-exp of the row's 128-column partials over this shard (0 for dead rows)
+__global__ __launch_bounds__(256) void shard_lse_kernel(const float* __restrict__ part, int64_t ntn, int64_t R,
+                                                        const int64_t* __restrict__ labels, float* __restrict__ lse) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= R) return;
+  if (labels[r] == 0) {
+    if (lane == 0) lse[r] = 0.f;
+    return;
+  }
+  float mx = -__builtin_inff(), sm = 0.f;
+  for (int64_t t = lane; t < ntn; t += 64) comb(mx, sm, part[(r * ntn + t) * 2], part[(r * ntn + t) * 2 + 1]);
+  for (int o = 32; o > 0; o >>= 1) comb(mx, sm, __shfl_xor(mx, o, 64), __shfl_xor(sm, o, 64));
+  if (lane == 0) lse[r] = mx + __logf(sm);
+}
+
+// one wave per row: the label's logit <h, E[label - v0]> + b when this shard holds the label, else 0
+__global__ __launch_bounds__(256) void shard_label_kernel(int64_t R, int64_t d, const bf16* __restrict__ h,
+                                                          int64_t ldh, const bf16* __restrict__ E, int64_t lde,
+                                                          const float* __restrict__ bias,
+                                                          const int64_t* __restrict__ labels, int64_t v0, int64_t v1,
+                                                          float* __restrict__ tgt) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= R) return;
+  const int64_t lb = labels[r];
+  if (lb == 0 || lb < v0 || lb >= v1) {
+    if (lane == 0) tgt[r] = 0.f;
+    return;
+  }
+  float dot = 0.f;
+  for (int64_t k = lane; k < d; k += 64) dot += (float)h[r * ldh + k] * (float)E[(lb - v0) * lde + k];
+  dot = wave_sum(dot);
+  if (lane == 0) tgt[r] = dot + (bias ? bias[lb - v0] : 0.f);
+}
+
+// every shard's per-row lse [N][R] -> the row's lse over the whole vocabulary; loss over live rows
+__global__ __launch_bounds__(256) void shard_combine_kernel(int N, int64_t R, const float* __restrict__ lse_parts,
+                                                            const float* __restrict__ tgt,
+                                                            const int64_t* __restrict__ labels,
+                                                            float* __restrict__ lse, float* __restrict__ out) {
+  float s = 0.f, c = 0.f;
+  for (int64_t r = threadIdx.x; r < R; r += blockDim.x) {
+    if (labels[r] == 0) {
+      lse[r] = 0.f;
+      continue;
+    }
+    float mx = -__builtin_inff();
+    for (int q = 0; q < N; ++q) mx = fmaxf(mx, lse_parts[q * R + r]);
+    float sm = 0.f;
+    for (int q = 0; q < N; ++q) sm += __expf(lse_parts[q * R + r] - mx);
+    const float L = mx + __logf(sm);
+    lse[r] = L;
+    s += L - tgt[r];
+    c += 1.f;
+  }
+  __shared__ float rs[4], rc[4];
+  s = wave_sum(s);
+  c = wave_sum(c);
+  if ((threadIdx.x & 63) == 0) { rs[threadIdx.x >> 6] = s; rc[threadIdx.x >> 6] = c; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float S = rs[0] + rs[1] + rs[2] + rs[3], Cn = rc[0] + rc[1] + rc[2] + rc[3];
+    out[0] = S;
+    out[1] = Cn;
+    out[2] = Cn > 0.f ? S / Cn : 0.f;
+  }
+}
+
+}  // namespace vh
+
+extern "C" {
+
+int rs_vocab_shard_lse(int64_t R, int64_t V1s, int64_t d, const void* h, int64_t ldh, const void* E, int64_t lde,
+                       const float* bias, const int64_t* labels, float* ws, float* lse, void* stream) {
+  if (!rs_vocab_head_supported(d) || R <= 0 || V1s <= 0 || ldh % 8 || lde % 8 || ((uintptr_t)h | (uintptr_t)E) % 16 ||
+      !labels || !ws || !lse)
+    return RS_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  vh::Args a{};
+  a.R = R; a.V1 = V1s; a.ntn = cdiv(V1s, 128);
+  a.h = (const __bf16*)h; a.ldh = ldh; a.E = (const __bf16*)E; a.lde = lde;
+  a.bias = bias; a.labels = labels;
+  a.part = ws;
+  a.tgt = ws + R * a.ntn * 2;
+  hipError_t e = vh::dispatch<false>(a, d, s);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(vh::shard_lse_kernel, dim3((unsigned)cdiv(R, 4)), dim3(256), 0, s, a.part, a.ntn, R, labels, lse);
+  return (int)hipGetLastError();
+}
+
+int rs_vocab_shard_label_logits(int64_t R, int64_t d, const void* h, int64_t ldh, const void* E, int64_t lde,
+                                const float* bias, const int64_t* labels, int64_t v0, int64_t v1, float* tgt,
+                                void* stream) {
+  if (R <= 0 || d <= 0 || !h || !E || !labels || !tgt) return RS_ERR_ARG;
+  hipLaunchKernelGGL(vh::shard_label_kernel, dim3((unsigned)cdiv(R, 4)), dim3(256), 0, (hipStream_t)stream, R, d,
+                     (const __bf16*)h, ldh, (const __bf16*)E, lde, bias, labels, v0, v1, tgt);
+  return (int)hipGetLastError();
+}
+
+int rs_vocab_shard_combine(int N, int64_t R, const float* lse_parts, const float* tgt, const int64_t* labels,
+                           float* lse, float* out, void* stream) {
+  if (N <= 0 || R <= 0 || !lse_parts || !tgt || !labels || !lse || !out) return RS_ERR_ARG;
+  hipLaunchKernelGGL(vh::shard_combine_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, N, R, lse_parts, tgt, labels,
+                     lse, out);
+  return (int)hipGetLastError();
 }
 
 }  // extern "C"

@@ -57,13 +57,18 @@ class BucketedExchange:
     all-reduce asynchronously; finish() waits for every launched one (on the current stream for
     NCCL/RCCL: no host block) and checks that every bucket went out exactly once."""
 
-    def __init__(self, flat_grad, buckets, group=None):
+    def __init__(self, flat_grad, buckets, group=None, partial=False):
+        """partial: the buckets may leave parts of the buffer out (rank-owned regions, e.g. a vocabulary shard);
+        else they must cover it."""
         self.flat_grad = flat_grad
         self.buckets = dict(buckets)
         self.group = group
         spans = sorted(self.buckets.values())
-        assert spans[0][0] == 0 and spans[-1][1] == flat_grad.numel(), "buckets must cover the buffer"
-        assert all(a[1] == b[0] for a, b in zip(spans, spans[1:])), "buckets must be disjoint and contiguous"
+        assert all(a[1] <= b[0] for a, b in zip(spans, spans[1:])), "buckets must be disjoint"
+        assert all(0 <= lo < hi <= flat_grad.numel() for lo, hi in spans), "bucket out of the buffer"
+        if not partial:
+            assert spans[0][0] == 0 and spans[-1][1] == flat_grad.numel(), "buckets must cover the buffer"
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:])), "buckets must be contiguous"
         self.works = []
         self.sent = []
 

@@ -403,6 +403,8 @@ class BERTEngine:
         ops.compact_rows(labels, cap, idx, rank, cnt)
         hl = self.ws.get("hl", (cap, d), self.dt)
         lab = self.ws.get("lab", (cap,), torch.int64)
+        if getattr(self, "vocab_shard", None) is not None:
+            return self._sharded_head_and_backward(s, xL, hl, lab, idx, rank, cnt, labels, cap, loss_out, grad, split)
         ops.gather_rows(xL, idx, cnt, cap, hl, labels, lab)
         head = os.environ.get("RS_BERT_VOCAB_HEAD", "tile")
         if self.dt == torch.bfloat16 and head == "tile" and ops.vocab_head_supported(d):
@@ -447,6 +449,63 @@ class BERTEngine:
                  split_k=sk, slab=slab_d)
         dxL = self._buf((M, d))
         ops.splitk_scatter_rows(slab_d, sk, cap, rank, dxL)
+        self.encode_backward(s, dxL, grad)
+
+
+    def _sharded_head_and_backward(self, s, xL, hl, lab, idx, rank, cnt, labels, cap, loss_out, grad, split):
+        """The vocabulary head with out.weight / out.bias sharded over the data-parallel ranks (vocab_parallel.py):
+        loss_out = (loss sum, labelled count, mean) of the GLOBAL batch on every rank; gradients are those of the
+        global mean (no later division); this rank's out.weight rows get complete gradients, the rest none."""
+        vs = self.vocab_shard
+        if not (self.dt == torch.bfloat16 and ops.vocab_head_supported(self.d)):
+            raise RuntimeError("the vocabulary-sharded head needs the bf16 path and d in {64, 128, 256}")
+        B, T = xL.shape[0] // self.T, self.T
+        M, d, N = xL.shape[0], self.d, vs.world
+        R = N * cap
+        v0, v1 = vs.v0, vs.v1
+        V1s = v1 - v0
+        hl.zero_()                       # rows past the labelled count: zero (they meet dlogits = 0 in dE)
+        lab.zero_()
+        ops.gather_rows(xL, idx, cnt, cap, hl, labels, lab)
+        H = self.ws.get("vs_H", (R, d), self.dt)
+        L = self.ws.get("vs_L", (R,), torch.int64)
+
+        def sync(tag, action):
+            if split is None:
+                action()
+            else:
+                if s.get("side") is not None and s["side"][0] is not None:     # join the side stream first
+                    torch.cuda.current_stream().wait_event(s["side"][0])
+                    s["side"] = (None, s["side"][1])
+                split(tag, action)
+
+        sync("vocab_gather", lambda: (vs.all_gather(H, hl), vs.all_gather(L, lab)))
+        Es, bs = self.W("out.weight")[v0:v1], self.Wf("out.bias")[v0:v1]
+        wce = self.ws.get("vs_ce", (ops.vocab_ce_ws_numel(R, V1s),), torch.float32)
+        lse_r = self.ws.get("vs_lse_r", (R,), torch.float32)
+        tgt = self.ws.get("vs_tgt", (R,), torch.float32)
+        ops.vocab_shard_lse(H, Es, bs, L, wce, lse_r)
+        ops.vocab_shard_label_logits(H, Es, bs, L, v0, v1, tgt)
+        lse_parts = self.ws.get("vs_lse_parts", (N, R), torch.float32)
+        sync("vocab_lse", lambda: (vs.all_gather(lse_parts.view(-1), lse_r), vs.all_reduce(tgt)))
+        ntn = -(-V1s // 128)
+        lse = wce[R * ntn * 2 + R:R * ntn * 2 + 2 * R]      # where rs_vocab_head_bwd reads the row lse
+        ops.vocab_shard_combine(lse_parts, tgt, L, lse, loss_out)
+        count = loss_out[1:2]
+        V1sp = -(-V1s // 8) * 8
+        dl = self.ws.get("vs_dlogits", (R, V1sp), self.dt)[:, :V1s]
+        ops.vocab_head_bwd(H, Es, bs, L, wce, count, dl, voff=v0)
+        slab = self.ws.get("vs_slab_out", (ops.wgrad_slab_numel(R, V1s, d),), torch.float32)
+        ops.linear_wgrad(dl, H, self.flat.view("out.weight", grad)[v0:v1], slab,
+                         db=self.flat.view("out.bias", grad)[v0:v1])
+        sk = int(max(1, min(64, -(-V1s // 2048))))
+        slab_d = self.ws.get("vs_slab_dh", (sk * R * d,), torch.float32)
+        ops.gemm(dl, Es, slab_d, R, d, V1s, False, True, ops.epilogue(), split_k=sk, slab=slab_d)
+        dH = self.ws.get("vs_dH", (R, d), torch.float32)
+        ops.reduce_slabs(slab_d, sk, dH)
+        sync("vocab_dh", lambda: vs.all_reduce(dH))
+        dxL = self._buf((M, d))
+        ops.splitk_scatter_rows(dH[vs.rank * cap:(vs.rank + 1) * cap], 1, cap, rank, dxL)
         self.encode_backward(s, dxL, grad)
 
 

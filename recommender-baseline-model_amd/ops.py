@@ -244,6 +244,12 @@ def scatter_rows(src, rank, dst):
     call("rs_scatter_rows", dtype_code(src), ptr(src), ld(src), d, ptr(rank), n, ptr(dst), ld(dst), stream())
 
 
+def reduce_slabs(slab, splits, out, accumulate=False):
+    """out (+)= sum over the `splits` leading slabs of slab (fixed order)."""
+    n = out.numel()
+    call("rs_reduce_slabs", ptr(slab), splits, n, ptr(out), int(accumulate), stream())
+
+
 def splitk_scatter_rows(slab, splits, cap, rank, dst):
     """dst[r] = sum_z slab[z][rank[r]] (0 where rank < 0): split-K reduce + cast + scatter, one launch."""
     n, d = dst.shape
@@ -306,12 +312,30 @@ def vocab_head_fwd(h, E, bias, labels, ws, out, rows_dev=None, count_override=No
          ptr(count_override), ptr(ws), ptr(out), stream())
 
 
-def vocab_head_bwd(h, E, bias, labels, ws, count, dl, rows_dev=None, dloss=None):
-    """vocab_ce_bwd's dlogits from the vocabulary-tile-stationary kernel (rs_vocab_head_bwd)."""
+def vocab_head_bwd(h, E, bias, labels, ws, count, dl, rows_dev=None, dloss=None, voff=0):
+    """vocab_ce_bwd's dlogits from the vocabulary-tile-stationary kernel (rs_vocab_head_bwd); E may be a shard of
+    the table starting at vocabulary id voff (labels stay absolute)."""
     R, d = h.shape
     V1 = E.shape[0]
     call("rs_vocab_head_bwd", R, V1, d, ptr(h), ld(h), ptr(E), ld(E), ptr(bias), ptr(labels), ptr(rows_dev),
-         ptr(count), ptr(dloss), ptr(ws), ptr(dl), ld(dl), stream())
+         ptr(count), ptr(dloss), ptr(ws), ptr(dl), ld(dl), int(voff), stream())
+
+
+def vocab_shard_lse(h, E, bias, labels, ws, lse):
+    R, d = h.shape
+    call("rs_vocab_shard_lse", R, E.shape[0], d, ptr(h), ld(h), ptr(E), ld(E), ptr(bias), ptr(labels), ptr(ws),
+         ptr(lse), stream())
+
+
+def vocab_shard_label_logits(h, E, bias, labels, v0, v1, tgt):
+    R, d = h.shape
+    call("rs_vocab_shard_label_logits", R, d, ptr(h), ld(h), ptr(E), ld(E), ptr(bias), ptr(labels), int(v0), int(v1),
+         ptr(tgt), stream())
+
+
+def vocab_shard_combine(lse_parts, tgt, labels, lse, out):
+    N, R = lse_parts.shape
+    call("rs_vocab_shard_combine", N, R, ptr(lse_parts), ptr(tgt), ptr(labels), ptr(lse), ptr(out), stream())
 
 
 def vocab_ce_bwd(h, E, bias, labels, ws, count, dl, rows_dev=None, dloss=None):

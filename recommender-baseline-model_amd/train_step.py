@@ -41,23 +41,27 @@ class FusedAdam:
         """StepLR hook (BS/trainers/base.py:40,87): lives on the device, so graph replays see it."""
         self.hyper[0] = lr
 
-    def step(self, grad_divisor=None, seed_base=None):
+    def step(self, grad_divisor=None, seed_base=None, ranges=None):
         """One Adam update; also clears the gradient buffer (the next step accumulates from zero) and
-        advances the dropout step seed when given."""
+        advances the dropout step seed when given.  ranges: [(lo, hi)] flat slices to update (default all; a
+        vocabulary-sharded rank skips the output rows other ranks own)."""
         ops.adam_prepare(self.state, self.hyper, grad_divisor, seed_base)
-        ops.adam_step(self.flat.data, self.flat.grad, self.m, self.v, self.flat.bf16, self.state, self.hyper,
-                      zero_grad=True)
+        f = self.flat
+        for lo, hi in ranges or [(0, f.numel)]:
+            ops.adam_step(f.data[lo:hi], f.grad[lo:hi], self.m[lo:hi], self.v[lo:hi],
+                          f.bf16[lo:hi] if f.bf16 is not None else None, self.state, self.hyper, zero_grad=True)
 
 
 class FusedTrainStep:
     def __init__(self, model, lr=1e-3, weight_decay=0.0, process_group=None, dp=None, max_labelled=None,
-                 bucket_numel=None, overlap=None):
+                 bucket_numel=None, overlap=None, vocab_shard=False):
         """model: rbm_amd SASModel or BERTModel on a CUDA device.
         dp: data-parallel mode (default: torch.distributed initialised with world size > 1).
         max_labelled (BERT): upper bound on labelled rows per batch (sizes the compacted
         vocabulary-logit buffers; default B*T).  overlap (DP, default on unless bucket_numel is given): each
         gradient bucket's all-reduce starts as soon as the backward has finished it (dp.BucketedExchange);
-        bucket_numel: otherwise ONE all-reduce after the backward, in buckets of that many floats."""
+        bucket_numel: otherwise ONE all-reduce after the backward, in buckets of that many floats.
+        vocab_shard (BERT, DP): out.weight / out.bias sharded over the ranks (rbm_amd.vocab_parallel)."""
         self.model = model
         self.kind = model.code()
         self.engine = model.sas.engine() if self.kind == "sas" else model.engine()
@@ -70,6 +74,14 @@ class FusedTrainStep:
         self.dp = dpx.world() > 1 if dp is None else bool(dp)
         self.bucket_numel = bucket_numel
         self.overlap = self.dp and (bucket_numel is None if overlap is None else bool(overlap))
+        self.vshard = None
+        if vocab_shard:
+            from .vocab_parallel import VocabShard
+            if not (self.dp and self.kind == "bert"):
+                raise ValueError("vocab_shard needs a data-parallel BERT step")
+            self.vshard = VocabShard(self.flat.shapes["out.weight"][0], self.pg)
+            self.engine.vocab_shard = self.vshard
+            self.overlap = True
         self.max_labelled = max_labelled
         dev = self.flat.device
         self.loss_out = torch.zeros(4, dtype=torch.float32, device=dev)
@@ -78,7 +90,8 @@ class FusedTrainStep:
         self.loss_val = torch.zeros(1, dtype=torch.float32, device=dev)
         self.graphs = None
         self.static = None
-        self.exchange = dpx.BucketedExchange(self.flat.grad, self._buckets(), self.pg) if self.overlap else None
+        self.exchange = dpx.BucketedExchange(self.flat.grad, self._buckets(), self.pg, partial=self.vshard is not None) \
+            if self.overlap else None
 
     # ---------------------------------------------------------------- pieces
     def _divisor(self, local_count):
@@ -96,6 +109,9 @@ class FusedTrainStep:
                 -(-f.view("pos_emb.weight").numel() // 64) * 64
             assert cut == min(o for n, o in f.offsets.items() if n not in ("item_emb.weight", "pos_emb.weight"))
             return {"final": (0, cut), "dense": (cut, f.grad.numel())}
+        if self.kind == "bert" and getattr(self, "vshard", None) is not None:
+            # the output layer's rows are rank-owned (complete gradients, no exchange); the loss is global already
+            return {"final": (0, f.offsets["out.weight"])}
         if self.kind == "bert":
             cut = f.offsets["out.weight"]
             assert f.offsets["out.bias"] > cut and all(o < cut for n, o in f.offsets.items()
@@ -109,9 +125,10 @@ class FusedTrainStep:
         eng = self.engine
         sp = None
         if split is not None:
-            def sp(tag):
-                self.flat.aux[dpx.LOSS_SUM:dpx.COUNT + 1].copy_(self.loss_out[0:2])
-                split(tag)
+            def sp(tag, action=None):
+                if action is None:
+                    self.flat.aux[dpx.LOSS_SUM:dpx.COUNT + 1].copy_(self.loss_out[0:2])
+                split(tag, action)
         if self.kind == "sas":
             seq, pos, neg = batch
             pl, nl, saved = eng.forward(seq, pos, neg, True, clone_seed=False)
@@ -139,9 +156,23 @@ class FusedTrainStep:
         if self.dp:
             dpx.allreduce_grads(self.flat.grad, self.pg, self.bucket_numel)
 
+    def _adam_ranges(self):
+        if self.vshard is None:
+            return None
+        f, vs = self.flat, self.vshard
+        ow = f.offsets["out.weight"]
+        V1, d = f.shapes["out.weight"]
+        lo, hi = vs.owned_ranges(ow, d)
+        # everything before out.weight, the owned rows, then out.bias (updated whole: 16-B aligned ranges) and on
+        return [(0, ow), (lo, hi), (ow + V1 * d, f.numel)]
+
     def _update(self):
         sb = self.engine.seed_base
-        if self.dp:
+        if self.vshard is not None:
+            # the sharded head normalised by the global count already; the loss is the global batch's
+            self.loss_val.copy_(self.loss_out[2:3])
+            self.opt.step(seed_base=sb, ranges=self._adam_ranges())
+        elif self.dp:
             torch.div(self.flat.aux[dpx.LOSS_SUM:dpx.LOSS_SUM + 1], self.flat.aux[dpx.COUNT:dpx.COUNT + 1],
                       out=self.loss_val)
             self.opt.step(grad_divisor=self.flat.aux[dpx.COUNT:dpx.COUNT + 1], seed_base=sb)
@@ -153,7 +184,7 @@ class FusedTrainStep:
         """batch: SAS (seq, pos, neg) / BERT (tokens, labels) int64 device tensors.  Returns the
         device loss (the global batch's mean loss, as the reference's calculate_loss)."""
         if self.overlap:
-            self._compute(*batch, split=self.exchange.launch)
+            self._compute(*batch, split=self._eager_split)
             self.exchange.launch("final")
             self.exchange.finish()
         else:
@@ -214,9 +245,21 @@ class FusedTrainStep:
         self.opt.state.zero_()
         self.opt.state[0] = steps.pop() if steps else 0.0
 
+    def gather_vocab_shards(self):
+        """Vocabulary-sharded step: make this rank's out.weight / out.bias (and their Adam moments) hold every
+        owner's rows -- the reference layout a checkpoint stores.  Collective: call on every rank."""
+        if self.vshard is None:
+            return
+        torch.cuda.synchronize()
+        for name in ("out.weight", "out.bias"):
+            for buf in (self.flat.data, self.opt.m, self.opt.v):
+                self.vshard.gather_rows(self.flat.view(name, buf))
+        self.engine.sync_compute_weights()
+
     def checkpoint(self, epoch=None):
         """{'model_state_dict', 'optimizer_state_dict'[, 'epoch']} as the reference's loggers save it
-        (BS/trainers/base.py:255-259, BS/loggers.py:48-58)."""
+        (BS/trainers/base.py:255-259, BS/loggers.py:48-58).  Vocabulary-sharded: collective (all ranks)."""
+        self.gather_vocab_shards()
         d = {"model_state_dict": self.model.state_dict(), "optimizer_state_dict": self.optimizer_state_dict()}
         if epoch is not None:
             d["epoch"] = epoch
@@ -278,12 +321,13 @@ class FusedTrainStep:
             self.g_update = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g_update):
                 self._update()
-        segs = [g for g, _ in self.g_segments] if self.g_segments else [self.g_compute]
+        segs = [seg[0] for seg in self.g_segments] if self.g_segments else [self.g_compute]
         self.graphs = tuple(segs) + ((self.g_update,) if self.dp else ())
 
     def _capture_segments(self, compute):
-        """Capture compute(split) as consecutive graphs, a new one begun at every split(tag): [(graph, tag)],
-        the last tagged "final".  All segments share one memory pool and one capture stream."""
+        """Capture compute(split) as consecutive graphs, a new one begun at every split(tag, action):
+        [(graph, tag, action)], the last tagged "final".  At replay, after each graph: its action (a collective of
+        the computation) or its bucket's all-reduce.  All segments share one memory pool and one capture stream."""
         torch.cuda.synchronize()
         pool = torch.cuda.graph_pool_handle()
         s = torch.cuda.Stream()
@@ -292,25 +336,34 @@ class FusedTrainStep:
         with torch.cuda.stream(s):
             cur[0].capture_begin(pool=pool)
 
-            def split(tag):
+            def split(tag, action=None):
                 cur[0].capture_end()
-                segs.append((cur[0], tag))
+                segs.append((cur[0], tag, action))
                 cur[0] = torch.cuda.CUDAGraph()
                 cur[0].capture_begin(pool=pool)
             try:
                 compute(split)
             finally:
                 cur[0].capture_end()
-            segs.append((cur[0], "final"))
+            segs.append((cur[0], "final", None))
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         return segs
 
+    def _eager_split(self, tag, action=None):
+        if action is not None:
+            action()
+        else:
+            self.exchange.launch(tag)
+
     def _replay_graphs(self):
         if self.overlap:
-            for g, tag in self.g_segments:
+            for g, tag, action in self.g_segments:
                 g.replay()
-                self.exchange.launch(tag)     # RCCL all-reduce of the bucket, overlapping the next segment
+                if action is not None:
+                    action()                  # a collective of the computation itself (vocabulary shards)
+                elif tag in self.exchange.buckets:
+                    self.exchange.launch(tag)  # RCCL all-reduce of the bucket, overlapping the next segment
             self.exchange.finish()
             self.g_update.replay()
             return self.loss_val

@@ -143,3 +143,35 @@ def test_ranks_have_different_counts():
     counts = [int((pos[r::2] != 0).sum()) for r in range(2)]
     assert counts[0] != counts[1]
     _ = np
+
+
+def _shard_worker(rank, world, port, V1, out_dir):
+    import sys
+    sys.path.insert(0, ROOT)
+    import rbm_amd  # noqa: F401
+    from rbm_amd.vocab_parallel import VocabShard
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        vs = VocabShard(V1)
+        full = torch.full((V1, 3), -1.0)
+        full[vs.v0:vs.v1] = torch.arange(vs.v0, vs.v1, dtype=torch.float32)[:, None]   # only owned rows are valid
+        vs.gather_rows(full)
+        torch.save({"v": (vs.v0, vs.v1), "full": full}, os.path.join(out_dir, f"s{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,V1", [(2, 1001), (3, 300), (2, 129)])
+def test_vocab_shard_ranges_and_gather(tmp_path, world, V1):
+    """rbm_amd.vocab_parallel.VocabShard: 128-aligned disjoint shards covering [0, V1); gather_rows assembles
+    the owners' rows on every rank (the checkpoint layout of the vocabulary-sharded BERT head)."""
+    mp.spawn(_shard_worker, args=(world, _free_port(), V1, str(tmp_path)), nprocs=world, join=True)
+    spans = []
+    for r in range(world):
+        d = torch.load(tmp_path / f"s{r}.pt", weights_only=True)
+        spans.append(tuple(d["v"]))
+        assert torch.equal(d["full"], torch.arange(V1, dtype=torch.float32)[:, None].expand(V1, 3))
+    assert spans[0][0] == 0 and spans[-1][1] == V1
+    assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+    assert all(v0 % 128 == 0 for v0, _ in spans)
