@@ -104,6 +104,7 @@ SIGNATURES = {
     "rs_kernel_stamp_count": [],
     "rs_kernel_stamp_kinds": [C.POINTER(i32), i32],
     "rs_wall_clock_khz": [C.POINTER(i32)],
+    "rs_attn_bwd_plan": [i64, i64, i64, i32, vp, C.POINTER(i32)],
     "rs_abi_version": [],
 }
 

@@ -783,6 +783,19 @@ static bool make_plan(AttnLdsArgs& a, int ntiles, bool dkv, int slots) {
   return true;
 }
 
+// host-only view of the causal backward plan (tests/test_attn_plan.py checks its invariants on the CPU)
+extern "C" int rs_attn_bwd_plan(int64_t B, int64_t T, int64_t H, int dkv, uint32_t* plan, int* nsplit) {
+  if (B <= 0 || T <= 0 || H <= 0 || !plan || !nsplit) return RS_ERR_ARG;
+  AttnLdsArgs a = {};
+  a.B = B; a.T = T; a.H = H; a.mask_kind = 0;
+  const int nq = (int)cdiv(T, 16);
+  a.nsplit = pick_split(B * H, nq);
+  *nsplit = a.nsplit;
+  const bool ok = nq >= 8 && make_plan(a, nq, dkv != 0, dkv ? DKV_SLOTS : DQ_SLOTS);
+  memcpy(plan, a.plan, sizeof(a.plan));
+  return ok ? 0 : RS_ERR_UNSUPPORTED;
+}
+
 template <int DH>
 static hipError_t bwd_t(AttnLdsArgs& a, hipStream_t s) {
   const int nq = (int)cdiv(a.T, 16);
