@@ -74,6 +74,13 @@ class FusedTrainStep:
         self.dp = dpx.world() > 1 if dp is None else bool(dp)
         self.bucket_numel = bucket_numel
         self.overlap = self.dp and (bucket_numel is None if overlap is None else bool(overlap))
+        if self.dp:
+            # dropout masks hash (site salt, step seed, local element index): without a per-rank seed every rank
+            # would draw the same masks for its local rows; rank r starts its step seed at r << 40
+            import torch.distributed as dist
+            r = dist.get_rank(self.pg)
+            if r:
+                self.engine.seed_base.fill_(r << 40)
         self.vshard = None
         if vocab_shard:
             from .vocab_parallel import VocabShard
