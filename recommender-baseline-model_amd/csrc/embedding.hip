@@ -79,13 +79,13 @@ __global__ __launch_bounds__(256) void embed_bwd_pos_kernel(const int64_t* __res
 
 // vectorized positional-gradient sum: block = position t, 256 threads = CPR chunk-columns x RG
 // batch groups, fixed-order LDS combine (deterministic)
-template <typename T, int CPR>
-__global__ __launch_bounds__(256) void embed_bwd_pos_v_kernel(const int64_t* __restrict__ ids, int64_t rows,
+template <typename T, int CPR, int NTB = 256>
+__global__ __launch_bounds__(NTB) void embed_bwd_pos_v_kernel(const int64_t* __restrict__ ids, int64_t rows,
                                                               int64_t T_, const T* __restrict__ dx, int64_t d,
                                                               int mode, float drop_p, uint64_t salt,
                                                               const uint64_t* seed_base, float* __restrict__ dpos,
                                                               int accumulate) {
-  constexpr int V = Vec<T>::N, RG = 256 / CPR;
+  constexpr int V = Vec<T>::N, RG = NTB / CPR;
   const uint64_t seed = eff_seed(salt, seed_base);
   const int64_t t = blockIdx.x, nb = rows / T_;
   const int cc = threadIdx.x % CPR, rg = threadIdx.x / CPR;
@@ -125,7 +125,7 @@ __global__ __launch_bounds__(256) void embed_bwd_pos_v_kernel(const int64_t* __r
 #pragma unroll
   for (int j = 0; j < V; ++j) red[rg][cc * V + j] = acc[j];
   __syncthreads();
-  for (int c = threadIdx.x; c < d; c += 256) {
+  for (int c = threadIdx.x; c < d; c += NTB) {
     float sum = 0.f;
     for (int g2 = 0; g2 < RG; ++g2) sum += red[g2][c];
     dpos[t * d + c] = accumulate ? dpos[t * d + c] + sum : sum;
@@ -206,8 +206,8 @@ static hipError_t embed_bwd_t(int mode, const int64_t* ids, int64_t rows, int64_
     constexpr int V = Vec<T>::N;
     const int64_t cpr = d / V;
     const bool vec = (d % V == 0) && ((uintptr_t)dx % 16 == 0);
-    if (vec && cpr <= 16)
-      hipLaunchKernelGGL((embed_bwd_pos_v_kernel<T, 16>), dim3((unsigned)T_), dim3(256), 0, s, ids, rows, T_,
+    if (vec && cpr <= 16)   // 512 threads: 32 batch groups, each row's loads and mask hashes spread over 8 waves
+      hipLaunchKernelGGL((embed_bwd_pos_v_kernel<T, 16, 512>), dim3((unsigned)T_), dim3(512), 0, s, ids, rows, T_,
                          (const T*)dx, d, mode, drop_p, seed, seed_base, dpos, acc_pos);
     else if (vec && cpr <= 32)
       hipLaunchKernelGGL((embed_bwd_pos_v_kernel<T, 32>), dim3((unsigned)T_), dim3(256), 0, s, ids, rows, T_,
