@@ -133,6 +133,9 @@ def _roof(kernel, us, flops, nbytes, dtype, note, live_us=None):
                  f"same launch re-timed alone with HIP events")
     ai = flops / nbytes if nbytes else float("inf")
     peak_f = MI355X_BF16_TFLOPS if dtype == "bf16" else MI355X_F32_TFLOPS
+    # both utilisations of the same live launch time, whichever bound the arithmetic intensity selects
+    util = {"mfma_util": round(flops / (us * 1e-6) / 1e12 / peak_f, 4),
+            "hbm_util": round(nbytes / (us * 1e-6) / 1e9 / MI355X_HBM_GBS, 4)}
     ridge = peak_f * 1e12 / (MI355X_HBM_GBS * 1e9)
     traffic = None
     tpath = os.path.join(ROOT, "profiles", "traffic.json")
@@ -144,13 +147,13 @@ def _roof(kernel, us, flops, nbytes, dtype, note, live_us=None):
                 "frac": round(ach / MI355X_HBM_GBS, 4), "traffic": traffic, "avg_launch_us": round(us, 2),
                 "isolated_launch_us": round(iso_us, 2), "live_samples": len(live_us or ()),
                 "algorithmic_bytes_per_launch": int(nbytes), "algorithmic_flops_per_launch": int(flops),
-                "arith_intensity": round(ai, 1), "note": note}
+                "arith_intensity": round(ai, 1), **util, "note": note}
     ach = flops / (us * 1e-6) / 1e12
     return {"kernel": kernel, "bound": "mfma", "achieved": round(ach, 2), "peak": peak_f, "unit": "TFLOP/s",
             "frac": round(ach / peak_f, 4), "traffic": traffic, "avg_launch_us": round(us, 2),
             "isolated_launch_us": round(iso_us, 2), "live_samples": len(live_us or ()),
             "algorithmic_bytes_per_launch": int(nbytes), "algorithmic_flops_per_launch": int(flops),
-            "arith_intensity": round(ai, 1), "note": note}
+            "arith_intensity": round(ai, 1), **util, "note": note}
 
 
 # ops wrapper of the dominant kernel per config (most device time per step in the rocprof profiles):
