@@ -69,6 +69,10 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse the "
                          "multi-process path with several ranks on one GPU)")
+    ap.add_argument("--steps-per-graph", default="auto",
+                    help="training steps unrolled into one graph replay (single GPU; 'auto' = 4 when --steps and "
+                         "--warmup are multiples of 4, else 1); every step still runs on its own batch with its "
+                         "own Adam update")
     ap.add_argument("--nbatches", type=int, default=8, help="distinct synthetic batches cycled through")
     ap.add_argument("--sampler", default="host", choices=["host", "device"],
                     help="SAS: 'device' = batches drawn each step by the on-device WarpSampler "
@@ -318,13 +322,20 @@ def main():
                                                   device="cuda")
     stamps = None if sbuf is None else (sbuf, (dominant(cfg),))
 
+    if args.steps_per_graph == "auto":
+        S = 4 if (world == 1 and not args.no_graph and args.steps % 4 == 0 and args.warmup % 4 == 0) else 1
+    else:
+        S = int(args.steps_per_graph)
+        if S > 1 and (world > 1 or args.no_graph or args.steps % S or args.warmup % S):
+            raise SystemExit("--steps-per-graph > 1 needs one GPU, graphs, and --steps/--warmup multiples of it")
+
     if args.sampler == "device" and cfg["model"] == "sas":
         import rbm_amd.data as synth
         from rbm_amd.dataloaders import DeviceWarpSampler
         users = synth.user_histories(np.random.default_rng(77 + rank), cfg.get("users", 6040), cfg["T"], cfg["V"],
                                      shape=cfg["shape"])
         sampler = DeviceWarpSampler(users, cfg["V"], B, cfg["T"], seed=5 + rank)
-        trainer.capture_sampled(sampler, stamps=stamps)
+        trainer.capture_sampled(sampler, stamps=stamps, steps_per_graph=S)
         batches = [()]
         run = trainer.replay_sampled
     elif args.sampler == "device":
@@ -336,16 +347,20 @@ def main():
                                      shape=cfg["shape"])
         sampler = DeviceBertMasker(users, cfg["V"], B, cfg["T"], cfg["mask"], seed=5 + rank)
         sampler.new_epoch()
-        trainer.capture_sampled(sampler, stamps=stamps)
+        trainer.capture_sampled(sampler, stamps=stamps, steps_per_graph=S)
         batches = [()]
         run = trainer.replay_sampled
     elif args.no_graph:
         run = trainer.step
     else:
-        trainer.capture(*batches[0], stamps=stamps)
-        batches = [(torch.stack(b),) for b in batches]     # one device copy per replay (replay_packed)
+        trainer.capture(*batches[0], stamps=stamps, steps_per_graph=S)
+        batches = [torch.stack(b) for b in batches]     # one device copy per replay (replay_packed)
+        if S > 1:   # S consecutive batches per replay, still cycling through all of them
+            batches = [torch.stack([batches[(j * S + k) % len(batches)] for k in range(S)])
+                       for j in range(max(1, len(batches) // S))]
+        batches = [(b,) for b in batches]
         run = trainer.replay_packed
-    for i in range(args.warmup):
+    for i in range(args.warmup // S):
         loss = run(*batches[i % len(batches)])
     torch.cuda.synchronize()
     if world > 1:
@@ -356,7 +371,7 @@ def main():
         sbuf[:4] = torch.tensor([int(trainer.opt.state[0].item()), args.steps, NMARK, WAVES], dtype=torch.int64)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
+    for i in range(args.steps // S):
         loss = run(*batches[i % len(batches)])
     if world > 1:
         dist.barrier()
@@ -366,7 +381,7 @@ def main():
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     elapsed = tt.item()
-    final_loss = float(loss.float().sum().item())
+    final_loss = float(loss.float().reshape(-1)[-1].item())
 
     live = None
     if sbuf is not None:
@@ -396,7 +411,7 @@ def main():
                        "global_batch": world * B, "per_gpu_batch": B, "seq_len": cfg["T"], "hidden": cfg["d"],
                        "blocks": cfg["L"], "heads": cfg["h"], "num_items": cfg["V"], "parallelism": f"dp{world}",
                        "hip_graph": not args.no_graph, "bench_config": args.config,
-                       "sampler": args.sampler},
+                       "sampler": args.sampler, "steps_per_graph": S},
             "final_loss": round(final_loss, 5),
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -292,12 +292,17 @@ class SASEngine:
                                  gl, s["muf"], s["rf"], dx, lnh)
             segs = ops.ln_partial_segments(lnh, M, d, G("last_layernorm.weight"), G("last_layernorm.bias"))
             torch.cuda.current_stream().wait_event(ev)
-            dx = self._backward_blocks_fused(s, dx, grad, segs)
+
+            def embedding_grads(dx):
+                ops.item_grad(iws, 3, M, dx, math.sqrt(d), p, self.salt["emb"], sb, s["f"], dpl, dnl,
+                              G("item_emb.weight"))
+                ops.embed_bwd(0, ids, T, dx, math.sqrt(d), p, self.salt["emb"], sb, None, G("pos_emb.weight"))
+            side = os.environ.get("RS_SAS_EMB_GRAD_SIDE", "1") != "0"
+            dx = self._backward_blocks_fused(s, dx, grad, segs, tail=embedding_grads if side else None)
+            if not side:
+                embedding_grads(dx)
             if split is not None:
-                split("dense")          # every block / LayerNorm gradient is final (data-parallel overlap)
-            ops.embed_bwd(0, ids, T, dx, math.sqrt(d), p, self.salt["emb"], sb, None, G("pos_emb.weight"))
-            ops.item_grad(iws, 3, M, dx, math.sqrt(d), p, self.salt["emb"], sb, s["f"], dpl, dnl,
-                          G("item_emb.weight"))
+                split("dense")          # every parameter gradient is final (data-parallel overlap)
             return
         df = e("df", (M, d))
         ops.sampled_logits_bwd(s["f"], self.W("item_emb.weight"), s["pos"], s["neg"], dpl, dnl, df,
@@ -386,11 +391,13 @@ class SASEngine:
         ops.transpose_bf16(self._wT_desc, self._wT_tiles, self.flat.bf16, self._wT)
         return self._wT
 
-    def _backward_blocks_fused(self, s, dx, grad, extra_segs=()):
+    def _backward_blocks_fused(self, s, dx, grad, extra_segs=(), tail=None):
         """SAS blocks' backward with rs_sas_block_out_bwd / rs_sas_block_in_bwd (rowfused.hip) for the
         row-local chains; then ALL ten weight gradients and the four LayerNorm affine partial sets in
         one grouped GEMM launch + one grouped reduction (rs_wgrad_grouped, wgrad.hip).  Returns the
-        gradient at the embedding output."""
+        gradient at the embedding output.  tail(dx): work on that gradient alone (the embedding tables'
+        gradients), issued on the side stream so it runs beside the grouped weight-gradient launch (both are
+        latency-bound; joined before returning)."""
         B, T, p, ids, sb = s["B"], s["T"], s["p"], s["ids"], s["sb"]
         M, d, H, Dh, L = B * T, self.d, self.H, self.Dh, self.L
         e = self._buf
@@ -428,7 +435,19 @@ class SASEngine:
         rows = self._wgrad_rows(M, L * 6)
         wslab = self.ws.get("wslab", (ops.wgrad_grouped_slab_numel([(d, d)] * 4 * L + [(2 * d, d)] * L, M, rows),),
                             torch.float32)
+        join = None
+        if tail is not None:
+            cur = torch.cuda.current_stream()
+            fork = torch.cuda.Event()
+            fork.record(cur)
+            self._side.wait_event(fork)
+            with torch.cuda.stream(self._side):
+                tail(dx)
+                join = torch.cuda.Event()
+                join.record(self._side)
         ops.wgrad_grouped(probs, M, rows, wslab, extra=segs)
+        if join is not None:
+            torch.cuda.current_stream().wait_event(join)
         return dx
 
     @staticmethod

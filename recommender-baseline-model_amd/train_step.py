@@ -97,6 +97,7 @@ class FusedTrainStep:
         self.loss_val = torch.zeros(1, dtype=torch.float32, device=dev)
         self.graphs = None
         self.static = None
+        self.steps_per_graph = 1
         self.exchange = dpx.BucketedExchange(self.flat.grad, self._buckets(), self.pg, partial=self.vshard is not None) \
             if self.overlap else None
 
@@ -278,17 +279,26 @@ class FusedTrainStep:
         self.load_optimizer_state_dict(d["optimizer_state_dict"])
 
     # ---------------------------------------------------------------- HIP graphs
-    def capture(self, *example_batch, warmup=2, stamps=None):
+    def capture(self, *example_batch, warmup=2, stamps=None, steps_per_graph=1):
         """Capture the step into HIP graphs; example_batch fixes the shapes.
         stamps: (int64 device buffer, kind names): the compute graph is captured with kernel stamps enabled
         for those kinds (ops.kernel_stamps against the optimizer's step count), so every replay records the
-        begin/end ticks of its rs_attn_bwd / rs_wgrad_grouped launches there (bench.py's in-step timing)."""
+        begin/end ticks of its rs_attn_bwd / rs_wgrad_grouped launches there (bench.py's in-step timing).
+        steps_per_graph=S > 1 (single device): S whole training steps -- each on its own batch, each with its
+        own Adam update -- are unrolled into ONE graph, so a replay costs one launch and one input copy per S
+        steps; replay_packed() then takes the S batches stacked as [S, n_inputs, ...] and returns the S
+        steps' losses."""
+        S = self._unroll_check(steps_per_graph)
         # one packed static buffer when the inputs share shape and dtype: replay_packed() then refills
         # all of them with ONE device copy (the bench stacks its batches the same way)
         same = all(t.shape == example_batch[0].shape and t.dtype == example_batch[0].dtype for t in example_batch)
+        if S > 1 and not same:
+            raise ValueError("steps_per_graph > 1 needs inputs of one shape and dtype (one packed buffer)")
         if same:
-            self.packed = torch.stack([t for t in example_batch]).contiguous()
-            self.static = list(self.packed.unbind(0))
+            one = torch.stack([t for t in example_batch])
+            self.packed = (torch.stack([one] * S) if S > 1 else one).contiguous()
+            self.static_steps = [list(p.unbind(0)) for p in (self.packed.unbind(0) if S > 1 else [self.packed])]
+            self.static = self.static_steps[0]
         else:
             self.packed = None
             self.static = [t.clone() for t in example_batch]
@@ -299,10 +309,34 @@ class FusedTrainStep:
                 self.step(*self.static)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        self._capture_graphs(lambda split=None: self._compute(*self.static, split=split), stamps)
+        if S > 1:
+            self._capture_graphs(self._unrolled(lambda k: self.static_steps[k]), stamps, unrolled=True)
+        else:
+            self._capture_graphs(lambda split=None: self._compute(*self.static, split=split), stamps)
         return self
 
-    def _capture_graphs(self, compute, stamps=None):
+    def _unroll_check(self, steps_per_graph):
+        S = int(steps_per_graph)
+        if S < 1:
+            raise ValueError("steps_per_graph must be >= 1")
+        if S > 1 and self.dp:
+            raise ValueError("steps_per_graph > 1 is single-device only (DP exchanges gradients between steps)")
+        self.steps_per_graph = S
+        self.loss_steps = torch.zeros(S, dtype=torch.float32, device=self.flat.device)
+        return S
+
+    def _unrolled(self, inputs, sample=None):
+        """compute() for an unrolled graph: S x (sample, forward + backward, Adam, keep the loss)."""
+        def compute(split=None):
+            for k in range(self.steps_per_graph):
+                if sample is not None:
+                    sample()
+                self._compute(*inputs(k))
+                self._update()
+                self.loss_steps[k:k + 1].copy_(self.loss_out[2:3])
+        return compute
+
+    def _capture_graphs(self, compute, stamps=None, unrolled=False):
         """The compute graph (+ the optimizer in the same graph on one device).  DP: the compute graph is cut at
         every bucket the backward finishes (overlap: segments replayed with that bucket's all-reduce launched
         between them) or ends after the backward, and the optimizer is a separate graph after the exchange."""
@@ -316,7 +350,7 @@ class FusedTrainStep:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     compute()
-                    if not self.dp:
+                    if not self.dp and not unrolled:
                         self._update()
                 self.g_compute = g
                 self.g_segments = None
@@ -375,12 +409,14 @@ class FusedTrainStep:
             self.g_update.replay()
             return self.loss_val
         self.g_compute.replay()
+        if self.steps_per_graph > 1:
+            return self.loss_steps
         if self.dp:
             self._exchange()            # RCCL all-reduce, eager, on the current stream
             self.g_update.replay()
         return self.loss_val if self.dp else self.loss_out[2:3]
 
-    def capture_sampled(self, sampler, warmup=2, stamps=None):
+    def capture_sampled(self, sampler, warmup=2, stamps=None, steps_per_graph=1):
         """Capture sampling (rbm_amd.dataloaders.DeviceWarpSampler for SAS, DeviceBertMasker for BERT, into
         static buffers) together with the step, so ``replay_sampled()`` runs a whole training iteration --
         batch construction included -- as one graph replay (the reference's sampler / DataLoader +
@@ -388,6 +424,7 @@ class FusedTrainStep:
         want = 3 if self.kind == "sas" else 2
         if getattr(sampler, "n_outputs", None) != want:
             raise ValueError(f"the {self.kind} step needs a sampler producing {want} tensors")
+        S = self._unroll_check(steps_per_graph)
         self.sampler = sampler
         shape = (sampler.batch_size, sampler.max_len)
         self.packed = torch.zeros((want,) + shape, dtype=torch.int64, device=self.flat.device)
@@ -401,6 +438,11 @@ class FusedTrainStep:
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
 
+        if S > 1:
+            self._capture_graphs(self._unrolled(lambda k: self.static, lambda: sampler.sample_into(*self.static)),
+                                 stamps, unrolled=True)
+            return self
+
         def compute(split=None):
             sampler.sample_into(*self.static)
             self._compute(*self.static, split=split)
@@ -412,13 +454,19 @@ class FusedTrainStep:
         return self._replay_graphs()
 
     def replay_packed(self, packed):
-        """replay() for a batch already stacked as one tensor [n_inputs, ...] (see capture)."""
+        """replay() for a batch already stacked as one tensor [n_inputs, ...] (see capture); with
+        steps_per_graph=S > 1, S batches stacked as [S, n_inputs, ...] -> the S steps' losses."""
+        if self.steps_per_graph > 1 and packed.shape != self.packed.shape:
+            raise ValueError(f"replay_packed: expected {tuple(self.packed.shape)} (steps_per_graph batches), "
+                             f"got {tuple(packed.shape)}")
         if self.packed is None:
             return self.replay(*packed.unbind(0))
         self.packed.copy_(packed, non_blocking=True)
         return self._replay_graphs()
 
     def replay(self, *batch):
+        if self.steps_per_graph > 1:
+            raise ValueError("an unrolled graph (steps_per_graph > 1) replays through replay_packed()")
         for dst, src in zip(self.static, batch):
             dst.copy_(src, non_blocking=True)
         return self._replay_graphs()
