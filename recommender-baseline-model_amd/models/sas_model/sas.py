@@ -407,6 +407,11 @@ class SASEngine:
         lnp = self.ws.get("lnp", (L, 2, 2 * d * nb), torch.float32)
         wat = self.ws.get("attn", (B * H * T,), torch.float32)
         probs, segs = [], list(extra_segs)
+        # opt-in (RS_SAS_WGRAD_SIDE=1): the upper blocks' weight gradients on the side stream while the lower
+        # blocks' backward proceeds.  Measured slower at cfg2 (0.385 -> 0.410 ms: the attention backward loses
+        # CUs to the grouped GEMM), neutral at cfg3, so off by default
+        early = tail is not None and L > 1 and os.environ.get("RS_SAS_WGRAD_SIDE", "0") == "1"
+        keep, rows1 = [], self._wgrad_rows(M, 6)
         for i in reversed(range(L)):
             pre, fw = f"attention_layers.{i}.", f"forward_layers.{i}."
             inT = wT[i, 0:3].reshape(d, 3 * d)
@@ -432,8 +437,23 @@ class SASEngine:
             segs += ops.ln_partial_segments(lnp[i, 1], M, d, G(f"attention_layernorms.{i}.weight"),
                                             G(f"attention_layernorms.{i}.bias"))
             dx = dxi
-        rows = self._wgrad_rows(M, L * 6)
-        wslab = self.ws.get("wslab", (ops.wgrad_grouped_slab_numel([(d, d)] * 4 * L + [(2 * d, d)] * L, M, rows),),
+            if early and i > 0:
+                # this block's five problems + its two LayerNorm partial sets, on the side stream
+                lseg = segs[-4:]
+                del segs[-4:]
+                ws1 = self.ws.get("wslab_side", (ops.wgrad_grouped_slab_numel([(d, d)] * 4 + [(2 * d, d)], M, rows1),),
+                                  torch.float32)
+                fork = torch.cuda.Event()
+                fork.record(torch.cuda.current_stream())
+                self._side.wait_event(fork)
+                with torch.cuda.stream(self._side):
+                    ops.wgrad_grouped(probs[-5:], M, rows1, ws1, extra=lseg)
+                keep.append(probs[-5:])
+                del probs[-5:]
+        nt = 6 * (1 if early else L)
+        rows = self._wgrad_rows(M, nt)
+        nl = 1 if early else L
+        wslab = self.ws.get("wslab", (ops.wgrad_grouped_slab_numel([(d, d)] * 4 * nl + [(2 * d, d)] * nl, M, rows),),
                             torch.float32)
         join = None
         if tail is not None:
