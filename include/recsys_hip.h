@@ -186,19 +186,25 @@ int rs_splitk_scatter_rows(int dtype, const float* slab, int splits, int64_t cap
 
 /* torch.optim.Adam step (BS/trainers/base.py:225-228; amsgrad=False) over a
  * flat fp32 buffer.  hyper (device fp32[5]) = {lr, beta1, beta2, eps, weight_decay}.
- * state (device double[4]): rs_adam_prepare does state[0] += 1 (the step count) and
- * forms state[1] = lr/(1-beta1^step), state[2] = sqrt(1-beta2^step) in double
- * precision, like torch's Python-float scalars, and state[3] = 1/(*grad_divisor) (1 when null: the
+ * state (device double[8]; double[144] for rs_adam_prepare_step; zero-initialised): rs_adam_prepare does state[0] += 1 (the step count t)
+ * and forms state[1] = lr/(1-beta1^t), state[2] = sqrt(1-beta2^t) (1-b^t as -expm1(t*log1p(b-1)) in
+ * fp32: no cancellation at beta2 near 1), state[3] = 1/(*grad_divisor) (1 when null: the
  * data-parallel step all-reduces UNnormalised gradients plus the valid-position count and
  * divides here, so the summed gradient equals the single-device mean's).  rs_adam_step then
  * updates (grad scaled by state[3])
  * p, m, v (and writes the bf16 copy of p to p_bf16 when non-null); zero_grad != 0 also clears g
  * (the next step's accumulation starts from zero without a separate fill).  rs_adam_prepare
- * also advances *seed_base when non-null (the next step's dropout masks, as rs_seed_advance). */
+ * also advances *seed_base when non-null (the next step's dropout masks, as rs_seed_advance).
+ * rs_adam_prepare_step = rs_adam_prepare + rs_adam_step in ONE launch (every workgroup derives step
+ * t's scalars; the last to finish publishes them; state[7] and state[16 + 16 k], k < 8, are its arrival
+ * counters and must be 0 between launches); further ranges of the same step then use rs_adam_step.  Same results bit for bit. */
 int rs_adam_prepare(double* state, const float* hyper, const float* grad_divisor, uint64_t* seed_base,
                     void* stream);
 int rs_adam_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16,
                  const double* state, const float* hyper, int zero_grad, void* stream);
+int rs_adam_prepare_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, double* state,
+                         const float* hyper, int zero_grad, const float* grad_divisor, uint64_t* seed_base,
+                         void* stream);
 
 /* dst_bf16[i] = bf16(src[i]) */
 int rs_cast_bf16(int64_t n, const float* src, void* dst, void* stream);

@@ -10,28 +10,54 @@
 #include "common.h"
 #include "../../include/recsys_hip.h"
 
-__global__ void adam_prepare_kernel(double* state, const float* hyper, const float* divisor, uint64_t* seed_base) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  if (seed_base) *seed_base += 1;   // next step's dropout masks (rs_seed_advance folded in)
-  state[3] = divisor ? 1.0 / (double)divisor[0] : 1.0;
-  const double step = state[0] + 1.0;
-  state[0] = step;
-  const double lr = hyper[0], b1 = hyper[1], b2 = hyper[2];
-  const double bc1 = 1.0 - pow(b1, step);
-  const double bc2 = 1.0 - pow(b2, step);
-  state[1] = lr / bc1;            // step_size
-  state[2] = sqrt(bc2);           // bias_correction2_sqrt
+// Bias corrections of step t, torch.optim.Adam (bias_correction1 = 1 - b1^t, step_size = lr / bc1,
+// bias_correction2_sqrt = sqrt(1 - b2^t)).  1 - b^t is formed as -expm1(t * log1p(b - 1)): no cancellation
+// for b2 near 1 (the float pow form loses ~3 digits at b2 = 0.999, t = 1).
+struct AdamScalars { float step_size, bc2s, gs; };
+__device__ __forceinline__ AdamScalars adam_scalars(double t, const float* hyper, const float* divisor) {
+  const float tf = (float)t, lr = hyper[0], b1 = hyper[1], b2 = hyper[2];
+  const float bc1 = -expm1f(tf * log1pf(b1 - 1.f));
+  const float bc2 = -expm1f(tf * log1pf(b2 - 1.f));
+  return {lr / bc1, sqrtf(bc2), divisor ? 1.f / divisor[0] : 1.f};
 }
 
-template <bool BF16OUT>
+__device__ __forceinline__ void adam_commit(double* state, double t, AdamScalars c, uint64_t* seed_base) {
+  if (seed_base) *seed_base += 1;   // next step's dropout masks (rs_seed_advance folded in)
+  state[0] = t;
+  state[1] = c.step_size;
+  state[2] = c.bc2s;
+  state[3] = c.gs;
+}
+
+__global__ void adam_prepare_kernel(double* state, const float* hyper, const float* divisor, uint64_t* seed_base) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const double t = state[0] + 1.0;
+  adam_commit(state, t, adam_scalars(t, hyper, divisor), seed_base);
+}
+
+// PREP: the launch also does rs_adam_prepare's work -- every workgroup derives step t = state[0] + 1's
+// scalars itself, and the LAST workgroup to finish (arrival counter in state[7]) writes them back, advances
+// the step count and the dropout seed, and re-arms the counter.  One launch instead of two on the step's
+// critical path.
+template <bool BF16OUT, bool PREP>
 __global__ __launch_bounds__(256) void adam_step_kernel(int64_t n, float* __restrict__ p, float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v,
-                                                        __bf16* __restrict__ pb, const double* __restrict__ state,
-                                                        const float* __restrict__ hyper, int zero_grad) {
+                                                        __bf16* __restrict__ pb, double* __restrict__ state,
+                                                        const float* __restrict__ hyper, int zero_grad,
+                                                        const float* __restrict__ divisor, uint64_t* seed_base) {
   const float b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
-  const float step_size = (float)state[1];
-  const float bc2s = (float)state[2];
-  const float gs = (float)state[3];
+  float step_size, bc2s, gs;
+  double t = 0.0;
+  AdamScalars c;
+  if (PREP) {
+    t = state[0] + 1.0;
+    c = adam_scalars(t, hyper, divisor);
+    step_size = c.step_size; bc2s = c.bc2s; gs = c.gs;
+  } else {
+    step_size = (float)state[1];
+    bc2s = (float)state[2];
+    gs = (float)state[3];
+  }
   const int64_t n4 = n / 4;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
     float4 pp = reinterpret_cast<float4*>(p)[i];
@@ -69,6 +95,31 @@ __global__ __launch_bounds__(256) void adam_step_kernel(int64_t n, float* __rest
     p[j] = p[j] - step_size * (m[j] / denom);
     if (BF16OUT) pb[j] = (__bf16)p[j];
     if (zero_grad) g[j] = 0.f;
+  }
+  if (PREP) {
+    // every lane of this workgroup has read state[0] above; once all workgroups have arrived, the
+    // last one publishes step t.  A relaxed counter suffices: nothing the other workgroups wrote is read
+    // by the last one (the kernel boundary publishes the parameters), only the order "all reads of state
+    // before its overwrite" matters, and each workgroup's reads complete before its arrival.  (A
+    // __threadfence() here -- an L2 writeback per workgroup on gfx950 -- made the launch 30 us.)
+    // Arrivals count per XCD group first (workgroup b runs on XCD b % 8; one counter per 128-B line), the
+    // last of each group then counts at the top: ~80 same-address atomics per line in parallel instead of
+    // every workgroup serialising on one address (13.8 us for the launch with a single counter).
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned x = blockIdx.x & 7u;
+      const unsigned in_x = (gridDim.x >> 3) + (x < (gridDim.x & 7u) ? 1u : 0u);
+      unsigned int* local = reinterpret_cast<unsigned int*>(state + 16 + 16 * x);
+      unsigned int* top = reinterpret_cast<unsigned int*>(state + 7);
+      const unsigned groups = gridDim.x < 8u ? gridDim.x : 8u;
+      if (__hip_atomic_fetch_add(local, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_x - 1) {
+        *local = 0u;
+        if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == groups - 1) {
+          adam_commit(state, t, c, seed_base);
+          *top = 0u;
+        }
+      }
+    }
   }
 }
 
@@ -229,12 +280,28 @@ int rs_adam_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16
   if (n <= 0 || ((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16) return RS_ERR_ARG;
   const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(cdiv(n / 4, 256), 8192));
   hipStream_t s = (hipStream_t)stream;
+  double* st = const_cast<double*>(state);   // read only without PREP
   if (p_bf16)
-    hipLaunchKernelGGL((adam_step_kernel<true>), dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
-                       (__bf16*)p_bf16, state, hyper, zero_grad);
+    hipLaunchKernelGGL((adam_step_kernel<true, false>), dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
+                       (__bf16*)p_bf16, st, hyper, zero_grad, nullptr, nullptr);
   else
-    hipLaunchKernelGGL((adam_step_kernel<false>), dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
-                       (__bf16*)nullptr, state, hyper, zero_grad);
+    hipLaunchKernelGGL((adam_step_kernel<false, false>), dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
+                       (__bf16*)nullptr, st, hyper, zero_grad, nullptr, nullptr);
+  return (int)hipGetLastError();
+}
+
+int rs_adam_prepare_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, double* state,
+                         const float* hyper, int zero_grad, const float* grad_divisor, uint64_t* seed_base,
+                         void* stream) {
+  if (n <= 0 || !state || ((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16) return RS_ERR_ARG;
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(cdiv(n / 4, 256), 8192));
+  hipStream_t s = (hipStream_t)stream;
+  if (p_bf16)
+    hipLaunchKernelGGL((adam_step_kernel<true, true>), dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
+                       (__bf16*)p_bf16, state, hyper, zero_grad, grad_divisor, seed_base);
+  else
+    hipLaunchKernelGGL((adam_step_kernel<false, true>), dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
+                       (__bf16*)nullptr, state, hyper, zero_grad, grad_divisor, seed_base);
   return (int)hipGetLastError();
 }
 

@@ -266,6 +266,14 @@ def adam_step(p, g, m, v, p_bf16, state, hyper, zero_grad=False):
          int(zero_grad), stream())
 
 
+def adam_prepare_step(p, g, m, v, p_bf16, state, hyper, zero_grad=False, grad_divisor=None, seed_base=None):
+    """adam_prepare + adam_step in one launch (state: double[144]; state[7], state[16 + 16 k] arrival counters)."""
+    if state.numel() < 144:
+        raise ValueError("adam_prepare_step needs the 8-entry optimizer state")
+    call("rs_adam_prepare_step", p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), ptr(p_bf16), ptr(state), ptr(hyper),
+         int(zero_grad), ptr(grad_divisor), ptr(seed_base), stream())
+
+
 def cast_bf16(src, dst):
     call("rs_cast_bf16", src.numel(), ptr(src), ptr(dst), stream())
 

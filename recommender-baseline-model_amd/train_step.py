@@ -27,14 +27,16 @@ from . import ops
 
 
 class FusedAdam:
-    """Device-side torch.optim.Adam over a FlatParams buffer (rs_adam_prepare/step)."""
+    """Device-side torch.optim.Adam over a FlatParams buffer (rs_adam_prepare_step / rs_adam_step)."""
 
     def __init__(self, flat, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
         dev = flat.device
         self.flat = flat
         self.m = torch.zeros(flat.numel, dtype=torch.float32, device=dev)
         self.v = torch.zeros(flat.numel, dtype=torch.float32, device=dev)
-        self.state = torch.zeros(4, dtype=torch.float64, device=dev)
+        # [t, lr/bc1, sqrt(bc2), grad scale, -, -, -, arrival counters of rs_adam_prepare_step (state[7],
+        # state[16 + 16 k], k < 8)]
+        self.state = torch.zeros(144, dtype=torch.float64, device=dev)
         self.hyper = torch.tensor([lr, betas[0], betas[1], eps, weight_decay], dtype=torch.float32, device=dev)
 
     def set_lr(self, lr):
@@ -45,11 +47,15 @@ class FusedAdam:
         """One Adam update; also clears the gradient buffer (the next step accumulates from zero) and
         advances the dropout step seed when given.  ranges: [(lo, hi)] flat slices to update (default all; a
         vocabulary-sharded rank skips the output rows other ranks own)."""
-        ops.adam_prepare(self.state, self.hyper, grad_divisor, seed_base)
         f = self.flat
-        for lo, hi in ranges or [(0, f.numel)]:
-            ops.adam_step(f.data[lo:hi], f.grad[lo:hi], self.m[lo:hi], self.v[lo:hi],
-                          f.bf16[lo:hi] if f.bf16 is not None else None, self.state, self.hyper, zero_grad=True)
+        for k, (lo, hi) in enumerate(ranges or [(0, f.numel)]):
+            bf = f.bf16[lo:hi] if f.bf16 is not None else None
+            if k == 0:   # the first range's launch also prepares the step's scalars (rs_adam_prepare_step)
+                ops.adam_prepare_step(f.data[lo:hi], f.grad[lo:hi], self.m[lo:hi], self.v[lo:hi], bf, self.state,
+                                      self.hyper, zero_grad=True, grad_divisor=grad_divisor, seed_base=seed_base)
+            else:
+                ops.adam_step(f.data[lo:hi], f.grad[lo:hi], self.m[lo:hi], self.v[lo:hi], bf, self.state,
+                              self.hyper, zero_grad=True)
 
 
 class FusedTrainStep:

@@ -1,0 +1,50 @@
+"""Fused Adam kernels against torch.optim.Adam (BS/trainers/base.py:225-228 builds torch.optim.Adam; the
+fused step replaces it): rs_adam_prepare_step (one launch) == rs_adam_prepare + rs_adam_step bit for bit,
+both within fp32 rounding of torch's update, step count / dropout seed / arrival counter bookkeeping."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _state():
+    return torch.zeros(144, dtype=torch.float64, device="cuda")
+
+
+@pytest.mark.parametrize("n", [1, 7, 4096 + 3, 662_019])
+@pytest.mark.parametrize("wd", [0.0, 0.01])
+def test_fused_prepare_step_matches_two_launches_and_torch(n, wd):
+    import rbm_amd  # noqa: F401
+    from rbm_amd import ops
+    g0 = torch.Generator().manual_seed(n)
+    p0 = torch.randn(n, generator=g0)
+    hyper = torch.tensor([1e-3, 0.9, 0.999, 1e-8, wd], dtype=torch.float32, device="cuda")
+    div = torch.tensor([3.0], device="cuda")
+    runs = []
+    for fused in (False, True):
+        p, m, v = p0.cuda().clone(), torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
+        pb = torch.empty(n, dtype=torch.bfloat16, device="cuda")
+        st, seed = _state(), torch.zeros(1, dtype=torch.int64, device="cuda")
+        gg = torch.Generator().manual_seed(1)
+        for _ in range(5):
+            g = torch.randn(n, generator=gg).cuda() * 3.0
+            if fused:
+                ops.adam_prepare_step(p, g, m, v, pb, st, hyper, zero_grad=True, grad_divisor=div, seed_base=seed)
+            else:
+                ops.adam_prepare(st, hyper, div, seed)
+                ops.adam_step(p, g, m, v, pb, st, hyper, zero_grad=True)
+            assert int(torch.count_nonzero(g)) == 0
+        torch.cuda.synchronize()
+        runs.append((p.clone(), pb.clone(), st.cpu(), int(seed.item())))
+    assert torch.equal(runs[0][0], runs[1][0]) and torch.equal(runs[0][1], runs[1][1])
+    assert runs[1][2][0].item() == 5.0 and runs[1][2][7].item() == 0.0 and not runs[1][2][16:].any() and runs[1][3] == 5
+    assert torch.equal(runs[0][2][:4], runs[1][2][:4])
+    # torch.optim.Adam (L2 weight decay as torch's Adam adds it to the gradient) on the same gradients / 3
+    tp = torch.nn.Parameter(p0.clone().double())
+    opt = torch.optim.Adam([tp], lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=wd)
+    gg = torch.Generator().manual_seed(1)
+    for _ in range(5):
+        tp.grad = (torch.randn(n, generator=gg) * 3.0 / 3.0).double()
+        opt.step()
+    err = (runs[1][0].cpu().double() - tp.detach()).abs().max().item()
+    assert err < 2e-6, err
