@@ -293,14 +293,19 @@ class SASEngine:
             segs = ops.ln_partial_segments(lnh, M, d, G("last_layernorm.weight"), G("last_layernorm.bias"))
             torch.cuda.current_stream().wait_event(ev)
 
-            def embedding_grads(dx):
+            def item_grads(dx):
                 ops.item_grad(iws, 3, M, dx, math.sqrt(d), p, self.salt["emb"], sb, s["f"], dpl, dnl,
                               G("item_emb.weight"))
-                ops.embed_bwd(0, ids, T, dx, math.sqrt(d), p, self.salt["emb"], sb, None, G("pos_emb.weight"))
+            # the item table's gradient (rs_item_grad, ~42 us beside the weight gradients) on the side stream;
+            # the positional table's (10 us) after the weight gradients on the main one: the two branches then
+            # end together and the join's cross-queue latency is hidden
             side = os.environ.get("RS_SAS_EMB_GRAD_SIDE", "1") != "0"
-            dx = self._backward_blocks_fused(s, dx, grad, segs, tail=embedding_grads if side else None)
-            if not side:
-                embedding_grads(dx)
+            dx = self._backward_blocks_fused(s, dx, grad, segs, tail=item_grads if side else None)
+            ops.embed_bwd(0, ids, T, dx, math.sqrt(d), p, self.salt["emb"], sb, None, G("pos_emb.weight"))
+            if side:
+                torch.cuda.current_stream().wait_event(self._tail_join)
+            else:
+                item_grads(dx)
             if split is not None:
                 split("dense")          # every parameter gradient is final (data-parallel overlap)
             return
@@ -395,9 +400,9 @@ class SASEngine:
         """SAS blocks' backward with rs_sas_block_out_bwd / rs_sas_block_in_bwd (rowfused.hip) for the
         row-local chains; then ALL ten weight gradients and the four LayerNorm affine partial sets in
         one grouped GEMM launch + one grouped reduction (rs_wgrad_grouped, wgrad.hip).  Returns the
-        gradient at the embedding output.  tail(dx): work on that gradient alone (the embedding tables'
-        gradients), issued on the side stream so it runs beside the grouped weight-gradient launch (both are
-        latency-bound; joined before returning)."""
+        gradient at the embedding output.  tail(dx): work on that gradient alone (the item table's
+        gradient), issued on the side stream so it runs beside the grouped weight-gradient launch (both are
+        latency-bound); the caller joins self._tail_join."""
         B, T, p, ids, sb = s["B"], s["T"], s["p"], s["ids"], s["sb"]
         M, d, H, Dh, L = B * T, self.d, self.H, self.Dh, self.L
         e = self._buf
@@ -455,19 +460,21 @@ class SASEngine:
         nl = 1 if early else L
         wslab = self.ws.get("wslab", (ops.wgrad_grouped_slab_numel([(d, d)] * 4 * nl + [(2 * d, d)] * nl, M, rows),),
                             torch.float32)
-        join = None
+        join, fork = None, None
         if tail is not None:
-            cur = torch.cuda.current_stream()
             fork = torch.cuda.Event()
-            fork.record(cur)
+            fork.record(torch.cuda.current_stream())
+        # the grouped launch is captured BEFORE the side branch: a HIP graph keeps a node's first child on its
+        # queue, so the weight gradients follow the blocks' backward with no cross-queue hop (side branch
+        # first: 11 us of fork latency before rs_wgrad_grouped and 11 us of join latency before Adam)
+        ops.wgrad_grouped(probs, M, rows, wslab, extra=segs)
+        if tail is not None:
             self._side.wait_event(fork)
             with torch.cuda.stream(self._side):
                 tail(dx)
                 join = torch.cuda.Event()
                 join.record(self._side)
-        ops.wgrad_grouped(probs, M, rows, wslab, extra=segs)
-        if join is not None:
-            torch.cuda.current_stream().wait_event(join)
+            self._tail_join = join
         return dx
 
     @staticmethod

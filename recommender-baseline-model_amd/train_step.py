@@ -26,6 +26,11 @@ from . import dp as dpx
 from . import ops
 
 
+# thread-local capture: the process group's watchdog thread polls its collectives' events while a step graph is
+# being captured, which global capture mode forbids (hipErrorStreamCaptureUnsupported aborts the process)
+CAPTURE_MODE = "thread_local"
+
+
 class FusedAdam:
     """Device-side torch.optim.Adam over a FlatParams buffer (rs_adam_prepare_step / rs_adam_step)."""
 
@@ -354,7 +359,7 @@ class FusedTrainStep:
                 self.g_compute = None
             else:
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
                     compute()
                     if not self.dp and not unrolled:
                         self._update()
@@ -366,7 +371,7 @@ class FusedTrainStep:
         self.g_update = None
         if self.dp:
             self.g_update = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.g_update):
+            with torch.cuda.graph(self.g_update, capture_error_mode=CAPTURE_MODE):
                 self._update()
         segs = [seg[0] for seg in self.g_segments] if self.g_segments else [self.g_compute]
         self.graphs = tuple(segs) + ((self.g_update,) if self.dp else ())
@@ -381,13 +386,13 @@ class FusedTrainStep:
         s.wait_stream(torch.cuda.current_stream())
         segs, cur = [], [torch.cuda.CUDAGraph()]
         with torch.cuda.stream(s):
-            cur[0].capture_begin(pool=pool)
+            cur[0].capture_begin(pool=pool, capture_error_mode=CAPTURE_MODE)
 
             def split(tag, action=None):
                 cur[0].capture_end()
                 segs.append((cur[0], tag, action))
                 cur[0] = torch.cuda.CUDAGraph()
-                cur[0].capture_begin(pool=pool)
+                cur[0].capture_begin(pool=pool, capture_error_mode=CAPTURE_MODE)
             try:
                 compute(split)
             finally:
