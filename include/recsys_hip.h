@@ -197,14 +197,18 @@ int rs_splitk_scatter_rows(int dtype, const float* slab, int splits, int64_t cap
  * also advances *seed_base when non-null (the next step's dropout masks, as rs_seed_advance).
  * rs_adam_prepare_step = rs_adam_prepare + rs_adam_step in ONE launch (every workgroup derives step
  * t's scalars; the last to finish publishes them; state[7] and state[16 + 16 k], k < 8, are its arrival
- * counters and must be 0 between launches); further ranges of the same step then use rs_adam_step.  Same results bit for bit. */
+ * counters and must be 0 between launches); further ranges of the same step then use rs_adam_step.  ntd > 0 (with p_bf16): the bf16
+ * result is also written TRANSPOSED for ntd matrices of the buffer, tdesc (device int64 [ntd][6]) = rows,
+ * cols, src_off (element offset of the matrix in the flat buffer whose element tbase is p[0]), lds
+ * (% 4 == 0), dst_off, ldd: wT[dst_off + c*ldd + r] = bf16(p[src_off + r*lds + c]) (rs_transpose_bf16's
+ * output, so the SAS backward's transposed weights need no separate launch).  Same results bit for bit. */
 int rs_adam_prepare(double* state, const float* hyper, const float* grad_divisor, uint64_t* seed_base,
                     void* stream);
 int rs_adam_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16,
                  const double* state, const float* hyper, int zero_grad, void* stream);
 int rs_adam_prepare_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, double* state,
                          const float* hyper, int zero_grad, const float* grad_divisor, uint64_t* seed_base,
-                         void* stream);
+                         const int64_t* tdesc, int ntd, int64_t tbase, void* wT, void* stream);
 
 /* dst_bf16[i] = bf16(src[i]) */
 int rs_cast_bf16(int64_t n, const float* src, void* dst, void* stream);

@@ -44,7 +44,9 @@ __global__ __launch_bounds__(256) void adam_step_kernel(int64_t n, float* __rest
                                                         float* __restrict__ m, float* __restrict__ v,
                                                         __bf16* __restrict__ pb, double* __restrict__ state,
                                                         const float* __restrict__ hyper, int zero_grad,
-                                                        const float* __restrict__ divisor, uint64_t* seed_base) {
+                                                        const float* __restrict__ divisor, uint64_t* seed_base,
+                                                        const int64_t* __restrict__ tdesc, int ntd, int64_t tbase,
+                                                        __bf16* __restrict__ wT) {
   const float b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
   float step_size, bc2s, gs;
   double t = 0.0;
@@ -82,6 +84,20 @@ __global__ __launch_bounds__(256) void adam_step_kernel(int64_t n, float* __rest
       bf16x4 o;
       o[0] = (__bf16)P[0]; o[1] = (__bf16)P[1]; o[2] = (__bf16)P[2]; o[3] = (__bf16)P[3];
       reinterpret_cast<bf16x4*>(pb)[i] = o;
+      // transposed bf16 copies of matrices inside the buffer (the SAS backward's [in][out] block weights,
+      // rs_transpose_bf16's desc layout): the 4 elements share a row (host checks lds % 4 == 0)
+      for (int k = 0; k < ntd; ++k) {
+        const int64_t* dk = tdesc + 6 * k;
+        const int64_t rel = tbase + 4 * i - dk[2];
+        if (rel >= 0 && rel < dk[0] * dk[3]) {
+          const int64_t r = rel / dk[3], c = rel - r * dk[3];
+          if (c < dk[1]) {
+            __bf16* t = wT + dk[4] + c * dk[5] + r;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) t[j * dk[5]] = o[j];
+          }
+        }
+      }
     }
   }
   // tail
@@ -283,25 +299,30 @@ int rs_adam_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16
   double* st = const_cast<double*>(state);   // read only without PREP
   if (p_bf16)
     hipLaunchKernelGGL((adam_step_kernel<true, false>), dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
-                       (__bf16*)p_bf16, st, hyper, zero_grad, nullptr, nullptr);
+                       (__bf16*)p_bf16, st, hyper, zero_grad, nullptr, nullptr, nullptr, 0, 0,
+                       nullptr);
   else
     hipLaunchKernelGGL((adam_step_kernel<false, false>), dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
-                       (__bf16*)nullptr, st, hyper, zero_grad, nullptr, nullptr);
+                       (__bf16*)nullptr, st, hyper, zero_grad, nullptr, nullptr, nullptr, 0, 0,
+                       nullptr);
   return (int)hipGetLastError();
 }
 
 int rs_adam_prepare_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, double* state,
                          const float* hyper, int zero_grad, const float* grad_divisor, uint64_t* seed_base,
-                         void* stream) {
+                         const int64_t* tdesc, int ntd, int64_t tbase, void* wT, void* stream) {
   if (n <= 0 || !state || ((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16) return RS_ERR_ARG;
+  if (ntd < 0 || (ntd > 0 && (!tdesc || !wT || !p_bf16))) return RS_ERR_ARG;
   const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(cdiv(n / 4, 256), 8192));
   hipStream_t s = (hipStream_t)stream;
   if (p_bf16)
     hipLaunchKernelGGL((adam_step_kernel<true, true>), dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
-                       (__bf16*)p_bf16, state, hyper, zero_grad, grad_divisor, seed_base);
+                       (__bf16*)p_bf16, state, hyper, zero_grad, grad_divisor, seed_base, tdesc, ntd,
+                       tbase, (__bf16*)wT);
   else
     hipLaunchKernelGGL((adam_step_kernel<false, true>), dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
-                       (__bf16*)nullptr, state, hyper, zero_grad, grad_divisor, seed_base);
+                       (__bf16*)nullptr, state, hyper, zero_grad, grad_divisor, seed_base, nullptr, 0,
+                       0, nullptr);
   return (int)hipGetLastError();
 }
 

@@ -150,6 +150,10 @@ class SASEngine:
         self.ws = Workspace(self.dev)
         self.seed_base = torch.zeros(1, dtype=torch.int64, device=self.dev)
         self.external_seed = False    # True: the fused train step's optimizer advances seed_base
+        # True: the fused train step's optimizer also writes the transposed bf16 block weights (transposed_spec),
+        # so the forward's side branch builds only the item index and the backward needs no join for it
+        self.adam_transposes = False
+        self._wT = None
         salt0 = int(torch.randint(0, 2 ** 62, (1,)).item())
         self.salt = {"emb": site_salt(salt0, 0)}
         for i in range(self.L):
@@ -161,6 +165,15 @@ class SASEngine:
     def sync_compute_weights(self):
         if self.flat.bf16 is not None:
             ops.cast_bf16(self.flat.data, self.flat.bf16)
+            if self._wT is not None:
+                self._refresh_transposed()
+
+    def transposed_spec(self):
+        """(desc, host desc, destination) of the backward's transposed block weights, for an optimizer that
+        writes them itself (rs_adam_prepare_step; adam_transposes=True), or None before they exist."""
+        if not self.adam_transposes or self._wT is None:
+            return None
+        return self._wT_desc, self._wT_desc_host, self._wT
 
     def W(self, n):
         return self.flat.cview(n)
@@ -291,7 +304,11 @@ class SASEngine:
                 ops.sas_head_bwd(None, None, None, None, None, dpl, dnl, None, None, s["pos"], s["neg"], E, s["xL"],
                                  gl, s["muf"], s["rf"], dx, lnh)
             segs = ops.ln_partial_segments(lnh, M, d, G("last_layernorm.weight"), G("last_layernorm.bias"))
-            torch.cuda.current_stream().wait_event(ev)
+            side = os.environ.get("RS_SAS_EMB_GRAD_SIDE", "1") != "0"
+            if self._side_refreshed or not side:
+                # the blocks' backward reads the transposed weights the side branch wrote this step (otherwise
+                # the previous step's optimizer wrote them), the item gradient on the main stream the index
+                torch.cuda.current_stream().wait_event(ev)
 
             def item_grads(dx):
                 ops.item_grad(iws, 3, M, dx, math.sqrt(d), p, self.salt["emb"], sb, s["f"], dpl, dnl,
@@ -299,7 +316,6 @@ class SASEngine:
             # the item table's gradient (rs_item_grad, ~42 us beside the weight gradients) on the side stream;
             # the positional table's (10 us) after the weight gradients on the main one: the two branches then
             # end together and the join's cross-queue latency is hidden
-            side = os.environ.get("RS_SAS_EMB_GRAD_SIDE", "1") != "0"
             dx = self._backward_blocks_fused(s, dx, grad, segs, tail=item_grads if side else None)
             ops.embed_bwd(0, ids, T, dx, math.sqrt(d), p, self.salt["emb"], sb, None, G("pos_emb.weight"))
             if side:
@@ -372,7 +388,9 @@ class SASEngine:
         with torch.cuda.stream(self._side):
             iws = self.ws.get("itemidx", (ops.item_index_ws_bytes(3, M, V1, d),), torch.uint8)
             ops.item_index_build([ids, pos, neg], V1, d, iws)
-            self._refresh_transposed()
+            self._side_refreshed = not self.adam_transposes or self._wT is None
+            if self._side_refreshed:
+                self._refresh_transposed()
             ev = torch.cuda.Event()
             ev.record(self._side)
         return ev, iws
@@ -382,7 +400,7 @@ class SASEngine:
         GEMMs (rs_transpose_bf16, one launch); per layer: in_proj^T [d][3d], out_proj^T, conv1^T,
         conv2^T [d][d]."""
         d, L = self.d, self.L
-        if getattr(self, "_wT", None) is None:
+        if self._wT is None:
             self._wT = torch.empty(L * 6 * d * d, dtype=torch.bfloat16, device=self.dev)
             desc = []
             for i in range(L):
@@ -392,6 +410,7 @@ class SASEngine:
                                         (fw + "conv1.weight", d, 4 * d * d), (fw + "conv2.weight", d, 5 * d * d)):
                     desc.append([rows, d, self.flat.offsets[name], d, base + off, rows])
             self._wT_desc = torch.tensor(desc, dtype=torch.int64, device=self.dev)
+            self._wT_desc_host = desc
             self._wT_tiles = max(-(-r // 64) * -(-c // 64) for r, c, *_ in desc)
         ops.transpose_bf16(self._wT_desc, self._wT_tiles, self.flat.bf16, self._wT)
         return self._wT

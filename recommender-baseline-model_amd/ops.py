@@ -266,12 +266,24 @@ def adam_step(p, g, m, v, p_bf16, state, hyper, zero_grad=False):
          int(zero_grad), stream())
 
 
-def adam_prepare_step(p, g, m, v, p_bf16, state, hyper, zero_grad=False, grad_divisor=None, seed_base=None):
-    """adam_prepare + adam_step in one launch (state: double[144]; state[7], state[16 + 16 k] arrival counters)."""
+def adam_prepare_step(p, g, m, v, p_bf16, state, hyper, zero_grad=False, grad_divisor=None, seed_base=None,
+                      transposed=None):
+    """adam_prepare + adam_step in one launch (state: double[144]; state[7], state[16 + 16 k] arrival counters).
+    transposed: (desc int64 device [n][6] as transpose_bf16's, its host copy, dst bf16 tensor) -- the bf16
+    result of those matrices is also written transposed (p[0] is element 0 of the flat buffer)."""
     if state.numel() < 144:
-        raise ValueError("adam_prepare_step needs the 8-entry optimizer state")
+        raise ValueError("adam_prepare_step needs the 144-entry optimizer state")
+    td, nt, wt = None, 0, None
+    if transposed is not None:
+        td, host, wt = transposed
+        nt = len(host)
+        for rows, cols, off, lds, doff, ldd in host:
+            if lds % 4 or off % 4 or off + rows * lds > (p.numel() // 4) * 4 or doff + (cols - 1) * ldd + rows > wt.numel():
+                raise ValueError("adam_prepare_step: transposed matrix outside the buffers or misaligned")
+        if p_bf16 is None:
+            raise ValueError("adam_prepare_step: transposed copies need the bf16 output")
     call("rs_adam_prepare_step", p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), ptr(p_bf16), ptr(state), ptr(hyper),
-         int(zero_grad), ptr(grad_divisor), ptr(seed_base), stream())
+         int(zero_grad), ptr(grad_divisor), ptr(seed_base), ptr(td), nt, 0, ptr(wt), stream())
 
 
 def cast_bf16(src, dst):

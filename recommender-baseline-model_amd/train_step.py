@@ -48,7 +48,7 @@ class FusedAdam:
         """StepLR hook (BS/trainers/base.py:40,87): lives on the device, so graph replays see it."""
         self.hyper[0] = lr
 
-    def step(self, grad_divisor=None, seed_base=None, ranges=None):
+    def step(self, grad_divisor=None, seed_base=None, ranges=None, transposed=None):
         """One Adam update; also clears the gradient buffer (the next step accumulates from zero) and
         advances the dropout step seed when given.  ranges: [(lo, hi)] flat slices to update (default all; a
         vocabulary-sharded rank skips the output rows other ranks own)."""
@@ -57,7 +57,8 @@ class FusedAdam:
             bf = f.bf16[lo:hi] if f.bf16 is not None else None
             if k == 0:   # the first range's launch also prepares the step's scalars (rs_adam_prepare_step)
                 ops.adam_prepare_step(f.data[lo:hi], f.grad[lo:hi], self.m[lo:hi], self.v[lo:hi], bf, self.state,
-                                      self.hyper, zero_grad=True, grad_divisor=grad_divisor, seed_base=seed_base)
+                                      self.hyper, zero_grad=True, grad_divisor=grad_divisor, seed_base=seed_base,
+                                      transposed=transposed if lo == 0 else None)
             else:
                 ops.adam_step(f.data[lo:hi], f.grad[lo:hi], self.m[lo:hi], self.v[lo:hi], bf, self.state,
                               self.hyper, zero_grad=True)
@@ -79,6 +80,8 @@ class FusedTrainStep:
         self.flat = self.engine.flat
         self.engine.sync_compute_weights()
         self.engine.external_seed = True       # advanced by the optimizer kernel at the end of each step
+        if hasattr(self.engine, "adam_transposes"):
+            self.engine.adam_transposes = True  # SAS: the optimizer kernel also writes the transposed block weights
         self.flat.grad.zero_()                 # then kept zero by the optimizer (zero_grad)
         self.opt = FusedAdam(self.flat, lr=lr, weight_decay=weight_decay)
         self.pg = process_group
@@ -191,12 +194,14 @@ class FusedTrainStep:
             # the sharded head normalised by the global count already; the loss is the global batch's
             self.loss_val.copy_(self.loss_out[2:3])
             self.opt.step(seed_base=sb, ranges=self._adam_ranges())
-        elif self.dp:
-            torch.div(self.flat.aux[dpx.LOSS_SUM:dpx.LOSS_SUM + 1], self.flat.aux[dpx.COUNT:dpx.COUNT + 1],
-                      out=self.loss_val)
-            self.opt.step(grad_divisor=self.flat.aux[dpx.COUNT:dpx.COUNT + 1], seed_base=sb)
         else:
-            self.opt.step(seed_base=sb)
+            tr = self.engine.transposed_spec() if hasattr(self.engine, "transposed_spec") else None
+            if self.dp:
+                torch.div(self.flat.aux[dpx.LOSS_SUM:dpx.LOSS_SUM + 1], self.flat.aux[dpx.COUNT:dpx.COUNT + 1],
+                          out=self.loss_val)
+                self.opt.step(grad_divisor=self.flat.aux[dpx.COUNT:dpx.COUNT + 1], seed_base=sb, transposed=tr)
+            else:
+                self.opt.step(seed_base=sb, transposed=tr)
 
     # ---------------------------------------------------------------- one step
     def step(self, *batch):

@@ -48,3 +48,37 @@ def test_fused_prepare_step_matches_two_launches_and_torch(n, wd):
         opt.step()
     err = (runs[1][0].cpu().double() - tp.detach()).abs().max().item()
     assert err < 2e-6, err
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_optimizer_written_transposed_weights_match_a_fresh_transpose(graph):
+    """SAS fused step: rs_adam_prepare_step writes the backward's transposed bf16 block weights; after
+    several steps they equal rs_transpose_bf16 of the current bf16 weights bit for bit."""
+    import argparse
+    import numpy as np
+    import rbm_amd  # noqa: F401
+    import rbm_amd.data as synth
+    from rbm_amd.models import model_factory
+    from rbm_amd.train_step import FusedTrainStep
+    torch.manual_seed(0)
+    a = argparse.Namespace(model_code="sas", num_items=500, max_len=64, device="cuda", sas_hidden_units=64,
+                           sas_num_blocks=2, sas_heads=1, sas_dropout=0.1, l2_emb=0.0, rs_dtype="bf16")
+    m = model_factory(a)
+    st = FusedTrainStep(m, lr=1e-2)
+    rng = np.random.default_rng(0)
+    b = [torch.from_numpy(x).cuda() for x in synth.sas_batch(rng, 16, 64, 500)]
+    if graph:
+        st.capture(*b, warmup=2)
+        for _ in range(3):
+            st.replay(*b)
+    else:
+        for _ in range(4):
+            st.step(*b)
+    torch.cuda.synchronize()
+    eng = st.engine
+    assert eng.adam_transposes and eng._wT is not None
+    got = eng._wT.clone()
+    eng.adam_transposes = False
+    eng._refresh_transposed()
+    torch.cuda.synchronize()
+    assert torch.equal(got, eng._wT)
