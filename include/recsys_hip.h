@@ -274,7 +274,7 @@ int rs_vocab_shard_label_logits(int64_t R, int64_t d, const void* h, int64_t ldh
 int rs_vocab_shard_combine(int N, int64_t R, const float* lse_parts, const float* tgt, const int64_t* labels,
                            float* lse, float* out, void* stream);
 
-/* Host-only: the causal attention backward's work plan for (B, T, H) -- per (split < 4, wave < 8, item < 4) a
+/* Host-only: the causal attention backward's work plan for (B, T, H) -- per (split < 4, wave < 8, item < 6) a
  * uint32 (valid << 31 | slot << 26 | role << 24 | chunk end << 16 | chunk begin << 8 | tile; attention_lds.hip
  * make_plan) of the dK/dV (dkv = 1) or dQ pass; *nsplit = workgroups per sequence.  Returns RS_ERR_UNSUPPORTED
  * where the kernels fall back to one tile per wave (T < 128 or no plan fits). */

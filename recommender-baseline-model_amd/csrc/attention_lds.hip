@@ -26,6 +26,8 @@
 typedef __attribute__((ext_vector_type(4))) __bf16 bf4;
 typedef __bf16 bf16;
 
+#define PLAN_S 4
+#define PLAN_I 6
 struct AttnLdsArgs {
   int64_t B, T, H;
   const bf16* q; int64_t ldq;
@@ -52,10 +54,8 @@ struct AttnLdsArgs {
   // << 8 | tile; chunks are 32 keys (dQ) / 32 queries (dK/dV); role 0 = whole tile, 1 = upper half (its
   // partial goes to LDS slot `slot`), 2 = lower half (adds that slot's partial, then writes the tile)
   int use_plan;
-  uint32_t plan[4][8][4];
+  uint32_t plan[PLAN_S][8][PLAN_I];
 };
-#define PLAN_S 4
-#define PLAN_I 4
 #define DQ_SLOTS 4    // fp32 partial dQ tiles (8 KB each at Dh = 128)
 #define DKV_SLOTS 3   // bf16 partial (dK, dV) tiles (8 KB each at Dh = 128)
 
@@ -196,18 +196,21 @@ __device__ __forceinline__ float masked(const AttnLdsArgs& a, const float* km, i
 // (sequence-head, split) of this workgroup.  Workgroups are dealt to the 8 XCDs round-robin in
 // dispatch order; the nsplit workgroups of one sequence stage the same K/V (or Q/dO) rows, so they
 // are given dispatch slots on ONE XCD and the second staging reads hit that XCD's L2.
-__device__ __forceinline__ void block_coords(const AttnLdsArgs& a, int64_t& bh, int& split) {
+// lin: the workgroup's linear index among the launch's workgroups of this pass (split fastest)
+__device__ __forceinline__ void block_coords(const AttnLdsArgs& a, int64_t lin, int64_t& bh, int& split) {
   const int ns = a.nsplit;
   const int64_t BH = a.B * a.H;
   if (ns > 1 && BH % 8 == 0) {
-    const int64_t lin = blockIdx.x + (int64_t)ns * blockIdx.y;
     const int64_t xcd = lin & 7, slot = lin >> 3;
     bh = (slot / ns) * 8 + xcd;
     split = (int)(slot % ns);
   } else {
-    bh = blockIdx.y;
-    split = blockIdx.x;
+    bh = lin / ns;
+    split = (int)(lin % ns);
   }
+}
+__device__ __forceinline__ void block_coords(const AttnLdsArgs& a, int64_t& bh, int& split) {
+  block_coords(a, blockIdx.x + (int64_t)a.nsplit * blockIdx.y, bh, split);
 }
 
 // tiles of 16 queries handled by this workgroup: split, split+nsplit, ...
@@ -349,15 +352,14 @@ __global__ __launch_bounds__(NT) void attn_fwd_lds_kernel(AttnLdsArgs a) {
 
 // ------------------------------------------------------------------ backward: delta + dQ
 template <int DH>
-__global__ __launch_bounds__(NT) void attn_bwd_dq_lds_kernel(AttnLdsArgs a) {
+__device__ __forceinline__ void attn_bwd_dq_body(const AttnLdsArgs& a, int64_t lin) {
   constexpr int LD = Img<DH>::LD, KC = DH / 32, DT = DH / 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  KStampBegin stamp_(a.ks);
   APROF(4);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4, cl = lane & 15;
   int64_t bh;
   int split;
-  block_coords(a, bh, split);
+  block_coords(a, lin, bh, split);
   const int64_t b = bh / a.H, h = bh % a.H;
   const int T = (int)a.T;
   const int nq = (T + 15) / 16;
@@ -509,17 +511,25 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_lds_kernel(AttnLdsArgs a) {
   APROF(6);
 }
 
-// ------------------------------------------------------------------ backward: dK, dV
 template <int DH>
-__global__ __launch_bounds__(NT) void attn_bwd_dkv_lds_kernel(AttnLdsArgs a) {
+__global__ __launch_bounds__(NT) void attn_bwd_dq_lds_kernel(AttnLdsArgs a) {
+  KStampBegin stamp_(a.ks);
+  attn_bwd_dq_body<DH>(a, blockIdx.x + (int64_t)a.nsplit * blockIdx.y);
+}
+
+// ------------------------------------------------------------------ backward: dK, dV
+// own_delta: delta = rowsum(dO * O) is formed here (from O rows and the staged dO image, in the dQ pass's
+// summation order, so bit for bit the same values) instead of read from the dQ pass -- the two passes then
+// run as ONE launch (attn_bwd_lds_kernel) with no ordering between their workgroups
+template <int DH>
+__device__ __forceinline__ void attn_bwd_dkv_body(const AttnLdsArgs& a, int64_t lin, bool own_delta) {
   constexpr int LD = Img<DH>::LD, KC = DH / 32, DT = DH / 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  KStampEnd stamp_(a.ks);
   APROF(7);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4, cl = lane & 15;
   int64_t bh;
   int split;
-  block_coords(a, bh, split);
+  block_coords(a, lin, bh, split);
   const int64_t b = bh / a.H, h = bh % a.H;
   const int T = (int)a.T;
   const int nk = (T + 15) / 16;  // key tiles
@@ -568,8 +578,17 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkv_lds_kernel(AttnLdsArgs a) {
     }
   }
   const int ti = min(tid, T - 1);            // branch-free: clamped load, masked value
-  float lse_v = a.lse[bh * a.T + ti] * LOG2E, dl_v = a.delta[bh * a.T + ti];
+  float lse_v = a.lse[bh * a.T + ti] * LOG2E, dl_v = own_delta ? 0.f : a.delta[bh * a.T + ti];
   if (tid >= T) lse_v = dl_v = 0.f;
+  // own_delta: this wave's first two 16-row groups of O, requested with the staging loads
+  const bf16* Og = a.o + b * a.T * a.ldo + h * DH;
+  bf16x8 op[2][KC];
+  if (own_delta) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) op[k][kc] = gload8(Og, a.ldo, (wave + k * NW) * 16 + cl, a.T, kc * 32 + 8 * g);
+  }
   stage2<DH>(Qs, a.q + b * a.T * a.ldq + h * DH, a.ldq, dOs, a.dout + b * a.T * a.lddo + h * DH, a.lddo, a.T, rows,
              tid);
   if (tid < rows) {
@@ -578,6 +597,26 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkv_lds_kernel(AttnLdsArgs a) {
   }
   stage_keymask(km, a, b, rows, tid);
   __syncthreads();
+  if (own_delta) {
+    for (int k = 0, rg = wave; rg * 16 < rows; ++k, rg += NW) {
+      const int row = rg * 16 + cl;
+      bf16x8 of[KC];
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc)
+        of[kc] = k == 0 ? op[0][kc] : k == 1 ? op[1][kc] : gload8(Og, a.ldo, row, a.T, kc * 32 + 8 * g);
+      float dl = 0.f;
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) {
+        const bf16x8 dfv = *reinterpret_cast<const bf16x8*>(dOs + row * LD + kc * 32 + 8 * g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dl += (float)dfv[j] * (float)of[kc][j];
+      }
+      dl += __shfl_xor(dl, 16, 64);
+      dl += __shfl_xor(dl, 32, 64);
+      if (g == 0) dl_s[row] = row < T ? dl : 0.f;
+    }
+    __syncthreads();
+  }
   APROF(8);
   const uint64_t seed = eff_seed(a.seed, a.seed_base);
 
@@ -679,6 +718,24 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkv_lds_kernel(AttnLdsArgs a) {
   APROF(9);
 }
 
+template <int DH>
+__global__ __launch_bounds__(NT) void attn_bwd_dkv_lds_kernel(AttnLdsArgs a) {
+  KStampEnd stamp_(a.ks);
+  attn_bwd_dkv_body<DH>(a, blockIdx.x + (int64_t)a.nsplit * blockIdx.y, false);
+}
+
+// both backward passes in one launch: workgroups [0, n_dq) are dQ ones (dispatched first), the rest dK/dV
+// ones, which take CUs as dQ workgroups retire -- their Q/dO staging overlaps other CUs' dQ compute instead
+// of following a launch boundary with the whole chip loading at once
+template <int DH>
+__global__ __launch_bounds__(NT) void attn_bwd_lds_kernel(AttnLdsArgs aq, AttnLdsArgs akv) {
+  KStampBegin begin_(aq.ks);
+  KStampEnd end_(aq.ks);
+  const int64_t nq = (int64_t)aq.nsplit * aq.B * aq.H;
+  if ((int64_t)blockIdx.x < nq) attn_bwd_dq_body<DH>(aq, blockIdx.x);
+  else attn_bwd_dkv_body<DH>(akv, blockIdx.x - nq, true);
+}
+
 // ------------------------------------------------------------------ launchers
 template <int DH>
 static size_t fwd_lds_bytes(int T) {
@@ -695,6 +752,19 @@ static int pick_split(int64_t BH, int ntiles) {
   // aim for >= 256 workgroups (one per CU at T ~ 200), at least 2 tiles per wave group
   int s = 1;
   while (BH * s < 256 && s * 2 <= std::max(1, ntiles / 4)) s *= 2;   // ~7 tiles per 8-wave group at T=200
+  return s;
+}
+
+// backward: the merged launch runs 2 * nsplit * BH workgroups (dQ + dK/dV); keep them to one round on the
+// chip's 256 CUs (one workgroup each) so every dK/dV workgroup runs BESIDE the dQ ones, not after them
+static bool bwd_merged() {
+  static const bool m = [] { const char* e = getenv("RS_ATTN_BWD_MERGED"); return !e || e[0] != '0'; }();
+  return m;
+}
+static int pick_split_bwd(int64_t BH, int ntiles) {
+  if (!bwd_merged()) return pick_split(BH, ntiles);
+  int s = 1;
+  while (2 * BH * s * 2 <= 256 && s * 2 <= std::max(1, ntiles / 4)) s *= 2;
   return s;
 }
 
@@ -789,7 +859,7 @@ extern "C" int rs_attn_bwd_plan(int64_t B, int64_t T, int64_t H, int dkv, uint32
   AttnLdsArgs a = {};
   a.B = B; a.T = T; a.H = H; a.mask_kind = 0;
   const int nq = (int)cdiv(T, 16);
-  a.nsplit = pick_split(B * H, nq);
+  a.nsplit = pick_split_bwd(B * H, nq);
   *nsplit = a.nsplit;
   const bool ok = nq >= 8 && make_plan(a, nq, dkv != 0, dkv ? DKV_SLOTS : DQ_SLOTS);
   memcpy(plan, a.plan, sizeof(a.plan));
@@ -799,7 +869,7 @@ extern "C" int rs_attn_bwd_plan(int64_t B, int64_t T, int64_t H, int dkv, uint32
 template <int DH>
 static hipError_t bwd_t(AttnLdsArgs& a, hipStream_t s) {
   const int nq = (int)cdiv(a.T, 16);
-  a.nsplit = pick_split(a.B * a.H, nq);
+  a.nsplit = pick_split_bwd(a.B * a.H, nq);
   constexpr int DT = DH / 16;
   const size_t lds_q = fwd_lds_bytes<DH>((int)a.T), lds_kv = dkv_lds_bytes<DH>((int)a.T);
   const size_t ext_q = (size_t)DQ_SLOTS * DT * 4 * 64 * 4 + 16, ext_kv = (size_t)DKV_SLOTS * 2 * DT * 4 * 64 * 2 + 16;
@@ -808,10 +878,16 @@ static hipError_t bwd_t(AttnLdsArgs& a, hipStream_t s) {
   const bool want = a.mask_kind == 0 && nq >= 8;
   aq.use_plan = want && lds_q + ext_q <= 160 * 1024 && make_plan(aq, nq, false, DQ_SLOTS);
   akv.use_plan = want && lds_kv + ext_kv <= 160 * 1024 && make_plan(akv, nq, true, DKV_SLOTS);
-  hipLaunchKernelGGL((attn_bwd_dq_lds_kernel<DH>), dim3((unsigned)a.nsplit, (unsigned)(a.B * a.H)), dim3(NT),
-                     lds_q + (aq.use_plan ? ext_q : 0), s, aq);
-  hipLaunchKernelGGL((attn_bwd_dkv_lds_kernel<DH>), dim3((unsigned)a.nsplit, (unsigned)(a.B * a.H)), dim3(NT),
-                     lds_kv + (akv.use_plan ? ext_kv : 0), s, akv);
+  const size_t bq = lds_q + (aq.use_plan ? ext_q : 0), bkv = lds_kv + (akv.use_plan ? ext_kv : 0);
+  if (bwd_merged()) {
+    hipLaunchKernelGGL((attn_bwd_lds_kernel<DH>), dim3((unsigned)(2 * a.nsplit * a.B * a.H)), dim3(NT),
+                       std::max(bq, bkv), s, aq, akv);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL((attn_bwd_dq_lds_kernel<DH>), dim3((unsigned)a.nsplit, (unsigned)(a.B * a.H)), dim3(NT), bq, s,
+                     aq);
+  hipLaunchKernelGGL((attn_bwd_dkv_lds_kernel<DH>), dim3((unsigned)a.nsplit, (unsigned)(a.B * a.H)), dim3(NT), bkv,
+                     s, akv);
   return hipGetLastError();
 }
 
@@ -822,6 +898,7 @@ static void set_lds_limits() {
                       160 * 1024);
   hipFuncSetAttribute((const void*)attn_bwd_dkv_lds_kernel<DH>, hipFuncAttributeMaxDynamicSharedMemorySize,
                       160 * 1024);
+  hipFuncSetAttribute((const void*)attn_bwd_lds_kernel<DH>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 
 static void init_once() {
