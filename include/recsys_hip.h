@@ -369,6 +369,15 @@ int64_t rs_wgrad_grouped_slab_numel(int nprob, const rs_wgrad_problem* probs, in
  * reduction launch.  Returns RS_ERR_UNSUPPORTED for shapes outside the contract. */
 int rs_wgrad_grouped(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_t rows_per_split, float* slab,
                      int64_t slab_numel, int nextra, const rs_reduce_segment* extra, void* stream);
+
+/* rs_wgrad_grouped followed by rs_item_grad (same arguments, same results bit for bit) in two launches on one
+ * stream: the weight-gradient tiles and the item-gradient chunks share the first launch, the slab reduction
+ * and the item-gradient span pass the second (grad_tail.hip; the SAS step's backward tail). */
+int rs_wgrad_grouped_items(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_t rows_per_split, float* slab,
+                           int64_t slab_numel, int nextra, const rs_reduce_segment* extra, const void* ws, int nsrc,
+                           int64_t rows, int64_t table_rows, int64_t d, const void* dx, float scale, float drop_p,
+                           uint64_t salt, const uint64_t* seed_base, const void* f, const float* w1, const float* w2,
+                           float* dtable, void* stream);
 /* The reduction alone: out (+)= sum over splits, for nseg segments (any number, 64 per launch). */
 int rs_reduce_segments(int nseg, const rs_reduce_segment* segs, int accumulate, void* stream);
 

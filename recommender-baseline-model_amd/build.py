@@ -29,10 +29,20 @@ def _headers_mtime():
     return max((os.path.getmtime(h) for h in hs), default=0.0)
 
 
+def _included(path):
+    with open(path) as fh:
+        return fh.readline().startswith("// rs-build: included")
+
+
+def _included_mtime():
+    inc = [p for p in glob.glob(os.path.join(CSRC, "*.hip")) if _included(p)]
+    return max((os.path.getmtime(p) for p in inc), default=0.0)
+
+
 def _compile(src, force):
     obj = os.path.join(OBJ, os.path.basename(src) + ".o")
     if not force and os.path.exists(obj):
-        if os.path.getmtime(obj) >= max(os.path.getmtime(src), _headers_mtime()):
+        if os.path.getmtime(obj) >= max(os.path.getmtime(src), _headers_mtime(), _included_mtime()):
             return obj, False
     cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -43,7 +53,8 @@ def _compile(src, force):
 
 def build(force=False, jobs=None):
     os.makedirs(OBJ, exist_ok=True)
-    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    # sources marked "rs-build: included" on line 1 are compiled inside the file that includes them
+    srcs = [p for p in sorted(glob.glob(os.path.join(CSRC, "*.hip"))) if not _included(p)]
     jobs = jobs or min(len(srcs), max(1, min(8, os.cpu_count() or 1)))
     with cf.ThreadPoolExecutor(jobs) as ex:
         results = list(ex.map(lambda s: _compile(s, force), srcs))

@@ -1,3 +1,4 @@
+// rs-build: included by grad_tail.hip (compiled once, as part of that translation unit)
 // Item-embedding gradient by inverted index (deterministic, no float atomics).
 //
 // The item table receives, per training step, one gradient row per token of the input sequence
@@ -242,16 +243,26 @@ struct GradArgs {
   float* dtable;
 };
 
-// one block per chunk of CH sorted entries.  Dependent global round trips: (keys, entries) ->
+// one workgroup per chunk of CH sorted entries.  Dependent global round trips: (keys, entries) ->
 // (contribution rows, key bounds, the table rows of run heads) -> stores.
 template <int D>
-__global__ __launch_bounds__(256) void item_chunk_kernel(GradArgs a) {
+struct ChunkLds {
+  float rowsum[CH][D + 4];   // +4: rows start on different banks
+  uint32_t skey[CH + 1], sent[CH];
+  int kst[CH], ken[CH];
+};
+
+// chunk `chunk` of the sorted entries (one 256-thread workgroup), LDS at `L`
+template <int D>
+__device__ __forceinline__ void item_chunk(const GradArgs& a, int64_t chunk, ChunkLds<D>& L) {
   constexpr int TPE = D / 8, EPP = 256 / TPE, NPASS = CH / EPP;   // threads per entry row, rows per pass
-  __shared__ __attribute__((aligned(16))) float rowsum[CH][D + 4];   // +4: rows start on different banks
-  __shared__ uint32_t skey[CH + 1], sent[CH];
-  __shared__ int kst[CH], ken[CH];
+  auto& rowsum = L.rowsum;
+  auto& skey = L.skey;
+  auto& sent = L.sent;
+  auto& kst = L.kst;
+  auto& ken = L.ken;
   const int tid = threadIdx.x;
-  const int64_t base = (int64_t)blockIdx.x * CH;
+  const int64_t base = chunk * CH;
   const int cnt = (int)min((int64_t)CH, a.n - base);
   const bool drop = a.drop_p > 0.f;
   const uint32_t s32 = drop ? seed32(eff_seed(a.salt, a.seed_base)) : 0u;
@@ -345,20 +356,26 @@ __global__ __launch_bounds__(256) void item_chunk_kernel(GradArgs a) {
       t[0] = t0;
       t[1] = t1;
     } else {
-      float4* o = reinterpret_cast<float4*>(a.part + ((int64_t)blockIdx.x * 2 + (j == 0 ? 0 : 1)) * D + c0);
+      float4* o = reinterpret_cast<float4*>(a.part + (chunk * 2 + (j == 0 ? 0 : 1)) * D + c0);
       o[0] = r0;
       o[1] = r1;
     }
   }
 }
 
+template <int D>
+__global__ __launch_bounds__(256) void item_chunk_kernel(GradArgs a) {
+  __shared__ __attribute__((aligned(16))) ChunkLds<D> L;
+  item_chunk<D>(a, blockIdx.x, L);
+}
+
 // one wave per chunk: the chunk holding the first entry of a key that continues past the chunk
 // sums that key's partials in chunk order and writes the table row
 template <int D>
-__global__ __launch_bounds__(256) void item_span_kernel(GradArgs a, int64_t nchunks) {
+__device__ __forceinline__ void item_span(const GradArgs& a, int64_t nchunks, int64_t blk) {
   constexpr int CPL = D / 64 > 0 ? D / 64 : 1;    // columns per lane
   const int lane = threadIdx.x & 63;
-  const int64_t ch = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t ch = blk * 4 + (threadIdx.x >> 6);
   if (ch >= nchunks) return;
   const int64_t base = ch * CH;
   const int64_t last = min(a.n, base + CH) - 1;
@@ -400,6 +417,11 @@ __global__ __launch_bounds__(256) void item_span_kernel(GradArgs a, int64_t nchu
     const int c = lane + 64 * q;
     if (c < D) a.dtable[(int64_t)k * D + c] += acc[q];
   }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void item_span_kernel(GradArgs a, int64_t nchunks) {
+  item_span<D>(a, nchunks, blockIdx.x);
 }
 
 }  // namespace ig
@@ -460,18 +482,31 @@ int rs_item_index_build(int nsrc, const int64_t* keys0, const int64_t* keys1, co
   return (int)hipGetLastError();
 }
 
-int rs_item_grad(const void* ws, int nsrc, int64_t rows, int64_t table_rows, int64_t d, const void* dx, float scale,
-                 float drop_p, uint64_t salt, const uint64_t* seed_base, const void* f, const float* w1,
-                 const float* w2, float* dtable, void* stream) {
+}  // extern "C"
+
+static int item_grad_args(const void* ws, int nsrc, int64_t rows, int64_t table_rows, int64_t d, const void* dx,
+                          float scale, float drop_p, uint64_t salt, const uint64_t* seed_base, const void* f,
+                          const float* w1, const float* w2, float* dtable, ig::GradArgs& a, ig::Layout& L) {
   if (nsrc < 1 || nsrc > 3 || rows <= 0 || !ws || !dtable || !dx || (nsrc > 1 && (!f || !w1)) || (nsrc > 2 && !w2))
     return RS_ERR_ARG;
-  ig::Layout L;
   hipError_t e = ig::layout(nsrc, rows, table_rows, d, L);
   if (e != hipSuccess) return (int)e;
   const char* w = (const char*)ws;
-  ig::GradArgs a = {(const uint32_t*)(w + L.sk), (const uint32_t*)(w + L.sv), (const int*)(w + L.start),
-                    (float*)(w + L.part), L.n, rows, (const __bf16*)dx, scale, drop_p, salt, seed_base,
-                    (const __bf16*)f, w1, w2, dtable};
+  a = {(const uint32_t*)(w + L.sk), (const uint32_t*)(w + L.sv), (const int*)(w + L.start), (float*)(w + L.part),
+       L.n, rows, (const __bf16*)dx, scale, drop_p, salt, seed_base, (const __bf16*)f, w1, w2, dtable};
+  return 0;
+}
+
+extern "C" {
+
+int rs_item_grad(const void* ws, int nsrc, int64_t rows, int64_t table_rows, int64_t d, const void* dx, float scale,
+                 float drop_p, uint64_t salt, const uint64_t* seed_base, const void* f, const float* w1,
+                 const float* w2, float* dtable, void* stream) {
+  ig::GradArgs a;
+  ig::Layout L;
+  if (int e = item_grad_args(ws, nsrc, rows, table_rows, d, dx, scale, drop_p, salt, seed_base, f, w1, w2, dtable,
+                             a, L))
+    return e;
   hipStream_t s = (hipStream_t)stream;
   const dim3 g1((unsigned)L.nchunks), g2((unsigned)cdiv(L.nchunks, 4));
   if (d == 64) {

@@ -1,3 +1,4 @@
+// rs-build: included by grad_tail.hip (compiled once, as part of that translation unit)
 // Grouped weight-gradient GEMMs + grouped slab reduction (bf16 operands, fp32 results).
 //
 // In a SASRec / BERT4Rec backward every Linear / Conv1d(k=1) weight gradient is
@@ -36,11 +37,14 @@ struct Args {
 };
 
 template <int T>
-__global__ __launch_bounds__(256, 2) void wgrad_group_kernel(Args a) {
-  KStampBegin stamp_(a.ks);
+constexpr int group_lds_bytes() { return 2 * 2 * gbf::Img<true, T>::ELEMS * (int)sizeof(bf16); }
+
+// one (split, output tile) of the grouped launch; bid_raw / nwg: this workgroup's index among the launch's
+// nwg weight-gradient workgroups (dispatch order, before the XCD remap)
+template <int T>
+__device__ __forceinline__ void group_tile(const Args& a, unsigned bid_raw, unsigned nwg, bf16* smem) {
   using I = gbf::Img<true, T>;          // k-major stage image [64 rows][T + 8]
   constexpr int STAGE = 2 * I::ELEMS;
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * STAGE];
   constexpr int BKT = gbf::BKT;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), wm = wave >> 1, wn = wave & 1;
   constexpr int FM = T / 32, FN = T / 32;
@@ -48,9 +52,9 @@ __global__ __launch_bounds__(256, 2) void wgrad_group_kernel(Args a) {
   // XCD-aware: workgroup b runs on XCD b % 8; give each XCD a contiguous range of (split, tile) pairs, so
   // the tiles that share a row range's dY / X column slices read them through ONE XCD's L2 (round-robin
   // dealing had every XCD fetch its own copy: ~2.5x the algorithmic HBM bytes at the BERT shapes)
-  unsigned bid = blockIdx.x;
+  unsigned bid = bid_raw;
   {
-    const unsigned nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, x = bid & 7;
+    const unsigned q = nwg >> 3, r = nwg & 7, x = bid & 7;
     bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
   }
   const int t = (int)(bid % (unsigned)a.ntiles);
@@ -150,6 +154,13 @@ __global__ __launch_bounds__(256, 2) void wgrad_group_kernel(Args a) {
     }
 }
 
+template <int T>
+__global__ __launch_bounds__(256, 2) void wgrad_group_kernel(Args a) {
+  KStampBegin stamp_(a.ks);
+  __shared__ __attribute__((aligned(16))) bf16 smem[group_lds_bytes<T>() / sizeof(bf16)];
+  group_tile<T>(a, blockIdx.x, gridDim.x, smem);
+}
+
 // ---------------------------------------------------------------- grouped slab reduction
 constexpr int MAXS = 64;
 struct Seg {
@@ -167,10 +178,9 @@ struct RArgs {
 
 // block = 16 float4 columns x 16 split groups; group g sums splits g, g+16, ... ; fixed-order
 // combine in LDS (deterministic)
-__global__ __launch_bounds__(256) void reduce_segments_kernel(RArgs a) {
-  KStampEnd stamp_(a.ks);
-  constexpr int C = 16, G = 16;
-  const int b = blockIdx.x;
+constexpr int RED_C = 16, RED_G = 16;
+__device__ __forceinline__ void reduce_segments_block(const RArgs& a, int b, float4 (*red)[RED_C]) {
+  constexpr int C = RED_C, G = RED_G;
   int si = 0;
 #pragma unroll 1
   for (int q = 1; q < a.nseg; ++q)
@@ -199,7 +209,6 @@ __global__ __launch_bounds__(256) void reduce_segments_kernel(RArgs a) {
       acc.x += u.x; acc.y += u.y; acc.z += u.z; acc.w += u.w;
     }
   }
-  __shared__ float4 red[G][C];
   red[grp][col] = acc;
   __syncthreads();
   if (grp == 0 && i4 < n4) {
@@ -218,11 +227,15 @@ __global__ __launch_bounds__(256) void reduce_segments_kernel(RArgs a) {
   }
 }
 
+__global__ __launch_bounds__(256) void reduce_segments_kernel(RArgs a) {
+  KStampEnd stamp_(a.ks);
+  __shared__ float4 red[RED_G][RED_C];
+  reduce_segments_block(a, blockIdx.x, red);
+}
+
 // few splits (<= 32): one float4 column per thread, all splits summed in order by that thread (4 loads
 // in flight), 1024 columns per block -- the large BERT-size segments stream at HBM rate
-__global__ __launch_bounds__(256) void reduce_cols_kernel(RArgs a) {
-  KStampEnd stamp_(a.ks);
-  const int b = blockIdx.x;
+__device__ __forceinline__ void reduce_cols_block(const RArgs& a, int b) {
   int si = 0;
 #pragma unroll 1
   for (int q = 1; q < a.nseg; ++q)
@@ -255,30 +268,45 @@ __global__ __launch_bounds__(256) void reduce_cols_kernel(RArgs a) {
   *o = acc;
 }
 
+__global__ __launch_bounds__(256) void reduce_cols_kernel(RArgs a) {
+  KStampEnd stamp_(a.ks);
+  reduce_cols_block(a, blockIdx.x);
+}
+
 }  // namespace wg
 
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// one reduction launch's arguments for segs[0, nseg <= MAXS): RS_ERR_ARG on a bad segment; blk = workgroups,
+// cols = the column-per-thread form (few splits)
+static int reduce_args(int nseg, const rs_reduce_segment* segs, int accumulate, wg::RArgs& ra, int& blk, bool& cols) {
+  ra = wg::RArgs{};
+  ra.nseg = nseg;
+  ra.accumulate = accumulate;
+  int64_t max_splits = 0;
+  for (int q = 0; q < nseg; ++q) max_splits = max(max_splits, segs[q].splits);
+  cols = max_splits <= 16;     // few splits: a column per thread (reduce_cols_kernel)
+  blk = 0;
+  for (int q = 0; q < nseg; ++q) {
+    const rs_reduce_segment& g = segs[q];
+    if (g.n <= 0 || g.n % 4 || g.stride % 4 || g.splits < 1 || !al16(g.src) || !al16(g.out)) return RS_ERR_ARG;
+    ra.s[q] = {g.src, g.stride, (int)g.splits, (int)g.n, g.out};
+    ra.blk0[q] = blk;
+    blk += (int)cdiv(g.n / 4, cols ? 256 : 16);
+  }
+  ra.blk0[nseg] = blk;
+  return 0;
+}
 
 static int launch_segments(int nseg, const rs_reduce_segment* segs, int accumulate, hipStream_t s,
                            KStamp end = KStamp{}) {
   if (nseg <= 0) return 0;
   for (int base = 0; base < nseg; base += wg::MAXS) {
-    wg::RArgs ra{};
-    ra.nseg = min(wg::MAXS, nseg - base);
-    ra.accumulate = accumulate;
+    wg::RArgs ra;
+    int blk;
+    bool cols;
+    if (int e = reduce_args(min(wg::MAXS, nseg - base), segs + base, accumulate, ra, blk, cols)) return e;
     if (base + wg::MAXS >= nseg) ra.ks = end;
-    int64_t max_splits = 0;
-    for (int q = 0; q < ra.nseg; ++q) max_splits = max(max_splits, segs[base + q].splits);
-    const bool cols = max_splits <= 16;     // few splits: a column per thread (reduce_cols_kernel)
-    int blk = 0;
-    for (int q = 0; q < ra.nseg; ++q) {
-      const rs_reduce_segment& g = segs[base + q];
-      if (g.n <= 0 || g.n % 4 || g.stride % 4 || g.splits < 1 || !al16(g.src) || !al16(g.out)) return RS_ERR_ARG;
-      ra.s[q] = {g.src, g.stride, (int)g.splits, (int)g.n, g.out};
-      ra.blk0[q] = blk;
-      blk += (int)cdiv(g.n / 4, cols ? 256 : 16);
-    }
-    ra.blk0[ra.nseg] = blk;
     if (cols) hipLaunchKernelGGL(wg::reduce_cols_kernel, dim3((unsigned)blk), dim3(256), 0, s, ra);
     else hipLaunchKernelGGL(wg::reduce_segments_kernel, dim3((unsigned)blk), dim3(256), 0, s, ra);
     const hipError_t e = hipGetLastError();
@@ -301,15 +329,20 @@ int rs_reduce_segments(int nseg, const rs_reduce_segment* segs, int accumulate, 
   return launch_segments(nseg, segs, accumulate, (hipStream_t)stream);
 }
 
-int rs_wgrad_grouped(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_t rows_per_split, float* slab,
-                     int64_t slab_numel, int nextra, const rs_reduce_segment* extra, void* stream) {
+}  // extern "C"
+
+// the grouped launch's arguments (T = output tile edge) and its reduction segments (problems' W and bias
+// segments, then the caller's extra ones)
+static int wgrad_group_args(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_t rows_per_split, float* slab,
+                            int64_t slab_numel, int nextra, const rs_reduce_segment* extra, wg::Args& a, int& T_,
+                            rs_reduce_segment* segs, int& ns) {
   if (nprob <= 0 || nprob > wg::MAXP || M <= 0 || rows_per_split <= 0 || rows_per_split % 64 || !slab)
     return RS_ERR_ARG;
   int64_t T = 128;
   for (int q = 0; q < nprob; ++q)
     if (probs[q].N % 128 || probs[q].K % 128) T = 64;
   const int64_t splits = cdiv(M, rows_per_split);
-  wg::Args a{};
+  a = wg::Args{};
   a.nprob = nprob;
   a.M = M;
   a.rows_per_split = (int)rows_per_split;
@@ -328,16 +361,8 @@ int rs_wgrad_grouped(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_
   }
   if (off > slab_numel) return RS_ERR_ARG;
   a.ntiles = tiles;
-  a.ks = kstamp_next(RS_STAMP_WGRAD_GROUPED);
-  hipStream_t s = (hipStream_t)stream;
-  const dim3 grid((unsigned)(tiles * splits));
-  if (T == 128) hipLaunchKernelGGL(wg::wgrad_group_kernel<128>, grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(wg::wgrad_group_kernel<64>, grid, dim3(256), 0, s, a);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return (int)e;
-  // reduce: per problem its W segment and (optional) bias segment, then the caller's extra segments
-  rs_reduce_segment segs[2 * wg::MAXP + wg::MAXS];
-  int ns = 0;
+  T_ = (int)T;
+  ns = 0;
   off = 0;
   for (int q = 0; q < nprob; ++q) {
     const rs_wgrad_problem& p = probs[q];
@@ -348,6 +373,25 @@ int rs_wgrad_grouped(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_
   }
   if (nextra < 0 || nextra > wg::MAXS) return RS_ERR_ARG;
   for (int q = 0; q < nextra; ++q) segs[ns++] = extra[q];
+  return 0;
+}
+
+extern "C" {
+
+int rs_wgrad_grouped(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_t rows_per_split, float* slab,
+                     int64_t slab_numel, int nextra, const rs_reduce_segment* extra, void* stream) {
+  wg::Args a;
+  int T, ns;
+  rs_reduce_segment segs[2 * wg::MAXP + wg::MAXS];
+  if (int e = wgrad_group_args(nprob, probs, M, rows_per_split, slab, slab_numel, nextra, extra, a, T, segs, ns))
+    return e;
+  a.ks = kstamp_next(RS_STAMP_WGRAD_GROUPED);
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((unsigned)(a.ntiles * a.splits));
+  if (T == 128) hipLaunchKernelGGL(wg::wgrad_group_kernel<128>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(wg::wgrad_group_kernel<64>, grid, dim3(256), 0, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
   return launch_segments(ns, segs, 1, s, a.ks);
 }
 

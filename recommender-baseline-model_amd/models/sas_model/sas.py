@@ -304,7 +304,11 @@ class SASEngine:
                 ops.sas_head_bwd(None, None, None, None, None, dpl, dnl, None, None, s["pos"], s["neg"], E, s["xL"],
                                  gl, s["muf"], s["rf"], dx, lnh)
             segs = ops.ln_partial_segments(lnh, M, d, G("last_layernorm.weight"), G("last_layernorm.bias"))
-            side = os.environ.get("RS_SAS_EMB_GRAD_SIDE", "1") != "0"
+            # the item table's gradient: "side" (default) = rs_item_grad on the side queue beside the grouped
+            # weight gradients; "fused" = inside those launches on this queue (rs_wgrad_grouped_items; measured
+            # 0.367 vs 0.356 ms/step at cfg2: the item chunks queue behind the weight-gradient tiles); "serial"
+            tail_mode = os.environ.get("RS_SAS_GRAD_TAIL", "side")
+            side = tail_mode == "side"
             if self._side_refreshed or not side:
                 # the blocks' backward reads the transposed weights the side branch wrote this step (otherwise
                 # the previous step's optimizer wrote them), the item gradient on the main stream the index
@@ -316,11 +320,13 @@ class SASEngine:
             # the item table's gradient (rs_item_grad, ~42 us beside the weight gradients) on the side stream;
             # the positional table's (10 us) after the weight gradients on the main one: the two branches then
             # end together and the join's cross-queue latency is hidden
-            dx = self._backward_blocks_fused(s, dx, grad, segs, tail=item_grads if side else None)
+            fused_items = (lambda dx: (iws, 3, M, dx, math.sqrt(d), p, self.salt["emb"], sb, s["f"], dpl, dnl,
+                                       G("item_emb.weight"))) if tail_mode == "fused" else None
+            dx = self._backward_blocks_fused(s, dx, grad, segs, tail=item_grads if side else None, items=fused_items)
             ops.embed_bwd(0, ids, T, dx, math.sqrt(d), p, self.salt["emb"], sb, None, G("pos_emb.weight"))
             if side:
                 torch.cuda.current_stream().wait_event(self._tail_join)
-            else:
+            elif tail_mode != "fused":
                 item_grads(dx)
             if split is not None:
                 split("dense")          # every parameter gradient is final (data-parallel overlap)
@@ -415,13 +421,14 @@ class SASEngine:
         ops.transpose_bf16(self._wT_desc, self._wT_tiles, self.flat.bf16, self._wT)
         return self._wT
 
-    def _backward_blocks_fused(self, s, dx, grad, extra_segs=(), tail=None):
+    def _backward_blocks_fused(self, s, dx, grad, extra_segs=(), tail=None, items=None):
         """SAS blocks' backward with rs_sas_block_out_bwd / rs_sas_block_in_bwd (rowfused.hip) for the
         row-local chains; then ALL ten weight gradients and the four LayerNorm affine partial sets in
         one grouped GEMM launch + one grouped reduction (rs_wgrad_grouped, wgrad.hip).  Returns the
         gradient at the embedding output.  tail(dx): work on that gradient alone (the item table's
         gradient), issued on the side stream so it runs beside the grouped weight-gradient launch (both are
-        latency-bound); the caller joins self._tail_join."""
+        latency-bound); the caller joins self._tail_join.  items(dx): item_grad's arguments, run inside the grouped
+        weight-gradient launches instead (ops.wgrad_grouped items=)."""
         B, T, p, ids, sb = s["B"], s["T"], s["p"], s["ids"], s["sb"]
         M, d, H, Dh, L = B * T, self.d, self.H, self.Dh, self.L
         e = self._buf
@@ -486,7 +493,7 @@ class SASEngine:
         # the grouped launch is captured BEFORE the side branch: a HIP graph keeps a node's first child on its
         # queue, so the weight gradients follow the blocks' backward with no cross-queue hop (side branch
         # first: 11 us of fork latency before rs_wgrad_grouped and 11 us of join latency before Adam)
-        ops.wgrad_grouped(probs, M, rows, wslab, extra=segs)
+        ops.wgrad_grouped(probs, M, rows, wslab, extra=segs, items=items(dx) if items is not None else None)
         if tail is not None:
             self._side.wait_event(fork)
             with torch.cuda.stream(self._side):

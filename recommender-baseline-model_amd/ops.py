@@ -418,15 +418,25 @@ def _segments(segs):
     return arr
 
 
-def wgrad_grouped(problems, M, rows_per_split, slab, extra=()):
+def wgrad_grouped(problems, M, rows_per_split, slab, extra=(), items=None):
     """problems: [(dY, X, dW, db|None)] with dW [N][K] fp32 (+=); extra: reduce segments
-    (src, stride, splits, n, out) summed (+=) in the same reduction launch."""
+    (src, stride, splits, n, out) summed (+=) in the same reduction launch.  items: item_grad's arguments
+    (ws, nsrc, rows, dx, scale, drop_p, salt, seed_base, f, w1, w2, dtable) -- that gradient then shares the two
+    launches (rs_wgrad_grouped_items)."""
     arr = (_lib.WgradProblem * len(problems))()
     for i, (dY, X, dW, db) in enumerate(problems):
         N, K = dY.shape[1], X.shape[1]
         assert dW.numel() == N * K and dY.shape[0] >= M and X.shape[0] >= M
         arr[i] = _lib.WgradProblem(ptr(dY), ld(dY), ptr(X), ld(X), N, K, ptr(dW), ptr(db) if db is not None else None)
     segs = _segments(list(extra))
+    if items is not None:
+        ws, nsrc, rows, dx, scale, drop_p, salt, seed_base, f, w1, w2, dtable = items
+        table_rows, d = dtable.shape
+        call("rs_wgrad_grouped_items", len(problems), arr, M, rows_per_split, ptr(slab), slab.numel(), len(extra),
+             segs, ptr(ws), nsrc, rows, table_rows, d, ptr(dx), scale, drop_p, salt, ptr(seed_base),
+             ptr(f) if f is not None else None, ptr(w1) if w1 is not None else None,
+             ptr(w2) if w2 is not None else None, ptr(dtable), stream())
+        return
     call("rs_wgrad_grouped", len(problems), arr, M, rows_per_split, ptr(slab), slab.numel(), len(extra), segs,
          stream())
 

@@ -86,3 +86,19 @@ def test_unrolled_rejects_wrong_shapes():
         st.replay_packed(bs[0])
     with pytest.raises(ValueError):
         st.replay(*bs[0].unbind(0))
+
+
+def test_grad_tail_modes_bitwise(monkeypatch):
+    """The SAS backward tail's three forms (item gradient on the side queue / inside the grouped weight-gradient
+    launches, rs_wgrad_grouped_items / after them) give the same parameters bit for bit."""
+    from rbm_amd.train_step import FusedTrainStep
+    bs = _batches("sas", 3)
+    runs = []
+    for mode in ("side", "fused", "serial"):
+        monkeypatch.setenv("RS_SAS_GRAD_TAIL", mode)
+        st = FusedTrainStep(_model("sas"), lr=1e-3)
+        for b in bs:
+            st.step(*b.unbind(0))
+        torch.cuda.synchronize()
+        runs.append(st.flat.data.clone())
+    assert torch.equal(runs[0], runs[1]) and torch.equal(runs[0], runs[2])
