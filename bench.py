@@ -204,8 +204,8 @@ def roofline(cfg, B, dtype, live_us=None, reps=50, labelled=None):
         # q,k,v,o,dO + lse, write dq,dk,dv once
         flops = 4 * 2.0 * (T * (T + 1) / 2) * Dh * B * H
         nbytes = 8 * M * d * es + B * H * T * 4 * 2
-        return _roof("rs_attn_bwd (attn_bwd_dq_lds + attn_bwd_dkv_lds)", us, flops, nbytes, dtype,
-                     f"causal attention backward, B={B} T={T} Dh={Dh} dropout {cfg['p']}; 2 kernels per launch",
+        return _roof("rs_attn_bwd (attn_bwd_lds: dQ + dK/dV workgroups)", us, flops, nbytes, dtype,
+                     f"causal attention backward, B={B} T={T} Dh={Dh} dropout {cfg['p']}; one launch, both passes",
                      live_us)
     if dominant(cfg) == "vocab_ce_fwd":
         # BERT, 1M-item vocabulary: h[R,d] . E^T + b with the online-softmax partial epilogue over the labelled

@@ -15,7 +15,7 @@ import json
 import os
 import sys
 
-KEYS = {"rs_attn_bwd (attn_bwd_dq_lds + attn_bwd_dkv_lds)": ["attn_bwd_dq_lds_kernel", "attn_bwd_dkv_lds_kernel"],
+KEYS = {"rs_attn_bwd (attn_bwd_lds: dQ + dK/dV workgroups)": ["attn_bwd_lds_kernel"],
         "rs_wgrad_grouped (wgrad_group_kernel + reduce_cols_kernel)": ["wgrad_group_kernel", "reduce_cols_kernel"]}
 
 
