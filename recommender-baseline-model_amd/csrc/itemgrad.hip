@@ -8,7 +8,7 @@
 // the memory-side atomic rate and serialise on the hot rows.  Instead:
 //
 //   rs_item_index_build: keys (ids | pos | neg) -> stable counting sort of the entries by key:
-//                        per-1024-entry-block key histograms (LDS), per-key exclusive prefix over
+//                        per-512-entry-block key histograms (LDS), per-key exclusive prefix over
 //                        blocks, a scan over keys, then each block places its entries with a
 //                        block radix sort for the in-block rank.  When the per-block histogram
 //                        table would exceed 2^26 ints a device radix sort (rocPRIM) is used
@@ -28,7 +28,7 @@
 namespace ig {
 
 constexpr int CH = 64;          // sorted entries per gradient chunk
-constexpr int BE = 1024;        // entries per counting-sort block
+constexpr int BE = 512;         // entries per counting-sort block (512: 150 blocks at cfg2, 1024 took 75)
 constexpr int VMAX_LDS = 32768;            // largest table for the LDS histogram
 constexpr int64_t HMAX = (int64_t)1 << 26;  // largest per-block histogram table (ints) for the counting sort
 
@@ -99,8 +99,10 @@ struct Keys {
 
 // ---- counting sort ------------------------------------------------------------------------
 // H[b][v] = number of entries of block b with key v
+// LDS sized to the table (dynamic, V ints): a 3.4k-row table takes 14 KB, so the block fits beside the
+// forward's kernels on the side queue (a static 128 KB array needed an idle CU and started late)
 __global__ __launch_bounds__(256) void hist_kernel(Keys K, int* __restrict__ H) {
-  __shared__ int hist[VMAX_LDS];
+  extern __shared__ int hist[];
   const int tid = threadIdx.x;
   const int V = (int)K.V;
   for (int v = tid; v < V; v += 256) hist[v] = 0;
@@ -455,7 +457,12 @@ int rs_item_index_build(int nsrc, const int64_t* keys0, const int64_t* keys1, co
     int* H = (int*)(w + L.H);
     int* total = (int*)(w + L.total);
     if (table_rows <= ig::VMAX_LDS) {
-      hipLaunchKernelGGL(ig::hist_kernel, dim3((unsigned)L.nb), dim3(256), 0, s, K, H);
+      static const bool attr = [] {
+        return hipFuncSetAttribute((const void*)ig::hist_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   ig::VMAX_LDS * (int)sizeof(int)) == hipSuccess;
+      }();
+      if (!attr) return RS_ERR_UNSUPPORTED;
+      hipLaunchKernelGGL(ig::hist_kernel, dim3((unsigned)L.nb), dim3(256), (size_t)L.V * sizeof(int), s, K, H);
     } else {
       if ((e = hipMemsetAsync(H, 0, (size_t)L.nb * table_rows * 4, s)) != hipSuccess) return (int)e;
       hipLaunchKernelGGL(ig::hist_global_kernel, dim3((unsigned)L.nb), dim3(256), 0, s, K, H);
