@@ -378,6 +378,13 @@ int rs_wgrad_grouped_items(int nprob, const rs_wgrad_problem* probs, int64_t M, 
                            int64_t rows, int64_t table_rows, int64_t d, const void* dx, float scale, float drop_p,
                            uint64_t salt, const uint64_t* seed_base, const void* f, const float* w1, const float* w2,
                            float* dtable, void* stream);
+
+/* rs_wgrad_grouped followed by rs_embed_bwd's positional part (bf16, SAS mode 0, scale 1, dpos +=): the
+ * positional table's gradient rides in the grouped reduction's launch as T extra workgroups (grad_tail.hip). */
+int rs_wgrad_grouped_pos(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_t rows_per_split, float* slab,
+                         int64_t slab_numel, int nextra, const rs_reduce_segment* extra, const int64_t* ids,
+                         int64_t T, const void* dx, int64_t d, float drop_p, uint64_t salt,
+                         const uint64_t* seed_base, float* dpos, void* stream);
 /* The reduction alone: out (+)= sum over splits, for nseg segments (any number, 64 per launch). */
 int rs_reduce_segments(int nseg, const rs_reduce_segment* segs, int accumulate, void* stream);
 

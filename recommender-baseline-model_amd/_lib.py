@@ -96,6 +96,8 @@ SIGNATURES = {
     "rs_sas_head_fwd": [i64, i64, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "rs_sas_head_bwd": [i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "rs_item_grad": [vp, i32, i64, i64, i64, vp, f32, f32, u64, vp, vp, vp, vp, vp, vp],
+    "rs_wgrad_grouped_pos": [i32, C.POINTER(WgradProblem), i64, i64, vp, i64, i32, C.POINTER(ReduceSegment),
+                             vp, i64, vp, i64, f32, u64, vp, vp, vp],
     "rs_wgrad_grouped_items": [i32, C.POINTER(WgradProblem), i64, i64, vp, i64, i32, C.POINTER(ReduceSegment),
                                vp, i32, i64, i64, i64, vp, f32, f32, u64, vp, vp, vp, vp, vp, vp],
     "rs_transpose_bf16": [i64, vp, i64, vp, vp, vp],

@@ -1,3 +1,4 @@
+// rs-build: included by grad_tail.hip (compiled once, as part of that translation unit)
 // Embedding stage and the SAS sampled-logit head (gfx950).  HBM-bound row
 // gathers / scatters: 16-byte vector loads along d, one row per 2..8 lanes.
 //
@@ -80,14 +81,13 @@ __global__ __launch_bounds__(256) void embed_bwd_pos_kernel(const int64_t* __res
 // vectorized positional-gradient sum: block = position t, 256 threads = CPR chunk-columns x RG
 // batch groups, fixed-order LDS combine (deterministic)
 template <typename T, int CPR, int NTB = 256>
-__global__ __launch_bounds__(NTB) void embed_bwd_pos_v_kernel(const int64_t* __restrict__ ids, int64_t rows,
-                                                              int64_t T_, const T* __restrict__ dx, int64_t d,
-                                                              int mode, float drop_p, uint64_t salt,
-                                                              const uint64_t* seed_base, float* __restrict__ dpos,
-                                                              int accumulate) {
+__device__ __forceinline__ void embed_pos_body(const int64_t* __restrict__ ids, int64_t rows, int64_t T_,
+                                               const T* __restrict__ dx, int64_t d, int mode, float drop_p,
+                                               uint64_t salt, const uint64_t* seed_base, float* __restrict__ dpos,
+                                               int accumulate, int64_t t) {
   constexpr int V = Vec<T>::N, RG = NTB / CPR;
   const uint64_t seed = eff_seed(salt, seed_base);
-  const int64_t t = blockIdx.x, nb = rows / T_;
+  const int64_t nb = rows / T_;
   const int cc = threadIdx.x % CPR, rg = threadIdx.x / CPR;
   float acc[V];
 #pragma unroll
@@ -130,6 +130,15 @@ __global__ __launch_bounds__(NTB) void embed_bwd_pos_v_kernel(const int64_t* __r
     for (int g2 = 0; g2 < RG; ++g2) sum += red[g2][c];
     dpos[t * d + c] = accumulate ? dpos[t * d + c] + sum : sum;
   }
+}
+
+template <typename T, int CPR, int NTB = 256>
+__global__ __launch_bounds__(NTB) void embed_bwd_pos_v_kernel(const int64_t* __restrict__ ids, int64_t rows,
+                                                              int64_t T_, const T* __restrict__ dx, int64_t d,
+                                                              int mode, float drop_p, uint64_t salt,
+                                                              const uint64_t* seed_base, float* __restrict__ dpos,
+                                                              int accumulate) {
+  embed_pos_body<T, CPR, NTB>(ids, rows, T_, dx, d, mode, drop_p, salt, seed_base, dpos, accumulate, blockIdx.x);
 }
 
 // one wave per row m

@@ -9,6 +9,7 @@
 //   queue it replaces a cross-queue fork + join of the step graph (~6 us of idle each, measured).
 #include "wgrad.hip"
 #include "itemgrad.hip"
+#include "embedding.hip"
 
 namespace gt {
 
@@ -36,6 +37,25 @@ __global__ __launch_bounds__(256) void reduce_span_kernel(wg::RArgs r, int rblk,
     else wg::reduce_segments_block(r, blockIdx.x, red);
   } else {
     ig::item_span<D>(g, nchunks, (int64_t)blockIdx.x - rblk);
+  }
+}
+
+// the grouped slab reduction AND the positional table's gradient (rs_embed_bwd's positional part, SAS mode):
+// workgroups [0, T_) sum one position each, the next rblk reduce
+__global__ __launch_bounds__(256) void reduce_pos_kernel(wg::RArgs r, int rblk, int cols, const int64_t* ids,
+                                                         int64_t rows, int64_t T_, const __bf16* dx, int64_t d,
+                                                         float drop_p, uint64_t salt, const uint64_t* seed_base,
+                                                         float* dpos) {
+  KStampEnd stamp_(r.ks);
+  __shared__ float4 red[wg::RED_G][wg::RED_C];
+  // the positions' workgroups (long: a 128-row column sum each) are dispatched first, the many short
+  // reduction workgroups fill the CUs around them
+  if ((int64_t)blockIdx.x < T_) {
+    embed_pos_body<__bf16, 16, 256>(ids, rows, T_, dx, d, 0, drop_p, salt, seed_base, dpos, 1, blockIdx.x);
+  } else {
+    const int b = (int)(blockIdx.x - T_);
+    if (cols) wg::reduce_cols_block(r, b);
+    else wg::reduce_segments_block(r, b, red);
   }
 }
 
@@ -91,6 +111,38 @@ int rs_wgrad_grouped_items(int nprob, const rs_wgrad_problem* probs, int64_t M, 
       : d == 128 ? gt::launch<64, 128>(a, g, r, rblk, cols, L.nchunks, s)
                  : gt::launch<64, 256>(a, g, r, rblk, cols, L.nchunks, s);
   return (int)e;
+}
+
+int rs_wgrad_grouped_pos(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_t rows_per_split, float* slab,
+                         int64_t slab_numel, int nextra, const rs_reduce_segment* extra, const int64_t* ids,
+                         int64_t T_, const void* dx, int64_t d, float drop_p, uint64_t salt,
+                         const uint64_t* seed_base, float* dpos, void* stream) {
+  if (!ids || !dx || !dpos || T_ <= 0 || M % T_) return RS_ERR_ARG;
+  wg::Args a;
+  int T, ns;
+  rs_reduce_segment segs[2 * wg::MAXP + wg::MAXS];
+  if (int e = wgrad_group_args(nprob, probs, M, rows_per_split, slab, slab_numel, nextra, extra, a, T, segs, ns))
+    return e;
+  const bool vec = d % 8 == 0 && d / 8 <= 16 && ((uintptr_t)dx % 16) == 0;
+  if (ns > wg::MAXS || !vec) {   // unfused: the two functions one after the other
+    if (int e = rs_wgrad_grouped(nprob, probs, M, rows_per_split, slab, slab_numel, nextra, extra, stream)) return e;
+    return rs_embed_bwd(RS_DTYPE_BF16, 0, ids, M, T_, dx, d, 1.f, drop_p, salt, seed_base, nullptr, dpos, 1, stream);
+  }
+  wg::RArgs r;
+  int rblk;
+  bool cols;
+  if (int e = reduce_args(ns, segs, 1, r, rblk, cols)) return e;
+  a.ks = kstamp_next(RS_STAMP_WGRAD_GROUPED);
+  r.ks = a.ks;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((unsigned)(a.ntiles * a.splits));
+  if (T == 128) hipLaunchKernelGGL(wg::wgrad_group_kernel<128>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(wg::wgrad_group_kernel<64>, grid, dim3(256), 0, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(gt::reduce_pos_kernel, dim3((unsigned)(rblk + T_)), dim3(256), 0, s, r, rblk, (int)cols, ids, M,
+                     T_, (const __bf16*)dx, d, drop_p, salt, seed_base, dpos);
+  return (int)hipGetLastError();
 }
 
 }  // extern "C"

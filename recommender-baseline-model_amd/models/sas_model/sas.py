@@ -322,8 +322,14 @@ class SASEngine:
             # end together and the join's cross-queue latency is hidden
             fused_items = (lambda dx: (iws, 3, M, dx, math.sqrt(d), p, self.salt["emb"], sb, s["f"], dpl, dnl,
                                        G("item_emb.weight"))) if tail_mode == "fused" else None
-            dx = self._backward_blocks_fused(s, dx, grad, segs, tail=item_grads if side else None, items=fused_items)
-            ops.embed_bwd(0, ids, T, dx, math.sqrt(d), p, self.salt["emb"], sb, None, G("pos_emb.weight"))
+            # the positional table's gradient rides in the grouped reduction's launch (RS_SAS_POS_MERGED=0: its
+            # own launch after it)
+            pos_merged = fused_items is None and os.environ.get("RS_SAS_POS_MERGED", "1") != "0"
+            pos_args = (lambda dx: (ids, T, dx, p, self.salt["emb"], sb, G("pos_emb.weight"))) if pos_merged else None
+            dx = self._backward_blocks_fused(s, dx, grad, segs, tail=item_grads if side else None, items=fused_items,
+                                             pos=pos_args)
+            if not pos_merged:
+                ops.embed_bwd(0, ids, T, dx, math.sqrt(d), p, self.salt["emb"], sb, None, G("pos_emb.weight"))
             if side:
                 torch.cuda.current_stream().wait_event(self._tail_join)
             elif tail_mode != "fused":
@@ -421,7 +427,7 @@ class SASEngine:
         ops.transpose_bf16(self._wT_desc, self._wT_tiles, self.flat.bf16, self._wT)
         return self._wT
 
-    def _backward_blocks_fused(self, s, dx, grad, extra_segs=(), tail=None, items=None):
+    def _backward_blocks_fused(self, s, dx, grad, extra_segs=(), tail=None, items=None, pos=None):
         """SAS blocks' backward with rs_sas_block_out_bwd / rs_sas_block_in_bwd (rowfused.hip) for the
         row-local chains; then ALL ten weight gradients and the four LayerNorm affine partial sets in
         one grouped GEMM launch + one grouped reduction (rs_wgrad_grouped, wgrad.hip).  Returns the
@@ -493,7 +499,8 @@ class SASEngine:
         # the grouped launch is captured BEFORE the side branch: a HIP graph keeps a node's first child on its
         # queue, so the weight gradients follow the blocks' backward with no cross-queue hop (side branch
         # first: 11 us of fork latency before rs_wgrad_grouped and 11 us of join latency before Adam)
-        ops.wgrad_grouped(probs, M, rows, wslab, extra=segs, items=items(dx) if items is not None else None)
+        ops.wgrad_grouped(probs, M, rows, wslab, extra=segs, items=items(dx) if items is not None else None,
+                          pos=pos(dx) if pos is not None else None)
         if tail is not None:
             self._side.wait_event(fork)
             with torch.cuda.stream(self._side):

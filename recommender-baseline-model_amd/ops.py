@@ -418,17 +418,24 @@ def _segments(segs):
     return arr
 
 
-def wgrad_grouped(problems, M, rows_per_split, slab, extra=(), items=None):
+def wgrad_grouped(problems, M, rows_per_split, slab, extra=(), items=None, pos=None):
     """problems: [(dY, X, dW, db|None)] with dW [N][K] fp32 (+=); extra: reduce segments
     (src, stride, splits, n, out) summed (+=) in the same reduction launch.  items: item_grad's arguments
     (ws, nsrc, rows, dx, scale, drop_p, salt, seed_base, f, w1, w2, dtable) -- that gradient then shares the two
-    launches (rs_wgrad_grouped_items)."""
+    launches (rs_wgrad_grouped_items).  pos: (ids, T, dx, drop_p, salt, seed_base, dpos) -- the SAS positional
+    table's gradient (embed_bwd mode 0, scale 1, +=) then rides in the reduction launch (rs_wgrad_grouped_pos)."""
     arr = (_lib.WgradProblem * len(problems))()
     for i, (dY, X, dW, db) in enumerate(problems):
         N, K = dY.shape[1], X.shape[1]
         assert dW.numel() == N * K and dY.shape[0] >= M and X.shape[0] >= M
         arr[i] = _lib.WgradProblem(ptr(dY), ld(dY), ptr(X), ld(X), N, K, ptr(dW), ptr(db) if db is not None else None)
     segs = _segments(list(extra))
+    if pos is not None:
+        assert items is None
+        ids, T, dx, drop_p, salt, seed_base, dpos = pos
+        call("rs_wgrad_grouped_pos", len(problems), arr, M, rows_per_split, ptr(slab), slab.numel(), len(extra),
+             segs, ptr(ids), T, ptr(dx), dx.shape[-1], drop_p, salt, ptr(seed_base), ptr(dpos), stream())
+        return
     if items is not None:
         ws, nsrc, rows, dx, scale, drop_p, salt, seed_base, f, w1, w2, dtable = items
         table_rows, d = dtable.shape
