@@ -338,18 +338,25 @@ class FusedTrainStep:
         if S > 1 and self.dp:
             raise ValueError("steps_per_graph > 1 is single-device only (DP exchanges gradients between steps)")
         self.steps_per_graph = S
-        self.loss_steps = torch.zeros(S, dtype=torch.float32, device=self.flat.device)
+        # one loss-statistics row per unrolled step: the step's kernels write its own row (a copy node between
+        # Adam and the next step's first kernel cost ~9 us of idle per step in the graph)
+        self.loss_rows = torch.zeros(S, 4, dtype=torch.float32, device=self.flat.device)
+        self.loss_steps = self.loss_rows[:, 2]
         return S
 
     def _unrolled(self, inputs, sample=None):
         """compute() for an unrolled graph: S x (sample, forward + backward, Adam, keep the loss)."""
         def compute(split=None):
-            for k in range(self.steps_per_graph):
-                if sample is not None:
-                    sample()
-                self._compute(*inputs(k))
-                self._update()
-                self.loss_steps[k:k + 1].copy_(self.loss_out[2:3])
+            base = self.loss_out
+            try:
+                for k in range(self.steps_per_graph):
+                    self.loss_out = self.loss_rows[k]
+                    if sample is not None:
+                        sample()
+                    self._compute(*inputs(k))
+                    self._update()
+            finally:
+                self.loss_out = base
         return compute
 
     def _capture_graphs(self, compute, stamps=None, unrolled=False):
