@@ -58,7 +58,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=24)
     ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None, help="sequences per GPU (default: the config's)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
@@ -70,8 +70,8 @@ def parse():
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse the "
                          "multi-process path with several ranks on one GPU)")
     ap.add_argument("--steps-per-graph", default="auto",
-                    help="training steps unrolled into one graph replay (single GPU; 'auto' = 4 when --steps and "
-                         "--warmup are multiples of 4, else 1); every step still runs on its own batch with its "
+                    help="training steps unrolled into one graph replay (single GPU; 'auto' = the largest of 8/4/2 "
+                         "dividing --steps and --warmup, else 1); every step still runs on its own batch with its "
                          "own Adam update")
     ap.add_argument("--nbatches", type=int, default=8, help="distinct synthetic batches cycled through")
     ap.add_argument("--sampler", default="host", choices=["host", "device"],
@@ -323,7 +323,9 @@ def main():
     stamps = None if sbuf is None else (sbuf, (dominant(cfg),))
 
     if args.steps_per_graph == "auto":
-        S = 4 if (world == 1 and not args.no_graph and args.steps % 4 == 0 and args.warmup % 4 == 0) else 1
+        # the largest of 8 / 4 / 2 steps per replay that divides both counts (a replay boundary costs ~25 us)
+        S = next((u for u in (8, 4, 2) if args.steps % u == 0 and args.warmup % u == 0), 1) \
+            if world == 1 and not args.no_graph else 1
     else:
         S = int(args.steps_per_graph)
         if S > 1 and (world > 1 or args.no_graph or args.steps % S or args.warmup % S):
