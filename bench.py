@@ -128,7 +128,7 @@ def _time_on_stream(fn, reps, stream):
     return e0.elapsed_time(e1) * 1e3 / reps
 
 
-def _roof(kernel, us, flops, nbytes, dtype, note, live_us=None):
+def _roof(kernel, us, flops, nbytes, dtype, note, live_us=None, live_expected=None):
     iso_us = us
     if live_us:
         us = sum(live_us) / len(live_us)
@@ -150,12 +150,14 @@ def _roof(kernel, us, flops, nbytes, dtype, note, live_us=None):
         return {"kernel": kernel, "bound": "hbm", "achieved": round(ach, 1), "peak": MI355X_HBM_GBS, "unit": "GB/s",
                 "frac": round(ach / MI355X_HBM_GBS, 4), "traffic": traffic, "avg_launch_us": round(us, 2),
                 "isolated_launch_us": round(iso_us, 2), "live_samples": len(live_us or ()),
+                "live_samples_expected": live_expected,
                 "algorithmic_bytes_per_launch": int(nbytes), "algorithmic_flops_per_launch": int(flops),
                 "arith_intensity": round(ai, 1), **util, "note": note}
     ach = flops / (us * 1e-6) / 1e12
     return {"kernel": kernel, "bound": "mfma", "achieved": round(ach, 2), "peak": peak_f, "unit": "TFLOP/s",
             "frac": round(ach / peak_f, 4), "traffic": traffic, "avg_launch_us": round(us, 2),
             "isolated_launch_us": round(iso_us, 2), "live_samples": len(live_us or ()),
+            "live_samples_expected": live_expected,
             "algorithmic_bytes_per_launch": int(nbytes), "algorithmic_flops_per_launch": int(flops),
             "arith_intensity": round(ai, 1), **util, "note": note}
 
@@ -169,7 +171,7 @@ def dominant(cfg):
     return "vocab_ce_fwd" if cfg["V"] >= 100000 else "wgrad_grouped"
 
 
-def roofline(cfg, B, dtype, live_us=None, reps=50, labelled=None):
+def roofline(cfg, B, dtype, live_us=None, reps=50, labelled=None, live_expected=None):
     """Dominant kernel of the step (by rocprof device time).  SAS: the attention backward (rs_attn_bwd:
     dQ+delta and dK/dV kernels); BERT: the grouped block weight gradients (rs_wgrad_grouped).
     live_us: its launch durations measured INSIDE the timed step replays (in-kernel begin/end stamps of
@@ -206,7 +208,7 @@ def roofline(cfg, B, dtype, live_us=None, reps=50, labelled=None):
         nbytes = 8 * M * d * es + B * H * T * 4 * 2
         return _roof("rs_attn_bwd (attn_bwd_lds: dQ + dK/dV workgroups)", us, flops, nbytes, dtype,
                      f"causal attention backward, B={B} T={T} Dh={Dh} dropout {cfg['p']}; one launch, both passes",
-                     live_us)
+                     live_us, live_expected)
     if dominant(cfg) == "vocab_ce_fwd":
         # BERT, 1M-item vocabulary: h[R,d] . E^T + b with the online-softmax partial epilogue over the labelled
         # rows (R = the batches' mean labelled count), E = out.weight [V+1, d] bf16
@@ -221,7 +223,7 @@ def roofline(cfg, B, dtype, live_us=None, reps=50, labelled=None):
         flops = 2.0 * R * V1 * d
         nbytes = (V1 * d + R * d) * es + R * -(-V1 // 128) * 2 * 4     # E, h once; (max, sum) partials
         return _roof("rs_vocab_head_fwd (E-tile-stationary logits + online-softmax partials)", us, flops, nbytes, dtype,
-                     f"R={R} labelled rows (batch mean) x V+1={V1} x d={d}", live_us)
+                     f"R={R} labelled rows (batch mean) x V+1={V1} x d={d}", live_us, live_expected)
     # BERT: the grouped weight-gradient launch of all block weights (rs_wgrad_grouped: GEMM + reduction),
     # the largest single kernel of the step
     from rbm_amd.models.bert_model.bert import BERTEngine
@@ -237,7 +239,7 @@ def roofline(cfg, B, dtype, live_us=None, reps=50, labelled=None):
     nbytes = sum(M * (n + k) * es + (n * k + n) * 4 * 2 for n, k in shapes)   # dY, X once; dW, db read+write
     return _roof("rs_wgrad_grouped (wgrad_group_kernel + reduce_cols_kernel)", us, flops, nbytes, dtype,
                  f"{len(shapes)} block weight gradients of M={M} token rows (d={d}, ff={Fd}, L={L}), "
-                 f"{-(-M // rows)} row splits; 2 kernels per launch", live_us)
+                 f"{-(-M // rows)} row splits; 2 kernels per launch", live_us, live_expected)
 
 
 # ------------------------------------------------------------------------------------ CPU baseline
@@ -362,6 +364,10 @@ def main():
                        for j in range(max(1, len(batches) // S))]
         batches = [(b,) for b in batches]
         run = trainer.replay_packed
+    # stamped launches per training step (mark numbering restarts at every unrolled step)
+    marks_per_step = len(ops.kernel_stamp_kinds()) if sbuf is not None else 0
+    if marks_per_step > NMARK:
+        raise SystemExit(f"{marks_per_step} stamped launches per step exceed the stamp buffer's {NMARK} marks")
     for i in range(args.warmup // S):
         loss = run(*batches[i % len(batches)])
     torch.cuda.synchronize()
@@ -385,13 +391,15 @@ def main():
     elapsed = tt.item()
     final_loss = float(loss.float().reshape(-1)[-1].item())
 
-    live = None
+    live, live_expected = None, None
     if sbuf is not None:
         live = [us for _, _, us in ops.read_kernel_stamps(sbuf, ops.wall_clock_khz())]
+        live_expected = args.steps * marks_per_step
         del sbuf
     labelled = (sum(float((lab != 0).sum()) for _, lab in host_batches) / len(host_batches)
                 if cfg["model"] == "bert" else None)
-    roof = roofline(cfg, B, args.dtype, live_us=live, labelled=labelled) if rank == 0 else None
+    roof = roofline(cfg, B, args.dtype, live_us=live, labelled=labelled, live_expected=live_expected) \
+        if rank == 0 else None
     if rank == 0:
         cpu = cpu_baseline(cfg, B, args.cpu_baseline_seconds) if world == 1 and args.cpu_baseline_seconds > 0 \
             else None

@@ -124,7 +124,9 @@ int rs_layernorm_bwd(int dtype, int variant, const void* X, int64_t ldx, const v
  * mask_kind 0 = causal, -inf above the diagonal (SAS, sas.py:70 + torch MHA baddbmm);
  * mask_kind 1 = key padding, scores of keys with ids==0 replaced by -1e9 (BERT,
  * bert_modules/bert.py:38 + attention/single.py:28).  S = scale * q.k^T;
- * P = softmax(S); P = dropout(P); O = P.v.  lse[(b*H+h)*T + t] = row logsumexp. */
+ * P = softmax(S); P = dropout(P); O = P.v.  lse[(b*H+h)*T + t] = row logsumexp.
+ * Dropout keep(seed, idx) of P[b,h,q,k] uses idx = ((b*H + h)*T + q)*Tp + k, Tp = T + (T & 1) (even row
+ * pitch), i.e. rs_dropout_rowmask over a (B*H*T, Tp) tensor draws the same mask (tests materialise it). */
 int rs_attn_fwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t Dh, const void* q, int64_t ldq,
                 const void* k, int64_t ldk, const void* v, int64_t ldv, void* o, int64_t ldo, float* lse,
                 float scale, int mask_kind, const int64_t* ids, float drop_p, uint64_t seed,
@@ -209,6 +211,15 @@ int rs_adam_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16
 int rs_adam_prepare_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, double* state,
                          const float* hyper, int zero_grad, const float* grad_divisor, uint64_t* seed_base,
                          const int64_t* tdesc, int ntd, int64_t tbase, void* wT, void* stream);
+
+/* SASRec's parameter-norm regulariser, BS/trainers/sas.py:51-52 (loss += l2_emb * torch.norm(p) for every
+ * parameter p): *loss += l2 * sum_seg ||p_seg||_2 and g += scale * l2 * p / ||p_seg|| (0 where the norm is 0,
+ * as torch's norm backward).  desc: device int64 [nchunk][4] = {lo, hi, first chunk of the segment, chunks of
+ * the segment} over the flat parameter buffer (chunks of one segment consecutive); ws: fp32 [nchunk]; scale:
+ * device float or null (= 1; the data-parallel step passes the global count its optimizer divides by);
+ * g and loss nullable.  Deterministic. */
+int rs_l2_penalty(const float* p, float* g, const int64_t* desc, int64_t nchunk, float l2, const float* scale,
+                  float* ws, float* loss, void* stream);
 
 /* dst_bf16[i] = bf16(src[i]) */
 int rs_cast_bf16(int64_t n, const float* src, void* dst, void* stream);

@@ -15,7 +15,8 @@
 // T is <= 256 for every reference config (max_len = 200 / 50), so no key-blocked
 // online softmax is needed; the backward recomputes P from the saved row
 // logsumexp.  Dropout masks are regenerated from the counter-based RNG with
-// index ((b*H + h)*T + query)*T + key.
+// index ((b*H + h)*T + query)*Tp + key, Tp = T rounded up to even (every mask row starts on a hash pair,
+// so the paired-hash kernels of attention_lds.hip draw the same masks for odd T).
 #include "common.h"
 #include "../../include/recsys_hip.h"
 
@@ -151,7 +152,7 @@ __global__ __launch_bounds__(64) void attn_fwd_kernel(AttnArgs a) {
     for (int r = 0; r < 4; ++r) {
       const int64_t qrow = q0 + 4 * g + r, key = (int64_t)kt * 16 + cl;
       float p = s[kt][r] / sm[r];
-      if (a.drop_p > 0.f) p *= drop_mul(a.drop_p, seed, (uint64_t)((bh * a.T + qrow) * a.T + key));
+      if (a.drop_p > 0.f) p *= drop_mul(a.drop_p, seed, (uint64_t)((bh * a.T + qrow) * (a.T + (a.T & 1)) + key));
       Ps[(4 * g + r) * PLD + kt * 16 + cl] = from_f<T>(p);
     }
   if (cl == 0) {
@@ -259,7 +260,7 @@ __global__ __launch_bounds__(64) void attn_bwd_dq_kernel(AttnArgs a) {
         float x = masked_score(a, b, qrow, key, s[r] * a.scale);
         float p = (x == NEG_INF || qrow >= a.T) ? 0.f : __expf(x - lse[r]);
         float dpe = dp[r];
-        if (a.drop_p > 0.f) dpe *= drop_mul(a.drop_p, seed, (uint64_t)((bh * a.T + qrow) * a.T + key));
+        if (a.drop_p > 0.f) dpe *= drop_mul(a.drop_p, seed, (uint64_t)((bh * a.T + qrow) * (a.T + (a.T & 1)) + key));
         dSs[(4 * g + r) * SLD + half * 16 + cl] = from_f<T>(p * (dpe - dl[r]) * a.scale);
       }
     }
@@ -337,7 +338,7 @@ __global__ __launch_bounds__(64) void attn_bwd_dkv_kernel(AttnArgs a) {
         const int64_t key = k0 + 4 * g + r;
         float x = masked_score(a, b, qrow, key, st[r] * a.scale);
         float p = (x == NEG_INF || qrow >= a.T || key >= a.T) ? 0.f : __expf(x - lq);
-        float dm = a.drop_p > 0.f ? drop_mul(a.drop_p, seed, (uint64_t)((bh * a.T + qrow) * a.T + key)) : 1.f;
+        float dm = a.drop_p > 0.f ? drop_mul(a.drop_p, seed, (uint64_t)((bh * a.T + qrow) * (a.T + (a.T & 1)) + key)) : 1.f;
         Pt[(4 * g + r) * SLD + half * 16 + cl] = from_f<T>(p * dm);
         dSt[(4 * g + r) * SLD + half * 16 + cl] = from_f<T>(p * (dpt[r] * dm - dq) * a.scale);
       }
@@ -412,13 +413,15 @@ hipError_t attn_lds_bwd(int64_t B, int64_t T, int64_t H, int64_t Dh, const void*
 // bf16 storage with T <= 256 takes the LDS-resident kernels (attention_lds.hip); fp32 (the
 // parity mode) and anything else the register/LDS-chunk kernels above.  RS_ATTN_LEGACY=1 forces
 // the latter (A/B testing).
-static bool use_lds_path(int dtype, int64_t T, int64_t Dh) {
+static bool use_lds_path(int dtype, int64_t BH, int64_t T, int64_t Dh) {
   static int legacy = -1;
   if (legacy < 0) {
     const char* e = getenv("RS_ATTN_LEGACY");
     legacy = (e && e[0] == '1') ? 1 : 0;
   }
-  return !legacy && dtype == RS_DTYPE_BF16 && attn_lds_supported(T, Dh);
+  // the LDS kernels form the dropout-mask element index in 32 bits
+  const bool idx32 = BH * T * (T + (T & 1)) < ((int64_t)1 << 32);
+  return !legacy && dtype == RS_DTYPE_BF16 && idx32 && attn_lds_supported(T, Dh);
 }
 
 static int check(int dtype, int64_t T, int64_t Dh, const int64_t* lds, int n) {
@@ -442,7 +445,7 @@ int rs_attn_fwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t Dh, const vo
   if (mask_kind == 1 && !ids) return RS_ERR_ARG;
   AttnArgs a = {};
   hipStream_t s = (hipStream_t)stream;
-  if (use_lds_path(dtype, T, Dh))
+  if (use_lds_path(dtype, B * H, T, Dh))
     return (int)attn_lds_fwd(B, T, H, Dh, q, ldq, k, ldk, v, ldv, o, ldo, lse, scale, mask_kind, ids, drop_p, seed,
                              seed_base, s);
   a.B = B; a.T = T; a.H = H; a.q = q; a.ldq = ldq; a.k = k; a.ldk = ldk; a.v = v; a.ldv = ldv;
@@ -460,7 +463,7 @@ int rs_attn_bwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t Dh, const vo
   int c = check(dtype, T, Dh, lds, 8);
   if (c) return c;
   if (mask_kind == 1 && !ids) return RS_ERR_ARG;
-  if (use_lds_path(dtype, T, Dh))
+  if (use_lds_path(dtype, B * H, T, Dh))
     return (int)attn_lds_bwd(B, T, H, Dh, q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, dq, lddq, dk, lddk, dv,
                              lddv, scale, mask_kind, ids, drop_p, seed, seed_base, ws, (hipStream_t)stream);
   AttnArgs a = {};

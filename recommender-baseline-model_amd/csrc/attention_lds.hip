@@ -308,7 +308,7 @@ __global__ __launch_bounds__(NT) void attn_fwd_lds_kernel(AttnLdsArgs a) {
     if (g == 0 && qrow < a.T) a.lse[bh * a.T + qrow] = (mx + __builtin_amdgcn_logf(sm)) * LN2;
     // P^T (+ dropout: one hash per pair of adjacent keys), packed pairwise as the B operand of O^T = V^T P^T
     const uint32_t s32 = seed32(seed);
-    const uint32_t rowidx = (uint32_t)(((int)bh * T + qi) * T);
+    const uint32_t rowidx = (uint32_t)(((int)bh * T + qi) * (T + (T & 1)));   // mask row pitch: even
     f32x4 o[DT];
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -436,7 +436,7 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnLdsArgs& a, int64_t l
     const float sl2 = a.scale * LOG2E;
     const int qi = q0 + cl;
     const uint32_t s32 = seed32(seed);
-    const uint32_t rowidx = (uint32_t)(((int)bh * T + qi) * T);
+    const uint32_t rowidx = (uint32_t)(((int)bh * T + qi) * (T + (T & 1)));   // mask row pitch: even
     const bool qok = qi < T;
     const int nkt = a.mask_kind == 0 ? qt + 1 : nq;
     f32x4 acc[DT];
@@ -660,7 +660,7 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnLdsArgs& a, int64_t 
           }
           const float x2 = st == 0 ? s[r] * sl2 : MASK2;
           const float p = st == 1 ? 0.f : ex2(x2 - lse_s[qr]);
-          const float m = a.drop_p > 0.f ? drop_mul(a.drop_p, seed, (uint64_t)(((int)bh * T + qr) * T + ki)) : 1.f;
+          const float m = a.drop_p > 0.f ? drop_mul(a.drop_p, seed, (uint64_t)(((int)bh * T + qr) * (T + (T & 1)) + ki)) : 1.f;
           pd2[hf][r] = p * m;
           ds2[hf][r] = st == 0 ? p * (dp[r] * m - dl_s[qr]) * a.scale : 0.f;
         }

@@ -51,6 +51,8 @@ class SAS(nn.Module):
         self.num_blocks = args.sas_num_blocks
         self.heads = args.sas_heads
         self.dropout_rate = args.sas_dropout
+        # the trainer's l2 regulariser weight (BS/trainers/sas.py:14,51-52), applied by FusedTrainStep
+        self.l2_emb = float(getattr(args, "l2_emb", 0.0) or 0.0)
         self.cdtype = compute_dtype(args)
         d = self.hidden
         if d % self.heads:

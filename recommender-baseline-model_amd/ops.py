@@ -286,6 +286,31 @@ def adam_prepare_step(p, g, m, v, p_bf16, state, hyper, zero_grad=False, grad_di
          int(zero_grad), ptr(grad_divisor), ptr(seed_base), ptr(td), nt, 0, ptr(wt), stream())
 
 
+L2_CHUNK = 16384
+
+
+def l2_chunk_desc(flat, device):
+    """rs_l2_penalty's chunk descriptor over a FlatParams buffer: one segment per parameter tensor (its exact
+    elements, alignment padding excluded), cut into chunks of at most L2_CHUNK elements.  int64 [n][4]."""
+    rows = []
+    for n in flat.names:
+        lo = flat.offsets[n]
+        cnt = 1
+        for s in flat.shapes[n]:
+            cnt *= s
+        first, nch = len(rows), max(1, -(-cnt // L2_CHUNK))
+        for k in range(nch):
+            rows.append([lo + k * L2_CHUNK, lo + min(cnt, (k + 1) * L2_CHUNK), first, nch])
+    return torch.tensor(rows, dtype=torch.int64, device=device)
+
+
+def l2_penalty(p, g, desc, l2, ws, loss=None, scale=None):
+    """loss += l2 * sum ||p_seg||, g += scale * l2 * p / ||p_seg|| (BS/trainers/sas.py:51-52; rs_l2_penalty)."""
+    assert ws.numel() >= desc.shape[0] and ws.dtype == torch.float32
+    call("rs_l2_penalty", ptr(p), ptr(g), ptr(desc), desc.shape[0], float(l2), ptr(scale), ptr(ws), ptr(loss),
+         stream())
+
+
 def cast_bf16(src, dst):
     call("rs_cast_bf16", src.numel(), ptr(src), ptr(dst), stream())
 

@@ -105,6 +105,12 @@ class FusedTrainStep:
             self.overlap = True
         self.max_labelled = max_labelled
         dev = self.flat.device
+        # SAS's parameter-norm regulariser (BS/trainers/sas.py:51-52: loss += l2_emb * ||p|| for every
+        # parameter); the BERT trainer has none (BS/trainers/bert.py:30-41)
+        self.l2 = float(getattr(model.sas, "l2_emb", 0.0)) if self.kind == "sas" else 0.0
+        if self.l2:
+            self.l2_desc = ops.l2_chunk_desc(self.flat, dev)
+            self.l2_ws = torch.zeros(self.l2_desc.shape[0], dtype=torch.float32, device=dev)
         self.loss_out = torch.zeros(4, dtype=torch.float32, device=dev)
         self.count = torch.zeros(1, dtype=torch.float32, device=dev)
         self.one = torch.ones(1, dtype=torch.float32, device=dev)
@@ -112,6 +118,7 @@ class FusedTrainStep:
         self.graphs = None
         self.static = None
         self.steps_per_graph = 1
+        self._stamps = None
         self.exchange = dpx.BucketedExchange(self.flat.grad, self._buckets(), self.pg, partial=self.vshard is not None) \
             if self.overlap else None
 
@@ -143,13 +150,24 @@ class FusedTrainStep:
 
     def _compute(self, *batch, split=None):
         """Forward + loss + backward into the flat gradient.  split(tag): called by the engine when the bucket
-        `tag` is final (DP only: the aux tail -- loss sum, count -- is written before it)."""
+        `tag` is final (DP only: the aux tail -- loss sum, count -- is written before it).
+
+        The aux tail is written exactly ONCE per step, before the all-reduce of the bucket holding it is issued:
+        by sp() when the engine finishes a bucket mid-backward (that bucket's all-reduce may still be running, or
+        be done, when the backward returns: writing the local values again then would overwrite the global
+        sums), else after the backward, before the all-reduce of the last bucket."""
         eng = self.engine
         sp = None
+        aux_written = [False]
+
+        def write_aux():
+            if self.dp and not aux_written[0]:
+                self.flat.aux[dpx.LOSS_SUM:dpx.COUNT + 1].copy_(self.loss_out[0:2])
+                aux_written[0] = True
         if split is not None:
             def sp(tag, action=None):
                 if action is None:
-                    self.flat.aux[dpx.LOSS_SUM:dpx.COUNT + 1].copy_(self.loss_out[0:2])
+                    write_aux()
                 split(tag, action)
         if self.kind == "sas":
             seq, pos, neg = batch
@@ -158,8 +176,7 @@ class FusedTrainStep:
                 # BCE forward/backward inside the fused head kernels (head.hip)
                 eng.backward(saved, None, None, self.flat.grad, loss_out=self.loss_out,
                              divisor=self.one if self.dp else None, split=sp)
-                if self.dp:
-                    self.flat.aux[dpx.LOSS_SUM:dpx.COUNT + 1].copy_(self.loss_out[0:2])
+                write_aux()
                 return
             ws = eng.ws.get("bce", (3 * 256,), torch.float32)
             ops.bce_fwd(pl, nl, pos, ws, self.loss_out)
@@ -171,8 +188,7 @@ class FusedTrainStep:
             tokens, labels = batch
             eng.train_loss_and_backward(tokens, labels, self.loss_out, self._divisor, self.flat.grad,
                                         max_labelled=self.max_labelled, split=sp)
-        if self.dp:
-            self.flat.aux[dpx.LOSS_SUM:dpx.COUNT + 1].copy_(self.loss_out[0:2])
+        write_aux()
 
     def _exchange(self):
         if self.dp:
@@ -188,6 +204,12 @@ class FusedTrainStep:
         # everything before out.weight, the owned rows, then out.bias (updated whole: 16-B aligned ranges) and on
         return [(0, ow), (lo, hi), (ow + V1 * d, f.numel)]
 
+    def _l2(self, loss, scale=None):
+        """The regulariser's loss term and gradient, added after the gradient exchange (every rank adds the same
+        term once; `scale` = the divisor the optimizer applies to the summed gradient)."""
+        if self.l2:
+            ops.l2_penalty(self.flat.data, self.flat.grad, self.l2_desc, self.l2, self.l2_ws, loss=loss, scale=scale)
+
     def _update(self):
         sb = self.engine.seed_base
         if self.vshard is not None:
@@ -199,8 +221,10 @@ class FusedTrainStep:
             if self.dp:
                 torch.div(self.flat.aux[dpx.LOSS_SUM:dpx.LOSS_SUM + 1], self.flat.aux[dpx.COUNT:dpx.COUNT + 1],
                           out=self.loss_val)
+                self._l2(self.loss_val, scale=self.flat.aux[dpx.COUNT:dpx.COUNT + 1])
                 self.opt.step(grad_divisor=self.flat.aux[dpx.COUNT:dpx.COUNT + 1], seed_base=sb, transposed=tr)
             else:
+                self._l2(self.loss_out[2:3])
                 self.opt.step(seed_base=sb, transposed=tr)
 
     # ---------------------------------------------------------------- one step
@@ -350,6 +374,10 @@ class FusedTrainStep:
             base = self.loss_out
             try:
                 for k in range(self.steps_per_graph):
+                    if k and self._stamps is not None:
+                        # restart the stamp marks: each unrolled step records under its own step slot with
+                        # marks numbered from 0, so every step's launches fit the per-step mark capacity
+                        ops.kernel_stamps(self._stamps[0], self.opt.state, self._stamps[1])
                     self.loss_out = self.loss_rows[k]
                     if sample is not None:
                         sample()
@@ -363,6 +391,7 @@ class FusedTrainStep:
         """The compute graph (+ the optimizer in the same graph on one device).  DP: the compute graph is cut at
         every bucket the backward finishes (overlap: segments replayed with that bucket's all-reduce launched
         between them) or ends after the backward, and the optimizer is a separate graph after the exchange."""
+        self._stamps = stamps
         if stamps is not None:
             ops.kernel_stamps(stamps[0], self.opt.state, stamps[1])
         try:
@@ -380,6 +409,7 @@ class FusedTrainStep:
         finally:
             if stamps is not None:
                 ops.kernel_stamps(None, None)
+            self._stamps = None
         self.g_update = None
         if self.dp:
             self.g_update = torch.cuda.CUDAGraph()

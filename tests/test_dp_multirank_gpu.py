@@ -1,0 +1,156 @@
+"""The data-parallel FusedTrainStep with TWO ranks (processes sharing one GPU; gloo moves the tensors, the product
+uses RCCL -- one GPU per test box).  Covers SAS (the headline model: bf16 fused path and fp32 parity path) and
+BERT, eager and HIP-graph-captured, with the gradient exchange overlapped with the backward (buckets launched as
+the backward finishes them) and as one all-reduce after it.  Each mode must
+
+  * keep the replicas bit-identical,
+  * all-reduce the aux tail exactly once: aux COUNT = the GLOBAL valid-position count (SAS: pos != 0, BS/trainers/
+    sas.py:41; BERT: labels != 0, BS/trainers/bert.py:40) -- a rank that re-wrote its local (loss sum, count) after
+    the overlapped bucket's all-reduce would divide the summed gradient by its local count,
+  * equal one process stepping the concatenated batch (the reference's single-device mean over the global batch).
+"""
+import argparse
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+V, T, BR, STEPS = 500, 50, 6, 3
+MODES = [(False, False), (False, True), (True, False), (True, True)]     # (graph, overlap)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _model(kind, dtype):
+    import rbm_amd  # noqa: F401
+    from rbm_amd.models import model_factory
+    torch.manual_seed(21)
+    if kind == "sas":
+        a = argparse.Namespace(model_code="sas", num_items=V, max_len=T, device="cuda", sas_hidden_units=64,
+                               sas_num_blocks=2, sas_heads=1, sas_dropout=0.0, l2_emb=0.01, rs_dtype=dtype)
+    else:
+        a = argparse.Namespace(model_code="bert", num_items=V, max_len=T, device="cuda", bert_hidden_units=64,
+                               bert_num_blocks=2, bert_num_heads=2, bert_dropout=0.0, bert_hidden_dropout=0.0,
+                               bert_mask_prob=0.2, model_init_seed=21, rs_dtype=dtype)
+    return model_factory(a)
+
+
+def _batches(kind, world):
+    import rbm_amd.data as synth
+    rng = np.random.default_rng(5)
+    mk = (lambda: synth.sas_batch(rng, BR, T, V)) if kind == "sas" else (lambda: synth.bert_batch(rng, BR, T, V, 0.3))
+    return [[mk() for _ in range(world)] for _ in range(STEPS)]
+
+
+def _valid(kind, b):
+    return int((b[1] != 0).sum())      # SAS: pos != 0; BERT: labels != 0
+
+
+def _reset(tr, sd):
+    """Back to the initial weights and a fresh optimizer (capture() ran warm-up steps)."""
+    tr.model.load_state_dict(sd)
+    tr.engine.sync_compute_weights()
+    tr.opt.m.zero_()
+    tr.opt.v.zero_()
+    tr.opt.state.zero_()
+
+
+def _worker(rank, world, port, kind, dtype, out_dir):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rbm_amd import dp as dpx
+        from rbm_amd.train_step import FusedTrainStep
+        batches = _batches(kind, world)
+        local = [tuple(torch.from_numpy(x).cuda() for x in b[rank]) for b in batches]
+        out = {}
+        for graph, overlap in MODES:
+            m = _model(kind, dtype)
+            sd0 = {k: v.detach().clone() for k, v in m.state_dict().items()}
+            tr = FusedTrainStep(m, lr=1e-3, dp=True, overlap=overlap, bucket_numel=None if overlap else 1 << 30,
+                                max_labelled=BR * T if kind == "bert" else None)
+            assert (tr.exchange is not None) == overlap
+            if graph:
+                tr.capture(*local[0])
+                _reset(tr, sd0)
+            losses, counts = [], []
+            for b in local:
+                losses.append(float((tr.replay(*b) if graph else tr.step(*b)).item()))
+                counts.append(float(tr.flat.aux[dpx.COUNT].item()))
+            torch.cuda.synchronize()
+            out[f"{int(graph)}{int(overlap)}"] = {
+                "losses": losses, "counts": counts,
+                "sd": {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}}
+        torch.save(out, os.path.join(out_dir, f"r{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def _skip_key(kind, k):
+    # attention key bias: analytically zero gradient -- Adam turns rounding noise into lr-sized steps
+    return (kind == "bert" and "linear_layers.1.bias" in k)
+
+
+def _np(kind, k, t):
+    t = t.float().numpy().astype(np.float64)
+    if kind == "sas" and k.endswith("in_proj_bias"):
+        d = t.shape[0] // 3
+        t = np.concatenate([t[:d], t[2 * d:]])
+    return t
+
+
+def _update_err(kind, k, a, ref, init):
+    """||a - ref|| relative to the reference's own update ||ref - init|| (Adam's early updates are ~lr per element
+    whatever the gradient's size, so a parameter-relative bound would say little about small tensors)."""
+    a, ref, init = _np(kind, k, a), _np(kind, k, ref), _np(kind, k, init)
+    return float(np.linalg.norm(a - ref) / max(np.linalg.norm(ref - init), 1e-30))
+
+
+@pytest.mark.parametrize("kind,dtype", [("sas", "bf16"), ("sas", "fp32"), ("bert", "bf16")])
+def test_two_rank_step_equals_single_process(tmp_path, kind, dtype):
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), kind, dtype, str(tmp_path)), nprocs=world, join=True)
+    from rbm_amd.train_step import FusedTrainStep
+    batches = _batches(kind, world)
+    m = _model(kind, dtype)
+    init = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    tr = FusedTrainStep(m, lr=1e-3, max_labelled=world * BR * T if kind == "bert" else None)
+    ref_losses = []
+    for b in batches:
+        cat = [torch.from_numpy(np.concatenate([x[i] for x in b])).cuda() for i in range(len(b[0]))]
+        ref_losses.append(float(tr.step(*cat).item()))
+    ref = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    counts = [float(sum(_valid(kind, x) for x in b)) for b in batches]
+    r0 = torch.load(tmp_path / "r0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "r1.pt", weights_only=True)
+    # fp32: the DP sum runs in another order than the single batch's (rounding-level differences); bf16: the
+    # per-rank partial sums round differently (LayerNorm bias gradients at 6 sequences per rank: ~0.1 of the update)
+    loss_tol, upd_tol = (1e-5, 1e-2) if dtype == "fp32" else (2e-3, 0.2)
+    for mode in r0:
+        a, b = r0[mode], r1[mode]
+        assert a["counts"] == counts and b["counts"] == counts, (mode, a["counts"], b["counts"], counts)
+        assert a["losses"] == b["losses"], mode
+        assert np.allclose(a["losses"], ref_losses, rtol=loss_tol), (mode, a["losses"], ref_losses)
+        for k in ref:
+            assert torch.equal(a["sd"][k], b["sd"][k]), (mode, k)         # replicas bit-identical
+            if _skip_key(kind, k):
+                continue
+            e = _update_err(kind, k, a["sd"][k], ref[k], init[k])
+            assert e < upd_tol, (mode, k, e)

@@ -1,0 +1,229 @@
+"""Dropout-ON parity of the training step (the benchmarked configuration runs SAS at p = 0.2, BERT at 0.1).
+
+The HIP kernels draw every dropout mask from a counter-based hash of (site salt, device step seed, element
+index) and regenerate it in the backward (common.h drop_mul).  The masks a training step used are materialised
+here through the C ABI -- rs_dropout_rowmask over a tensor of ones, with the site's salt, the step's seed and
+the site's element indexing (include/recsys_hip.h: token sites m*ld + c, attention ((b*H+h)*T+q)*Tp + k) -- and
+injected into the oracle, which then replays the reference's dropout sites exactly:
+
+  SAS  (BS/models/sas_model/sas.py)  emb :64, attn{i} (MHA attention-prob dropout) :75, ffn1_{i} / ffn2_{i} :17-19
+  BERT (BS/models/bert_modules/)     emb embedding/bert.py:31, attn{i} attention/single.py:33,
+                                     res1_{i} / res2_{i} utils/sublayer.py:18, ffn_{i} utils/feed_forward.py:16,
+                                     blk_{i} transformer.py:32
+
+fp32 mode is held to the fp32 bars (1e-5 forward / loss, 1e-4 gradients, norm-relative); the bf16 fused path
+(the one bench.py times) to its bf16 bars.  Statistical tests check every site's keep rate and that masks
+are uncorrelated across sites, steps (the optimizer advances the device seed) and data-parallel ranks (rank r
+starts its seed at r << 40, train_step.py).
+"""
+import argparse
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import rel
+
+pytestmark = pytest.mark.gpu
+
+FWD_TOL_F32, GRAD_TOL_F32 = 1e-5, 1e-4
+FWD_TOL_BF16, GRAD_TOL_BF16 = 3e-2, 0.15
+
+
+def _ones_mask(M, N, p, salt, sb):
+    """keep mask (bool, [M, N]) of a site with element index m*N + c."""
+    from rbm_amd import ops
+    ones = torch.ones(M, N, dtype=torch.float32, device="cuda")
+    out = torch.empty_like(ones)
+    ops.dropout_rowmask(ones, p, salt, sb, None, out)
+    return out > 0
+
+
+def token_mask(M, N, p, salt, sb):
+    return _ones_mask(M, N, p, salt, sb)
+
+
+def attn_mask(B, H, T, p, salt, sb):
+    Tp = T + (T & 1)
+    return _ones_mask(B * H * T, Tp, p, salt, sb)[:, :T].reshape(B, H, T, T)
+
+
+def sas_masks(eng, B, T, sb):
+    d, H, p = eng.d, eng.H, eng.p
+    M = B * T
+    out = {"emb": token_mask(M, d, p, eng.salt["emb"], sb).view(B, T, d)}
+    for i in range(eng.L):
+        out[f"attn{i}"] = attn_mask(B, H, T, p, eng.salt[f"attn{i}"], sb)
+        out[f"ffn1_{i}"] = token_mask(M, d, p, eng.salt[f"ffn1_{i}"], sb).view(B, T, d)
+        out[f"ffn2_{i}"] = token_mask(M, d, p, eng.salt[f"ffn2_{i}"], sb).view(B, T, d)
+    return out
+
+
+def bert_masks(eng, B, T, sb):
+    d, H, p, hp, Fd = eng.d, eng.H, eng.p, eng.hp, eng.F
+    M = B * T
+    out = {"emb": token_mask(M, d, hp, eng.salt["emb"], sb).view(B, T, d)}
+    for i in range(eng.L):
+        out[f"attn{i}"] = attn_mask(B, H, T, p, eng.salt[f"attn{i}"], sb)
+        out[f"res1_{i}"] = token_mask(M, d, hp, eng.salt[f"res1{i}"], sb).view(B, T, d)
+        out[f"ffn_{i}"] = token_mask(M, Fd, hp, eng.salt[f"ffn{i}"], sb).view(B, T, Fd)
+        out[f"res2_{i}"] = token_mask(M, d, hp, eng.salt[f"res2{i}"], sb).view(B, T, d)
+        out[f"blk_{i}"] = token_mask(M, d, hp, eng.salt[f"blk{i}"], sb).view(B, T, d)
+    return out
+
+
+def _sas_model(V, T, d, L, h, p, dtype, seed):
+    import rbm_amd  # noqa: F401
+    from rbm_amd.models import model_factory
+    torch.manual_seed(seed)
+    a = argparse.Namespace(model_code="sas", num_items=V, max_len=T, device="cuda", sas_hidden_units=d,
+                           sas_num_blocks=L, sas_heads=h, sas_dropout=p, l2_emb=0.0, rs_dtype=dtype)
+    return model_factory(a)
+
+
+def _bert_model(V, T, d, L, h, p, dtype, seed):
+    import rbm_amd  # noqa: F401
+    from rbm_amd.models import model_factory
+    a = argparse.Namespace(model_code="bert", num_items=V, max_len=T, device="cuda", bert_hidden_units=d,
+                           bert_num_blocks=L, bert_num_heads=h, bert_dropout=p, bert_hidden_dropout=p,
+                           bert_mask_prob=0.2, model_init_seed=seed, rs_dtype=dtype)
+    return model_factory(a)
+
+
+def _step_grads(tr, batch, seed):
+    """One training step's loss and gradient (before the optimizer) exactly as FusedTrainStep computes it."""
+    tr.engine.seed_base.fill_(seed)
+    tr.flat.grad.zero_()
+    tr._compute(*batch)
+    torch.cuda.synchronize()
+    return float(tr.loss_out[2].item()), tr.flat.grad[:tr.flat.numel].clone()
+
+
+def _check(grads, g64, flat, tol, d=None, kbias=None):
+    scale = max(float(np.linalg.norm(v.numpy())) for v in g64.values())
+    worst = {}
+    for k, ref in g64.items():
+        name = k[4:] if k.startswith("sas.") else k
+        g = flat.view(name, grads).cpu().numpy().astype(np.float64)
+        r = ref.numpy()
+        if kbias is not None and kbias(name):
+            # the attention key bias: analytically zero gradient (softmax shift invariance); on scale
+            assert np.linalg.norm(g[d:2 * d] if g.shape[0] == 3 * d else g) <= max(1e-5, tol) * scale, name
+            if g.shape[0] != 3 * d:
+                continue
+            g, r = np.concatenate([g[:d], g[2 * d:]]), np.concatenate([r[:d], r[2 * d:]])
+        worst[name] = rel(g, r)
+    bad = {k: v for k, v in worst.items() if v >= tol}
+    assert not bad, (bad, max(worst.values()))
+    return worst
+
+
+@pytest.mark.parametrize("dtype,V,T,d,L,h,B", [
+    ("fp32", 500, 50, 64, 2, 1, 4),      # sas_mid-like, fp32 parity kernels
+    ("fp32", 300, 37, 64, 2, 2, 3),      # odd T (mask row pitch), two heads
+    ("bf16", 500, 50, 64, 2, 1, 4),      # fused bf16 kernels (bench path)
+    ("bf16", 300, 37, 128, 2, 1, 3),     # fused, odd T
+    ("bf16", 3416, 200, 128, 2, 1, 8),   # cfg2 shape (B reduced for the fp64 oracle)
+])
+def test_sas_dropout_step_matches_oracle(dtype, V, T, d, L, h, B):
+    import rbm_amd.data as synth
+    from oracle import sas as osas
+    from rbm_amd.train_step import FusedTrainStep
+    p = 0.2
+    m = _sas_model(V, T, d, L, h, p, dtype, seed=V + T)
+    tr = FusedTrainStep(m, lr=1e-3)
+    rng = np.random.default_rng(T)
+    seq, pos, neg = (torch.from_numpy(a).cuda() for a in synth.sas_batch(rng, B, T, V))
+    seed = 977
+    loss, grads = _step_grads(tr, (seq, pos, neg), seed)
+    sb = torch.full((1,), seed, dtype=torch.int64, device="cuda")
+    masks = {k: v.cpu().double() for k, v in sas_masks(tr.engine, B, T, sb).items()}
+    for k, v in masks.items():          # the sites really drop ~p of their elements
+        assert abs(1 - v.mean().item() - p) < 0.05, k
+    P = {k: v.detach().cpu().double() for k, v in m.state_dict().items()}
+    l64, _, _, g64 = osas.loss_and_grads(P, seq.cpu(), pos.cpu(), neg.cpu(), L, h, p=p, masks=masks)
+    ftol, gtol = (FWD_TOL_F32, GRAD_TOL_F32) if dtype == "fp32" else (FWD_TOL_BF16, GRAD_TOL_BF16)
+    assert abs(loss - l64.item()) < ftol * max(1.0, abs(l64.item())), (loss, l64.item())
+    worst = _check(grads, g64, tr.flat, gtol, d=d, kbias=lambda n: n.endswith("in_proj_bias"))
+    print(dtype, (V, T, d), "loss", loss, float(l64), "worst grad rel", max(worst.items(), key=lambda kv: kv[1]))
+
+
+@pytest.mark.parametrize("dtype,V,T,d,L,h,B", [
+    ("fp32", 200, 30, 64, 2, 2, 3),
+    ("bf16", 200, 30, 64, 2, 2, 3),
+])
+def test_bert_dropout_step_matches_oracle(dtype, V, T, d, L, h, B):
+    import rbm_amd.data as synth
+    from oracle import bert as obert
+    from rbm_amd.train_step import FusedTrainStep
+    p = 0.1
+    m = _bert_model(V, T, d, L, h, p, dtype, seed=3)
+    tr = FusedTrainStep(m, lr=1e-3)
+    rng = np.random.default_rng(4)
+    tok, lab = (torch.from_numpy(a).cuda() for a in synth.bert_batch(rng, B, T, V, mask_prob=0.3))
+    seed = 4242
+    loss, grads = _step_grads(tr, (tok, lab), seed)
+    sb = torch.full((1,), seed, dtype=torch.int64, device="cuda")
+    masks = {k: v.cpu().double() for k, v in bert_masks(tr.engine, B, T, sb).items()}
+    P = {k: v.detach().cpu().double() for k, v in m.state_dict().items()}
+    l64, _, g64 = obert.loss_and_grads(P, tok.cpu(), lab.cpu(), L, h, p=p, hp=p, masks=masks)
+    ftol, gtol = (FWD_TOL_F32, GRAD_TOL_F32) if dtype == "fp32" else (FWD_TOL_BF16, GRAD_TOL_BF16)
+    assert abs(loss - l64.item()) < ftol * max(1.0, abs(l64.item())), (loss, l64.item())
+    worst = _check(grads, g64, tr.flat, gtol, d=d, kbias=lambda n: "linear_layers.1.bias" in n)
+    print(dtype, "BERT loss", loss, float(l64), "worst grad rel", max(worst.items(), key=lambda kv: kv[1]))
+
+
+def _corr(a, b):
+    a = a.double().flatten() - a.double().mean()
+    b = b.double().flatten() - b.double().mean()
+    return float((a * b).sum() / math.sqrt(float((a * a).sum() * (b * b).sum())))
+
+
+def test_dropout_masks_statistics():
+    """Keep rate 1-p within 4 sigma at every SAS site; masks uncorrelated (|r| < 4/sqrt(n)) across sites, across
+    consecutive steps (seed + 1, what the optimizer kernel advances) and across data-parallel ranks
+    (seed + (1 << 40))."""
+    m = _sas_model(3416, 200, 128, 2, 1, 0.2, "bf16", seed=1)
+    eng = m.sas.engine()
+    B, T, p = 16, 200, 0.2
+    sb0 = torch.full((1,), 5, dtype=torch.int64, device="cuda")
+    sb_next = torch.full((1,), 6, dtype=torch.int64, device="cuda")
+    sb_rank = torch.full((1,), 5 + (1 << 40), dtype=torch.int64, device="cuda")
+    a = sas_masks(eng, B, T, sb0)
+    nxt = sas_masks(eng, B, T, sb_next)
+    rk = sas_masks(eng, B, T, sb_rank)
+    for k, v in a.items():
+        n = v.numel()
+        keep = v.double().mean().item()
+        assert abs(keep - (1 - p)) < 4 * math.sqrt(p * (1 - p) / n), (k, keep)
+        lim = 4 / math.sqrt(n)
+        assert abs(_corr(v, nxt[k])) < lim, (k, "step", _corr(v, nxt[k]))
+        assert abs(_corr(v, rk[k])) < lim, (k, "rank", _corr(v, rk[k]))
+    tok = [k for k in a if not k.startswith("attn")]
+    for i, k1 in enumerate(tok):
+        for k2 in tok[i + 1:]:
+            r = _corr(a[k1], a[k2])
+            assert abs(r) < 4 / math.sqrt(a[k1].numel()), (k1, k2, r)
+    r = _corr(a["attn0"], a["attn1"])
+    assert abs(r) < 4 / math.sqrt(a["attn0"].numel()), r
+
+
+def test_dropout_seed_advances_per_step_and_differs_per_rank():
+    """FusedTrainStep: the optimizer kernel advances the device seed by one per step (so every step draws new
+    masks, also inside replayed graphs), and a data-parallel rank r starts at r << 40."""
+    import rbm_amd.data as synth
+    from rbm_amd.train_step import FusedTrainStep
+    m = _sas_model(500, 50, 64, 2, 1, 0.2, "bf16", seed=2)
+    tr = FusedTrainStep(m, lr=1e-3)
+    rng = np.random.default_rng(0)
+    b = tuple(torch.from_numpy(x).cuda() for x in synth.sas_batch(rng, 4, 50, 500))
+    s0 = int(tr.engine.seed_base.item())
+    tr.step(*b)
+    tr.step(*b)
+    assert int(tr.engine.seed_base.item()) == s0 + 2
+    tr.capture(*b, warmup=1)
+    s1 = int(tr.engine.seed_base.item())
+    tr.replay(*b)
+    tr.replay(*b)
+    assert int(tr.engine.seed_base.item()) == s1 + 2

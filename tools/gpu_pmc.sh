@@ -15,6 +15,6 @@ P4="WRITE_SIZE TCC_HIT_sum TCC_MISS_sum"
 i=0
 for P in "$P1" "$P2" "$P3" "$P4"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $P -d $OUT/pmc_$i -o pmc --output-format csv -- python3 tools/kbench.py --config $CFG --reps 5 --only "$ONLY" > $OUT/pmc_$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/pmc_$i.log; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $P -d $OUT/pmc_$i -o pmc --output-format csv -- python3 tools/kbench.py --config $CFG --reps 5 --only "$ONLY" > $OUT/pmc_$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/pmc_$i.log; exit 1; }
 done
 python3 tools/pmc_summary.py $OUT > $OUT/summary.txt 2>&1; cat $OUT/summary.txt
