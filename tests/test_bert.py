@@ -16,7 +16,7 @@ import torch
 from conftest import golden_params, load_golden, rel
 
 FWD_TOL_F32, GRAD_TOL_F32 = 1e-5, 1e-4
-FWD_TOL_BF16, GRAD_TOL_BF16 = 3e-2, 0.15
+FWD_TOL_BF16, GRAD_TOL_BF16 = 3e-2, 3e-2   # BERT bf16 gradients measure <= 1e-2 (no ReLU: GELU)
 SEEDS = {"bert_tiny": 3, "bert_mid": 4, "bert_curve": 7}   # tools/gen_golden.py
 
 
