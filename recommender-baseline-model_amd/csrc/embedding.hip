@@ -39,6 +39,24 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
   store_chunk<T>(out + r * d + c, o);
 }
 
+// any width / alignment (e.g. the reference's default SAS d = 50): one element per thread, same math
+template <typename T>
+__global__ __launch_bounds__(256) void embed_fwd_any_kernel(const int64_t* __restrict__ ids, int64_t rows,
+                                                            int64_t T_, const T* __restrict__ table,
+                                                            const T* __restrict__ pos, int64_t d, float scale,
+                                                            int mode, float drop_p, uint64_t salt,
+                                                            const uint64_t* seed_base, T* __restrict__ out) {
+  const uint64_t seed = eff_seed(salt, seed_base);
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= rows * d) return;
+  const int64_t r = i / d, c = i % d, t = r % T_;
+  const int64_t id = ids[r];
+  const float e = to_f(table[id * d + c]), p = to_f(pos[t * d + c]);
+  float x = mode == 0 ? e * scale + p : e + p;
+  if (drop_p > 0.f) x *= drop_mul(drop_p, seed, (uint64_t)i);
+  out[i] = from_f<T>((mode == 0 && id == 0) ? 0.f : x);
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void embed_bwd_table_kernel(const int64_t* __restrict__ ids, int64_t rows,
                                                               const T* __restrict__ dx, int64_t d, float scale,
@@ -198,6 +216,12 @@ template <typename T>
 static hipError_t embed_fwd_t(int mode, const int64_t* ids, int64_t rows, int64_t T_, const void* table,
                               const void* pos, int64_t d, float scale, float drop_p, uint64_t seed,
                               const uint64_t* seed_base, void* out, hipStream_t s) {
+  const bool vec = d % Vec<T>::N == 0 && ((uintptr_t)table | (uintptr_t)pos | (uintptr_t)out) % 16 == 0;
+  if (!vec) {
+    hipLaunchKernelGGL((embed_fwd_any_kernel<T>), dim3((unsigned)cdiv(rows * d, 256)), dim3(256), 0, s, ids, rows, T_,
+                       (const T*)table, (const T*)pos, d, scale, mode, drop_p, seed, seed_base, (T*)out);
+    return hipGetLastError();
+  }
   const int64_t n = rows * (d / Vec<T>::N);
   hipLaunchKernelGGL((embed_fwd_kernel<T>), dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, ids, rows, T_,
                      (const T*)table, (const T*)pos, d, scale, mode, drop_p, seed, seed_base, (T*)out);
@@ -236,8 +260,7 @@ extern "C" {
 int rs_embed_fwd(int dtype, int mode, const int64_t* ids, int64_t rows, int64_t T, const void* table,
                  const void* pos, int64_t d, float scale, float drop_p, uint64_t seed, const uint64_t* seed_base,
                  void* out, void* stream) {
-  const int vec = dtype == RS_DTYPE_BF16 ? 8 : 4;
-  if (rows <= 0 || T <= 0 || rows % T || d % vec) return RS_ERR_ARG;
+  if (rows <= 0 || T <= 0 || rows % T || d <= 0) return RS_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   return (int)(dtype == RS_DTYPE_BF16
                    ? embed_fwd_t<__bf16>(mode, ids, rows, T, table, pos, d, scale, drop_p, seed, seed_base, out, s)

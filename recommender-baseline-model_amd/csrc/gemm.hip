@@ -19,7 +19,7 @@
 // b and b+8 share an XCD, so consecutive tile ids go to the same XCD's L2.
 #include "gemm_common.h"
 
-template <typename T, bool KMAJ, int ROWS>
+template <typename T, bool KMAJ, int ROWS, bool ALIGNED = true>
 struct TileLoader {
   // Tile of logical (ROWS x 32) over (row, k).  Global chunks are 16 B along
   // the contiguous axis.  For KMAJ=false: R=ROWS rows of 32 k; for KMAJ=true:
@@ -44,7 +44,7 @@ struct TileLoader {
       if (ch < NCH) {
         int r = ch / CPR, c = (ch % CPR) * V;
         int64_t gr = r0 + r, gc = c0 + c;
-        if (gr < rlim && gc + V <= clim) {
+        if (ALIGNED && gr < rlim && gc + V <= clim) {
           load_chunk<T>(buf[i], base + gr * ld + gc);
         } else {
 #pragma unroll
@@ -98,10 +98,12 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& a, int64_t m, int
   }
 }
 
-template <typename T, bool AK, bool BK, int BM, int BN>
+// ALIGNED = false: operands whose leading dimensions / base addresses are not 16-byte multiples (e.g. the
+// reference's default SAS width d = 50) are read element by element; everything else is the same kernel.
+template <typename T, bool AK, bool BK, int BM, int BN, bool ALIGNED = true>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
-  using LA = TileLoader<T, AK, BM>;
-  using LB = TileLoader<T, BK, BN>;
+  using LA = TileLoader<T, AK, BM, ALIGNED>;
+  using LB = TileLoader<T, BK, BN, ALIGNED>;
   __shared__ __attribute__((aligned(16))) T lds[LA::LDS_ELEMS + LB::LDS_ELEMS];
   T* As = lds;
   T* Bs = lds + LA::LDS_ELEMS;
@@ -217,6 +219,21 @@ static hipError_t launch_t(GemmArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <typename T, bool AK, bool BK>
+static hipError_t launch_unaligned_t(GemmArgs& a, hipStream_t s) {
+  dim3 grid((unsigned)(cdiv(a.M, 64) * cdiv(a.N, 64)), 1, a.split_k);
+  hipLaunchKernelGGL((gemm_kernel<T, AK, BK, 64, 64, false>), grid, dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+template <typename T>
+static hipError_t launch_unaligned(int ak, int bk, GemmArgs& a, hipStream_t s) {
+  if (!ak && !bk) return launch_unaligned_t<T, false, false>(a, s);
+  if (!ak && bk) return launch_unaligned_t<T, false, true>(a, s);
+  if (ak && bk) return launch_unaligned_t<T, true, true>(a, s);
+  return launch_unaligned_t<T, true, false>(a, s);
+}
+
 template <typename T>
 static hipError_t launch_dt(int ak, int bk, GemmArgs& a, hipStream_t s) {
   if (!ak && !bk) return launch_t<T, false, false>(a, s);
@@ -233,7 +250,8 @@ int rs_gemm(int dtype, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t
   if (M <= 0 || N <= 0 || K < 0 || split_k < 1) return RS_ERR_ARG;
   const int esz = dtype == RS_DTYPE_BF16 ? 2 : 4;
   const int vec = 16 / esz;
-  if ((lda % vec) || (ldb % vec) || ((uintptr_t)A % 16) || ((uintptr_t)B % 16)) return RS_ERR_ARG;
+  const bool aligned = !((lda % vec) || (ldb % vec) || ((uintptr_t)A % 16) || ((uintptr_t)B % 16));
+  if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) % esz) return RS_ERR_ARG;
   if (split_k > 1 && !slab) return RS_ERR_ARG;
   GemmArgs a{};
   a.M = M; a.N = N; a.K = K; a.A = A; a.lda = lda; a.B = B; a.ldb = ldb; a.C = C; a.ldc = ldc;
@@ -245,6 +263,9 @@ int rs_gemm(int dtype, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t
   if (epi) a.epi = *epi;
   else { a.epi = rs_epilogue{}; a.epi.alpha = 1.0f; }
   hipStream_t s = (hipStream_t)stream;
+  if (!aligned)
+    return (int)(dtype == RS_DTYPE_BF16 ? launch_unaligned<__bf16>(a_kmajor, b_kmajor, a, s)
+                                        : launch_unaligned<float>(a_kmajor, b_kmajor, a, s));
   hipError_t err = dtype == RS_DTYPE_BF16 ? gemm_bf16_launch(a_kmajor, b_kmajor, a, s)
                                           : launch_dt<float>(a_kmajor, b_kmajor, a, s);
   return (int)err;
@@ -258,11 +279,11 @@ int rs_linear_wgrad(int dtype, int64_t M, int64_t N, int64_t K, const void* dY, 
   if (M <= 0 || N <= 0 || K <= 0 || splits < 1 || !slab || !dW) return RS_ERR_ARG;
   const int esz = dtype == RS_DTYPE_BF16 ? 2 : 4;
   const int vec = 16 / esz;
-  if ((lddy % vec) || (ldx % vec) || ((uintptr_t)dY % 16) || ((uintptr_t)X % 16) || ((uintptr_t)slab % 16))
-    return RS_ERR_ARG;
+  const bool aligned = !((lddy % vec) || (ldx % vec) || ((uintptr_t)dY % 16) || ((uintptr_t)X % 16));
+  if (((uintptr_t)slab % 16) || ((uintptr_t)dY | (uintptr_t)X) % esz) return RS_ERR_ARG;
   GemmArgs a{};
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == RS_DTYPE_BF16 && splits == 1 && K % 8 == 0 && ((uintptr_t)dW % 16) == 0) {
+  if (aligned && dtype == RS_DTYPE_BF16 && splits == 1 && K % 8 == 0 && ((uintptr_t)dW % 16) == 0) {
     // one split: the tiles accumulate straight into dW (and the ones-operand column sums into db)
     a.M = N; a.N = K; a.K = M; a.A = dY; a.lda = lddy; a.B = X; a.ldb = ldx; a.C = dW; a.ldc = K;
     a.c_f32 = 1; a.split_k = 1; a.k_per_split = M;
@@ -283,7 +304,9 @@ int rs_linear_wgrad(int dtype, int64_t M, int64_t N, int64_t K, const void* dY, 
   a.epi = rs_epilogue{};
   a.epi.alpha = 1.0f;
   a.epi.rows_dev = rows_dev;
-  hipError_t err = dtype == RS_DTYPE_BF16 ? gemm_bf16_launch(1, 1, a, s) : launch_t<float, true, true>(a, s);
+  hipError_t err = !aligned ? (dtype == RS_DTYPE_BF16 ? launch_unaligned_t<__bf16, true, true>(a, s)
+                                                     : launch_unaligned_t<float, true, true>(a, s))
+                  : dtype == RS_DTYPE_BF16 ? gemm_bf16_launch(1, 1, a, s) : launch_t<float, true, true>(a, s);
   if (err != hipSuccess) return (int)err;
   // one pass over the slabs: columns [0, N*K) -> dW, [N*K, N*K+N) -> db
   return (int)launch_reduce_slabs(slab, splits, a.slab_stride, N * K, dW, db, accumulate, s);

@@ -46,9 +46,13 @@ EMU_TOL = 2e-2
 BF16_ABS_TOL = 3e-2
 
 
-def check_bf16_grads(get, g_emu, g_exact, d, kbias=lambda n: False, strip=""):
+def check_bf16_grads(get, g_emu, g_exact, d, kbias=lambda n: False, strip="", emu_tol=EMU_TOL):
     """get(name) -> the HIP gradient (numpy); g_emu / g_exact: oracle gradient dicts keyed like the state dict.
-    Returns {name: (err vs emulation, err vs exact, bound vs exact)}."""
+    Returns {name: (err vs emulation, err vs exact, bound vs exact)}.  emu_tol: EMU_TOL for the fused kernels
+    (whose storage points the emulation models).  The unfused generic bf16 kernels round at other points (e.g.
+    the online-softmax attention packs the unnormalised P, the dropout/residual gradient splits are stored), and
+    one extra rounding anywhere in the forward moves the ill-conditioned FFN weight gradients by ~5 % (tools/diag/
+    bf16_budget.py), so there the emulation is only a coarse check (0.1) and the bound vs the exact math decides."""
     out, bad = {}, {}
     scale = max(float(np.linalg.norm(v.numpy())) for v in g_exact.values())
     for k in g_exact:
@@ -64,7 +68,7 @@ def check_bf16_grads(get, g_emu, g_exact, d, kbias=lambda n: False, strip=""):
         r_emu, r_ex, fmt = rel(g, e), rel(g, x), rel(e, x)
         bound = max(BF16_ABS_TOL, 2 * fmt)
         out[name] = (r_emu, r_ex, bound)
-        if r_emu >= EMU_TOL or r_ex >= bound:
+        if r_emu >= emu_tol or r_ex >= bound:
             bad[name] = out[name]
     assert not bad, bad
     return out

@@ -205,3 +205,54 @@ def test_bert_fused_vocab_ce_matches_materialised(monkeypatch, head, d, B, cap):
         if "linear_layers.1.bias" in k:
             continue
         assert rel(g1[k], g0[k]) < 2e-3, (k, rel(g1[k], g0[k]))
+
+
+@pytest.mark.gpu
+def test_bert_cfg5_vocabulary_step_matches_oracle():
+    """BASELINE configs[4] vocabulary: 1,000,000 items (out.weight 1,000,001 x 256, the token table 1,000,002 x 256),
+    d = 256, 2 heads, one block, a few labelled rows.  The fused bf16 training step (vocabulary-tile-stationary
+    head, rs_vocab_head_fwd/bwd + the dE / dh GEMMs; token-table gradient by inverted index) against the fp64
+    oracle CE over the full vocabulary (BS/models/bert.py:16, BS/trainers/bert.py:36-40): loss, out.weight /
+    out.bias gradients (dense over all 1M rows), the token table and the block weights."""
+    import rbm_amd  # noqa: F401
+    import rbm_amd.data as synth
+    from oracle import bert as obert
+    from rbm_amd.models import model_factory
+    from rbm_amd.train_step import FusedTrainStep
+    V, T, B = 1_000_000, 20, 2
+    a = argparse.Namespace(model_code="bert", num_items=V, max_len=T, device="cuda", bert_hidden_units=256,
+                           bert_num_blocks=1, bert_num_heads=2, bert_dropout=0.0, bert_hidden_dropout=0.0,
+                           bert_mask_prob=0.2, model_init_seed=5, rs_dtype="bf16")
+    m = model_factory(a)
+    tr = FusedTrainStep(m, lr=1e-3, max_labelled=128)
+    rng = np.random.default_rng(6)
+    tok, lab = (torch.from_numpy(t).cuda() for t in synth.bert_batch(rng, B, T, V, mask_prob=0.3))
+    n_lab = int((lab != 0).sum())
+    assert 0 < n_lab <= 128
+    tr.flat.grad.zero_()
+    tr._compute(tok, lab)
+    torch.cuda.synchronize()
+    loss = float(tr.loss_out[2].item())
+    assert float(tr.loss_out[1].item()) == n_lab
+    P = {k: v.detach().cpu().double() for k, v in m.state_dict().items()}
+    torch.set_num_threads(16)
+    l64, _, g64 = obert.loss_and_grads(P, tok.cpu(), lab.cpu(), 1, 2)
+    assert abs(loss - l64.item()) < FWD_TOL_BF16 * abs(l64.item()), (loss, l64.item())
+    scale = max(float(g.norm()) for g in g64.values())
+    worst = {}
+    for k, r in g64.items():
+        g = tr.flat.view(k, tr.flat.grad).cpu().double()
+        if "linear_layers.1.bias" in k:
+            assert float(g.norm()) <= 1e-2 * scale, k
+            continue
+        worst[k] = rel(g.numpy(), r.numpy())
+    print("cfg5 vocabulary: loss", loss, float(l64), "worst", max(worst.items(), key=lambda kv: kv[1]))
+    bad = {k: v for k, v in worst.items() if v >= GRAD_TOL_BF16}
+    assert not bad, bad
+    # rows of out.weight no labelled row's softmax touches still get the dense softmax gradient; the token table
+    # gets gradient only on the batch's tokens
+    tok_rows = torch.unique(tok.cpu())
+    gt = tr.flat.view("bert.embedding.token.weight", tr.flat.grad).cpu()
+    untouched = torch.ones(gt.shape[0], dtype=torch.bool)
+    untouched[tok_rows] = False
+    assert gt[untouched].abs().max().item() == 0.0

@@ -103,9 +103,12 @@ def test_sas_predict_matches_reference():
 
 
 @pytest.mark.parametrize("V,T,d,L,h,B", [(3416, 200, 128, 2, 1, 3), (500, 50, 64, 2, 2, 5),
-                                         (300, 37, 128, 1, 4, 2), (1000, 200, 256, 2, 2, 2)])
+                                         (300, 37, 128, 1, 4, 2), (1000, 200, 256, 2, 2, 2),
+                                         # BASELINE configs[0] = the reference's default config (BS/config.json:
+                                         # d = 50, 1 head, T = 200), its 2-head variant (Dh = 25), --max_len 300
+                                         (3416, 200, 50, 2, 1, 4), (400, 60, 50, 2, 2, 3), (500, 300, 64, 2, 1, 2)])
 def test_sas_fp32_matches_oracle_shapes(V, T, d, L, h, B):
-    """Random weights / batches at several shapes (odd T, Dh 32/64/128) vs the fp64 oracle."""
+    """Random weights / batches at several shapes (odd T, Dh 25/32/50/64/128, T up to 300) vs the fp64 oracle."""
     import rbm_amd  # noqa: F401
     import rbm_amd.data as synth
     from rbm_amd.models import model_factory
