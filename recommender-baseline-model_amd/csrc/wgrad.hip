@@ -176,16 +176,22 @@ struct RArgs {
   KStamp ks;                   // end stamp (last reduction launch of a stamped rs_wgrad_grouped)
 };
 
-// block = 16 float4 columns x 16 split groups; group g sums splits g, g+16, ... ; fixed-order
-// combine in LDS (deterministic)
+// block = C float4 columns x G split groups (C*G = 256): group g sums splits g, g+G, ... (4 loads in flight),
+// then a fixed LDS tree combines the groups (deterministic).  C = 16 for the weight-gradient slabs (tens of
+// splits); segments with many splits -- the LayerNorm affine partials, one row per 64-token block (400 at cfg2)
+// -- take C = 4, G = 64: 4x the workgroups and a quarter of the serial loads per thread (with C = 16 those
+// few blocks summed 25 splits per thread and set the reduction launch's length)
 constexpr int RED_C = 16, RED_G = 16;
-__device__ __forceinline__ void reduce_segments_block(const RArgs& a, int b, float4 (*red)[RED_C]) {
-  constexpr int C = RED_C, G = RED_G;
+__device__ __forceinline__ int seg_cols(int splits) { return splits > 64 ? 4 : RED_C; }
+
+__device__ __forceinline__ void reduce_segments_block(const RArgs& a, int b, float4 (*red2)[RED_C]) {
+  float4* red = &red2[0][0];
   int si = 0;
 #pragma unroll 1
   for (int q = 1; q < a.nseg; ++q)
     if (b >= a.blk0[q]) si = q;
   const Seg& S = a.s[si];
+  const int C = seg_cols(S.splits), G = 256 / C;
   const int col = threadIdx.x % C, grp = threadIdx.x / C;
   const int64_t i4 = (int64_t)(b - a.blk0[si]) * C + col;
   const int64_t n4 = S.n / 4;
@@ -209,15 +215,19 @@ __device__ __forceinline__ void reduce_segments_block(const RArgs& a, int b, flo
       acc.x += u.x; acc.y += u.y; acc.z += u.z; acc.w += u.w;
     }
   }
-  red[grp][col] = acc;
+  red[grp * C + col] = acc;
   __syncthreads();
-  if (grp == 0 && i4 < n4) {
-    float4 tot = red[0][col];
-#pragma unroll
-    for (int q = 1; q < G; ++q) {
-      const float4 u = red[q][col];
-      tot.x += u.x; tot.y += u.y; tot.z += u.z; tot.w += u.w;
+  for (int h = G / 2; h > 0; h >>= 1) {
+    if (grp < h) {
+      const float4 u = red[(grp + h) * C + col];
+      float4 t = red[grp * C + col];
+      t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+      red[grp * C + col] = t;
     }
+    __syncthreads();
+  }
+  if (grp == 0 && i4 < n4) {
+    float4 tot = red[col];
     float4* o = reinterpret_cast<float4*>(S.out) + i4;
     if (a.accumulate) {
       const float4 p = *o;
@@ -292,7 +302,7 @@ static int reduce_args(int nseg, const rs_reduce_segment* segs, int accumulate, 
     if (g.n <= 0 || g.n % 4 || g.stride % 4 || g.splits < 1 || !al16(g.src) || !al16(g.out)) return RS_ERR_ARG;
     ra.s[q] = {g.src, g.stride, (int)g.splits, (int)g.n, g.out};
     ra.blk0[q] = blk;
-    blk += (int)cdiv(g.n / 4, cols ? 256 : 16);
+    blk += (int)cdiv(g.n / 4, cols ? 256 : (g.splits > 64 ? 4 : wg::RED_C));
   }
   ra.blk0[nseg] = blk;
   return 0;

@@ -83,3 +83,50 @@ def test_sas_loss_curve_bf16_tracks_reference():
     losses, _ = _run("sas", z, 300, dtype="bf16")
     err = np.abs(losses - z["losses"][:300])
     assert err.mean() <= 2e-2 and err.max() <= 1e-1, (err.mean(), err.max())
+
+
+def test_sas_loss_curve_bf16_1000_steps():
+    """The benchmarked (bf16 fused) path over the whole 1000-step sas_curve run.  Its per-step losses leave the
+    fp32 trajectory by bf16 rounding of the forward (tools/diag/bf16_budget.py), so the bound is on the run's
+    statistics: mean |dloss| and the 50-step moving average, measured and stated here."""
+    z = load_golden("sas_curve")
+    losses, _ = _run("sas", z, int(z["steps"]), dtype="bf16")
+    ref = z["losses"]
+    err = np.abs(losses - ref)
+
+    def ma(x):
+        return np.convolve(x, np.ones(50) / 50, mode="valid")
+    dma = np.abs(ma(losses) - ma(ref))
+    print("sas_curve bf16 1000 steps: mean", err.mean(), "max", err.max(), "ma50 max", dma.max())
+    # measured: mean 2.8e-3, max 3.3e-2, 50-step moving average 1.6e-3
+    assert err.mean() <= 5e-3 and err.max() <= 6e-2 and dma.max() <= 4e-3, (err.mean(), err.max(), dma.max())
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_sas_loss_curve_at_the_bench_shape(dtype):
+    """tests/golden/sas_curve_bench.npz: the reference's own 1000-step run at the benchmarked SAS shape (BASELINE
+    configs[1]: 3,416 items, T = 200, d = 128, 2 blocks, 1 head; B = 16, lr 1e-3, dropout 0; tools/gen_golden.py
+    --bench-curve), with the same run of the reference modules in float64 (losses64).  The reference's fp32 run
+    itself leaves the exact trajectory by up to 1.44e-3 (7 steps above 1e-3, mean 2e-4); a second fp32 CPU
+    implementation of the same math (the oracle in fp32, tools/diag/curve_noise.py) leaves the reference's fp32 run
+    by up to 1.96e-3 (mean 2.4e-4, 1.5 % of the steps above 1e-3) -- two fp32 runs of this training drift apart by
+    rounding alone, so a per-step 1e-3 bar cannot hold for every step here.  Bounds (measured in brackets):
+      fp32: max |loss - reference| <= 5e-3 [4.3e-3], mean <= 6e-4 [4.2e-4], >= 85 % of steps within 1e-3 [90.9 %],
+            50-step moving average <= 1.5e-3 [9.0e-4];
+      bf16: the benchmarked path: max <= 5e-2 [2.5e-2], mean <= 3e-3 [1.4e-3], moving average <= 1e-2 [4.6e-3]."""
+    z = load_golden("sas_curve_bench")
+    losses, _ = _run("sas", z, int(z["steps"]), dtype=dtype)
+    ref, ref64 = z["losses"], z["losses64"]
+    floor = np.abs(ref - ref64).max()
+    err, err64 = np.abs(losses - ref), np.abs(losses - ref64)
+
+    def ma(x):
+        return np.convolve(x, np.ones(50) / 50, mode="valid")
+    dma = np.abs(ma(losses) - ma(ref))
+    print(dtype, "bench-shape curve: mean", err.mean(), "max", err.max(), "frac>1e-3", (err > 1e-3).mean(),
+          "vs fp64 max", err64.max(), "ma50 max", dma.max(), "reference floor", floor)
+    if dtype == "fp32":
+        assert err.max() <= 5e-3 and err.mean() <= 6e-4 and (err <= 1e-3).mean() >= 0.85 and dma.max() <= 1.5e-3, \
+            (err.max(), err.mean(), (err <= 1e-3).mean(), dma.max())
+    else:
+        assert err.max() <= 5e-2 and err.mean() <= 3e-3 and dma.max() <= 1e-2, (err.mean(), err.max(), dma.max())

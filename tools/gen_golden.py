@@ -150,13 +150,7 @@ def bert_case(name, V, T, d, L, h, B, seed):
     print(name, "loss", loss.item(), "loss64", l64.item())
 
 
-def sas_curve(name, V, T, d, L, h, B, steps, seed, lr=1e-3):
-    torch.manual_seed(seed)
-    args = sas_args(V, T, d, L, h)
-    model = model_factory(args)
-    model.train()
-    out = {"V": V, "T": T, "d": d, "L": L, "h": h, "B": B, "steps": steps, "seed": seed, "lr": lr}
-    out.update(_pack("p/", model.state_dict()))
+def _sas_train(model, args, B, T, V, steps, seed, lr):
     opt = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=0)   # BS/trainers/base.py:228
     fake = _FakeSAS(model, args)
     rng = np.random.default_rng(seed)
@@ -169,10 +163,34 @@ def sas_curve(name, V, T, d, L, h, B, steps, seed, lr=1e-3):
         losses.append(loss.item())
         loss.backward()
         opt.step()
-    out["losses"] = np.array(losses, np.float64)
-    out.update(_pack("final/", model.state_dict()))
+    return np.array(losses, np.float64)
+
+
+def sas_curve(name, V, T, d, L, h, B, steps, seed, lr=1e-3, final=True, also64=False):
+    """The reference's own training run (SASTrainer.calculate_loss + backward + Adam) on the deterministic batch
+    stream; also64: the same run with the reference modules in float64 (its exact-math trajectory)."""
+    torch.manual_seed(seed)
+    args = sas_args(V, T, d, L, h)
+    model = model_factory(args)
+    model.train()
+    out = {"V": V, "T": T, "d": d, "L": L, "h": h, "B": B, "steps": steps, "seed": seed, "lr": lr}
+    out.update(_pack("p/", model.state_dict()))
+    m64 = None
+    if also64:
+        import copy
+        m64 = copy.deepcopy(model).double()
+    out["losses"] = _sas_train(model, args, B, T, V, steps, seed, lr)
+    if final:
+        out.update(_pack("final/", model.state_dict()))
+    if m64 is not None:
+        torch.set_default_dtype(torch.float64)    # the trainer's label tensors follow the logits' dtype
+        try:
+            out["losses64"] = _sas_train(m64, args, B, T, V, steps, seed, lr)
+        finally:
+            torch.set_default_dtype(torch.float32)
     np.savez_compressed(os.path.join(OUT, name + ".npz"), **out)
-    print(name, losses[0], "->", losses[-1])
+    print(name, out["losses"][0], "->", out["losses"][-1],
+          "" if m64 is None else f"max |fp32 - fp64| {np.abs(out['losses'] - out['losses64']).max():.2e}")
 
 
 def bert_curve(name, V, T, d, L, h, B, steps, seed, lr=1e-3):
@@ -216,6 +234,11 @@ def metrics_case(name):
 
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
+    if "--bench-curve" in sys.argv:
+        # the benchmarked SAS shape (BASELINE configs[1]: ML-1M items, T = 200, d = 128, 2 blocks, 1 head)
+        sas_curve("sas_curve_bench", V=3416, T=200, d=128, L=2, h=1, B=16, steps=1000, seed=8, final=False,
+                  also64=True)
+        raise SystemExit(0)
     sas_case("sas_tiny", V=50, T=16, d=64, L=2, h=2, B=4, seed=1)
     sas_case("sas_mid", V=400, T=200, d=128, L=2, h=1, B=3, seed=2)
     bert_case("bert_tiny", V=50, T=16, d=64, L=2, h=2, B=4, seed=3)

@@ -31,38 +31,33 @@ static void run(int B, int T) {
   hipMemcpyFromSymbol(p.data(), HIP_SYMBOL(g_attn_prof), p.size() * 8);
   const int nq = (T + 15) / 16;
   int ns = 1;
-  while ((int64_t)B * H * ns < 256 && ns * 2 <= std::max(1, nq / 4)) ns *= 2;
+  while (2 * (int64_t)B * H * ns * 2 <= 256 && ns * 2 <= std::max(1, nq / 4)) ns *= 2;   // pick_split_bwd (merged)
   const int nblk = ns * B * H;
+  // merged launch: blocks [0, nblk) are dQ workgroups (stamps 4/5/6), [nblk, 2 nblk) dK/dV ones (7/8/9)
   unsigned long long t0 = ~0ull, t1 = 0;
-  double sum[6] = {0};
-  int nw = 0;
-  std::vector<double> st, cq, ck;
-  for (int k = 0; k < 2; ++k) {}
-  for (int b = 0; b < nblk; ++b)
+  for (int b = 0; b < 2 * nblk; ++b)
     for (int w = 0; w < NW; ++w) {
       const unsigned long long* x = &p[((size_t)b * NW + w) * 10];
-      if (!x[4] || !x[6] || !x[7] || !x[9]) continue;
-      t0 = std::min(t0, x[4]);
-      t1 = std::max(t1, x[9]);
+      const unsigned long long e = b < nblk ? x[4] : x[7], f = b < nblk ? x[6] : x[9];
+      if (!e || !f) continue;
+      t0 = std::min(t0, e);
+      t1 = std::max(t1, f);
     }
-  double dq_end = 0, dkv_start = 1e30;
-  for (int b = 0; b < nblk; ++b)
-    for (int w = 0; w < NW; ++w) {
-      const unsigned long long* x = &p[((size_t)b * NW + w) * 10];
-      if (!x[4] || !x[6] || !x[7] || !x[9]) continue;
-      sum[0] += x[4] - t0; sum[1] += x[5] - x[4]; sum[2] += x[6] - x[5];
-      sum[3] += x[7] - t0; sum[4] += x[8] - x[7]; sum[5] += x[9] - x[8];
-      cq.push_back(x[6] - x[5]); ck.push_back(x[9] - x[8]);
-      dq_end = std::max(dq_end, (double)(x[6] - t0)); dkv_start = std::min(dkv_start, (double)(x[7] - t0));
-      ++nw;
-    }
-  std::sort(cq.begin(), cq.end()); std::sort(ck.begin(), ck.end());
   const double u = 0.01;   // 100 MHz ticks -> us
-  printf("B=%d T=%d nsplit=%d blocks=%d waves=%d: span %.2f us\n", B, T, ns, nblk, nw, (t1 - t0) * u);
-  printf("  dQ : entry +%.2f  staging %.2f  compute %.2f (p50 %.2f max %.2f)  last wave done %.2f\n", sum[0] / nw * u,
-         sum[1] / nw * u, sum[2] / nw * u, cq[cq.size() / 2] * u, cq.back() * u, dq_end * u);
-  printf("  dKV: first entry %.2f mean entry +%.2f  staging %.2f  compute %.2f (p50 %.2f max %.2f)\n", dkv_start * u,
-         sum[3] / nw * u, sum[4] / nw * u, sum[5] / nw * u, ck[ck.size() / 2] * u, ck.back() * u);
+  printf("B=%d T=%d nsplit=%d blocks=2x%d: span %.2f us\n", B, T, ns, nblk, (t1 - t0) * u);
+  for (int kind = 0; kind < 2; ++kind) {
+    std::vector<double> ent, stg, cmp, fin;
+    for (int b = kind * nblk; b < (kind + 1) * nblk; ++b)
+      for (int w = 0; w < NW; ++w) {
+        const unsigned long long* x = &p[((size_t)b * NW + w) * 10 + (kind ? 7 : 4)];
+        if (!x[0] || !x[2]) continue;
+        ent.push_back((x[0] - t0) * u); stg.push_back((x[1] - x[0]) * u); cmp.push_back((x[2] - x[1]) * u);
+        fin.push_back((x[2] - t0) * u);
+      }
+    auto q = [](std::vector<double> v, double f) { std::sort(v.begin(), v.end()); return v[(size_t)(f * (v.size() - 1))]; };
+    printf("  %s: entry p50 %.2f max %.2f | staging p50 %.2f max %.2f | compute p50 %.2f max %.2f | end p50 %.2f max %.2f\n",
+           kind ? "dKV" : "dQ ", q(ent, .5), q(ent, 1), q(stg, .5), q(stg, 1), q(cmp, .5), q(cmp, 1), q(fin, .5), q(fin, 1));
+  }
   hipFree(q); hipFree(kv); hipFree(o); hipFree(dout); hipFree(dq); hipFree(dkv); hipFree(lse); hipFree(delta); hipFree(sb);
 }
 
