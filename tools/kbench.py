@@ -42,7 +42,7 @@ def main():
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--reps", type=int, default=50)
-    ap.add_argument("--only", default="", help="time only the ops whose name contains this")
+    ap.add_argument("--only", default="", help="time only the ops whose name contains one of these |-separated strings")
     a = ap.parse_args()
     c = SHAPES[a.config]
     B, T, d, V, H, ff = c["B"], c["T"], c["d"], c["V"], c["H"], c["ff"]
@@ -66,7 +66,7 @@ def main():
     rows = []
 
     def run(name, fn, nbytes, flops=0.0):
-        if a.only and a.only not in name:
+        if a.only and not any(o in name for o in a.only.split("|")):
             return
         us = timeit(fn, a.reps)
         rows.append((name, us, nbytes / (us * 1e-6) / 1e9, flops / (us * 1e-6) / 1e12))
