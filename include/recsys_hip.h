@@ -312,8 +312,10 @@ int rs_wall_clock_khz(int* khz);
 int rs_seed_advance(uint64_t* seed_base, void* stream);
 
 /* ---- fused SAS sublayers (bf16, d in {64, 128}; rowfused.hip) ----------------------------
- * One workgroup per 64 token rows, activations kept in LDS.  Same outputs, saved tensors and
- * dropout masks as the unfused kernel sequence, so rs_* backward kernels consume them unchanged.
+ * rowchain.hip: one workgroup per CU stages the block's weights in LDS once, each wave carries 16
+ * tokens through the whole chain in registers (RS_ROWCHAIN=0: rowfused.hip's 64-row LDS tiles).
+ * Same outputs, saved tensors and dropout masks as the unfused kernel sequence, so rs_* backward
+ * kernels consume them unchanged.
  *
  * Replaces, for SASRec block i (BS/models/sas_model/sas.py:73-76, the attention input side):
  *   Q = LN1(x) [mean/rstd saved];  q = Q Wq^T + bq;  kv = x Wkv^T + bkv   (kv: [M][2d])
@@ -332,11 +334,14 @@ int rs_sas_block_out(int64_t M, int64_t d, const void* o, const void* Q, const v
                      const int64_t* ids, float drop_p, uint64_t salt1, uint64_t salt2, const uint64_t* seed_base,
                      void* stream);
 
-/* Backward of rs_sas_block_out (sas.py:75-84 reversed), one 64-row block per workgroup:
+/* Number of LayerNorm affine partial sets the two backward kernels below write for M token rows
+ * (one per workgroup). */
+int64_t rs_sas_block_parts(int64_t M);
+/* Backward of rs_sas_block_out (sas.py:75-84 reversed):
  *   dzres = dxn*(ids!=0); dy2 = drop2(dzres) [out]; da1 = relu'(h1)*drop1(dy2 W2) [out];
  *   dz = da1 W1 + dzres; dx1 = LN2'(x1, dz) [out]; dout = dx1 Wo [out];
- *   part[b][0][:] / part[b][1][:] = LN2 dgamma / dbeta partials of 64-row block b (part >= 2*d*ceil(M/64)
- *   floats; sum them with rs_reduce_segments / rs_wgrad_grouped: stride 2d, splits ceil(M/64)).
+ *   part[b][0][:] / part[b][1][:] = LN2 dgamma / dbeta partial set b (part >= 2*d*rs_sas_block_parts(M)
+ *   floats; sum them with rs_reduce_segments / rs_wgrad_grouped: stride 2d, splits rs_sas_block_parts(M)).
  *   W*T are bf16 TRANSPOSED weights ([in][out], rs_transpose_bf16).
  * Replaces rs_dropout_rowmask + 3 rs_gemm dgrads + rs_layernorm_bwd of the unfused sequence. */
 int rs_sas_block_out_bwd(int64_t M, int64_t d, const void* dxn, const int64_t* ids, const void* h1, const void* x1,

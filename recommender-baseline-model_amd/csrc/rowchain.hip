@@ -1,0 +1,781 @@
+// Wave-resident row chains for the SASRec sublayers (bf16, gfx950): the kernels behind
+// rs_sas_block_in / rs_sas_block_out / rs_sas_block_out_bwd / rs_sas_block_in_bwd.
+//
+// Same math, saved tensors and dropout indices as rowfused.hip (the reference lines are
+// listed there: sas.py:73-76 and sas.py:75-84 with PointWiseFeedForward sas.py:8-24), laid
+// out for the CDNA4 execution model instead of a 64-row workgroup tile:
+//
+//  * one workgroup per CU (NW = 8 waves) stages the block's three d x d weight matrices ONCE
+//    into LDS (110 KB at d = 128), then every wave runs its own 16-token chain with no
+//    workgroup barrier: 16-row tiles are dealt round robin over all workgroups
+//    (tile = b + G*(w + NW*k)), so at cfg2 (1,600 tiles) every CU gets 6-7 of them instead of
+//    one or two 64-row tiles (400 tiles on 256 CUs);
+//  * the activations never leave registers: every GEMM is computed TRANSPOSED,
+//    Y^T = W . X^T, with the weight as the MFMA A operand (LDS) and the 16 tokens as the B
+//    operand, so the accumulator (lane (g, cl) holds feature 16j + 4g + r of token cl) packed
+//    pairwise to bf16 IS the next GEMM's B operand: the k order inside a 32-deep step is then
+//    {4g + e, 16 + 4g + e}, and the weights are staged into LDS with that permutation
+//    (conflict-free ds_read_b128 at a 32-byte row pad);
+//  * a token's features sit on one lane group (4 lanes x D/4 values), so LayerNorm's row
+//    statistics are 2 cross-group shuffles;
+//  * global loads/stores of activations use the same layout (8 bytes per lane per 16
+//    features), LayerNorm affine partials accumulate per lane over the wave's tiles and are
+//    reduced once per workgroup (partial set = workgroup: rs_sas_block_parts sets).
+#include "common.h"
+#include "../../include/recsys_hip.h"
+
+namespace rc {
+
+// phase timestamps for tools/micro/rowchain_phase.hip (compiled out of the library)
+#ifdef RC_PROF
+__device__ unsigned long long g_rc_prof[4096 * 8 * 8];
+#define RCPROF(slot)                                                                                 \
+  do {                                                                                               \
+    if ((threadIdx.x & 63) == 0) g_rc_prof[(blockIdx.x * 8 + (threadIdx.x >> 6)) * 8 + (slot)] = wall_clock64(); \
+  } while (0)
+#else
+#define RCPROF(slot) \
+  do {               \
+  } while (0)
+#endif
+
+typedef __bf16 bf16;
+typedef __attribute__((address_space(3))) void* lds_ptr;
+
+constexpr int NW = 8;                 // waves per workgroup
+constexpr int NT = 64 * NW;
+constexpr int TR = 16;                // tokens per wave tile
+
+template <int D> struct Lay {
+  static constexpr int J = D / 16;    // accumulator tiles per token row
+  static constexpr int S = D / 32;    // 32-deep k steps = 16-byte chunks per lane per row
+  static constexpr int CPR = D / 8;   // 16-byte chunks per weight row
+  static constexpr int WBYTES = D * D * 2;
+};
+
+// Feature convention: lane (g, cl) holds token cl; accumulator tile j = 2s + h, element r holds feature
+// 32s + 8g + 4h + r, i.e. step s's 8 features 32s + 8g .. +7 are contiguous (one 16-byte global access, one
+// natural-order B fragment).  The MFMA writes tile j, lane g, element r to output row 16j + 4g + r, so the
+// weight rows are staged in the order perm(n) = 32(n >> 5) + 8((n >> 2) & 3) + 4((n >> 4) & 1) + (n & 3).
+__device__ __forceinline__ int perm_row(int n) { return 32 * (n >> 5) + 8 * ((n >> 2) & 3) + 4 * ((n >> 4) & 1) + (n & 3); }
+// LDS weight image: unpadded rows, 16-byte chunk c of row n stored at chunk c ^ swz(n) (conflict-free
+// ds_read_b128 of the A fragments: rows 16j + cl, chunk 4s + g)
+template <int D> __device__ __forceinline__ int swz(int n) { return (n / (128 / D)) & (Lay<D>::CPR - 1); }
+
+// stage NM weight matrices ([D rows][D] at row stride ldw each) into LDS by LDS-DMA (global_load_lds_dwordx4:
+// lane-linear 1 KB per wave instruction, so the swizzle and row permutation go on the source address)
+template <int D, int NM>
+__device__ __forceinline__ void stage_w(char* lds, const bf16* const (&W)[NM], const int64_t (&ldw)[NM], int wave,
+                                        int lane) {
+  constexpr int IPM = Lay<D>::WBYTES / 1024, CPR = Lay<D>::CPR;
+  static_assert(NM * IPM % NW == 0, "staging split");
+#pragma unroll
+  for (int u = 0; u < NM * IPM / NW; ++u) {
+    const int q = wave + NW * u, mtx = q / IPM, qi = q % IPM;
+    const int idx = qi * 64 + lane, n = idx / CPR, pc = idx % CPR, lc = pc ^ swz<D>(n);
+    const bf16* src = W[mtx] + (int64_t)perm_row(n) * ldw[mtx] + 8 * lc;
+    __builtin_amdgcn_global_load_lds(src, (lds_ptr)(lds + mtx * Lay<D>::WBYTES + qi * 1024), 16, 0, 0);
+  }
+}
+// NV fp32 vectors of D (bias, LN affine) -> LDS, plain loads
+template <int D, int NV>
+__device__ __forceinline__ void stage_v(float* lv, const float* const (&V)[NV], int tid) {
+  for (int i = tid; i < NV * D; i += NT) lv[i] = V[i / D][i % D];
+}
+
+// activations of 16 tokens: Act in fp32 (tile j = 2s + h, element r), Raw as stored (bf16, step s, element
+// 4h + r) -- both hold features 32s + 8g + 4h + r of token cl
+template <int D> struct Act { f32x4 v[Lay<D>::J]; };
+template <int D> struct Raw { bf16x8 v[Lay<D>::S]; };
+
+template <int D>
+__device__ __forceinline__ void load_raw(Raw<D>& a, const bf16* base, int64_t ld, int64_t m, int g) {
+  const bf16* p = base + m * ld + 8 * g;
+#pragma unroll
+  for (int s = 0; s < Lay<D>::S; ++s) a.v[s] = *reinterpret_cast<const bf16x8*>(p + 32 * s);
+}
+template <int D>
+__device__ __forceinline__ void to_act(Act<D>& a, const Raw<D>& r) {
+#pragma unroll
+  for (int j = 0; j < Lay<D>::J; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) a.v[j][e] = (float)r.v[j >> 1][4 * (j & 1) + e];
+}
+// round to bf16 (the stored value) and keep both forms
+template <int D>
+__device__ __forceinline__ void round_act(Act<D>& a, Raw<D>& r) {
+#pragma unroll
+  for (int j = 0; j < Lay<D>::J; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      r.v[j >> 1][4 * (j & 1) + e] = (bf16)a.v[j][e];
+      a.v[j][e] = (float)r.v[j >> 1][4 * (j & 1) + e];
+    }
+}
+template <int D>
+__device__ __forceinline__ void store_raw(bf16* base, int64_t ld, int64_t m, bool ok, const Raw<D>& r, int g) {
+  if (!ok) return;
+  bf16* p = base + m * ld + 8 * g;
+#pragma unroll
+  for (int s = 0; s < Lay<D>::S; ++s) *reinterpret_cast<bf16x8*>(p + 32 * s) = r.v[s];
+}
+// acc[j] += W[feature of (j, g, r)][:] . x[token cl][:]  (W staged at wl)
+// Two-stage pipeline over the output tiles: tile j+1's fragments are read while tile j's MFMAs run, and the
+// scheduler may not batch more (all fragments of a chain in flight spill at d = 128).
+template <int D>
+__device__ __forceinline__ void mm(const bf16* wl, const Raw<D>& b, Act<D>& acc, int lane) {
+  constexpr int J = Lay<D>::J, S = Lay<D>::S;
+  const int g = lane >> 4, cl = lane & 15;
+  auto frag = [&](int j, int s) {
+    const int n = 16 * j + cl;
+    return *reinterpret_cast<const bf16x8*>(wl + n * D + 8 * ((4 * s + g) ^ swz<D>(n)));
+  };
+  bf16x8 f[2][S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) f[0][s] = frag(0, s);
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    if (j + 1 < J) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) f[(j + 1) & 1][s] = frag(j + 1, s);
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+      acc.v[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[j & 1][s], b.v[s], acc.v[j], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+template <int D>
+__device__ __forceinline__ void zero(Act<D>& a) {
+#pragma unroll
+  for (int j = 0; j < Lay<D>::J; ++j) a.v[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+}
+// this lane's 4 values of tile j of a staged fp32 vector
+template <int D>
+__device__ __forceinline__ f32x4 vec4(const float* lv, int j, int g) {
+  return *reinterpret_cast<const f32x4*>(lv + 32 * (j >> 1) + 8 * g + 4 * (j & 1));
+}
+__device__ __forceinline__ int feat(int j, int g, int r) { return 32 * (j >> 1) + 8 * g + 4 * (j & 1) + r; }
+// sum over the token's features: this lane's values, then the other 3 lane groups
+__device__ __forceinline__ float row_sum(float s) {
+  s += __shfl_xor(s, 16, 64);
+  s += __shfl_xor(s, 32, 64);
+  return s;
+}
+
+// torch.nn.LayerNorm (biased variance, eps inside the sqrt), in place; returns (mean, rstd)
+template <int D>
+__device__ __forceinline__ void ln_fwd(Act<D>& x, const float* gw, const float* gb, float eps, int g, float& mu,
+                                       float& rs) {
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < Lay<D>::J; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s += x.v[j][e];
+  mu = row_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < Lay<D>::J; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float u = x.v[j][e] - mu;
+      q += u * u;
+    }
+  rs = 1.0f / sqrtf(row_sum(q) / (float)D + eps);
+#pragma unroll
+  for (int j = 0; j < Lay<D>::J; ++j) {
+    const f32x4 w = vec4<D>(gw, j, g), b = vec4<D>(gb, j, g);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) x.v[j][e] = (x.v[j][e] - mu) * rs * w[e] + b[e];
+  }
+}
+
+// LayerNorm backward (layernorm.hip ln_bwd, VAR 0): t = rstd*(dy*g - mean(dy*g)) - rstd^3*mean(dy*g*u)*u,
+// u = x - mean; dy zeroed on invalid tokens; pg/pb receive this lane's dgamma/dbeta terms
+template <int D>
+__device__ __forceinline__ void ln_bwd(Act<D>& t, const Act<D>& x, const Act<D>& dy, bool valid, const float* gw,
+                                       float mu, float a, int g, Act<D>& pg, Act<D>& pb) {
+  float sg = 0.f, sgu = 0.f;
+#pragma unroll
+  for (int j = 0; j < Lay<D>::J; ++j) {
+    const f32x4 w = vec4<D>(gw, j, g);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float gy = valid ? dy.v[j][e] : 0.f;
+      const float u = x.v[j][e] - mu;
+      const float gq = gy * w[e];
+      pg.v[j][e] = gy * (u * a);
+      pb.v[j][e] = gy;
+      sg += gq;
+      sgu += gq * u;
+      t.v[j][e] = gq;   // dy*g for now
+    }
+  }
+  sg = row_sum(sg);
+  sgu = row_sum(sgu);
+  const float mg = sg / (float)D, coef = a * a * a * sgu / (float)D;
+#pragma unroll
+  for (int j = 0; j < Lay<D>::J; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) t.v[j][e] = a * (t.v[j][e] - mg) - coef * (x.v[j][e] - mu);
+}
+
+// add this tile's dgamma/dbeta terms, summed over its 16 tokens (xor tree over the lanes of a group),
+// to the wave's own LDS row red[wave][2][D] (no other wave touches it before ln_partials' barrier)
+template <int D>
+__device__ __forceinline__ void ln_accum(float* red, const Act<D>& pg, const Act<D>& pb, int lane, int wave) {
+  const int g = lane >> 4, cl = lane & 15;
+  float* rw = red + wave * 2 * D;
+#pragma unroll
+  for (int j = 0; j < Lay<D>::J; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float a = pg.v[j][e], b = pb.v[j][e];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        a += __shfl_xor(a, o, 64);
+        b += __shfl_xor(b, o, 64);
+      }
+      if (cl == 0) {
+        rw[feat(j, g, e)] += a;
+        rw[D + feat(j, g, e)] += b;
+      }
+    }
+}
+__device__ __forceinline__ void ln_zero(float* red, int D, int lane, int wave) {
+  for (int i = lane; i < 2 * D; i += 64) red[wave * 2 * D + i] = 0.f;
+}
+// the workgroup's partial set (waves summed in order 0..NW-1) -> part[blockIdx.x][2][D]
+template <int D>
+__device__ __forceinline__ void ln_partials(const float* red, float* part, int tid) {
+  __syncthreads();
+  if (tid < 2 * D) {
+    const int which = tid / D, c = tid % D;
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) s += red[(w * 2 + which) * D + c];
+    part[((int64_t)blockIdx.x * 2 + which) * D + c] = s;
+  }
+}
+
+__device__ __forceinline__ int64_t n_tiles(int64_t M) { return (M + TR - 1) / TR; }
+
+// ------------------------------------------------------------------ block input side
+struct InArgs {
+  int64_t M;
+  const bf16* x; int64_t ldx;
+  const float* ln_w; const float* ln_b; float eps;
+  bf16* Q; float* mean; float* rstd;
+  const bf16* Wq; const float* bq; bf16* q;
+  const bf16* Wkv; const float* bkv; bf16* kv;
+};
+
+// LDS: NM weight images, then NV fp32 vectors of D, then (backward) the LN partial rows red[NW][2][D]
+template <int D, int NM, int NV> struct Smem {
+  static constexpr size_t W = (size_t)NM * Lay<D>::WBYTES;
+  static constexpr size_t V = W + (size_t)NV * D * 4;
+  static constexpr size_t BYTES = V + (size_t)NW * 2 * D * 4;
+};
+
+// X -> Q = LN1(X) [saved], q = Q Wq^T + bq, kv = X Wkv^T + bkv
+template <int D>
+__global__ __launch_bounds__(NT) void block_in_kernel(InArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  typedef Smem<D, 3, 5> L;
+  const bf16* wl = reinterpret_cast<const bf16*>(smem);
+  const float* lv = reinterpret_cast<const float*>(smem + L::W);
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
+            cl = lane & 15;
+  const int64_t G = gridDim.x, nt = n_tiles(a.M);
+  int64_t t = blockIdx.x + G * wave;
+  Raw<D> xr;
+  if (t < nt) {
+    const int64_t m = t * TR + cl;
+    load_raw<D>(xr, a.x, a.ldx, m < a.M ? m : a.M - 1, g);
+  }
+  {
+    const bf16* const W[3] = {a.Wq, a.Wkv, a.Wkv + (int64_t)D * D};
+    const int64_t ldw[3] = {D, D, D};
+    stage_w<D, 3>(smem, W, ldw, wave, lane);
+    const float* const V[5] = {a.ln_w, a.ln_b, a.bq, a.bkv, a.bkv + D};
+    stage_v<D, 5>(reinterpret_cast<float*>(smem + L::W), V, tid);
+  }
+  __syncthreads();
+  for (; t < nt; t += G * NW) {
+    asm volatile("" ::: "memory");   // no hoisting of the loop-invariant weight fragment reads
+    const int64_t m = t * TR + cl;
+    const bool ok = m < a.M;
+    if (t != blockIdx.x + G * wave) load_raw<D>(xr, a.x, a.ldx, ok ? m : a.M - 1, g);
+    Act<D> y;
+    to_act<D>(y, xr);
+    float mu, rs;
+    ln_fwd<D>(y, lv, lv + D, a.eps, g, mu, rs);
+    Raw<D> Qr;
+    round_act<D>(y, Qr);
+    store_raw<D>(a.Q, D, m, ok, Qr, g);
+    if (ok && g == 0) {
+      a.mean[m] = mu;
+      a.rstd[m] = rs;
+    }
+    Act<D> acc;
+    Raw<D> outr;
+#pragma unroll
+    for (int h = 0; h < 3; ++h) {        // q = Q Wq^T + bq; k, v = X Wk^T + bk, X Wv^T + bv
+      zero<D>(acc);
+      mm<D>(wl + h * (Lay<D>::WBYTES / 2), h == 0 ? Qr : xr, acc, lane);
+#pragma unroll
+      for (int j = 0; j < Lay<D>::J; ++j) acc.v[j] += vec4<D>(lv + (2 + h) * D, j, g);
+      round_act<D>(acc, outr);
+      if (h == 0) store_raw<D>(a.q, D, m, ok, outr, g);
+      else store_raw<D>(a.kv + (h - 1) * D, 2 * D, m, ok, outr, g);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ block output side
+struct OutArgs {
+  int64_t M;
+  const bf16* o; const bf16* Q;
+  const bf16* Wo; const float* bo; bf16* x1;
+  const float* ln_w; const float* ln_b; float eps; bf16* z; float* mean; float* rstd;
+  const bf16* W1; const float* b1; bf16* h1;
+  const bf16* W2; const float* b2; bf16* xn;
+  const int64_t* ids;
+  float drop_p; uint64_t salt1, salt2; const uint64_t* seed_base;
+};
+
+// dropout multipliers of this lane's 4 features of tile j (pairs share one hash, as drop_mul2)
+__device__ __forceinline__ void drop4(float p, uint32_t s32, int64_t m, int D, int j, int g, float (&dm)[4]) {
+  const uint64_t idx = (uint64_t)(m * D + feat(j, g, 0));
+  drop_mul2(p, s32, idx, dm[0], dm[1]);
+  drop_mul2(p, s32, idx + 2, dm[2], dm[3]);
+}
+
+// O -> x1 = Q + O Wo^T + bo [saved], z = LN2(x1) [saved], h1 = relu(drop(z W1^T + b1)) [saved],
+// x' = (drop(h1 W2^T + b2) + z) * (ids != 0)
+template <int D>
+__global__ __launch_bounds__(NT) void block_out_kernel(OutArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  typedef Smem<D, 3, 5> L;
+  const bf16* wl = reinterpret_cast<const bf16*>(smem);
+  const float* lv = reinterpret_cast<const float*>(smem + L::W);   // bo, ln_w, ln_b, b1, b2
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
+            cl = lane & 15;
+  RCPROF(0);
+  const int64_t G = gridDim.x, nt = n_tiles(a.M);
+  const bool drop = a.drop_p > 0.f;
+  const uint32_t s1 = drop ? seed32(eff_seed(a.salt1, a.seed_base)) : 0u;
+  const uint32_t s2 = drop ? seed32(eff_seed(a.salt2, a.seed_base)) : 0u;
+  int64_t t = blockIdx.x + G * wave;
+  Raw<D> orr, Qr;
+  if (t < nt) {
+    const int64_t m = t * TR + cl, mc = m < a.M ? m : a.M - 1;
+    load_raw<D>(orr, a.o, D, mc, g);
+    load_raw<D>(Qr, a.Q, D, mc, g);
+  }
+  {
+    const bf16* const W[3] = {a.Wo, a.W1, a.W2};
+    const int64_t ldw[3] = {D, D, D};
+    stage_w<D, 3>(smem, W, ldw, wave, lane);
+    const float* const V[5] = {a.bo, a.ln_w, a.ln_b, a.b1, a.b2};
+    stage_v<D, 5>(reinterpret_cast<float*>(smem + L::W), V, tid);
+  }
+  __syncthreads();
+  RCPROF(1);
+  for (; t < nt; t += G * NW) {
+    asm volatile("" ::: "memory");
+    const int64_t m = t * TR + cl, mc = m < a.M ? m : a.M - 1;
+    const bool ok = m < a.M;
+    if (t != blockIdx.x + G * wave) {
+      load_raw<D>(orr, a.o, D, mc, g);
+      load_raw<D>(Qr, a.Q, D, mc, g);
+    }
+    const bool keep = ok && a.ids[mc] != 0;
+    Act<D> acc;
+    Raw<D> r;
+    // x1 = Q + o Wo^T + bo
+    zero<D>(acc);
+    mm<D>(wl, orr, acc, lane);
+    RCPROF(2);
+#pragma unroll
+    for (int j = 0; j < Lay<D>::J; ++j) {
+      const f32x4 bb = vec4<D>(lv, j, g);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc.v[j][e] = acc.v[j][e] + bb[e] + (float)Qr.v[j >> 1][4 * (j & 1) + e];
+    }
+    round_act<D>(acc, r);
+    store_raw<D>(a.x1, D, m, ok, r, g);
+    RCPROF(3);
+    // z = LN2(x1)
+    float mu, rs;
+    ln_fwd<D>(acc, lv + D, lv + 2 * D, a.eps, g, mu, rs);
+    Raw<D> zr;
+    round_act<D>(acc, zr);
+    store_raw<D>(a.z, D, m, ok, zr, g);
+    if (ok && g == 0) {
+      a.mean[m] = mu;
+      a.rstd[m] = rs;
+    }
+    // h1 = relu(drop(z W1^T + b1))
+    zero<D>(acc);
+    mm<D>(wl + Lay<D>::WBYTES / 2, zr, acc, lane);
+#pragma unroll
+    for (int j = 0; j < Lay<D>::J; ++j) {
+      float dm[4] = {1.f, 1.f, 1.f, 1.f};
+      if (drop) drop4(a.drop_p, s1, m, D, j, g, dm);
+      const f32x4 bb = vec4<D>(lv + 3 * D, j, g);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc.v[j][e] = fmaxf(acc.v[j][e] + bb[e], 0.f) * dm[e];
+    }
+    round_act<D>(acc, r);
+    store_raw<D>(a.h1, D, m, ok, r, g);
+    // x' = (drop(h1 W2^T + b2) + z) * (ids != 0)
+    zero<D>(acc);
+    mm<D>(wl + Lay<D>::WBYTES, r, acc, lane);
+#pragma unroll
+    for (int j = 0; j < Lay<D>::J; ++j) {
+      float dm[4] = {1.f, 1.f, 1.f, 1.f};
+      if (drop) drop4(a.drop_p, s2, m, D, j, g, dm);
+      const f32x4 bb = vec4<D>(lv + 4 * D, j, g);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float v = __builtin_fmaf(acc.v[j][e] + bb[e], dm[e], (float)zr.v[j >> 1][4 * (j & 1) + e]);
+        acc.v[j][e] = keep ? v : 0.f;
+      }
+    }
+    round_act<D>(acc, r);
+    RCPROF(4);
+    store_raw<D>(a.xn, D, m, ok, r, g);
+  }
+  RCPROF(5);
+}
+
+// ------------------------------------------------------------------ block output side, backward
+struct OutBwdArgs {
+  int64_t M;
+  const bf16* dxn; const int64_t* ids;
+  const bf16* h1; const bf16* x1; const float* mean2; const float* rstd2; const float* ln_w;
+  const bf16* W2T; const bf16* W1T; const bf16* WoT;      // transposed [in][out] copies
+  bf16* dy2; bf16* da1; bf16* dx1; bf16* dout; float* part;
+  float drop_p; uint64_t salt1, salt2; const uint64_t* seed_base;
+};
+
+// dzres = dxn*mask; dy2 = drop2(dzres) [saved]; da1 = relu'(h1)*drop1(dy2 W2) [saved]; dz = da1 W1 + dzres;
+// dx1 = LN2'(x1, dz) [saved, + affine partials]; dout = dx1 Wo
+template <int D>
+__global__ __launch_bounds__(NT) void block_out_bwd_kernel(OutBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  typedef Smem<D, 3, 1> L;
+  const bf16* wl = reinterpret_cast<const bf16*>(smem);
+  const float* lv = reinterpret_cast<const float*>(smem + L::W);   // ln_w
+  float* red = reinterpret_cast<float*>(smem + L::V);
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
+            cl = lane & 15;
+  const int64_t G = gridDim.x, nt = n_tiles(a.M);
+  const bool drop = a.drop_p > 0.f;
+  const uint32_t s1 = drop ? seed32(eff_seed(a.salt1, a.seed_base)) : 0u;
+  const uint32_t s2 = drop ? seed32(eff_seed(a.salt2, a.seed_base)) : 0u;
+  int64_t t = blockIdx.x + G * wave;
+  Raw<D> dr, hr;
+  if (t < nt) {
+    const int64_t m = t * TR + cl, mc = m < a.M ? m : a.M - 1;
+    load_raw<D>(dr, a.dxn, D, mc, g);
+    load_raw<D>(hr, a.h1, D, mc, g);
+  }
+  {
+    const bf16* const W[3] = {a.W2T, a.W1T, a.WoT};
+    const int64_t ldw[3] = {D, D, D};
+    stage_w<D, 3>(smem, W, ldw, wave, lane);
+    const float* const V[1] = {a.ln_w};
+    stage_v<D, 1>(reinterpret_cast<float*>(smem + L::W), V, tid);
+  }
+  ln_zero(red, D, lane, wave);
+  __syncthreads();
+  for (; t < nt; t += G * NW) {
+    asm volatile("" ::: "memory");
+    const int64_t m = t * TR + cl, mc = m < a.M ? m : a.M - 1;
+    const bool ok = m < a.M;
+    if (t != blockIdx.x + G * wave) {
+      load_raw<D>(dr, a.dxn, D, mc, g);
+      load_raw<D>(hr, a.h1, D, mc, g);
+    }
+    Raw<D> xr;
+    load_raw<D>(xr, a.x1, D, mc, g);
+    const float mu = a.mean2[mc], rs = a.rstd2[mc];
+    const bool keep = ok && a.ids[mc] != 0;
+    Act<D> dz, acc;
+    Raw<D> r;
+    // dzres (kept in dz) and dy2
+#pragma unroll
+    for (int j = 0; j < Lay<D>::J; ++j) {
+      float dm[4] = {1.f, 1.f, 1.f, 1.f};
+      if (drop) drop4(a.drop_p, s2, m, D, j, g, dm);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        dz.v[j][e] = keep ? (float)dr.v[j >> 1][4 * (j & 1) + e] : 0.f;
+        acc.v[j][e] = dz.v[j][e] * dm[e];
+      }
+    }
+    round_act<D>(acc, r);
+    store_raw<D>(a.dy2, D, m, ok, r, g);
+    // da1 = relu'(h1) * drop1(dy2 W2)
+    zero<D>(acc);
+    mm<D>(wl, r, acc, lane);
+#pragma unroll
+    for (int j = 0; j < Lay<D>::J; ++j) {
+      float dm[4] = {1.f, 1.f, 1.f, 1.f};
+      if (drop) drop4(a.drop_p, s1, m, D, j, g, dm);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        acc.v[j][e] = ((float)hr.v[j >> 1][4 * (j & 1) + e] > 0.f ? acc.v[j][e] : 0.f) * dm[e];
+    }
+    round_act<D>(acc, r);
+    store_raw<D>(a.da1, D, m, ok, r, g);
+    // dz = da1 W1 + dzres (rounded to bf16 as the stored tile)
+    mm<D>(wl + Lay<D>::WBYTES / 2, r, dz, lane);
+    round_act<D>(dz, r);
+    // dx1 = LN2'(x1, dz)
+    Act<D> xa, t1;
+    to_act<D>(xa, xr);
+    {
+      Act<D> pg, pb;
+      ln_bwd<D>(t1, xa, dz, ok, lv, mu, rs, g, pg, pb);
+      ln_accum<D>(red, pg, pb, lane, wave);
+    }
+    round_act<D>(t1, r);
+    store_raw<D>(a.dx1, D, m, ok, r, g);
+    // dout = dx1 Wo
+    zero<D>(acc);
+    mm<D>(wl + Lay<D>::WBYTES, r, acc, lane);
+    round_act<D>(acc, r);
+    store_raw<D>(a.dout, D, m, ok, r, g);
+  }
+  ln_partials<D>(red, a.part, tid);
+}
+
+// ------------------------------------------------------------------ block input side, backward
+struct InBwdArgs {
+  int64_t M;
+  const bf16* dq; const bf16* dkv; const bf16* dx1; const bf16* x;
+  const float* mean1; const float* rstd1; const float* ln_w;
+  const bf16* WinT; int64_t ldwt;                       // in_proj^T [d][3d]
+  bf16* dx; float* part;
+};
+
+// dx_kv = dk Wk + dv Wv; dQ = dq Wq + dx1; dx = dx_kv + LN1'(x, dQ) (+ affine partials)
+template <int D>
+__global__ __launch_bounds__(NT) void block_in_bwd_kernel(InBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  typedef Smem<D, 3, 1> L;
+  const bf16* wl = reinterpret_cast<const bf16*>(smem);
+  const float* lv = reinterpret_cast<const float*>(smem + L::W);   // ln_w
+  float* red = reinterpret_cast<float*>(smem + L::V);
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
+            cl = lane & 15;
+  const int64_t G = gridDim.x, nt = n_tiles(a.M);
+  int64_t t = blockIdx.x + G * wave;
+  Raw<D> kr, vr;
+  if (t < nt) {
+    const int64_t m = t * TR + cl, mc = m < a.M ? m : a.M - 1;
+    load_raw<D>(kr, a.dkv, 2 * D, mc, g);
+    load_raw<D>(vr, a.dkv + D, 2 * D, mc, g);
+  }
+  {
+    const bf16* const W[3] = {a.WinT + D, a.WinT + 2 * D, a.WinT};   // Wk^T, Wv^T, Wq^T rows
+    const int64_t ldw[3] = {a.ldwt, a.ldwt, a.ldwt};
+    stage_w<D, 3>(smem, W, ldw, wave, lane);
+    const float* const V[1] = {a.ln_w};
+    stage_v<D, 1>(reinterpret_cast<float*>(smem + L::W), V, tid);
+  }
+  ln_zero(red, D, lane, wave);
+  __syncthreads();
+  for (; t < nt; t += G * NW) {
+    asm volatile("" ::: "memory");
+    const int64_t m = t * TR + cl, mc = m < a.M ? m : a.M - 1;
+    const bool ok = m < a.M;
+    if (t != blockIdx.x + G * wave) {
+      load_raw<D>(kr, a.dkv, 2 * D, mc, g);
+      load_raw<D>(vr, a.dkv + D, 2 * D, mc, g);
+    }
+    Raw<D> qr, rr, xr;
+    load_raw<D>(qr, a.dq, D, mc, g);
+    load_raw<D>(rr, a.dx1, D, mc, g);
+    load_raw<D>(xr, a.x, D, mc, g);
+    const float mu = a.mean1[mc], rs = a.rstd1[mc];
+    Act<D> dxkv, dQ;
+    Raw<D> r;
+    zero<D>(dxkv);
+    mm<D>(wl, kr, dxkv, lane);
+    mm<D>(wl + Lay<D>::WBYTES / 2, vr, dxkv, lane);
+    round_act<D>(dxkv, r);
+    to_act<D>(dQ, rr);
+    mm<D>(wl + Lay<D>::WBYTES, qr, dQ, lane);
+    round_act<D>(dQ, r);
+    Act<D> xa, t1;
+    to_act<D>(xa, xr);
+    {
+      Act<D> pg, pb;
+      ln_bwd<D>(t1, xa, dQ, ok, lv, mu, rs, g, pg, pb);
+      ln_accum<D>(red, pg, pb, lane, wave);
+    }
+#pragma unroll
+    for (int j = 0; j < Lay<D>::J; ++j) t1.v[j] += dxkv.v[j];
+    round_act<D>(t1, r);
+    store_raw<D>(a.dx, D, m, ok, r, g);
+  }
+  ln_partials<D>(red, a.part, tid);
+}
+
+// ------------------------------------------------------------------ launch geometry
+static int g_ncu = 0;
+static int64_t grid_for(int64_t M) {
+  if (g_ncu == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) ==
+                                                 hipSuccess && n > 0)
+      g_ncu = n;
+    else
+      g_ncu = 256;
+  }
+  const int64_t nt = (M + TR - 1) / TR;
+  return nt < g_ncu ? nt : g_ncu;
+}
+template <int D> static size_t lds_fwd() { return Smem<D, 3, 5>::V; }
+template <int D> static size_t lds_bwd() { return Smem<D, 3, 1>::BYTES; }
+
+template <typename K>
+static void set_lds(K kern, size_t bytes) {
+  hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+}  // namespace rc
+
+// rowfused.hip's 64-row-tile kernels (RS_ROWCHAIN=0)
+int rf_sas_block_in(int64_t M, int64_t d, const void* x, int64_t ldx, const float* ln_w, const float* ln_b, float eps,
+                    void* Q, float* mean, float* rstd, const void* Wq, const float* bq, void* q, const void* Wkv,
+                    const float* bkv, void* kv, void* stream);
+int rf_sas_block_out(int64_t M, int64_t d, const void* o, const void* Q, const void* Wo, const float* bo, void* x1,
+                     const float* ln_w, const float* ln_b, float eps, void* z, float* mean, float* rstd,
+                     const void* W1, const float* b1, void* h1, const void* W2, const float* b2, void* xn,
+                     const int64_t* ids, float drop_p, uint64_t salt1, uint64_t salt2, const uint64_t* seed_base,
+                     void* stream);
+int rf_sas_block_out_bwd(int64_t M, int64_t d, const void* dxn, const int64_t* ids, const void* h1, const void* x1,
+                         const float* mean2, const float* rstd2, const float* ln_w, const void* W2T, const void* W1T,
+                         const void* WoT, void* dy2, void* da1, void* dx1, void* dout, float* part, float drop_p,
+                         uint64_t salt1, uint64_t salt2, const uint64_t* seed_base, void* stream);
+int rf_sas_block_in_bwd(int64_t M, int64_t d, const void* dq, const void* dkv, const void* dx1, const void* x,
+                        const float* mean1, const float* rstd1, const float* ln_w, const void* WinT, void* dx,
+                        float* part, void* stream);
+
+static bool use_chain() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("RS_ROWCHAIN");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
+extern "C" {
+
+int64_t rs_sas_block_parts(int64_t M) {
+  if (M <= 0) return 0;
+  return use_chain() ? rc::grid_for(M) : cdiv(M, 64);
+}
+
+int rs_sas_block_in(int64_t M, int64_t d, const void* x, int64_t ldx, const float* ln_w, const float* ln_b, float eps,
+                    void* Q, float* mean, float* rstd, const void* Wq, const float* bq, void* q, const void* Wkv,
+                    const float* bkv, void* kv, void* stream) {
+  if (!use_chain())
+    return rf_sas_block_in(M, d, x, ldx, ln_w, ln_b, eps, Q, mean, rstd, Wq, bq, q, Wkv, bkv, kv, stream);
+  if (M <= 0 || ldx % 8) return RS_ERR_ARG;
+  rc::InArgs a = {M, (const __bf16*)x, ldx, ln_w, ln_b, eps, (__bf16*)Q, mean, rstd, (const __bf16*)Wq, bq,
+                  (__bf16*)q, (const __bf16*)Wkv, bkv, (__bf16*)kv};
+  const dim3 grid((unsigned)rc::grid_for(M));
+  hipStream_t s = (hipStream_t)stream;
+  if (d == 64) {
+    rc::set_lds(rc::block_in_kernel<64>, rc::lds_fwd<64>());
+    hipLaunchKernelGGL(rc::block_in_kernel<64>, grid, dim3(rc::NT), rc::lds_fwd<64>(), s, a);
+  } else if (d == 128) {
+    rc::set_lds(rc::block_in_kernel<128>, rc::lds_fwd<128>());
+    hipLaunchKernelGGL(rc::block_in_kernel<128>, grid, dim3(rc::NT), rc::lds_fwd<128>(), s, a);
+  } else {
+    return RS_ERR_UNSUPPORTED;
+  }
+  return (int)hipGetLastError();
+}
+
+int rs_sas_block_out(int64_t M, int64_t d, const void* o, const void* Q, const void* Wo, const float* bo, void* x1,
+                     const float* ln_w, const float* ln_b, float eps, void* z, float* mean, float* rstd,
+                     const void* W1, const float* b1, void* h1, const void* W2, const float* b2, void* xn,
+                     const int64_t* ids, float drop_p, uint64_t salt1, uint64_t salt2, const uint64_t* seed_base,
+                     void* stream) {
+  if (!use_chain())
+    return rf_sas_block_out(M, d, o, Q, Wo, bo, x1, ln_w, ln_b, eps, z, mean, rstd, W1, b1, h1, W2, b2, xn, ids,
+                            drop_p, salt1, salt2, seed_base, stream);
+  if (M <= 0) return RS_ERR_ARG;
+  rc::OutArgs a = {M, (const __bf16*)o, (const __bf16*)Q, (const __bf16*)Wo, bo, (__bf16*)x1, ln_w, ln_b, eps,
+                   (__bf16*)z, mean, rstd, (const __bf16*)W1, b1, (__bf16*)h1, (const __bf16*)W2, b2, (__bf16*)xn,
+                   ids, drop_p, salt1, salt2, seed_base};
+  const dim3 grid((unsigned)rc::grid_for(M));
+  hipStream_t s = (hipStream_t)stream;
+  if (d == 64) {
+    rc::set_lds(rc::block_out_kernel<64>, rc::lds_fwd<64>());
+    hipLaunchKernelGGL(rc::block_out_kernel<64>, grid, dim3(rc::NT), rc::lds_fwd<64>(), s, a);
+  } else if (d == 128) {
+    rc::set_lds(rc::block_out_kernel<128>, rc::lds_fwd<128>());
+    hipLaunchKernelGGL(rc::block_out_kernel<128>, grid, dim3(rc::NT), rc::lds_fwd<128>(), s, a);
+  } else {
+    return RS_ERR_UNSUPPORTED;
+  }
+  return (int)hipGetLastError();
+}
+
+int rs_sas_block_out_bwd(int64_t M, int64_t d, const void* dxn, const int64_t* ids, const void* h1, const void* x1,
+                         const float* mean2, const float* rstd2, const float* ln_w, const void* W2T, const void* W1T,
+                         const void* WoT, void* dy2, void* da1, void* dx1, void* dout, float* part, float drop_p,
+                         uint64_t salt1, uint64_t salt2, const uint64_t* seed_base, void* stream) {
+  if (!use_chain())
+    return rf_sas_block_out_bwd(M, d, dxn, ids, h1, x1, mean2, rstd2, ln_w, W2T, W1T, WoT, dy2, da1, dx1, dout, part,
+                                drop_p, salt1, salt2, seed_base, stream);
+  if (M <= 0) return RS_ERR_ARG;
+  rc::OutBwdArgs a = {M, (const __bf16*)dxn, ids, (const __bf16*)h1, (const __bf16*)x1, mean2, rstd2, ln_w,
+                      (const __bf16*)W2T, (const __bf16*)W1T, (const __bf16*)WoT, (__bf16*)dy2, (__bf16*)da1,
+                      (__bf16*)dx1, (__bf16*)dout, part, drop_p, salt1, salt2, seed_base};
+  const dim3 grid((unsigned)rc::grid_for(M));
+  hipStream_t s = (hipStream_t)stream;
+  if (d == 64) {
+    rc::set_lds(rc::block_out_bwd_kernel<64>, rc::lds_bwd<64>());
+    hipLaunchKernelGGL(rc::block_out_bwd_kernel<64>, grid, dim3(rc::NT), rc::lds_bwd<64>(), s, a);
+  } else if (d == 128) {
+    rc::set_lds(rc::block_out_bwd_kernel<128>, rc::lds_bwd<128>());
+    hipLaunchKernelGGL(rc::block_out_bwd_kernel<128>, grid, dim3(rc::NT), rc::lds_bwd<128>(), s, a);
+  } else {
+    return RS_ERR_UNSUPPORTED;
+  }
+  return (int)hipGetLastError();
+}
+
+int rs_sas_block_in_bwd(int64_t M, int64_t d, const void* dq, const void* dkv, const void* dx1, const void* x,
+                        const float* mean1, const float* rstd1, const float* ln_w, const void* WinT, void* dx,
+                        float* part, void* stream) {
+  if (!use_chain())
+    return rf_sas_block_in_bwd(M, d, dq, dkv, dx1, x, mean1, rstd1, ln_w, WinT, dx, part, stream);
+  if (M <= 0) return RS_ERR_ARG;
+  rc::InBwdArgs a = {M, (const __bf16*)dq, (const __bf16*)dkv, (const __bf16*)dx1, (const __bf16*)x, mean1, rstd1,
+                     ln_w, (const __bf16*)WinT, 3 * d, (__bf16*)dx, part};
+  const dim3 grid((unsigned)rc::grid_for(M));
+  hipStream_t s = (hipStream_t)stream;
+  if (d == 64) {
+    rc::set_lds(rc::block_in_bwd_kernel<64>, rc::lds_bwd<64>());
+    hipLaunchKernelGGL(rc::block_in_bwd_kernel<64>, grid, dim3(rc::NT), rc::lds_bwd<64>(), s, a);
+  } else if (d == 128) {
+    rc::set_lds(rc::block_in_bwd_kernel<128>, rc::lds_bwd<128>());
+    hipLaunchKernelGGL(rc::block_in_bwd_kernel<128>, grid, dim3(rc::NT), rc::lds_bwd<128>(), s, a);
+  } else {
+    return RS_ERR_UNSUPPORTED;
+  }
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

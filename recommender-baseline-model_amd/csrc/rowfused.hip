@@ -684,9 +684,8 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const int64_t* __re
 
 }  // namespace rf
 
-extern "C" {
-
-int rs_sas_block_in(int64_t M, int64_t d, const void* x, int64_t ldx, const float* ln_w, const float* ln_b, float eps,
+// 64-row-tile launchers, called by rowchain.hip's C-ABI entry points when RS_ROWCHAIN=0
+int rf_sas_block_in(int64_t M, int64_t d, const void* x, int64_t ldx, const float* ln_w, const float* ln_b, float eps,
                     void* Q, float* mean, float* rstd, const void* Wq, const float* bq, void* q, const void* Wkv,
                     const float* bkv, void* kv, void* stream) {
   if (M <= 0 || ldx % 8) return RS_ERR_ARG;
@@ -700,7 +699,7 @@ int rs_sas_block_in(int64_t M, int64_t d, const void* x, int64_t ldx, const floa
   return (int)hipGetLastError();
 }
 
-int rs_sas_block_out(int64_t M, int64_t d, const void* o, const void* Q, const void* Wo, const float* bo, void* x1,
+int rf_sas_block_out(int64_t M, int64_t d, const void* o, const void* Q, const void* Wo, const float* bo, void* x1,
                      const float* ln_w, const float* ln_b, float eps, void* z, float* mean, float* rstd,
                      const void* W1, const float* b1, void* h1, const void* W2, const float* b2, void* xn,
                      const int64_t* ids, float drop_p, uint64_t salt1, uint64_t salt2, const uint64_t* seed_base,
@@ -717,7 +716,7 @@ int rs_sas_block_out(int64_t M, int64_t d, const void* o, const void* Q, const v
   return (int)hipGetLastError();
 }
 
-int rs_sas_block_out_bwd(int64_t M, int64_t d, const void* dxn, const int64_t* ids, const void* h1, const void* x1,
+int rf_sas_block_out_bwd(int64_t M, int64_t d, const void* dxn, const int64_t* ids, const void* h1, const void* x1,
                          const float* mean2, const float* rstd2, const float* ln_w, const void* W2T, const void* W1T,
                          const void* WoT, void* dy2, void* da1, void* dx1, void* dout, float* part, float drop_p,
                          uint64_t salt1, uint64_t salt2, const uint64_t* seed_base, void* stream) {
@@ -733,7 +732,7 @@ int rs_sas_block_out_bwd(int64_t M, int64_t d, const void* dxn, const int64_t* i
   return (int)hipGetLastError();
 }
 
-int rs_sas_block_in_bwd(int64_t M, int64_t d, const void* dq, const void* dkv, const void* dx1, const void* x,
+int rf_sas_block_in_bwd(int64_t M, int64_t d, const void* dq, const void* dkv, const void* dx1, const void* x,
                         const float* mean1, const float* rstd1, const float* ln_w, const void* WinT, void* dx,
                         float* part, void* stream) {
   if (M <= 0) return RS_ERR_ARG;
@@ -746,6 +745,8 @@ int rs_sas_block_in_bwd(int64_t M, int64_t d, const void* dq, const void* dkv, c
   else return RS_ERR_UNSUPPORTED;
   return (int)hipGetLastError();
 }
+
+extern "C" {
 
 int rs_transpose_bf16(int64_t nmat, const int64_t* desc, int64_t max_tiles, const void* src, void* dst,
                       void* stream) {

@@ -305,7 +305,8 @@ class SASEngine:
             else:
                 ops.sas_head_bwd(None, None, None, None, None, dpl, dnl, None, None, s["pos"], s["neg"], E, s["xL"],
                                  gl, s["muf"], s["rf"], dx, lnh)
-            segs = ops.ln_partial_segments(lnh, M, d, G("last_layernorm.weight"), G("last_layernorm.bias"))
+            segs = ops.ln_partial_segments(lnh, M, d, G("last_layernorm.weight"), G("last_layernorm.bias"),
+                                           nb=-(-M // 64))
             # the item table's gradient: "side" (default) = rs_item_grad on the side queue beside the grouped
             # weight gradients; "fused" = inside those launches on this queue (rs_wgrad_grouped_items; measured
             # 0.367 vs 0.356 ms/step at cfg2: the item chunks queue behind the weight-gradient tiles); "serial"
@@ -442,7 +443,7 @@ class SASEngine:
         e = self._buf
         G = lambda n: self.flat.view(n, grad)  # noqa: E731
         wT = self._wT.view(L, 6, d, d)              # refreshed by _side_prologue
-        nb = -(-M // 64)
+        nb = ops.sas_block_parts(M)
         lnp = self.ws.get("lnp", (L, 2, 2 * d * nb), torch.float32)
         wat = self.ws.get("attn", (B * H * T,), torch.float32)
         probs, segs = [], list(extra_segs)

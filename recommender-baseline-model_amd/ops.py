@@ -417,7 +417,7 @@ def sas_block_out(o, Q, Wo, bo, x1, ln_w, ln_b, eps, z, mean, rstd, W1, b1, h1, 
 
 def sas_block_out_bwd(dxn, ids, h1, x1, mean2, rstd2, ln_w, W2T, W1T, WoT, dy2, da1, dx1, dout, part, drop_p, salt1,
                       salt2, seed_base):
-    """part: fp32 >= 2*d*ceil(M/64), receives the LN2 affine partials (ln_partial_segments)."""
+    """part: fp32 >= 2*d*sas_block_parts(M), receives the LN2 affine partials (ln_partial_segments)."""
     M, d = dxn.shape
     call("rs_sas_block_out_bwd", M, d, ptr(dxn), ptr(ids), ptr(h1), ptr(x1), ptr(mean2), ptr(rstd2), ptr(ln_w),
          ptr(W2T), ptr(W1T), ptr(WoT), ptr(dy2), ptr(da1), ptr(dx1), ptr(dout), ptr(part), drop_p, salt1, salt2,
@@ -430,9 +430,15 @@ def sas_block_in_bwd(dq, dkv, dx1, x, mean1, rstd1, ln_w, WinT, dx, part):
          ptr(WinT), ptr(dx), ptr(part), stream())
 
 
-def ln_partial_segments(part, M, d, dgamma, dbeta):
-    """The two reduce segments of a fused kernel's LayerNorm partials (part[b][2][d], b < ceil(M/64))."""
-    nb = -(-M // 64)
+def sas_block_parts(M):
+    """LayerNorm affine partial sets written by rs_sas_block_out_bwd / rs_sas_block_in_bwd for M rows."""
+    return int(_lib.lib().rs_sas_block_parts(M))
+
+
+def ln_partial_segments(part, M, d, dgamma, dbeta, nb=None):
+    """The two reduce segments of a fused kernel's LayerNorm partials (part[b][2][d], b < nb; default: the
+    SAS row-block backward kernels' set count)."""
+    nb = sas_block_parts(M) if nb is None else nb
     return [(part, 2 * d, nb, d, dgamma), (part[d:], 2 * d, nb, d, dbeta)]
 
 

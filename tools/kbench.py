@@ -174,7 +174,7 @@ def main():
                                                           W, bias, xn, ids, 0.2, 3, 4, sb), 6 * mb)
         WT, WinT = rn(d, d), rn(d, 3 * d)
         dy2, da1, dx1, do_ = rn(M, d), rn(M, d), rn(M, d), rn(M, d)
-        part = torch.empty(2 * d * (-(-M // 64)), device=dev)
+        part = torch.empty(2 * d * max(-(-M // 64), ops.sas_block_parts(M)), device=dev)
         run("fused block_out_bwd", lambda: ops.sas_block_out_bwd(y, ids, h1, x1, m1_, r1_, gam, WT, WT, WT, dy2, da1,
                                                                   dx1, do_, part, 0.2, 3, 4, sb), 8 * mb)
         dqkv = rn(M, 2 * d)
