@@ -28,15 +28,19 @@ namespace rc {
 
 // phase timestamps for tools/micro/rowchain_phase.hip (compiled out of the library)
 #ifdef RC_PROF
-__device__ unsigned long long g_rc_prof[4096 * 8 * 8];
+__device__ unsigned long long g_rc_prof[4096 * 8 * 16];
 #define RCPROF(slot)                                                                                 \
   do {                                                                                               \
-    if ((threadIdx.x & 63) == 0) g_rc_prof[(blockIdx.x * 8 + (threadIdx.x >> 6)) * 8 + (slot)] = wall_clock64(); \
+    if ((threadIdx.x & 63) == 0) g_rc_prof[(blockIdx.x * 8 + (threadIdx.x >> 6)) * 16 + (slot)] = wall_clock64(); \
   } while (0)
 #else
 #define RCPROF(slot) \
   do {               \
   } while (0)
+#endif
+
+#ifndef RC_NOSTORE
+#define RC_NOSTORE 0   // tools/micro/rowchain_phase.hip: 1 = skip block_out's saved-tensor stores (cost probe)
 #endif
 
 typedef __bf16 bf16;
@@ -190,11 +194,15 @@ __device__ __forceinline__ void ln_fwd(Act<D>& x, const float* gw, const float* 
   }
 }
 
-// LayerNorm backward (layernorm.hip ln_bwd, VAR 0): t = rstd*(dy*g - mean(dy*g)) - rstd^3*mean(dy*g*u)*u,
-// u = x - mean; dy zeroed on invalid tokens; pg/pb receive this lane's dgamma/dbeta terms
+// LayerNorm backward (layernorm.hip ln_bwd, VAR 0), in place on dy: t = rstd*(dy*g - mean(dy*g))
+// - rstd^3*mean(dy*g*u)*u, u = x - mean (x as stored, bf16); dy zeroed on invalid tokens.  The dgamma/dbeta
+// terms of the tile's 16 tokens are summed by an xor tree over the lanes of a group as they are formed and added
+// to the wave's own LDS row red[wave][2][D] (no other wave touches it before ln_partials' barrier)
 template <int D>
-__device__ __forceinline__ void ln_bwd(Act<D>& t, const Act<D>& x, const Act<D>& dy, bool valid, const float* gw,
-                                       float mu, float a, int g, Act<D>& pg, Act<D>& pb) {
+__device__ __forceinline__ void ln_bwd(Act<D>& dy, const Raw<D>& xr, bool valid, const float* gw, float mu, float a,
+                                       float* red, int lane, int wave) {
+  const int g = lane >> 4, cl = lane & 15;
+  float* rw = red + wave * 2 * D;
   float sg = 0.f, sgu = 0.f;
 #pragma unroll
   for (int j = 0; j < Lay<D>::J; ++j) {
@@ -202,13 +210,21 @@ __device__ __forceinline__ void ln_bwd(Act<D>& t, const Act<D>& x, const Act<D>&
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const float gy = valid ? dy.v[j][e] : 0.f;
-      const float u = x.v[j][e] - mu;
+      const float u = (float)xr.v[j >> 1][4 * (j & 1) + e] - mu;
       const float gq = gy * w[e];
-      pg.v[j][e] = gy * (u * a);
-      pb.v[j][e] = gy;
+      float pg = gy * (u * a), pb = gy;
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        pg += __shfl_xor(pg, o, 64);
+        pb += __shfl_xor(pb, o, 64);
+      }
+      if (cl == 0) {
+        rw[feat(j, g, e)] += pg;
+        rw[D + feat(j, g, e)] += pb;
+      }
       sg += gq;
       sgu += gq * u;
-      t.v[j][e] = gq;   // dy*g for now
+      dy.v[j][e] = gq;   // dy*g for now
     }
   }
   sg = row_sum(sg);
@@ -217,31 +233,10 @@ __device__ __forceinline__ void ln_bwd(Act<D>& t, const Act<D>& x, const Act<D>&
 #pragma unroll
   for (int j = 0; j < Lay<D>::J; ++j)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) t.v[j][e] = a * (t.v[j][e] - mg) - coef * (x.v[j][e] - mu);
+    for (int e = 0; e < 4; ++e)
+      dy.v[j][e] = a * (dy.v[j][e] - mg) - coef * ((float)xr.v[j >> 1][4 * (j & 1) + e] - mu);
 }
 
-// add this tile's dgamma/dbeta terms, summed over its 16 tokens (xor tree over the lanes of a group),
-// to the wave's own LDS row red[wave][2][D] (no other wave touches it before ln_partials' barrier)
-template <int D>
-__device__ __forceinline__ void ln_accum(float* red, const Act<D>& pg, const Act<D>& pb, int lane, int wave) {
-  const int g = lane >> 4, cl = lane & 15;
-  float* rw = red + wave * 2 * D;
-#pragma unroll
-  for (int j = 0; j < Lay<D>::J; ++j)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float a = pg.v[j][e], b = pb.v[j][e];
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        a += __shfl_xor(a, o, 64);
-        b += __shfl_xor(b, o, 64);
-      }
-      if (cl == 0) {
-        rw[feat(j, g, e)] += a;
-        rw[D + feat(j, g, e)] += b;
-      }
-    }
-}
 __device__ __forceinline__ void ln_zero(float* red, int D, int lane, int wave) {
   for (int i = lane; i < 2 * D; i += 64) red[wave * 2 * D + i] = 0.f;
 }
@@ -260,7 +255,245 @@ __device__ __forceinline__ void ln_partials(const float* red, float* part, int t
 
 __device__ __forceinline__ int64_t n_tiles(int64_t M) { return (M + TR - 1) / TR; }
 
-// ------------------------------------------------------------------ block input side
+// ------------------------------------------------------------------ LDS layout
+// NM weight images, then NV fp32 vectors of D, then NR LayerNorm partial blocks red[NW][2][D]
+template <int D, int NM, int NV, int NR> struct Smem {
+  static constexpr size_t W = (size_t)NM * Lay<D>::WBYTES;
+  static constexpr size_t V = W + (size_t)NV * D * 4;
+  static constexpr size_t BYTES = V + (size_t)NR * NW * 2 * D * 4;
+};
+__device__ __forceinline__ const bf16* wslot(const char* smem, int i, int wbytes) {
+  return reinterpret_cast<const bf16*>(smem + (size_t)i * wbytes);
+}
+
+// per-tile context: this wave's 16 tokens
+struct Tile {
+  int64_t m, mc;   // this lane's token row, clamped for loads
+  bool ok;         // row < M
+};
+__device__ __forceinline__ Tile tile_of(int64_t t, int64_t M, int cl) {
+  Tile x;
+  x.m = t * TR + cl;
+  x.ok = x.m < M;
+  x.mc = x.ok ? x.m : M - 1;
+  return x;
+}
+// ------------------------------------------------------------------ chain stages (one 16-token tile per wave)
+// Forward, block input side (sas.py:73-76): Q = LN1(x) [saved], q = Q Wq^T + bq.  Weights/vectors: Wq at wq;
+// lv: ln1_w, ln1_b, bq, bk, bv (5 x D).  Returns nothing; k/v follow in fwd_in_kv.
+template <int D>
+__device__ __forceinline__ void fwd_in_q(const Raw<D>& xr, const Tile& T, const bf16* wq, const float* lv, float eps,
+                                         bf16* Q, float* mean, float* rstd, bf16* q, int lane) {
+  const int g = lane >> 4;
+  Act<D> y;
+  to_act<D>(y, xr);
+  float mu, rs;
+  ln_fwd<D>(y, lv, lv + D, eps, g, mu, rs);
+  Raw<D> Qr;
+  round_act<D>(y, Qr);
+  store_raw<D>(Q, D, T.m, T.ok, Qr, g);
+  if (T.ok && g == 0) {
+    mean[T.m] = mu;
+    rstd[T.m] = rs;
+  }
+  Act<D> acc;
+  zero<D>(acc);
+  mm<D>(wq, Qr, acc, lane);
+#pragma unroll
+  for (int j = 0; j < Lay<D>::J; ++j) acc.v[j] += vec4<D>(lv + 2 * D, j, g);
+  Raw<D> r;
+  round_act<D>(acc, r);
+  store_raw<D>(q, D, T.m, T.ok, r, g);
+}
+// k, v = x Wk^T + bk, x Wv^T + bv -> kv [M][2D]
+template <int D>
+__device__ __forceinline__ void fwd_in_kv(const Raw<D>& xr, const Tile& T, const bf16* wk, const bf16* wv,
+                                          const float* lv, bf16* kv, int lane) {
+  const int g = lane >> 4;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    Act<D> acc;
+    zero<D>(acc);
+    mm<D>(h == 0 ? wk : wv, xr, acc, lane);
+#pragma unroll
+    for (int j = 0; j < Lay<D>::J; ++j) acc.v[j] += vec4<D>(lv + (3 + h) * D, j, g);
+    Raw<D> r;
+    round_act<D>(acc, r);
+    store_raw<D>(kv + h * D, 2 * D, T.m, T.ok, r, g);
+  }
+}
+
+struct OutFwd {
+  bf16 *x1, *z, *h1, *xn;
+  float *mean, *rstd;
+  const int64_t* ids;
+  float drop_p, eps;
+  uint32_t s1, s2;
+};
+// dropout multipliers of this lane's 4 features of tile j (pairs share one hash, as drop_mul2)
+__device__ __forceinline__ void drop4(float p, uint32_t s32, int64_t m, int D, int j, int g, float (&dm)[4]) {
+  const uint64_t idx = (uint64_t)(m * D + feat(j, g, 0));
+  drop_mul2(p, s32, idx, dm[0], dm[1]);
+  drop_mul2(p, s32, idx + 2, dm[2], dm[3]);
+}
+// Forward, block output side part 1 (sas.py:75-80): x1 = Q + o Wo^T + bo [saved], z = LN2(x1) [saved],
+// h1 = relu(drop(z W1^T + b1)) [saved].  lv: bo, ln2_w, ln2_b, b1, b2.
+template <int D>
+__device__ __forceinline__ void fwd_out_a(const Raw<D>& orr, const Raw<D>& Qr, const Tile& T, const bf16* wo,
+                                          const bf16* w1, const float* lv, const OutFwd& o, Raw<D>& zr, Raw<D>& hr,
+                                          int lane) {
+  const int g = lane >> 4;
+  Act<D> acc;
+  Raw<D> r;
+  zero<D>(acc);
+  mm<D>(wo, orr, acc, lane);
+#pragma unroll
+  for (int j = 0; j < Lay<D>::J; ++j) {
+    const f32x4 bb = vec4<D>(lv, j, g);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc.v[j][e] = acc.v[j][e] + bb[e] + (float)Qr.v[j >> 1][4 * (j & 1) + e];
+  }
+  round_act<D>(acc, r);
+  if (!RC_NOSTORE) store_raw<D>(o.x1, D, T.m, T.ok, r, g);
+  float mu, rs;
+  ln_fwd<D>(acc, lv + D, lv + 2 * D, o.eps, g, mu, rs);
+  round_act<D>(acc, zr);
+  if (!RC_NOSTORE) store_raw<D>(o.z, D, T.m, T.ok, zr, g);
+  if (T.ok && g == 0) {
+    o.mean[T.m] = mu;
+    o.rstd[T.m] = rs;
+  }
+  zero<D>(acc);
+  mm<D>(w1, zr, acc, lane);
+  const bool drop = o.drop_p > 0.f;
+#pragma unroll
+  for (int j = 0; j < Lay<D>::J; ++j) {
+    float dm[4] = {1.f, 1.f, 1.f, 1.f};
+    if (drop) drop4(o.drop_p, o.s1, T.m, D, j, g, dm);
+    const f32x4 bb = vec4<D>(lv + 3 * D, j, g);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc.v[j][e] = fmaxf(acc.v[j][e] + bb[e], 0.f) * dm[e];
+  }
+  round_act<D>(acc, hr);
+  if (!RC_NOSTORE) store_raw<D>(o.h1, D, T.m, T.ok, hr, g);
+}
+// part 2 (sas.py:81-84): x' = (drop(h1 W2^T + b2) + z) * (ids != 0) [saved] -> xr
+template <int D>
+__device__ __forceinline__ void fwd_out_b(const Raw<D>& hr, const Raw<D>& zr, const Tile& T, const bf16* w2,
+                                          const float* lv, const OutFwd& o, Raw<D>& xr, int lane) {
+  const int g = lane >> 4;
+  const bool keep = T.ok && o.ids[T.mc] != 0;
+  Act<D> acc;
+  zero<D>(acc);
+  mm<D>(w2, hr, acc, lane);
+  const bool drop = o.drop_p > 0.f;
+#pragma unroll
+  for (int j = 0; j < Lay<D>::J; ++j) {
+    float dm[4] = {1.f, 1.f, 1.f, 1.f};
+    if (drop) drop4(o.drop_p, o.s2, T.m, D, j, g, dm);
+    const f32x4 bb = vec4<D>(lv + 4 * D, j, g);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float v = __builtin_fmaf(acc.v[j][e] + bb[e], dm[e], (float)zr.v[j >> 1][4 * (j & 1) + e]);
+      acc.v[j][e] = keep ? v : 0.f;
+    }
+  }
+  round_act<D>(acc, xr);
+  store_raw<D>(o.xn, D, T.m, T.ok, xr, g);
+}
+
+// Backward, block input side (sas.py:73-76 reversed), part 1: dx_kv = dk Wk + dv Wv (WkT, WvT images)
+template <int D>
+__device__ __forceinline__ void bwd_in_a(const Raw<D>& kr, const Raw<D>& vr, const bf16* wk, const bf16* wv,
+                                         Raw<D>& dxkv, int lane) {
+  Act<D> acc;
+  zero<D>(acc);
+  mm<D>(wk, kr, acc, lane);
+  mm<D>(wv, vr, acc, lane);
+  round_act<D>(acc, dxkv);
+}
+// part 2: dQ = dq Wq + dx1; dx = dx_kv + LN1'(x, dQ) (+ affine partials into red) -> dxr
+template <int D>
+__device__ __forceinline__ void bwd_in_b(const Raw<D>& qr, const Raw<D>& rr, const Raw<D>& xr, const Raw<D>& dxkv,
+                                         const Tile& T, float mu, float rs, const bf16* wq, const float* lnw,
+                                         float* red, Raw<D>& dxr, int lane, int wave) {
+  const int g = lane >> 4;
+  Act<D> dQ;
+  Raw<D> r;
+  to_act<D>(dQ, rr);
+  mm<D>(wq, qr, dQ, lane);
+  round_act<D>(dQ, r);
+  ln_bwd<D>(dQ, xr, T.ok, lnw, mu, rs, red, lane, wave);
+#pragma unroll
+  for (int j = 0; j < Lay<D>::J; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dQ.v[j][e] += (float)dxkv.v[j >> 1][4 * (j & 1) + e];
+  round_act<D>(dQ, dxr);
+}
+
+struct OutBwd {
+  bf16 *dy2, *da1, *dx1, *dout;
+  const int64_t* ids;
+  float drop_p;
+  uint32_t s1, s2;
+};
+// Backward, block output side (sas.py:75-84 reversed), part 1: dzres = dxn*mask; dy2 = drop2(dzres) [saved];
+// da1 = relu'(h1) * drop1(dy2 W2) [saved] -> dz (holding dzres), dar (da1)
+template <int D>
+__device__ __forceinline__ void bwd_out_a(const Raw<D>& dr, const Raw<D>& hr, const Tile& T, const bf16* w2,
+                                          const OutBwd& o, Raw<D>& dzr, Raw<D>& dar, int lane) {
+  const int g = lane >> 4;
+  const bool keep = T.ok && o.ids[T.mc] != 0;
+  const bool drop = o.drop_p > 0.f;
+  Act<D> acc;
+  Raw<D> r;
+#pragma unroll
+  for (int j = 0; j < Lay<D>::J; ++j) {
+    float dm[4] = {1.f, 1.f, 1.f, 1.f};
+    if (drop) drop4(o.drop_p, o.s2, T.m, D, j, g, dm);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const bf16 v = keep ? dr.v[j >> 1][4 * (j & 1) + e] : (bf16)0.f;
+      dzr.v[j >> 1][4 * (j & 1) + e] = v;
+      acc.v[j][e] = (float)v * dm[e];
+    }
+  }
+  round_act<D>(acc, r);
+  store_raw<D>(o.dy2, D, T.m, T.ok, r, g);
+  zero<D>(acc);
+  mm<D>(w2, r, acc, lane);
+#pragma unroll
+  for (int j = 0; j < Lay<D>::J; ++j) {
+    float dm[4] = {1.f, 1.f, 1.f, 1.f};
+    if (drop) drop4(o.drop_p, o.s1, T.m, D, j, g, dm);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc.v[j][e] = ((float)hr.v[j >> 1][4 * (j & 1) + e] > 0.f ? acc.v[j][e] : 0.f) * dm[e];
+  }
+  round_act<D>(acc, dar);
+  store_raw<D>(o.da1, D, T.m, T.ok, dar, g);
+}
+// part 2: dz = da1 W1 + dzres; dx1 = LN2'(x1, dz) [saved, + affine partials into red]; dout = dx1 Wo [saved]
+template <int D>
+__device__ __forceinline__ void bwd_out_b(const Raw<D>& dar, const Raw<D>& xr, const Raw<D>& dzr, const Tile& T,
+                                          float mu, float rs, const bf16* w1, const bf16* wo, const float* lnw,
+                                          const OutBwd& o, float* red, int lane, int wave) {
+  const int g = lane >> 4;
+  Raw<D> r;
+  Act<D> dz;
+  to_act<D>(dz, dzr);
+  mm<D>(w1, dar, dz, lane);
+  round_act<D>(dz, r);
+  ln_bwd<D>(dz, xr, T.ok, lnw, mu, rs, red, lane, wave);
+  round_act<D>(dz, r);
+  store_raw<D>(o.dx1, D, T.m, T.ok, r, g);
+  Act<D> acc;
+  zero<D>(acc);
+  mm<D>(wo, r, acc, lane);
+  round_act<D>(acc, r);
+  store_raw<D>(o.dout, D, T.m, T.ok, r, g);
+}
+
+// ------------------------------------------------------------------ single-block kernels
 struct InArgs {
   int64_t M;
   const bf16* x; int64_t ldx;
@@ -270,29 +503,19 @@ struct InArgs {
   const bf16* Wkv; const float* bkv; bf16* kv;
 };
 
-// LDS: NM weight images, then NV fp32 vectors of D, then (backward) the LN partial rows red[NW][2][D]
-template <int D, int NM, int NV> struct Smem {
-  static constexpr size_t W = (size_t)NM * Lay<D>::WBYTES;
-  static constexpr size_t V = W + (size_t)NV * D * 4;
-  static constexpr size_t BYTES = V + (size_t)NW * 2 * D * 4;
-};
-
 // X -> Q = LN1(X) [saved], q = Q Wq^T + bq, kv = X Wkv^T + bkv
 template <int D>
 __global__ __launch_bounds__(NT) void block_in_kernel(InArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  typedef Smem<D, 3, 5> L;
-  const bf16* wl = reinterpret_cast<const bf16*>(smem);
+  typedef Smem<D, 3, 5, 0> L;
+  constexpr int WB = Lay<D>::WBYTES;
   const float* lv = reinterpret_cast<const float*>(smem + L::W);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
             cl = lane & 15;
   const int64_t G = gridDim.x, nt = n_tiles(a.M);
   int64_t t = blockIdx.x + G * wave;
   Raw<D> xr;
-  if (t < nt) {
-    const int64_t m = t * TR + cl;
-    load_raw<D>(xr, a.x, a.ldx, m < a.M ? m : a.M - 1, g);
-  }
+  if (t < nt) load_raw<D>(xr, a.x, a.ldx, tile_of(t, a.M, cl).mc, g);
   {
     const bf16* const W[3] = {a.Wq, a.Wkv, a.Wkv + (int64_t)D * D};
     const int64_t ldw[3] = {D, D, D};
@@ -303,36 +526,13 @@ __global__ __launch_bounds__(NT) void block_in_kernel(InArgs a) {
   __syncthreads();
   for (; t < nt; t += G * NW) {
     asm volatile("" ::: "memory");   // no hoisting of the loop-invariant weight fragment reads
-    const int64_t m = t * TR + cl;
-    const bool ok = m < a.M;
-    if (t != blockIdx.x + G * wave) load_raw<D>(xr, a.x, a.ldx, ok ? m : a.M - 1, g);
-    Act<D> y;
-    to_act<D>(y, xr);
-    float mu, rs;
-    ln_fwd<D>(y, lv, lv + D, a.eps, g, mu, rs);
-    Raw<D> Qr;
-    round_act<D>(y, Qr);
-    store_raw<D>(a.Q, D, m, ok, Qr, g);
-    if (ok && g == 0) {
-      a.mean[m] = mu;
-      a.rstd[m] = rs;
-    }
-    Act<D> acc;
-    Raw<D> outr;
-#pragma unroll
-    for (int h = 0; h < 3; ++h) {        // q = Q Wq^T + bq; k, v = X Wk^T + bk, X Wv^T + bv
-      zero<D>(acc);
-      mm<D>(wl + h * (Lay<D>::WBYTES / 2), h == 0 ? Qr : xr, acc, lane);
-#pragma unroll
-      for (int j = 0; j < Lay<D>::J; ++j) acc.v[j] += vec4<D>(lv + (2 + h) * D, j, g);
-      round_act<D>(acc, outr);
-      if (h == 0) store_raw<D>(a.q, D, m, ok, outr, g);
-      else store_raw<D>(a.kv + (h - 1) * D, 2 * D, m, ok, outr, g);
-    }
+    const Tile T = tile_of(t, a.M, cl);
+    if (t != blockIdx.x + G * wave) load_raw<D>(xr, a.x, a.ldx, T.mc, g);
+    fwd_in_q<D>(xr, T, wslot(smem, 0, WB), lv, a.eps, a.Q, a.mean, a.rstd, a.q, lane);
+    fwd_in_kv<D>(xr, T, wslot(smem, 1, WB), wslot(smem, 2, WB), lv, a.kv, lane);
   }
 }
 
-// ------------------------------------------------------------------ block output side
 struct OutArgs {
   int64_t M;
   const bf16* o; const bf16* Q;
@@ -343,12 +543,10 @@ struct OutArgs {
   const int64_t* ids;
   float drop_p; uint64_t salt1, salt2; const uint64_t* seed_base;
 };
-
-// dropout multipliers of this lane's 4 features of tile j (pairs share one hash, as drop_mul2)
-__device__ __forceinline__ void drop4(float p, uint32_t s32, int64_t m, int D, int j, int g, float (&dm)[4]) {
-  const uint64_t idx = (uint64_t)(m * D + feat(j, g, 0));
-  drop_mul2(p, s32, idx, dm[0], dm[1]);
-  drop_mul2(p, s32, idx + 2, dm[2], dm[3]);
+__device__ __forceinline__ OutFwd out_fwd_of(const OutArgs& a) {
+  const bool drop = a.drop_p > 0.f;
+  return OutFwd{a.x1, a.z, a.h1, a.xn, a.mean, a.rstd, a.ids, a.drop_p, a.eps,
+                drop ? seed32(eff_seed(a.salt1, a.seed_base)) : 0u, drop ? seed32(eff_seed(a.salt2, a.seed_base)) : 0u};
 }
 
 // O -> x1 = Q + O Wo^T + bo [saved], z = LN2(x1) [saved], h1 = relu(drop(z W1^T + b1)) [saved],
@@ -356,20 +554,18 @@ __device__ __forceinline__ void drop4(float p, uint32_t s32, int64_t m, int D, i
 template <int D>
 __global__ __launch_bounds__(NT) void block_out_kernel(OutArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  typedef Smem<D, 3, 5> L;
-  const bf16* wl = reinterpret_cast<const bf16*>(smem);
+  typedef Smem<D, 3, 5, 0> L;
+  constexpr int WB = Lay<D>::WBYTES;
   const float* lv = reinterpret_cast<const float*>(smem + L::W);   // bo, ln_w, ln_b, b1, b2
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
             cl = lane & 15;
   RCPROF(0);
   const int64_t G = gridDim.x, nt = n_tiles(a.M);
-  const bool drop = a.drop_p > 0.f;
-  const uint32_t s1 = drop ? seed32(eff_seed(a.salt1, a.seed_base)) : 0u;
-  const uint32_t s2 = drop ? seed32(eff_seed(a.salt2, a.seed_base)) : 0u;
+  const OutFwd of = out_fwd_of(a);
   int64_t t = blockIdx.x + G * wave;
   Raw<D> orr, Qr;
   if (t < nt) {
-    const int64_t m = t * TR + cl, mc = m < a.M ? m : a.M - 1;
+    const int64_t mc = tile_of(t, a.M, cl).mc;
     load_raw<D>(orr, a.o, D, mc, g);
     load_raw<D>(Qr, a.Q, D, mc, g);
   }
@@ -384,73 +580,20 @@ __global__ __launch_bounds__(NT) void block_out_kernel(OutArgs a) {
   RCPROF(1);
   for (; t < nt; t += G * NW) {
     asm volatile("" ::: "memory");
-    const int64_t m = t * TR + cl, mc = m < a.M ? m : a.M - 1;
-    const bool ok = m < a.M;
+    const Tile T = tile_of(t, a.M, cl);
     if (t != blockIdx.x + G * wave) {
-      load_raw<D>(orr, a.o, D, mc, g);
-      load_raw<D>(Qr, a.Q, D, mc, g);
+      load_raw<D>(orr, a.o, D, T.mc, g);
+      load_raw<D>(Qr, a.Q, D, T.mc, g);
     }
-    const bool keep = ok && a.ids[mc] != 0;
-    Act<D> acc;
-    Raw<D> r;
-    // x1 = Q + o Wo^T + bo
-    zero<D>(acc);
-    mm<D>(wl, orr, acc, lane);
+    Raw<D> zr, hr, xr;
+    fwd_out_a<D>(orr, Qr, T, wslot(smem, 0, WB), wslot(smem, 1, WB), lv, of, zr, hr, lane);
     RCPROF(2);
-#pragma unroll
-    for (int j = 0; j < Lay<D>::J; ++j) {
-      const f32x4 bb = vec4<D>(lv, j, g);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) acc.v[j][e] = acc.v[j][e] + bb[e] + (float)Qr.v[j >> 1][4 * (j & 1) + e];
-    }
-    round_act<D>(acc, r);
-    store_raw<D>(a.x1, D, m, ok, r, g);
-    RCPROF(3);
-    // z = LN2(x1)
-    float mu, rs;
-    ln_fwd<D>(acc, lv + D, lv + 2 * D, a.eps, g, mu, rs);
-    Raw<D> zr;
-    round_act<D>(acc, zr);
-    store_raw<D>(a.z, D, m, ok, zr, g);
-    if (ok && g == 0) {
-      a.mean[m] = mu;
-      a.rstd[m] = rs;
-    }
-    // h1 = relu(drop(z W1^T + b1))
-    zero<D>(acc);
-    mm<D>(wl + Lay<D>::WBYTES / 2, zr, acc, lane);
-#pragma unroll
-    for (int j = 0; j < Lay<D>::J; ++j) {
-      float dm[4] = {1.f, 1.f, 1.f, 1.f};
-      if (drop) drop4(a.drop_p, s1, m, D, j, g, dm);
-      const f32x4 bb = vec4<D>(lv + 3 * D, j, g);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) acc.v[j][e] = fmaxf(acc.v[j][e] + bb[e], 0.f) * dm[e];
-    }
-    round_act<D>(acc, r);
-    store_raw<D>(a.h1, D, m, ok, r, g);
-    // x' = (drop(h1 W2^T + b2) + z) * (ids != 0)
-    zero<D>(acc);
-    mm<D>(wl + Lay<D>::WBYTES, r, acc, lane);
-#pragma unroll
-    for (int j = 0; j < Lay<D>::J; ++j) {
-      float dm[4] = {1.f, 1.f, 1.f, 1.f};
-      if (drop) drop4(a.drop_p, s2, m, D, j, g, dm);
-      const f32x4 bb = vec4<D>(lv + 4 * D, j, g);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float v = __builtin_fmaf(acc.v[j][e] + bb[e], dm[e], (float)zr.v[j >> 1][4 * (j & 1) + e]);
-        acc.v[j][e] = keep ? v : 0.f;
-      }
-    }
-    round_act<D>(acc, r);
+    fwd_out_b<D>(hr, zr, T, wslot(smem, 2, WB), lv, of, xr, lane);
     RCPROF(4);
-    store_raw<D>(a.xn, D, m, ok, r, g);
   }
   RCPROF(5);
 }
 
-// ------------------------------------------------------------------ block output side, backward
 struct OutBwdArgs {
   int64_t M;
   const bf16* dxn; const int64_t* ids;
@@ -459,26 +602,29 @@ struct OutBwdArgs {
   bf16* dy2; bf16* da1; bf16* dx1; bf16* dout; float* part;
   float drop_p; uint64_t salt1, salt2; const uint64_t* seed_base;
 };
+__device__ __forceinline__ OutBwd out_bwd_of(const OutBwdArgs& a) {
+  const bool drop = a.drop_p > 0.f;
+  return OutBwd{a.dy2, a.da1, a.dx1, a.dout, a.ids, a.drop_p,
+                drop ? seed32(eff_seed(a.salt1, a.seed_base)) : 0u, drop ? seed32(eff_seed(a.salt2, a.seed_base)) : 0u};
+}
 
 // dzres = dxn*mask; dy2 = drop2(dzres) [saved]; da1 = relu'(h1)*drop1(dy2 W2) [saved]; dz = da1 W1 + dzres;
 // dx1 = LN2'(x1, dz) [saved, + affine partials]; dout = dx1 Wo
 template <int D>
 __global__ __launch_bounds__(NT) void block_out_bwd_kernel(OutBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  typedef Smem<D, 3, 1> L;
-  const bf16* wl = reinterpret_cast<const bf16*>(smem);
+  typedef Smem<D, 3, 1, 1> L;
+  constexpr int WB = Lay<D>::WBYTES;
   const float* lv = reinterpret_cast<const float*>(smem + L::W);   // ln_w
   float* red = reinterpret_cast<float*>(smem + L::V);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
             cl = lane & 15;
   const int64_t G = gridDim.x, nt = n_tiles(a.M);
-  const bool drop = a.drop_p > 0.f;
-  const uint32_t s1 = drop ? seed32(eff_seed(a.salt1, a.seed_base)) : 0u;
-  const uint32_t s2 = drop ? seed32(eff_seed(a.salt2, a.seed_base)) : 0u;
+  const OutBwd ob = out_bwd_of(a);
   int64_t t = blockIdx.x + G * wave;
   Raw<D> dr, hr;
   if (t < nt) {
-    const int64_t m = t * TR + cl, mc = m < a.M ? m : a.M - 1;
+    const int64_t mc = tile_of(t, a.M, cl).mc;
     load_raw<D>(dr, a.dxn, D, mc, g);
     load_raw<D>(hr, a.h1, D, mc, g);
   }
@@ -493,67 +639,21 @@ __global__ __launch_bounds__(NT) void block_out_bwd_kernel(OutBwdArgs a) {
   __syncthreads();
   for (; t < nt; t += G * NW) {
     asm volatile("" ::: "memory");
-    const int64_t m = t * TR + cl, mc = m < a.M ? m : a.M - 1;
-    const bool ok = m < a.M;
+    const Tile T = tile_of(t, a.M, cl);
     if (t != blockIdx.x + G * wave) {
-      load_raw<D>(dr, a.dxn, D, mc, g);
-      load_raw<D>(hr, a.h1, D, mc, g);
+      load_raw<D>(dr, a.dxn, D, T.mc, g);
+      load_raw<D>(hr, a.h1, D, T.mc, g);
     }
     Raw<D> xr;
-    load_raw<D>(xr, a.x1, D, mc, g);
-    const float mu = a.mean2[mc], rs = a.rstd2[mc];
-    const bool keep = ok && a.ids[mc] != 0;
-    Act<D> dz, acc;
-    Raw<D> r;
-    // dzres (kept in dz) and dy2
-#pragma unroll
-    for (int j = 0; j < Lay<D>::J; ++j) {
-      float dm[4] = {1.f, 1.f, 1.f, 1.f};
-      if (drop) drop4(a.drop_p, s2, m, D, j, g, dm);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        dz.v[j][e] = keep ? (float)dr.v[j >> 1][4 * (j & 1) + e] : 0.f;
-        acc.v[j][e] = dz.v[j][e] * dm[e];
-      }
-    }
-    round_act<D>(acc, r);
-    store_raw<D>(a.dy2, D, m, ok, r, g);
-    // da1 = relu'(h1) * drop1(dy2 W2)
-    zero<D>(acc);
-    mm<D>(wl, r, acc, lane);
-#pragma unroll
-    for (int j = 0; j < Lay<D>::J; ++j) {
-      float dm[4] = {1.f, 1.f, 1.f, 1.f};
-      if (drop) drop4(a.drop_p, s1, m, D, j, g, dm);
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        acc.v[j][e] = ((float)hr.v[j >> 1][4 * (j & 1) + e] > 0.f ? acc.v[j][e] : 0.f) * dm[e];
-    }
-    round_act<D>(acc, r);
-    store_raw<D>(a.da1, D, m, ok, r, g);
-    // dz = da1 W1 + dzres (rounded to bf16 as the stored tile)
-    mm<D>(wl + Lay<D>::WBYTES / 2, r, dz, lane);
-    round_act<D>(dz, r);
-    // dx1 = LN2'(x1, dz)
-    Act<D> xa, t1;
-    to_act<D>(xa, xr);
-    {
-      Act<D> pg, pb;
-      ln_bwd<D>(t1, xa, dz, ok, lv, mu, rs, g, pg, pb);
-      ln_accum<D>(red, pg, pb, lane, wave);
-    }
-    round_act<D>(t1, r);
-    store_raw<D>(a.dx1, D, m, ok, r, g);
-    // dout = dx1 Wo
-    zero<D>(acc);
-    mm<D>(wl + Lay<D>::WBYTES, r, acc, lane);
-    round_act<D>(acc, r);
-    store_raw<D>(a.dout, D, m, ok, r, g);
+    load_raw<D>(xr, a.x1, D, T.mc, g);
+    const float mu = a.mean2[T.mc], rs = a.rstd2[T.mc];
+    Raw<D> dzr, dar;
+    bwd_out_a<D>(dr, hr, T, wslot(smem, 0, WB), ob, dzr, dar, lane);
+    bwd_out_b<D>(dar, xr, dzr, T, mu, rs, wslot(smem, 1, WB), wslot(smem, 2, WB), lv, ob, red, lane, wave);
   }
   ln_partials<D>(red, a.part, tid);
 }
 
-// ------------------------------------------------------------------ block input side, backward
 struct InBwdArgs {
   int64_t M;
   const bf16* dq; const bf16* dkv; const bf16* dx1; const bf16* x;
@@ -566,8 +666,8 @@ struct InBwdArgs {
 template <int D>
 __global__ __launch_bounds__(NT) void block_in_bwd_kernel(InBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  typedef Smem<D, 3, 1> L;
-  const bf16* wl = reinterpret_cast<const bf16*>(smem);
+  typedef Smem<D, 3, 1, 1> L;
+  constexpr int WB = Lay<D>::WBYTES;
   const float* lv = reinterpret_cast<const float*>(smem + L::W);   // ln_w
   float* red = reinterpret_cast<float*>(smem + L::V);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
@@ -576,7 +676,7 @@ __global__ __launch_bounds__(NT) void block_in_bwd_kernel(InBwdArgs a) {
   int64_t t = blockIdx.x + G * wave;
   Raw<D> kr, vr;
   if (t < nt) {
-    const int64_t m = t * TR + cl, mc = m < a.M ? m : a.M - 1;
+    const int64_t mc = tile_of(t, a.M, cl).mc;
     load_raw<D>(kr, a.dkv, 2 * D, mc, g);
     load_raw<D>(vr, a.dkv + D, 2 * D, mc, g);
   }
@@ -591,37 +691,20 @@ __global__ __launch_bounds__(NT) void block_in_bwd_kernel(InBwdArgs a) {
   __syncthreads();
   for (; t < nt; t += G * NW) {
     asm volatile("" ::: "memory");
-    const int64_t m = t * TR + cl, mc = m < a.M ? m : a.M - 1;
-    const bool ok = m < a.M;
+    const Tile T = tile_of(t, a.M, cl);
     if (t != blockIdx.x + G * wave) {
-      load_raw<D>(kr, a.dkv, 2 * D, mc, g);
-      load_raw<D>(vr, a.dkv + D, 2 * D, mc, g);
+      load_raw<D>(kr, a.dkv, 2 * D, T.mc, g);
+      load_raw<D>(vr, a.dkv + D, 2 * D, T.mc, g);
     }
-    Raw<D> qr, rr, xr;
-    load_raw<D>(qr, a.dq, D, mc, g);
-    load_raw<D>(rr, a.dx1, D, mc, g);
-    load_raw<D>(xr, a.x, D, mc, g);
-    const float mu = a.mean1[mc], rs = a.rstd1[mc];
-    Act<D> dxkv, dQ;
-    Raw<D> r;
-    zero<D>(dxkv);
-    mm<D>(wl, kr, dxkv, lane);
-    mm<D>(wl + Lay<D>::WBYTES / 2, vr, dxkv, lane);
-    round_act<D>(dxkv, r);
-    to_act<D>(dQ, rr);
-    mm<D>(wl + Lay<D>::WBYTES, qr, dQ, lane);
-    round_act<D>(dQ, r);
-    Act<D> xa, t1;
-    to_act<D>(xa, xr);
-    {
-      Act<D> pg, pb;
-      ln_bwd<D>(t1, xa, dQ, ok, lv, mu, rs, g, pg, pb);
-      ln_accum<D>(red, pg, pb, lane, wave);
-    }
-#pragma unroll
-    for (int j = 0; j < Lay<D>::J; ++j) t1.v[j] += dxkv.v[j];
-    round_act<D>(t1, r);
-    store_raw<D>(a.dx, D, m, ok, r, g);
+    Raw<D> qr, rr, xr, dxr;
+    load_raw<D>(qr, a.dq, D, T.mc, g);
+    load_raw<D>(rr, a.dx1, D, T.mc, g);
+    load_raw<D>(xr, a.x, D, T.mc, g);
+    const float mu = a.mean1[T.mc], rs = a.rstd1[T.mc];
+    Raw<D> dxkv;
+    bwd_in_a<D>(kr, vr, wslot(smem, 0, WB), wslot(smem, 1, WB), dxkv, lane);
+    bwd_in_b<D>(qr, rr, xr, dxkv, T, mu, rs, wslot(smem, 2, WB), lv, red, dxr, lane, wave);
+    store_raw<D>(a.dx, D, T.m, T.ok, dxr, g);
   }
   ln_partials<D>(red, a.part, tid);
 }
@@ -640,8 +723,8 @@ static int64_t grid_for(int64_t M) {
   const int64_t nt = (M + TR - 1) / TR;
   return nt < g_ncu ? nt : g_ncu;
 }
-template <int D> static size_t lds_fwd() { return Smem<D, 3, 5>::V; }
-template <int D> static size_t lds_bwd() { return Smem<D, 3, 1>::BYTES; }
+template <int D> static size_t lds_fwd() { return Smem<D, 3, 5, 0>::BYTES; }
+template <int D> static size_t lds_bwd() { return Smem<D, 3, 1, 1>::BYTES; }
 
 template <typename K>
 static void set_lds(K kern, size_t bytes) {

@@ -212,29 +212,19 @@ class SASEngine:
             # issued after the first forward launch: in the captured graph the forward chain is then the
             # first child of the step's root and keeps the launch queue; the side branch gets the second
             s["side"] = self._side_prologue(ids, pos, neg, after=fork)
-        for i in range(L):
-            pre = f"attention_layers.{i}."
-            Q, mu1, r1 = e("Q", (M, d)), e("mu", (M,), torch.float32), e("r", (M,), torch.float32)
-            Win, bin_ = self.W(pre + "in_proj_weight"), self.Wf(pre + "in_proj_bias")
-            q, kv = e("q", (M, d)), e("kv", (M, 2 * d))
-            o, lse = e("o", (M, d)), e("lse", (B * H * T,), torch.float32)
-            x1 = e("x1", (M, d))
-            z, mu2, r2 = e("z", (M, d)), e("mu", (M,), torch.float32), e("r", (M,), torch.float32)
-            fw = f"forward_layers.{i}."
-            h1, xn = e("h1", (M, d)), e("x", (M, d))
-            if fused:
-                # one row-block kernel on each side of the attention core (rowfused.hip)
-                ops.sas_block_in(x, self.Wf(f"attention_layernorms.{i}.weight"),
-                                 self.Wf(f"attention_layernorms.{i}.bias"), LN_EPS, Q, mu1, r1, Win[:d], bin_[:d], q,
-                                 Win[d:], bin_[d:], kv)
-                ops.attn_fwd(B, T, H, Dh, q, kv[:, :d], kv[:, d:], o, lse, 1.0 / math.sqrt(Dh), 0, ids, p,
-                             self.salt[f"attn{i}"], sb)
-                ops.sas_block_out(o, Q, self.W(pre + "out_proj.weight"), self.Wf(pre + "out_proj.bias"), x1,
-                                  self.Wf(f"forward_layernorms.{i}.weight"), self.Wf(f"forward_layernorms.{i}.bias"),
-                                  LN_EPS, z, mu2, r2, self.W(fw + "conv1.weight"), self.Wf(fw + "conv1.bias"), h1,
-                                  self.W(fw + "conv2.weight"), self.Wf(fw + "conv2.bias"), xn, ids, p,
-                                  self.salt[f"ffn1_{i}"], self.salt[f"ffn2_{i}"], sb)
-            else:
+        if fused:
+            x = self._forward_blocks_fused(s, x)
+        else:
+            for i in range(L):
+                pre = f"attention_layers.{i}."
+                Q, mu1, r1 = e("Q", (M, d)), e("mu", (M,), torch.float32), e("r", (M,), torch.float32)
+                Win, bin_ = self.W(pre + "in_proj_weight"), self.Wf(pre + "in_proj_bias")
+                q, kv = e("q", (M, d)), e("kv", (M, 2 * d))
+                o, lse = e("o", (M, d)), e("lse", (B * H * T,), torch.float32)
+                x1 = e("x1", (M, d))
+                z, mu2, r2 = e("z", (M, d)), e("mu", (M,), torch.float32), e("r", (M,), torch.float32)
+                fw = f"forward_layers.{i}."
+                h1, xn = e("h1", (M, d)), e("x", (M, d))
                 ops.layernorm_fwd(x, self.Wf(f"attention_layernorms.{i}.weight"),
                                   self.Wf(f"attention_layernorms.{i}.bias"), LN_EPS, Q, mu1, r1, 0)
                 ops.linear_fwd(Q, Win[:d], q, bias=bin_[:d])
@@ -249,10 +239,10 @@ class SASEngine:
                 ops.linear_fwd(h1, self.W(fw + "conv2.weight").view(d, d), xn, bias=self.Wf(fw + "conv2.bias"),
                                drop_p=p, drop_seed=self.salt[f"ffn2_{i}"], seed_base=sb, drop_ld=d, resid=z,
                                rowmask_ids=ids)
-            for k_, v_ in (("x", x), ("Q", Q), ("mu1", mu1), ("r1", r1), ("q", q), ("kv", kv), ("o", o),
-                           ("lse", lse), ("x1", x1), ("z", z), ("mu2", mu2), ("r2", r2), ("h1", h1)):
-                s[k_].append(v_)
-            x = xn
+                for k_, v_ in (("x", x), ("Q", Q), ("mu1", mu1), ("r1", r1), ("q", q), ("kv", kv), ("o", o),
+                               ("lse", lse), ("x1", x1), ("z", z), ("mu2", mu2), ("r2", r2), ("h1", h1)):
+                    s[k_].append(v_)
+                x = xn
         f, muf, rf = e("f", (M, d)), e("mu", (M,), torch.float32), e("r", (M,), torch.float32)
         s.update(xL=x, f=f, muf=muf, rf=rf)
         if fused and need_logits:
@@ -269,6 +259,53 @@ class SASEngine:
         pl, nl = e("pl", (B, T), torch.float32), e("nl", (B, T), torch.float32)
         ops.sampled_logits_fwd(f, self.W("item_emb.weight"), pos, neg, pl, nl)
         return pl, nl, s
+
+    def _forward_blocks_fused(self, s, x):
+        """SAS blocks' forward with the row-chain kernels (rowchain.hip) on each side of the attention core
+        (rs_sas_block_in, rs_attn_fwd, rs_sas_block_out per block).  Fills s's per-block saved tensors; returns the
+        last block's output."""
+        B, T, p, ids, sb = s["B"], s["T"], s["p"], s["ids"], s["sb"]
+        M, d, H, Dh, L = B * T, self.d, self.H, self.Dh, self.L
+        e = self._buf
+        f32 = torch.float32
+        lay = [dict(Q=e("Q", (M, d)), mu1=e("mu", (M,), f32), r1=e("r", (M,), f32), q=e("q", (M, d)),
+                    kv=e("kv", (M, 2 * d)), o=e("o", (M, d)), lse=e("lse", (B * H * T,), f32), x1=e("x1", (M, d)),
+                    z=e("z", (M, d)), mu2=e("mu", (M,), f32), r2=e("r", (M,), f32), h1=e("h1", (M, d)),
+                    xn=e("x", (M, d))) for _ in range(L)]
+
+        def in_args(i):
+            pre = f"attention_layers.{i}."
+            Win, bin_ = self.W(pre + "in_proj_weight"), self.Wf(pre + "in_proj_bias")
+            b = lay[i]
+            return (self.Wf(f"attention_layernorms.{i}.weight"), self.Wf(f"attention_layernorms.{i}.bias"),
+                    b["Q"], b["mu1"], b["r1"], Win[:d], bin_[:d], b["q"], Win[d:], bin_[d:], b["kv"])
+
+        def out_args(i):
+            pre, fw, b = f"attention_layers.{i}.", f"forward_layers.{i}.", lay[i]
+            return (b["o"], b["Q"], self.W(pre + "out_proj.weight"), self.Wf(pre + "out_proj.bias"), b["x1"],
+                    self.Wf(f"forward_layernorms.{i}.weight"), self.Wf(f"forward_layernorms.{i}.bias"), LN_EPS,
+                    b["z"], b["mu2"], b["r2"], self.W(fw + "conv1.weight"), self.Wf(fw + "conv1.bias"), b["h1"],
+                    self.W(fw + "conv2.weight"), self.Wf(fw + "conv2.bias"), b["xn"], ids, p,
+                    self.salt[f"ffn1_{i}"], self.salt[f"ffn2_{i}"], sb)
+
+        ln_w, ln_b, Q, mu1, r1, Wq, bq, q, Wkv, bkv, kv = in_args(0)
+        ops.sas_block_in(x, ln_w, ln_b, LN_EPS, Q, mu1, r1, Wq, bq, q, Wkv, bkv, kv)
+        xs = [x]
+        for i in range(L):
+            b = lay[i]
+            ops.attn_fwd(B, T, H, Dh, b["q"], b["kv"][:, :d], b["kv"][:, d:], b["o"], b["lse"], 1.0 / math.sqrt(Dh),
+                         0, ids, p, self.salt[f"attn{i}"], sb)
+            ops.sas_block_out(*out_args(i))
+            if i + 1 < L:
+                ln_w, ln_b, Q, mu1, r1, Wq, bq, q, Wkv, bkv, kv = in_args(i + 1)
+                ops.sas_block_in(b["xn"], ln_w, ln_b, LN_EPS, Q, mu1, r1, Wq, bq, q, Wkv, bkv, kv)
+            xs.append(b["xn"])
+        for i in range(L):
+            b = lay[i]
+            for k_ in ("Q", "mu1", "r1", "q", "kv", "o", "lse", "x1", "z", "mu2", "r2", "h1"):
+                s[k_].append(b[k_])
+            s["x"].append(xs[i])
+        return xs[L]
 
     @property
     def fused_head(self):
@@ -447,53 +484,42 @@ class SASEngine:
         lnp = self.ws.get("lnp", (L, 2, 2 * d * nb), torch.float32)
         wat = self.ws.get("attn", (B * H * T,), torch.float32)
         probs, segs = [], list(extra_segs)
-        # opt-in (RS_SAS_WGRAD_SIDE=1): the upper blocks' weight gradients on the side stream while the lower
-        # blocks' backward proceeds.  Measured slower at cfg2 (0.385 -> 0.410 ms: the attention backward loses
-        # CUs to the grouped GEMM), neutral at cfg3, so off by default
-        early = tail is not None and L > 1 and os.environ.get("RS_SAS_WGRAD_SIDE", "0") == "1"
-        keep, rows1 = [], self._wgrad_rows(M, 6)
+        # per block: the out-side backward's outputs (dy2, da1, dx1, do) and the attention backward's (dq, dkv)
+        g = [dict(dy2=e("dy2", (M, d)), da1=e("da1", (M, d)), dx1=e("dx1", (M, d)), do=e("do", (M, d)),
+                  dq=e("dq", (M, d)), dkv=e("dkv", (M, 2 * d))) for _ in range(L)]
+
+        def out_bwd_args(i):
+            return (ids, s["h1"][i], s["x1"][i], s["mu2"][i], s["r2"][i], self.Wf(f"forward_layernorms.{i}.weight"),
+                    wT[i, 5], wT[i, 4], wT[i, 3], g[i]["dy2"], g[i]["da1"], g[i]["dx1"], g[i]["do"], lnp[i, 0], p,
+                    self.salt[f"ffn1_{i}"], self.salt[f"ffn2_{i}"], sb)
+
+        def in_bwd_args(i):
+            return (g[i]["dq"], g[i]["dkv"], g[i]["dx1"], s["x"][i], s["mu1"][i], s["r1"][i],
+                    self.Wf(f"attention_layernorms.{i}.weight"), wT[i, 0:3].reshape(d, 3 * d))
+
+        ops.sas_block_out_bwd(dx, *out_bwd_args(L - 1))
         for i in reversed(range(L)):
             pre, fw = f"attention_layers.{i}.", f"forward_layers.{i}."
-            inT = wT[i, 0:3].reshape(d, 3 * d)
-            dy2, da1, dx1, do = e("dy2", (M, d)), e("da1", (M, d)), e("dx1", (M, d)), e("do", (M, d))
-            ops.sas_block_out_bwd(dx, ids, s["h1"][i], s["x1"][i], s["mu2"][i], s["r2"][i],
-                                  self.Wf(f"forward_layernorms.{i}.weight"), wT[i, 5], wT[i, 4], wT[i, 3],
-                                  dy2, da1, dx1, do, lnp[i, 0], p, self.salt[f"ffn1_{i}"], self.salt[f"ffn2_{i}"], sb)
-            dq, dkv = e("dq", (M, d)), e("dkv", (M, 2 * d))
-            kv = s["kv"][i]
-            ops.attn_bwd(B, T, H, Dh, s["q"][i], kv[:, :d], kv[:, d:], s["o"][i], do, s["lse"][i], dq,
+            dq, dkv, kv = g[i]["dq"], g[i]["dkv"], s["kv"][i]
+            ops.attn_bwd(B, T, H, Dh, s["q"][i], kv[:, :d], kv[:, d:], s["o"][i], g[i]["do"], s["lse"][i], dq,
                          dkv[:, :d], dkv[:, d:], 1.0 / math.sqrt(Dh), 0, ids, p, self.salt[f"attn{i}"], sb, wat)
             dxi = e("dxi", (M, d))
-            ops.sas_block_in_bwd(dq, dkv, dx1, s["x"][i], s["mu1"][i], s["r1"][i],
-                                 self.Wf(f"attention_layernorms.{i}.weight"), inT, dxi, lnp[i, 1])
+            ops.sas_block_in_bwd(*in_bwd_args(i), dxi, lnp[i, 1])
+            if i > 0:
+                ops.sas_block_out_bwd(dxi, *out_bwd_args(i - 1))
+            dx = dxi
             Gin, Gb = G(pre + "in_proj_weight"), G(pre + "in_proj_bias")
-            probs += [(dy2, s["h1"][i], G(fw + "conv2.weight"), G(fw + "conv2.bias")),
-                      (da1, s["z"][i], G(fw + "conv1.weight"), G(fw + "conv1.bias")),
-                      (dx1, s["o"][i], G(pre + "out_proj.weight"), G(pre + "out_proj.bias")),
+            probs += [(g[i]["dy2"], s["h1"][i], G(fw + "conv2.weight"), G(fw + "conv2.bias")),
+                      (g[i]["da1"], s["z"][i], G(fw + "conv1.weight"), G(fw + "conv1.bias")),
+                      (g[i]["dx1"], s["o"][i], G(pre + "out_proj.weight"), G(pre + "out_proj.bias")),
                       (dq, s["Q"][i], Gin[:d], Gb[:d]),
                       (dkv, s["x"][i], Gin[d:], Gb[d:])]
             segs += ops.ln_partial_segments(lnp[i, 0], M, d, G(f"forward_layernorms.{i}.weight"),
                                             G(f"forward_layernorms.{i}.bias"))
             segs += ops.ln_partial_segments(lnp[i, 1], M, d, G(f"attention_layernorms.{i}.weight"),
                                             G(f"attention_layernorms.{i}.bias"))
-            dx = dxi
-            if early and i > 0:
-                # this block's five problems + its two LayerNorm partial sets, on the side stream
-                lseg = segs[-4:]
-                del segs[-4:]
-                ws1 = self.ws.get("wslab_side", (ops.wgrad_grouped_slab_numel([(d, d)] * 4 + [(2 * d, d)], M, rows1),),
-                                  torch.float32)
-                fork = torch.cuda.Event()
-                fork.record(torch.cuda.current_stream())
-                self._side.wait_event(fork)
-                with torch.cuda.stream(self._side):
-                    ops.wgrad_grouped(probs[-5:], M, rows1, ws1, extra=lseg)
-                keep.append(probs[-5:])
-                del probs[-5:]
-        nt = 6 * (1 if early else L)
-        rows = self._wgrad_rows(M, nt)
-        nl = 1 if early else L
-        wslab = self.ws.get("wslab", (ops.wgrad_grouped_slab_numel([(d, d)] * 4 * nl + [(2 * d, d)] * nl, M, rows),),
+        rows = self._wgrad_rows(M, 6 * L)
+        wslab = self.ws.get("wslab", (ops.wgrad_grouped_slab_numel([(d, d)] * 4 * L + [(2 * d, d)] * L, M, rows),),
                             torch.float32)
         join, fork = None, None
         if tail is not None:

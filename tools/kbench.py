@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--drop", type=float, default=0.2, help="dropout rate of the dropout-carrying ops")
     ap.add_argument("--only", default="", help="time only the ops whose name contains one of these |-separated strings")
     a = ap.parse_args()
     c = SHAPES[a.config]
@@ -112,12 +113,12 @@ def main():
     lse = torch.empty(B * H * T, device=dev)
     aflops = 2.0 * T * (T + 1) * Dh * B * H
     run("attn_fwd causal drop",lambda: ops.attn_fwd(B, T, H, Dh, q, kv[:, :d], kv[:, d:], o, lse,
-                                                            1 / math.sqrt(Dh), 0, ids, 0.2, 9, sb),
+                                                            1 / math.sqrt(Dh), 0, ids, a.drop, 9, sb),
         4 * mb, aflops)
     dq, dkv = rn(M, d), rn(M, 2 * d)
     wat = torch.empty(B * H * T, device=dev)
     run("attn_bwd causal drop",lambda: ops.attn_bwd(B, T, H, Dh, q, kv[:, :d], kv[:, d:], o, y, lse, dq,
-                                                            dkv[:, :d], dkv[:, d:], 1 / math.sqrt(Dh), 0, ids, 0.2,
+                                                            dkv[:, :d], dkv[:, d:], 1 / math.sqrt(Dh), 0, ids, a.drop,
                                                             9, sb, wat), 8 * mb, 2.5 * aflops)
     if a.config in ("cfg3", "cfg5"):
         # BERT block GEMMs with their fused epilogues (bert.py encode / encode_backward)
@@ -171,12 +172,12 @@ def main():
         run("fused block_in", lambda: ops.sas_block_in(x, gam, bet, 1e-8, Q, m1_, r1_, Win[:d], bin_[:d], qq, Win[d:],
                                                         bin_[d:], kvb), 6 * mb)
         run("fused block_out", lambda: ops.sas_block_out(oo, Q, W, bias, x1, gam, bet, 1e-8, zz, m1_, r1_, W, bias, h1,
-                                                          W, bias, xn, ids, 0.2, 3, 4, sb), 6 * mb)
+                                                          W, bias, xn, ids, a.drop, 3, 4, sb), 6 * mb)
         WT, WinT = rn(d, d), rn(d, 3 * d)
         dy2, da1, dx1, do_ = rn(M, d), rn(M, d), rn(M, d), rn(M, d)
         part = torch.empty(2 * d * max(-(-M // 64), ops.sas_block_parts(M)), device=dev)
         run("fused block_out_bwd", lambda: ops.sas_block_out_bwd(y, ids, h1, x1, m1_, r1_, gam, WT, WT, WT, dy2, da1,
-                                                                  dx1, do_, part, 0.2, 3, 4, sb), 8 * mb)
+                                                                  dx1, do_, part, a.drop, 3, 4, sb), 8 * mb)
         dqkv = rn(M, 2 * d)
         run("fused block_in_bwd", lambda: ops.sas_block_in_bwd(qq, dqkv, dx1, x, m1_, r1_, gam, WinT, z, part),
             6 * mb)

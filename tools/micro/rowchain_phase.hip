@@ -31,7 +31,7 @@ int main(int argc, char** argv) {
   hipMemset(b, 0, d * 4); hipMemset(lw, 0, d * 4); hipMemset(lb, 0, d * 4); hipMemset(ids, 1, M * 8);
   hipMemset(sb, 0, 8);
   const __bf16* Wb = (const __bf16*)W;
-  std::vector<unsigned long long> p(4096 * 8 * 8);
+  std::vector<unsigned long long> p(4096 * 8 * 16);
   hipEvent_t e0, e1;
   hipEventCreate(&e0); hipEventCreate(&e1);
   float ms = 0.f;
@@ -49,17 +49,17 @@ int main(int argc, char** argv) {
   unsigned long long t0 = ~0ull, t1 = 0;
   for (int b_ = 0; b_ < G; ++b_)
     for (int w = 0; w < 8; ++w) {
-      const unsigned long long* x = &p[((size_t)b_ * 8 + w) * 8];
+      const unsigned long long* x = &p[((size_t)b_ * 8 + w) * 16];
       if (x[0]) t0 = std::min(t0, x[0]);
       if (x[5]) t1 = std::max(t1, x[5]);
     }
   const double u = 0.01;   // 100 MHz ticks -> us
   printf("block_out M=%lld grid=%d: event %.2f us, first entry -> last exit %.2f us\n", (long long)M, G, ms * 1e3,
          (t1 - t0) * u);
-  std::vector<double> ent, stg, g1, x1s, rest, ex, tot;
+  std::vector<double> ent, stg, g1, x1s, rest, ex, tot, ln2, mm1, ep1, mm2;
   for (int b_ = 0; b_ < G; ++b_)
     for (int w = 0; w < 8; ++w) {
-      const unsigned long long* x = &p[((size_t)b_ * 8 + w) * 8];
+      const unsigned long long* x = &p[((size_t)b_ * 8 + w) * 16];
       if (!x[0]) continue;
       ent.push_back((x[0] - t0) * u);
       stg.push_back((x[1] - x[0]) * u);
@@ -67,6 +67,10 @@ int main(int argc, char** argv) {
         g1.push_back((x[2] - x[1]) * u);
         x1s.push_back((x[3] - x[2]) * u);
         rest.push_back((x[4] - x[3]) * u);
+        ln2.push_back((x[6] - x[3]) * u);
+        mm1.push_back((x[7] - x[6]) * u);
+        ep1.push_back((x[8] - x[7]) * u);
+        mm2.push_back((x[9] - x[8]) * u);
       }
       ex.push_back((x[5] - t0) * u);
       tot.push_back((x[5] - x[0]) * u);
@@ -76,6 +80,10 @@ int main(int argc, char** argv) {
   pct("inputs + first GEMM", g1);
   pct("x1 epilogue + store", x1s);
   pct("LN2 + FFN (2 GEMMs)", rest);
+  pct(" .. LN2 + z store", ln2);
+  pct(" .. GEMM W1", mm1);
+  pct(" .. h1 epilogue + store", ep1);
+  pct(" .. GEMM W2", mm2);
   pct("exit after first entry", ex);
   pct("wave lifetime", tot);
   return 0;
