@@ -334,6 +334,20 @@ int rs_sas_block_out(int64_t M, int64_t d, const void* o, const void* Q, const v
                      const int64_t* ids, float drop_p, uint64_t salt1, uint64_t salt2, const uint64_t* seed_base,
                      void* stream);
 
+/* Union-of-touched-rows exchange of an embedding-table gradient (sparse_rows.hip; data parallel,
+ * replaces the dense all-reduce of the token / item table gradient -- the reference has no
+ * multi-GPU path, BS/trainers/base.py:32-34).  rs_touched_rows: flags[v] = (v occurs in ids[0..n)),
+ * index[v] = rank of v among flagged rows (ascending) or -1, *count = flagged rows; flags/index int32[rows],
+ * ws int32[rs_touched_rows_ws_numel(rows)].  rs_rows_pack: compact[index[v]][:] = src[v][:] for flagged v,
+ * compact rows [*count, cap) zeroed (cap >= *count).  rs_rows_unpack: dst[v][:] = compact[index[v]][:].
+ * fp32 rows of d (d % 4 == 0, 16-B aligned). */
+int64_t rs_touched_rows_ws_numel(int64_t rows);
+int rs_touched_rows(const int64_t* ids, int64_t n, int64_t rows, int32_t* flags, int32_t* index, int32_t* count,
+                    int32_t* ws, void* stream);
+int rs_rows_pack(const float* src, int64_t rows, int64_t d, const int32_t* index, const int32_t* count,
+                 float* compact, int64_t cap, void* stream);
+int rs_rows_unpack(float* dst, int64_t rows, int64_t d, const int32_t* index, const float* compact, void* stream);
+
 /* Number of LayerNorm affine partial sets the two backward kernels below write for M token rows
  * (one per workgroup). */
 int64_t rs_sas_block_parts(int64_t M);

@@ -84,6 +84,10 @@ SIGNATURES = {
     "rs_vocab_shard_combine": [i32, i64, vp, vp, vp, vp, vp, vp],
     "rs_seed_advance": [vp, vp],
     "rs_sas_block_parts": [i64],
+    "rs_touched_rows_ws_numel": [i64],
+    "rs_touched_rows": [vp, i64, i64, vp, vp, vp, vp, vp],
+    "rs_rows_pack": [vp, i64, i64, vp, vp, vp, i64, vp],
+    "rs_rows_unpack": [vp, i64, i64, vp, vp, vp],
     "rs_sas_block_in": [i64, i64, vp, i64, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "rs_sas_block_out": [i64, i64, vp, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32,
                          u64, u64, vp, vp],
@@ -115,7 +119,8 @@ SIGNATURES = {
     "rs_abi_version": [],
 }
 
-RESTYPES = {"rs_wgrad_grouped_slab_numel": C.c_int64, "rs_sas_block_parts": C.c_int64, "rs_item_index_ws_bytes": C.c_int64,
+RESTYPES = {"rs_wgrad_grouped_slab_numel": C.c_int64, "rs_sas_block_parts": C.c_int64,
+            "rs_touched_rows_ws_numel": C.c_int64, "rs_item_index_ws_bytes": C.c_int64,
             "rs_vocab_ce_ws_numel": C.c_int64}
 
 _lib = None

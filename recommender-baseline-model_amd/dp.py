@@ -18,7 +18,17 @@ bucket's all-reduce (async, on the backend's stream, ordered after the work alre
 current stream) as soon as it is final, so it overlaps the rest of the backward; finish() makes the
 current stream wait for all of them before the optimizer.
 
-These helpers only move tensors; they work for any device / backend (gloo on CPU in the tests).
+Large embedding tables (SparseRowExchange): a step touches few rows of a 1M-row token table,
+and the others' gradients are zero on every rank.  The ranks all-gather their batch ids, build the same sorted
+union of touched rows on the device (rs_touched_rows: no host sync, graph-capturable), pack those rows of the
+table gradient into a fixed-capacity compact buffer (capacity = gathered id count, at most the table), all-reduce
+that instead of the dense table, and unpack it.  Rows outside the union stay zero, as the dense all-reduce leaves
+them; every element is summed over the same ranks (two ranks: bit for bit the dense result).  Bytes per rank at
+cfg5 on 8 GPUs (1,000,002 x 256 fp32 table, 12,800 token ids per rank): 1,024 MB dense -> at most 102,400 rows x
+1 KB = 105 MB + 0.8 MB of ids.
+
+The bucket helpers only move tensors (gloo on CPU in the tests); SparseRowExchange's index/pack kernels need the
+HIP library.
 """
 import torch
 import torch.distributed as dist
@@ -58,12 +68,13 @@ class BucketedExchange:
     NCCL/RCCL: no host block) and checks that every bucket went out exactly once."""
 
     def __init__(self, flat_grad, buckets, group=None, partial=False):
-        """partial: the buckets may leave parts of the buffer out (rank-owned regions, e.g. a vocabulary shard);
-        else they must cover it."""
+        """buckets: {tag: (lo, hi) or [(lo, hi), ...]}.  partial: the buckets may leave parts of the buffer out
+        (rank-owned regions, e.g. a vocabulary shard, or a table exchanged by SparseRowExchange); else they must
+        cover it."""
         self.flat_grad = flat_grad
-        self.buckets = dict(buckets)
+        self.buckets = {t: ([r] if isinstance(r, tuple) else list(r)) for t, r in dict(buckets).items()}
         self.group = group
-        spans = sorted(self.buckets.values())
+        spans = sorted(x for rs in self.buckets.values() for x in rs)
         assert all(a[1] <= b[0] for a, b in zip(spans, spans[1:])), "buckets must be disjoint"
         assert all(0 <= lo < hi <= flat_grad.numel() for lo, hi in spans), "bucket out of the buffer"
         if not partial:
@@ -73,9 +84,9 @@ class BucketedExchange:
         self.sent = []
 
     def launch(self, tag):
-        lo, hi = self.buckets[tag]
         self.sent.append(tag)
-        self.works.append(dist.all_reduce(self.flat_grad[lo:hi], group=self.group, async_op=True))
+        for lo, hi in self.buckets[tag]:
+            self.works.append(dist.all_reduce(self.flat_grad[lo:hi], group=self.group, async_op=True))
 
     def finish(self):
         assert sorted(self.sent) == sorted(self.buckets), (self.sent, list(self.buckets))
@@ -83,3 +94,75 @@ class BucketedExchange:
             w.wait()
         self.works, self.sent = [], []
         return self.flat_grad
+
+
+def carve(buckets, lo, hi):
+    """The buckets {tag: (lo, hi) | [ranges]} with [lo, hi) removed from every range (a region exchanged another
+    way); tags left with no range are dropped."""
+    out = {}
+    for tag, rs in buckets.items():
+        rs = [rs] if isinstance(rs, tuple) else list(rs)
+        keep = []
+        for a, b in rs:
+            if b <= lo or a >= hi:
+                keep.append((a, b))
+                continue
+            if a < lo:
+                keep.append((a, lo))
+            if b > hi:
+                keep.append((hi, b))
+        if keep:
+            out[tag] = keep
+    return out
+
+
+class SparseRowExchange:
+    """Union-of-touched-rows all-reduce of one embedding table's gradient (see the module docstring).
+
+    grad_rows: the table's fp32 gradient rows [rows, d] (a view into the flat gradient buffer); n_local: ids per
+    rank per step.  Per step: gather_ids(ids) (collective) -> index_rows() -> [table gradient complete] ->
+    pack() -> allreduce() (collective) -> unpack().  Collectives run on the current stream's order (eager, between
+    graph segments); the kernels are graph-capturable."""
+
+    def __init__(self, grad_rows, n_local, group=None):
+        from . import ops
+        self.ops = ops
+        self.g = grad_rows
+        self.rows, self.d = grad_rows.shape
+        self.W = world()
+        self.n_local = int(n_local)
+        self.group = group
+        self.cap = min(self.rows, self.W * self.n_local)
+        dev = grad_rows.device
+        self.ids_all = torch.zeros(self.W * self.n_local, dtype=torch.int64, device=dev)
+        self.flags = torch.zeros(self.rows, dtype=torch.int32, device=dev)
+        self.index = torch.zeros(self.rows, dtype=torch.int32, device=dev)
+        self.count = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.ws = torch.zeros(ops.touched_rows_ws_numel(self.rows), dtype=torch.int32, device=dev)
+        self.compact = torch.zeros(self.cap, self.d, dtype=torch.float32, device=dev)
+
+    @staticmethod
+    def worthwhile(rows, n_local, n_ranks):
+        """Sparse when the compact buffer is at most half the dense table."""
+        return n_ranks > 1 and n_ranks * n_local <= rows // 2
+
+    def bytes_per_step(self):
+        """(dense all-reduce bytes, sparse all-reduce + all-gather bytes) of this table."""
+        return self.rows * self.d * 4, self.cap * self.d * 4 + self.W * self.n_local * 8
+
+    def gather_ids(self, ids):
+        flat = ids.reshape(-1)
+        assert flat.numel() == self.n_local, (flat.numel(), self.n_local)
+        dist.all_gather(list(self.ids_all.view(self.W, self.n_local).unbind(0)), flat, group=self.group)
+
+    def index_rows(self):
+        self.ops.touched_rows(self.ids_all, self.rows, self.flags, self.index, self.count, self.ws)
+
+    def pack(self):
+        self.ops.rows_pack(self.g, self.index, self.count, self.compact)
+
+    def allreduce(self):
+        dist.all_reduce(self.compact, group=self.group)
+
+    def unpack(self):
+        self.ops.rows_unpack(self.g, self.index, self.compact)

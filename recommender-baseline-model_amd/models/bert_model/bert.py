@@ -328,6 +328,13 @@ class BERTEngine:
         else:
             ops.embed_bwd(1, ids, T, dx, 1.0, hp, self.salt["emb"], sb, G("bert.embedding.token.weight"),
                           G("bert.embedding.position.pe.weight"))
+        ex, sp = getattr(self, "sparse_tok", None), getattr(self, "_split", None)
+        if ex is not None and sp is not None:
+            # data parallel, union-of-touched-rows exchange of the token table's gradient (dp.SparseRowExchange):
+            # its all-reduce runs beside the grouped weight-gradient launches below
+            ex.pack()
+            sp("tok_rows", ex.allreduce)
+            ex.unpack()
         for c in range(0, len(probs), 16):              # rs_wgrad_grouped takes up to 16 problems
             chunk = probs[c:c + 16]
             shapes = [(p[0].shape[1], p[1].shape[1]) for p in chunk]
@@ -389,7 +396,14 @@ class BERTEngine:
     # ---- fused training loss (labelled rows only) -------------------------------------
     def train_loss_and_backward(self, tokens, labels, loss_out, global_count, grad, max_labelled=None, split=None):
         """Forward + CE(ignore_index=0) + backward of one batch.  loss_out[0] = loss sum, [1] = local
-        labelled count, [2] = local mean; ``global_count(local)`` returns the divisor (DP)."""
+        labelled count, [2] = local mean; ``global_count(local)`` returns the divisor (DP).
+        split(tag, action): data-parallel segment points (train_step.FusedTrainStep); with a sparse token-table
+        exchange (self.sparse_tok) the step starts with the all-gather of the batch ids."""
+        ex = getattr(self, "sparse_tok", None)
+        self._split = split
+        if ex is not None and split is not None:
+            split("tok_ids", lambda: ex.gather_ids(tokens))
+            ex.index_rows()
         side = self._token_index(tokens) if self._det_table() else None
         xL, s = self.encode(tokens, True, clone_seed=False)
         if side is not None:

@@ -430,6 +430,29 @@ def sas_block_in_bwd(dq, dkv, dx1, x, mean1, rstd1, ln_w, WinT, dx, part):
          ptr(WinT), ptr(dx), ptr(part), stream())
 
 
+# ---- union-of-touched-rows table-gradient exchange (sparse_rows.hip) -------------------------
+def touched_rows_ws_numel(rows):
+    return int(_lib.lib().rs_touched_rows_ws_numel(rows))
+
+
+def touched_rows(ids, rows, flags, index, count, ws):
+    """flags/index int32[rows]: index[v] = rank of table row v among the rows occurring in ids (ascending), else
+    -1; count int32[1] = their number (device-side, no sync)."""
+    call("rs_touched_rows", ptr(ids), ids.numel(), rows, ptr(flags), ptr(index), ptr(count), ptr(ws), stream())
+
+
+def rows_pack(src, index, count, compact):
+    """compact[index[v]] = src[v] for the touched rows; compact rows [count, cap) = 0.  src fp32 [rows, d]."""
+    rows, d = src.shape
+    call("rs_rows_pack", ptr(src), rows, d, ptr(index), ptr(count), ptr(compact), compact.shape[0], stream())
+
+
+def rows_unpack(dst, index, compact):
+    """dst[v] = compact[index[v]] for the touched rows (the others are left as they are)."""
+    rows, d = dst.shape
+    call("rs_rows_unpack", ptr(dst), rows, d, ptr(index), ptr(compact), stream())
+
+
 def sas_block_parts(M):
     """LayerNorm affine partial sets written by rs_sas_block_out_bwd / rs_sas_block_in_bwd for M rows."""
     return int(_lib.lib().rs_sas_block_parts(M))

@@ -66,14 +66,17 @@ class FusedAdam:
 
 class FusedTrainStep:
     def __init__(self, model, lr=1e-3, weight_decay=0.0, process_group=None, dp=None, max_labelled=None,
-                 bucket_numel=None, overlap=None, vocab_shard=False):
+                 bucket_numel=None, overlap=None, vocab_shard=False, sparse_rows="auto"):
         """model: rbm_amd SASModel or BERTModel on a CUDA device.
         dp: data-parallel mode (default: torch.distributed initialised with world size > 1).
         max_labelled (BERT): upper bound on labelled rows per batch (sizes the compacted
         vocabulary-logit buffers; default B*T).  overlap (DP, default on unless bucket_numel is given): each
         gradient bucket's all-reduce starts as soon as the backward has finished it (dp.BucketedExchange);
         bucket_numel: otherwise ONE all-reduce after the backward, in buckets of that many floats.
-        vocab_shard (BERT, DP): out.weight / out.bias sharded over the ranks (rbm_amd.vocab_parallel)."""
+        vocab_shard (BERT, DP): out.weight / out.bias sharded over the ranks (rbm_amd.vocab_parallel).
+        sparse_rows (BERT, DP with overlap): "auto" (default: when the gathered ids are at most half the table),
+        "on" or "off" -- the token table's gradient is exchanged as the union of the rows the ranks touched
+        (dp.SparseRowExchange) instead of inside the dense buckets."""
         self.model = model
         self.kind = model.code()
         self.engine = model.sas.engine() if self.kind == "sas" else model.engine()
@@ -121,6 +124,9 @@ class FusedTrainStep:
         self._stamps = None
         self.exchange = dpx.BucketedExchange(self.flat.grad, self._buckets(), self.pg, partial=self.vshard is not None) \
             if self.overlap else None
+        self.sparse_mode = sparse_rows
+        self.sparse = None
+        self._sparse_checked = False
 
     # ---------------------------------------------------------------- pieces
     def _divisor(self, local_count):
@@ -147,6 +153,25 @@ class FusedTrainStep:
                                                        if n not in ("out.weight", "out.bias"))
             return {"final": (0, cut), "out": (cut, f.grad.numel())}
         return {"final": (0, f.grad.numel())}
+
+    def _maybe_sparse(self, tokens):
+        """Decide (once, at the first batch: the exchange is sized by its id count) whether the BERT token table's
+        gradient goes through dp.SparseRowExchange; if so, carve it out of the dense buckets."""
+        if self._sparse_checked:
+            return
+        self._sparse_checked = True
+        if not (self.dp and self.overlap and self.kind == "bert") or self.sparse_mode == "off":
+            return
+        name = "bert.embedding.token.weight"
+        rows, d = self.flat.shapes[name]
+        n = tokens.numel()
+        if self.sparse_mode == "auto" and not dpx.SparseRowExchange.worthwhile(rows, n, dpx.world()):
+            return
+        self.sparse = dpx.SparseRowExchange(self.flat.view(name, self.flat.grad), n, self.pg)
+        self.engine.sparse_tok = self.sparse
+        lo = self.flat.offsets[name]
+        self.exchange = dpx.BucketedExchange(self.flat.grad, dpx.carve(self._buckets(), lo, lo + rows * d), self.pg,
+                                             partial=True)
 
     def _compute(self, *batch, split=None):
         """Forward + loss + backward into the flat gradient.  split(tag): called by the engine when the bucket
@@ -186,6 +211,9 @@ class FusedTrainStep:
             eng.backward(saved, dpl, dnl, self.flat.grad)
         else:
             tokens, labels = batch
+            self._maybe_sparse(tokens)
+            if self.sparse is not None and split is None:
+                raise RuntimeError("the sparse token-table exchange needs the overlapped (segmented) step")
             eng.train_loss_and_backward(tokens, labels, self.loss_out, self._divisor, self.flat.grad,
                                         max_labelled=self.max_labelled, split=sp)
         write_aux()

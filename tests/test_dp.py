@@ -175,3 +175,53 @@ def test_vocab_shard_ranges_and_gather(tmp_path, world, V1):
     assert spans[0][0] == 0 and spans[-1][1] == V1
     assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
     assert all(v0 % 128 == 0 for v0, _ in spans)
+
+
+def _carve_worker(rank, world, port, out_dir):
+    import sys
+    sys.path.insert(0, ROOT)
+    import rbm_amd  # noqa: F401
+    from rbm_amd import dp
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(rank)
+        flat = torch.randn(1000, generator=g)
+        mine = flat.clone()
+        ref = flat.clone()
+        dist.all_reduce(ref)
+        # the table region [100, 400) leaves the dense buckets (exchanged by dp.SparseRowExchange instead)
+        b = dp.carve({"final": (0, 600), "out": (600, 1000)}, 100, 400)
+        assert b == {"final": [(0, 100), (400, 600)], "out": [(600, 1000)]}, b
+        ex = dp.BucketedExchange(flat, b, partial=True)
+        ex.launch("out")
+        ex.launch("final")
+        ex.finish()
+        torch.save({"flat": flat, "ref": ref, "mine": mine}, os.path.join(out_dir, f"c{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_carved_buckets_leave_the_table_region(tmp_path):
+    """dp.carve + multi-range buckets (the BERT step with a sparse token-table exchange): every range but the carved
+    one is all-reduced exactly as one dense all-reduce sums it; the carved region keeps this rank's values."""
+    mp.spawn(_carve_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        d = torch.load(tmp_path / f"c{r}.pt", weights_only=True)
+        out = torch.ones(1000, dtype=torch.bool)
+        out[100:400] = False
+        assert torch.equal(d["flat"][out], d["ref"][out])
+        assert torch.equal(d["flat"][100:400], d["mine"][100:400])
+
+
+def test_sparse_exchange_sizing():
+    """The bytes the union-of-touched-rows exchange moves at cfg5 on 8 GPUs, and when it is used."""
+    import sys
+    sys.path.insert(0, ROOT)
+    from rbm_amd import dp
+    rows, d, n = 1_000_002, 256, 64 * 200
+    assert dp.SparseRowExchange.worthwhile(rows, n, 8)
+    assert not dp.SparseRowExchange.worthwhile(rows, n, 1)
+    assert not dp.SparseRowExchange.worthwhile(54_543, 128 * 50 * 3, 8)     # SAS cfg4 item table: dense
+    cap = min(rows, 8 * n)
+    assert cap * d * 4 == 104_857_600 and rows * d * 4 == 1_024_002_048

@@ -1,0 +1,114 @@
+"""Union-of-touched-rows exchange of the BERT token table's gradient (dp.SparseRowExchange, sparse_rows.hip;
+SURVEY.md §8(e)).  The kernels against a torch restatement, then two data-parallel ranks -- processes on ONE GPU,
+gloo moving the tensors (the product uses RCCL) -- whose parameters after three steps equal, bit for bit, the same
+ranks exchanging the dense table (two ranks: every element is a + b either way)."""
+import argparse
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def test_touched_rows_pack_unpack():
+    import rbm_amd  # noqa: F401
+    from rbm_amd import ops
+    g = torch.Generator(device="cuda").manual_seed(0)
+    for rows, d, n in ((1000, 8, 300), (5003, 64, 4096), (100_000, 16, 50_000), (7, 4, 0)):
+        ids = torch.randint(0, rows, (n,), device="cuda", generator=g)
+        flags = torch.full((rows,), 7, dtype=torch.int32, device="cuda")
+        index = torch.empty(rows, dtype=torch.int32, device="cuda")
+        count = torch.zeros(1, dtype=torch.int32, device="cuda")
+        ws = torch.empty(ops.touched_rows_ws_numel(rows), dtype=torch.int32, device="cuda")
+        ops.touched_rows(ids, rows, flags, index, count, ws)
+        uniq = torch.unique(ids)
+        ref = torch.full((rows,), -1, dtype=torch.int32, device="cuda")
+        ref[uniq] = torch.arange(uniq.numel(), dtype=torch.int32, device="cuda")
+        assert int(count.item()) == uniq.numel()
+        assert torch.equal(index, ref)
+        src = torch.randn(rows, d, device="cuda", generator=g)
+        cap = max(1, min(rows, n + 5))
+        compact = torch.full((cap, d), 3.0, device="cuda")
+        ops.rows_pack(src, index, count, compact)
+        assert torch.equal(compact[:uniq.numel()], src[uniq])
+        assert not compact[uniq.numel():].any()
+        dst = torch.zeros(rows, d, device="cuda")
+        ops.rows_unpack(dst, index, compact * 2)
+        assert torch.equal(dst[uniq], 2 * src[uniq])
+        mask = torch.ones(rows, dtype=torch.bool, device="cuda")
+        mask[uniq] = False
+        assert not dst[mask].any()
+
+
+V, T, D, BR = 20000, 50, 64, 4      # items, max_len, hidden, sequences per rank (2*200 ids << 20,002 rows)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _model():
+    import rbm_amd  # noqa: F401
+    from rbm_amd.models import model_factory
+    a = argparse.Namespace(model_code="bert", num_items=V, max_len=T, device="cuda", bert_hidden_units=D,
+                           bert_num_blocks=1, bert_num_heads=2, bert_dropout=0.1, bert_hidden_dropout=0.1,
+                           bert_mask_prob=0.2, model_init_seed=7, rs_dtype="bf16")
+    return model_factory(a)
+
+
+def _worker(rank, world, port, graph, mode, out_dir):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import rbm_amd.data as synth
+        from rbm_amd.train_step import FusedTrainStep
+        m = _model()
+        tr = FusedTrainStep(m, lr=1e-3, max_labelled=BR * T, sparse_rows=mode)
+        rng = np.random.default_rng(3)
+        batches = [[synth.bert_batch(rng, BR, T, V, mask_prob=0.3) for _ in range(world)] for _ in range(3)]
+        batches = [tuple(torch.from_numpy(x).cuda() for x in b[rank]) for b in batches]
+        if graph:
+            tr.capture(*batches[0])
+            m.load_state_dict(_model().state_dict())
+            tr.engine.sync_compute_weights()
+            tr.opt.m.zero_(); tr.opt.v.zero_(); tr.opt.state.zero_()
+            tr.engine.seed_base.fill_(rank << 40)
+        losses = [float((tr.replay(*b) if graph else tr.step(*b)).item()) for b in batches]
+        torch.cuda.synchronize()
+        sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+        torch.save({"losses": losses, "sd": sd, "sparse": tr.sparse is not None},
+                   os.path.join(out_dir, f"{mode}_r{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_sparse_token_exchange_equals_dense(tmp_path, graph):
+    world = 2
+    for mode in ("on", "off"):
+        mp.spawn(_worker, args=(world, _free_port(), graph, mode, str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        a = torch.load(tmp_path / f"on_r{r}.pt", weights_only=True)
+        b = torch.load(tmp_path / f"off_r{r}.pt", weights_only=True)
+        assert a["sparse"] and not b["sparse"]
+        assert a["losses"] == b["losses"]
+        for k in b["sd"]:
+            assert torch.equal(a["sd"][k], b["sd"][k]), k
+    r0 = torch.load(tmp_path / "on_r0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "on_r1.pt", weights_only=True)
+    for k in r0["sd"]:
+        assert torch.equal(r0["sd"][k], r1["sd"][k]), k        # the replicas stay identical
