@@ -39,7 +39,50 @@ __global__ void adam_prepare_kernel(double* state, const float* hyper, const flo
 // scalars itself, and the LAST workgroup to finish (arrival counter in state[7]) writes them back, advances
 // the step count and the dropout seed, and re-arms the counter.  One launch instead of two on the step's
 // critical path.
-template <bool BF16OUT, bool PREP>
+// one float4 of the Adam update (torch.optim.Adam, BS/trainers/base.py:225-228) + its stores
+template <bool BF16OUT>
+__device__ __forceinline__ void adam4(int64_t i, float4 pp, float4 gg, float4 mm, float4 vv, float* __restrict__ p,
+                                      float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
+                                      __bf16* __restrict__ pb, float b1, float b2, float eps, float wd,
+                                      float step_size, float bc2s, float gs, int zero_grad,
+                                      const int64_t* __restrict__ tdesc, int ntd, int64_t tbase,
+                                      __bf16* __restrict__ wT) {
+  float* P = &pp.x; float* G = &gg.x; float* Mv = &mm.x; float* Vv = &vv.x;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float gj = gs == 1.f ? G[j] : G[j] * gs;
+    if (wd != 0.f) gj = gj + wd * P[j];
+    Mv[j] = Mv[j] + (1.f - b1) * (gj - Mv[j]);            // exp_avg.lerp_(grad, 1-beta1)
+    Vv[j] = Vv[j] * b2 + (1.f - b2) * gj * gj;            // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
+    const float denom = sqrtf(Vv[j]) / bc2s + eps;
+    P[j] = P[j] - step_size * (Mv[j] / denom);            // param.addcdiv_(exp_avg, denom, -step_size)
+  }
+  reinterpret_cast<float4*>(p)[i] = pp;
+  reinterpret_cast<float4*>(m)[i] = mm;
+  reinterpret_cast<float4*>(v)[i] = vv;
+  if (zero_grad) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (BF16OUT) {
+    bf16x4 o;
+    o[0] = (__bf16)P[0]; o[1] = (__bf16)P[1]; o[2] = (__bf16)P[2]; o[3] = (__bf16)P[3];
+    reinterpret_cast<bf16x4*>(pb)[i] = o;
+    // transposed bf16 copies of matrices inside the buffer (the SAS backward's [in][out] block weights,
+    // rs_transpose_bf16's desc layout): the 4 elements share a row (host checks lds % 4 == 0)
+    for (int k = 0; k < ntd; ++k) {
+      const int64_t* dk = tdesc + 6 * k;
+      const int64_t rel = tbase + 4 * i - dk[2];
+      if (rel >= 0 && rel < dk[0] * dk[3]) {
+        const int64_t r = rel / dk[3], c = rel - r * dk[3];
+        if (c < dk[1]) {
+          __bf16* t = wT + dk[4] + c * dk[5] + r;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) t[j * dk[5]] = o[j];
+        }
+      }
+    }
+  }
+}
+
+template <bool BF16OUT, bool PREP, int U>
 __global__ __launch_bounds__(256) void adam_step_kernel(int64_t n, float* __restrict__ p, float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v,
                                                         __bf16* __restrict__ pb, double* __restrict__ state,
@@ -61,44 +104,30 @@ __global__ __launch_bounds__(256) void adam_step_kernel(int64_t n, float* __rest
     gs = (float)state[3];
   }
   const int64_t n4 = n / 4;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  // U float4 per thread in flight: every load of the group is issued before the first store
+  for (; i + (U - 1) * stride < n4; i += U * stride) {
+    float4 pq[U], gq[U], mq[U], vq[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      pq[u] = reinterpret_cast<float4*>(p)[i + u * stride];
+      gq[u] = reinterpret_cast<const float4*>(g)[i + u * stride];
+      mq[u] = reinterpret_cast<float4*>(m)[i + u * stride];
+      vq[u] = reinterpret_cast<float4*>(v)[i + u * stride];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      adam4<BF16OUT>(i + u * stride, pq[u], gq[u], mq[u], vq[u], p, g, m, v, pb, b1, b2, eps, wd, step_size, bc2s, gs,
+                     zero_grad, tdesc, ntd, tbase, wT);
+  }
+  for (; i < n4; i += stride) {
     float4 pp = reinterpret_cast<float4*>(p)[i];
     float4 gg = reinterpret_cast<const float4*>(g)[i];
     float4 mm = reinterpret_cast<float4*>(m)[i];
     float4 vv = reinterpret_cast<float4*>(v)[i];
-    float* P = &pp.x; float* G = &gg.x; float* Mv = &mm.x; float* Vv = &vv.x;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float gj = gs == 1.f ? G[j] : G[j] * gs;
-      if (wd != 0.f) gj = gj + wd * P[j];
-      Mv[j] = Mv[j] + (1.f - b1) * (gj - Mv[j]);            // exp_avg.lerp_(grad, 1-beta1)
-      Vv[j] = Vv[j] * b2 + (1.f - b2) * gj * gj;            // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
-      const float denom = sqrtf(Vv[j]) / bc2s + eps;
-      P[j] = P[j] - step_size * (Mv[j] / denom);            // param.addcdiv_(exp_avg, denom, -step_size)
-    }
-    reinterpret_cast<float4*>(p)[i] = pp;
-    reinterpret_cast<float4*>(m)[i] = mm;
-    reinterpret_cast<float4*>(v)[i] = vv;
-    if (zero_grad) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (BF16OUT) {
-      bf16x4 o;
-      o[0] = (__bf16)P[0]; o[1] = (__bf16)P[1]; o[2] = (__bf16)P[2]; o[3] = (__bf16)P[3];
-      reinterpret_cast<bf16x4*>(pb)[i] = o;
-      // transposed bf16 copies of matrices inside the buffer (the SAS backward's [in][out] block weights,
-      // rs_transpose_bf16's desc layout): the 4 elements share a row (host checks lds % 4 == 0)
-      for (int k = 0; k < ntd; ++k) {
-        const int64_t* dk = tdesc + 6 * k;
-        const int64_t rel = tbase + 4 * i - dk[2];
-        if (rel >= 0 && rel < dk[0] * dk[3]) {
-          const int64_t r = rel / dk[3], c = rel - r * dk[3];
-          if (c < dk[1]) {
-            __bf16* t = wT + dk[4] + c * dk[5] + r;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) t[j * dk[5]] = o[j];
-          }
-        }
-      }
-    }
+    adam4<BF16OUT>(i, pp, gg, mm, vv, p, g, m, v, pb, b1, b2, eps, wd, step_size, bc2s, gs, zero_grad, tdesc, ntd,
+                   tbase, wT);
   }
   // tail
   if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
@@ -291,6 +320,24 @@ int rs_adam_prepare(double* state, const float* hyper, const float* grad_divisor
   return (int)hipGetLastError();
 }
 
+// float4 groups in flight per thread (RS_ADAM_UNROLL, default 2) and the grid cap
+static int adam_unroll() {
+  static int u = -1;
+  if (u < 0) {
+    const char* e = getenv("RS_ADAM_UNROLL");
+    u = e ? atoi(e) : 2;
+    if (u != 1 && u != 2 && u != 4) u = 2;
+  }
+  return u;
+}
+#define ADAM_LAUNCH(BO, PR, ...)                                                                       \
+  do {                                                                                                 \
+    const int u_ = adam_unroll();                                                                      \
+    if (u_ == 1) hipLaunchKernelGGL((adam_step_kernel<BO, PR, 1>), __VA_ARGS__);                       \
+    else if (u_ == 4) hipLaunchKernelGGL((adam_step_kernel<BO, PR, 4>), __VA_ARGS__);                  \
+    else hipLaunchKernelGGL((adam_step_kernel<BO, PR, 2>), __VA_ARGS__);                               \
+  } while (0)
+
 int rs_adam_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, const double* state,
                  const float* hyper, int zero_grad, void* stream) {
   if (n <= 0 || ((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16) return RS_ERR_ARG;
@@ -298,11 +345,11 @@ int rs_adam_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16
   hipStream_t s = (hipStream_t)stream;
   double* st = const_cast<double*>(state);   // read only without PREP
   if (p_bf16)
-    hipLaunchKernelGGL((adam_step_kernel<true, false>), dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
+    ADAM_LAUNCH(true, false, dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
                        (__bf16*)p_bf16, st, hyper, zero_grad, nullptr, nullptr, nullptr, 0, 0,
                        nullptr);
   else
-    hipLaunchKernelGGL((adam_step_kernel<false, false>), dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
+    ADAM_LAUNCH(false, false, dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
                        (__bf16*)nullptr, st, hyper, zero_grad, nullptr, nullptr, nullptr, 0, 0,
                        nullptr);
   return (int)hipGetLastError();
@@ -316,11 +363,11 @@ int rs_adam_prepare_step(int64_t n, float* p, float* g, float* m, float* v, void
   const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(cdiv(n / 4, 256), 8192));
   hipStream_t s = (hipStream_t)stream;
   if (p_bf16)
-    hipLaunchKernelGGL((adam_step_kernel<true, true>), dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
+    ADAM_LAUNCH(true, true, dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
                        (__bf16*)p_bf16, state, hyper, zero_grad, grad_divisor, seed_base, tdesc, ntd,
                        tbase, (__bf16*)wT);
   else
-    hipLaunchKernelGGL((adam_step_kernel<false, true>), dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
+    ADAM_LAUNCH(false, true, dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
                        (__bf16*)nullptr, state, hyper, zero_grad, grad_divisor, seed_base, nullptr, 0,
                        0, nullptr);
   return (int)hipGetLastError();

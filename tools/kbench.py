@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--adam-params", type=int, default=662400, help="parameter count of the adam_step entry")
     ap.add_argument("--drop", type=float, default=0.2, help="dropout rate of the dropout-carrying ops")
     ap.add_argument("--only", default="", help="time only the ops whose name contains one of these |-separated strings")
     a = ap.parse_args()
@@ -207,13 +208,16 @@ def main():
         dpl_, dnl_ = torch.empty(M, device=dev), torch.empty(M, device=dev)
         run("head_bwd", lambda: ops.sas_head_bwd(hp, None, lout, pl, nl, None, None, dpl_, dnl_, pos, neg, table, x,
                                                  gam, mu, ri, z, part), 4 * mb)
-    n = 662400
+    n = a.adam_params
     p, gg, m1, v1 = (torch.randn(n, device=dev) for _ in range(4))
     v1.abs_()
     pbf = torch.empty(n, dtype=torch.bfloat16, device=dev)
     st = torch.tensor([1.0, 0.001, 1.0, 1.0], dtype=torch.float64, device=dev)
     hy = torch.tensor([1e-3, 0.9, 0.999, 1e-8, 0.0], device=dev)
-    run("adam_step (662k params)",lambda: ops.adam_step(p, gg, m1, v1, pbf, st, hy, zero_grad=True), n * 4 * 7 + n * 2)
+    run(f"adam_step ({n} params)",lambda: ops.adam_step(p, gg, m1, v1, pbf, st, hy, zero_grad=True), n * 4 * 8 + n * 2)
+    st144 = torch.zeros(144, dtype=torch.float64, device=dev)
+    run(f"adam_prepare_step ({n} params)", lambda: ops.adam_prepare_step(p, gg, m1, v1, pbf, st144, hy, zero_grad=True),
+        n * 4 * 8 + n * 2)
     print(f"{'op':45s} {'us':>9s} {'GB/s':>9s} {'TFLOP/s':>8s}")
     for name, us, gbs, tf in rows:
         print(f"{name:45s} {us:9.2f} {gbs:9.1f} {tf:8.2f}")
