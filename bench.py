@@ -70,9 +70,9 @@ def parse():
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse the "
                          "multi-process path with several ranks on one GPU)")
     ap.add_argument("--steps-per-graph", default="auto",
-                    help="training steps unrolled into one graph replay (single GPU; 'auto' = the largest of 8/4/2 "
-                         "dividing --steps and --warmup, else 1); every step still runs on its own batch with its "
-                         "own Adam update")
+                    help="training steps unrolled into one graph replay (single GPU; 'auto' = the largest of "
+                         "10/8/5/4/2 dividing --steps, else 1); every step still runs on its own batch with its own "
+                         "Adam update; warmup steps beyond a multiple of it run as eager steps")
     ap.add_argument("--nbatches", type=int, default=8, help="distinct synthetic batches cycled through")
     ap.add_argument("--sampler", default="host", choices=["host", "device"],
                     help="SAS: 'device' = batches drawn each step by the on-device WarpSampler "
@@ -325,13 +325,13 @@ def main():
     stamps = None if sbuf is None else (sbuf, (dominant(cfg),))
 
     if args.steps_per_graph == "auto":
-        # the largest of 8 / 4 / 2 steps per replay that divides both counts (a replay boundary costs ~25 us)
-        S = next((u for u in (8, 4, 2) if args.steps % u == 0 and args.warmup % u == 0), 1) \
-            if world == 1 and not args.no_graph else 1
+        # the largest of 10 / 8 / 5 / 4 / 2 steps per replay that divides the timed count (a replay boundary costs
+        # ~25 us); the warmup need not be a multiple: its remainder runs as eager steps (below)
+        S = next((u for u in (10, 8, 5, 4, 2) if args.steps % u == 0), 1) if world == 1 and not args.no_graph else 1
     else:
         S = int(args.steps_per_graph)
-        if S > 1 and (world > 1 or args.no_graph or args.steps % S or args.warmup % S):
-            raise SystemExit("--steps-per-graph > 1 needs one GPU, graphs, and --steps/--warmup multiples of it")
+        if S > 1 and (world > 1 or args.no_graph or args.steps % S):
+            raise SystemExit("--steps-per-graph > 1 needs one GPU, graphs, and --steps a multiple of it")
 
     if args.sampler == "device" and cfg["model"] == "sas":
         import rbm_amd.data as synth
@@ -342,6 +342,7 @@ def main():
         trainer.capture_sampled(sampler, stamps=stamps, steps_per_graph=S)
         batches = [()]
         run = trainer.replay_sampled
+        eager = lambda i: (sampler.sample_into(*trainer.static), trainer.step(*trainer.static))  # noqa: E731
     elif args.sampler == "device":
         # BERT: on-device cloze masking (rs_bert_mask) in the step graph; the labelled-row cap stays
         # B*T (default), every vocabulary GEMM is bounded by the device-side labelled count
@@ -354,10 +355,13 @@ def main():
         trainer.capture_sampled(sampler, stamps=stamps, steps_per_graph=S)
         batches = [()]
         run = trainer.replay_sampled
+        eager = lambda i: (sampler.sample_into(*trainer.static), trainer.step(*trainer.static))  # noqa: E731
     elif args.no_graph:
         run = trainer.step
     else:
         trainer.capture(*batches[0], stamps=stamps, steps_per_graph=S)
+        step_batches = batches
+        eager = lambda i: trainer.step(*step_batches[i % len(step_batches)])  # noqa: E731
         batches = [torch.stack(b) for b in batches]     # one device copy per replay (replay_packed)
         if S > 1:   # S consecutive batches per replay, still cycling through all of them
             batches = [torch.stack([batches[(j * S + k) % len(batches)] for k in range(S)])
@@ -368,8 +372,12 @@ def main():
     marks_per_step = len(ops.kernel_stamp_kinds()) if sbuf is not None else 0
     if marks_per_step > NMARK:
         raise SystemExit(f"{marks_per_step} stamped launches per step exceed the stamp buffer's {NMARK} marks")
+    # W warmup steps: whole replays, then the remainder (W mod S) as eager steps of the same trainer -- every
+    # warmup step is a full training step with its own Adam update
     for i in range(args.warmup // S):
         loss = run(*batches[i % len(batches)])
+    for i in range(args.warmup % S):
+        loss = eager(i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
