@@ -131,7 +131,10 @@ int rs_attn_fwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t Dh, const vo
                 const void* k, int64_t ldk, const void* v, int64_t ldv, void* o, int64_t ldo, float* lse,
                 float scale, int mask_kind, const int64_t* ids, float drop_p, uint64_t seed,
                 const uint64_t* seed_base, void* stream);
-/* Backward: dq, dk, dv (overwritten).  ws: >= B*H*T floats (row deltas). */
+/* Backward: dq, dk, dv (overwritten).  ws: >= B*H*T floats (row deltas).  mask_kind | RS_ATTN_DELTA_IN: ws
+ * already holds delta[(b*H+h)*T + t] = rowsum(dO * O) over the head's columns (rs_sas_block_out_bwd with o given
+ * forms it); the bf16 LDS path then reads neither O nor recomputes it (other paths recompute it into ws). */
+#define RS_ATTN_DELTA_IN 0x100
 int rs_attn_bwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t Dh, const void* q, int64_t ldq,
                 const void* k, int64_t ldk, const void* v, int64_t ldv, const void* o, int64_t ldo,
                 const void* dout, int64_t lddo, const float* lse, void* dq, int64_t lddq, void* dk,
@@ -362,6 +365,14 @@ int rs_sas_block_out_bwd(int64_t M, int64_t d, const void* dxn, const int64_t* i
                          const float* mean2, const float* rstd2, const float* ln_w, const void* W2T, const void* W1T,
                          const void* WoT, void* dy2, void* da1, void* dx1, void* dout, float* part, float drop_p,
                          uint64_t salt1, uint64_t salt2, const uint64_t* seed_base, void* stream);
+/* rs_sas_block_out_bwd, and with o (the attention output [M][d] bf16, one head) also
+ * delta[m] = rowsum(dout[m] * o[m]) -- the attention backward's row term, so rs_attn_bwd (mask_kind |
+ * RS_ATTN_DELTA_IN, ws = delta) reads neither o nor recomputes it.  o and delta: both or neither. */
+int rs_sas_block_out_bwd_delta(int64_t M, int64_t d, const void* dxn, const int64_t* ids, const void* h1,
+                               const void* x1, const float* mean2, const float* rstd2, const float* ln_w,
+                               const void* W2T, const void* W1T, const void* WoT, void* dy2, void* da1, void* dx1,
+                               void* dout, float* part, float drop_p, uint64_t salt1, uint64_t salt2,
+                               const uint64_t* seed_base, const void* o, float* delta, void* stream);
 /* Backward of rs_sas_block_in (sas.py:73-76 reversed):
  *   dQ = dq Wq + dx1;  dx = dk Wk + dv Wv + LN1'(x, dQ) [out];  LN1 affine partials -> part (as above).
  * WinT = in_proj_weight^T ([d][3d] bf16). */

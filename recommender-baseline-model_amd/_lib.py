@@ -93,6 +93,8 @@ SIGNATURES = {
                          u64, u64, vp, vp],
     "rs_sas_block_out_bwd": [i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32, u64, u64,
                              vp, vp],
+    "rs_sas_block_out_bwd_delta": [i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32, u64,
+                                   u64, vp, vp, vp, vp],
     "rs_sas_block_in_bwd": [i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "rs_wgrad_grouped": [i32, C.POINTER(WgradProblem), i64, i64, vp, i64, i32, C.POINTER(ReduceSegment), vp],
     "rs_reduce_segments": [i32, C.POINTER(ReduceSegment), i32, vp],

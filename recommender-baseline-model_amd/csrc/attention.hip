@@ -491,6 +491,8 @@ int rs_attn_bwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t Dh, const vo
                 int64_t lddk, void* dv, int64_t lddv, float scale, int mask_kind, const int64_t* ids,
                 float drop_p, uint64_t seed, const uint64_t* seed_base, float* ws, void* stream) {
   const int64_t lds[8] = {ldq, ldk, ldv, ldo, lddo, lddq, lddk, lddv};
+  const int delta_in = mask_kind & RS_ATTN_DELTA_IN;
+  mask_kind &= ~RS_ATTN_DELTA_IN;
   int c = check(B, T, H, Dh);
   if (c) return c;
   if (mask_kind == 1 && !ids) return RS_ERR_ARG;
@@ -498,7 +500,8 @@ int rs_attn_bwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t Dh, const vo
   const int vec = vec_ok(dtype, Dh, ptrs, 8, lds, 8);
   if (vec && use_lds_path(dtype, B * H, T, Dh))
     return (int)attn_lds_bwd(B, T, H, Dh, q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, dq, lddq, dk, lddk, dv,
-                             lddv, scale, mask_kind, ids, drop_p, seed, seed_base, ws, (hipStream_t)stream);
+                             lddv, scale, mask_kind | delta_in, ids, drop_p, seed, seed_base, ws, (hipStream_t)stream);
+  // the generic kernels always form delta themselves (into ws)
   AttnArgs a = {};
   a.B = B; a.T = T; a.H = H; a.Dh = (int)Dh; a.vec = vec;
   a.q = q; a.ldq = ldq; a.k = k; a.ldk = ldk; a.v = v; a.ldv = ldv;

@@ -40,7 +40,8 @@ struct AttnLdsArgs {
   bf16* dk; int64_t lddk;
   bf16* dv; int64_t lddv;
   float* lse;                    // forward writes; backward reads
-  float* delta;                  // dQ pass writes, dK/dV pass reads
+  float* delta;                  // dQ pass writes, dK/dV pass reads (delta_in: precomputed, both read)
+  int delta_in;                  // delta = rowsum(dO * O) given by the caller (rs_sas_block_out_bwd): O is not read
   float scale;
   int mask_kind;                 // 0 causal (-inf), 1 key padding (-1e9)
   const int64_t* ids;
@@ -402,7 +403,7 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnLdsArgs& a, int64_t l
     for (int kc = 0; kc < KC; ++kc) {
       qf[kc] = gload8(Qg, a.ldq, qrow0, a.T, kc * 32 + 8 * g);
       df[kc] = gload8(dOg, a.lddo, qrow0, a.T, kc * 32 + 8 * g);
-      of[kc] = gload8(Og, a.ldo, qrow0, a.T, kc * 32 + 8 * g);
+      if (!a.delta_in) of[kc] = gload8(Og, a.ldo, qrow0, a.T, kc * 32 + 8 * g);
     }
   }
   stage2<DH>(Ks, a.k + b * a.T * a.ldk + h * DH, a.ldk, Vs, a.v + b * a.T * a.ldv + h * DH, a.ldv, a.T, rows, tid);
@@ -420,18 +421,22 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnLdsArgs& a, int64_t l
       for (int kc = 0; kc < KC; ++kc) {
         qf[kc] = gload8(Qg, a.ldq, qrow, a.T, kc * 32 + 8 * g);
         df[kc] = gload8(dOg, a.lddo, qrow, a.T, kc * 32 + 8 * g);
-        of[kc] = gload8(Og, a.ldo, qrow, a.T, kc * 32 + 8 * g);
+        if (!a.delta_in) of[kc] = gload8(Og, a.ldo, qrow, a.T, kc * 32 + 8 * g);
       }
     }
     float dl = 0.f;
+    if (a.delta_in) {
+      dl = a.delta[bh * a.T + (qrow < a.T ? qrow : a.T - 1)];
+    } else {
 #pragma unroll
-    for (int kc = 0; kc < KC; ++kc) {
+      for (int kc = 0; kc < KC; ++kc) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) dl += (float)df[kc][j] * (float)of[kc][j];
+        for (int j = 0; j < 8; ++j) dl += (float)df[kc][j] * (float)of[kc][j];
+      }
+      dl += __shfl_xor(dl, 16, 64);
+      dl += __shfl_xor(dl, 32, 64);  // delta = rowsum(dO * O) for query qrow
+      if (role != 1 && g == 0 && qrow < a.T) a.delta[bh * a.T + qrow] = dl;
     }
-    dl += __shfl_xor(dl, 16, 64);
-    dl += __shfl_xor(dl, 32, 64);  // delta = rowsum(dO * O) for query qrow
-    if (role != 1 && g == 0 && qrow < a.T) a.delta[bh * a.T + qrow] = dl;
     const float lq2 = (qrow < a.T ? a.lse[bh * a.T + qrow] : 0.f) * LOG2E;
     const float sl2 = a.scale * LOG2E;
     const int qi = q0 + cl;
@@ -442,39 +447,64 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnLdsArgs& a, int64_t l
     f32x4 acc[DT];
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) acc[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    for (int c = cb; c < ce; ++c) {
-      f32x4 ds2[2];
+    // two-stage pipeline over 16-key half steps: the S / dP products of the next half step are issued before
+    // the softmax-gradient VALU of the current one, so the MFMA chains run under it.  Half steps past the
+    // tile's keys (t >= nkt) are computed on a clamped row and masked (branch-free issue).
+    const int tmax = rows / 16 - 1;
+    auto sdp = [&](int t, f32x4& sv, f32x4& dp) {
+      const int tr = min(t, tmax);
+      bf16x8 fk[KC], fv[KC];
 #pragma unroll
-      for (int hf = 0; hf < 2; ++hf) {
-        const int t = 2 * c + hf;
-        f32x4 sv = (f32x4){0.f, 0.f, 0.f, 0.f}, dp = (f32x4){0.f, 0.f, 0.f, 0.f};
-        if (t < nkt) {
+      for (int kc = 0; kc < KC; ++kc) {
+        fk[kc] = row_frag(Ks, LD, tr * 16 + cl, kc * 32 + 8 * g);
+        fv[kc] = row_frag(Vs, LD, tr * 16 + cl, kc * 32 + 8 * g);
+      }
+      sv = (f32x4){0.f, 0.f, 0.f, 0.f};
+      dp = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int kc = 0; kc < KC; ++kc) {
-            sv = mfma16(row_frag(Ks, LD, t * 16 + cl, kc * 32 + 8 * g), qf[kc], sv);
-            dp = mfma16(row_frag(Vs, LD, t * 16 + cl, kc * 32 + 8 * g), df[kc], dp);
-          }
-        }
-        const bool need = a.mask_kind != 0 || t >= qt || t * 16 + 16 > T;
-        const int kb = t * 16 + 4 * g;
-        float m[4] = {1.f, 1.f, 1.f, 1.f};
-        if (a.drop_p > 0.f) {
-          drop_mul2(a.drop_p, s32, rowidx + (uint32_t)kb, m[0], m[1]);
-          drop_mul2(a.drop_p, s32, rowidx + (uint32_t)kb + 2, m[2], m[3]);
-        }
+      for (int kc = 0; kc < KC; ++kc) {
+        sv = mfma16(fk[kc], qf[kc], sv);
+        dp = mfma16(fv[kc], df[kc], dp);
+      }
+    };
+    // dS^T for half step t: P = exp2(S*scale*log2e - lse), dS = P*(dP*mask - delta)*scale; 0 where masked
+    // (branch-free per element: the masks are selects; only the wave-uniform `need` picks the masked variant)
+    auto dsv = [&](int t, const f32x4& sv, const f32x4& dp, f32x4& ds) {
+      const bool need = a.mask_kind != 0 || t >= qt || t * 16 + 16 > T;
+      const int kb = t * 16 + 4 * g;
+      float m[4] = {1.f, 1.f, 1.f, 1.f};
+      if (a.drop_p > 0.f) {
+        drop_mul2(a.drop_p, s32, rowidx + (uint32_t)kb, m[0], m[1]);
+        drop_mul2(a.drop_p, s32, rowidx + (uint32_t)kb + 2, m[2], m[3]);
+      }
+      const bool tok = (t < nkt) & qok, causal = a.mask_kind == 0;
+      float pe[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pe[r] = ex2(sv[r] * sl2 - lq2) * a.scale;
+      if (need) {
+        // masked_fill has no gradient: dS = 0 on masked scores (-inf and -1e9 alike)
+        const f32x4 kmv = *reinterpret_cast<const f32x4*>(km + kb);   // key-padding flags (0 when causal)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          // masked_fill has no gradient: dS = 0 on masked scores (-inf and -1e9 alike)
-          bool live = t < nkt && qok;
-          if (need) {
-            const int k = kb + r;
-            live = live && k < T && !(a.mask_kind == 0 && k > qi) && !(a.mask_kind == 1 && km[k] != 0.f);
-          }
-          const float p = ex2(sv[r] * sl2 - lq2);
-          ds2[hf][r] = live ? p * (dp[r] * m[r] - dl) * a.scale : 0.f;
+          const int k = kb + r;
+          // non-short-circuit (&): selects, no exec-mask branches
+          const bool live = tok & (k < T) & !(causal & (k > qi)) & (kmv[r] == 0.f);
+          const float v = pe[r] * (dp[r] * m[r] - dl);
+          ds[r] = live ? v : 0.f;
         }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ds[r] = tok ? pe[r] * (dp[r] * m[r] - dl) : 0.f;
       }
-      const bf16x8 bds = pack8(ds2[0], ds2[1]);
+    };
+    f32x4 sA, dA, sB, dB, dsA, dsB;
+    sdp(2 * cb, sA, dA);
+    for (int c = cb; c < ce; ++c) {
+      sdp(2 * c + 1, sB, dB);
+      dsv(2 * c, sA, dA, dsA);
+      sdp(2 * c + 2, sA, dA);      // past the range on the last chunk: clamped, unused
+      dsv(2 * c + 1, sB, dB, dsB);
+      const bf16x8 bds = pack8(dsA, dsB);
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) acc[dt] = mfma16(tr_frag(Ks, LD, 32 * c, 16 * dt, lane), bds, acc[dt]);
     }
@@ -518,6 +548,30 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_lds_kernel(AttnLdsArgs a) {
 }
 
 // ------------------------------------------------------------------ backward: dK, dV
+// Dropout multipliers of P[q0 + r*... ] for this lane's key ki and its 4 queries (row indices rq0 + r*Tp): the
+// pair hash of (query, key pair) is shared by the lanes of keys ki and ki^1 (lanes l and l^1), so each lane hashes
+// two of the four queries and takes the other two from its partner (one DPP move each) -- the same multipliers as
+// drop_mul(p, seed, rowq + ki), one hash per element pair instead of per element.
+__device__ __forceinline__ void drop_keys4(float p, uint32_t s32, uint32_t rq0, uint32_t Tp, uint32_t ki, int lane,
+                                           float (&m)[4]) {
+  const uint32_t odd = (uint32_t)(lane & 1), r0 = 2 * odd;
+  const uint32_t h0 = pair_hash(s32, rq0 + r0 * Tp + ki), h1 = pair_hash(s32, rq0 + (r0 + 1) * Tp + ki);
+  const uint32_t x0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)h0, 0xB1, 0xF, 0xF, true);   // quad_perm [1,0,3,2]
+  const uint32_t x1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)h1, 0xB1, 0xF, 0xF, true);
+  uint32_t h[4];
+  h[0] = odd ? x0 : h0;
+  h[1] = odd ? x1 : h1;
+  h[2] = odd ? h0 : x0;
+  h[3] = odd ? h1 : x1;
+  const uint32_t thr = drop_thr(p);
+  const float k = 1.0f / (1.0f - p);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const uint32_t u = (ki & 1) ? (h[r] >> 16) : (h[r] & 0xFFFFu);
+    m[r] = u >= thr ? k : 0.f;
+  }
+}
+
 // own_delta: delta = rowsum(dO * O) is formed here (from O rows and the staged dO image, in the dQ pass's
 // summation order, so bit for bit the same values) instead of read from the dQ pass -- the two passes then
 // run as ONE launch (attn_bwd_lds_kernel) with no ordering between their workgroups
@@ -619,6 +673,7 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnLdsArgs& a, int64_t 
   }
   APROF(8);
   const uint64_t seed = eff_seed(a.seed, a.seed_base);
+  const uint32_t s32 = seed32(seed), Tp = (uint32_t)(T + (T & 1));   // mask row pitch: even
 
   const float sl2 = a.scale * LOG2E;
   int kt, cb, ce, role, slot;
@@ -638,35 +693,64 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnLdsArgs& a, int64_t 
       dk[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
       dv[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
     }
-    for (int c = cb; c < ce; ++c) {
-      f32x4 pd2[2], ds2[2];
+    // two-stage pipeline over 16-query half steps (as the dQ pass): the next half step's S / dP MFMAs run under
+    // this one's VALU; half steps past the image are computed on a clamped row and unused
+    const int tmax = rows / 16 - 1;
+    auto sdp = [&](int t, f32x4& sv, f32x4& dp) {
+      const int tr = min(t, tmax);
+      bf16x8 fq[KC], fo[KC];
 #pragma unroll
-      for (int hf = 0; hf < 2; ++hf) {
-        const int t = 2 * c + hf;
-        f32x4 s = (f32x4){0.f, 0.f, 0.f, 0.f}, dp = (f32x4){0.f, 0.f, 0.f, 0.f};
+      for (int kc = 0; kc < KC; ++kc) {
+        fq[kc] = row_frag(Qs, LD, tr * 16 + cl, kc * 32 + 8 * g);
+        fo[kc] = row_frag(dOs, LD, tr * 16 + cl, kc * 32 + 8 * g);
+      }
+      sv = (f32x4){0.f, 0.f, 0.f, 0.f};
+      dp = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int kc = 0; kc < KC; ++kc) {
-          s = mfma16(row_frag(Qs, LD, t * 16 + cl, kc * 32 + 8 * g), kf[kc], s);
-          dp = mfma16(row_frag(dOs, LD, t * 16 + cl, kc * 32 + 8 * g), vf[kc], dp);
-        }
-        const bool need = a.mask_kind != 0 || t <= kt || t * 16 + 16 > T || kt * 16 + 16 > T;
+      for (int kc = 0; kc < KC; ++kc) {
+        sv = mfma16(fq[kc], kf[kc], sv);
+        dp = mfma16(fo[kc], vf[kc], dp);
+      }
+    };
+    // P (dropped) and dS for this lane's key and the 4 queries t*16 + 4g + r
+    // (branch-free per element: masks are selects; the wave-uniform `need` picks the masked variant)
+    const bool kdead = ki >= T, kfill = km[min(ki, rows - 1)] != 0.f;   // key beyond T / key padding (-1e9)
+    auto pds = [&](int t, const f32x4& sv, const f32x4& dp, f32x4& pd, f32x4& ds) {
+      const f32x4 ls = *reinterpret_cast<const f32x4*>(lse_s + t * 16 + 4 * g);
+      const f32x4 dd = *reinterpret_cast<const f32x4*>(dl_s + t * 16 + 4 * g);
+      float m[4] = {1.f, 1.f, 1.f, 1.f};
+      if (a.drop_p > 0.f) drop_keys4(a.drop_p, s32, ((uint32_t)bh * (uint32_t)T + (uint32_t)(t * 16 + 4 * g)) * Tp,
+                                     Tp, (uint32_t)ki, lane, m);
+      const bool need = a.mask_kind != 0 || t <= kt || t * 16 + 16 > T || kt * 16 + 16 > T;
+      if (need) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int qr = t * 16 + 4 * g + r;
-          int st = 0;   // 0 live, 1 -inf, 2 -1e9 fill
-          if (need) {
-            if (qr >= T || ki >= T || (a.mask_kind == 0 && ki > qr)) st = 1;
-            else if (a.mask_kind == 1 && km[ki] != 0.f) st = 2;
-          }
-          const float x2 = st == 0 ? s[r] * sl2 : MASK2;
-          const float p = st == 1 ? 0.f : ex2(x2 - lse_s[qr]);
-          const float m = a.drop_p > 0.f ? drop_mul(a.drop_p, seed, (uint64_t)(((int)bh * T + qr) * (T + (T & 1)) + ki)) : 1.f;
-          pd2[hf][r] = p * m;
-          ds2[hf][r] = st == 0 ? p * (dp[r] * m - dl_s[qr]) * a.scale : 0.f;
+          const bool dead = kdead | (qr >= T) | ((a.mask_kind == 0) & (ki > qr));   // -inf: P = 0
+          const float x2 = kfill ? MASK2 : sv[r] * sl2;                          // -1e9 fill: P from the fill
+          const float p = ex2(dead ? NEG_INF : x2 - ls[r]);                      // select, not a branch
+          pd[r] = p * m[r];
+          const float v = p * (dp[r] * m[r] - dd[r]) * a.scale;
+          ds[r] = dead | kfill ? 0.f : v;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = ex2(sv[r] * sl2 - ls[r]);
+          pd[r] = p * m[r];
+          ds[r] = p * (dp[r] * m[r] - dd[r]) * a.scale;
         }
       }
-      const bf16x8 bp = pack8(pd2[0], pd2[1]);
-      const bf16x8 bds = pack8(ds2[0], ds2[1]);
+    };
+    f32x4 sA, dA, sB, dB, pdA, dsA, pdB, dsB;
+    sdp(2 * cb, sA, dA);
+    for (int c = cb; c < ce; ++c) {
+      sdp(2 * c + 1, sB, dB);
+      pds(2 * c, sA, dA, pdA, dsA);
+      sdp(2 * c + 2, sA, dA);
+      pds(2 * c + 1, sB, dB, pdB, dsB);
+      const bf16x8 bp = pack8(pdA, pdB);
+      const bf16x8 bds = pack8(dsA, dsB);
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         dv[dt] = mfma16(tr_frag(dOs, LD, 32 * c, 16 * dt, lane), bp, dv[dt]);
@@ -733,7 +817,7 @@ __global__ __launch_bounds__(NT) void attn_bwd_lds_kernel(AttnLdsArgs aq, AttnLd
   KStampEnd end_(aq.ks);
   const int64_t nq = (int64_t)aq.nsplit * aq.B * aq.H;
   if ((int64_t)blockIdx.x < nq) attn_bwd_dq_body<DH>(aq, blockIdx.x);
-  else attn_bwd_dkv_body<DH>(akv, blockIdx.x - nq, true);
+  else attn_bwd_dkv_body<DH>(akv, blockIdx.x - nq, !akv.delta_in);
 }
 
 // ------------------------------------------------------------------ launchers
@@ -934,6 +1018,8 @@ hipError_t attn_lds_bwd(int64_t B, int64_t T, int64_t H, int64_t Dh, const void*
   init_once();
   AttnLdsArgs a = {};
   a.B = B; a.T = T; a.H = H;
+  a.delta_in = (mask_kind & RS_ATTN_DELTA_IN) != 0;
+  mask_kind &= ~RS_ATTN_DELTA_IN;
   a.q = (const bf16*)q; a.ldq = ldq; a.k = (const bf16*)k; a.ldk = ldk; a.v = (const bf16*)v; a.ldv = ldv;
   a.o = (const bf16*)o; a.ldo = ldo; a.dout = (const bf16*)dout; a.lddo = lddo;
   a.dq = (bf16*)dq; a.lddq = lddq; a.dk = (bf16*)dk; a.lddk = lddk; a.dv = (bf16*)dv; a.lddv = lddv;

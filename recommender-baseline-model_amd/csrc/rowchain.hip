@@ -433,6 +433,7 @@ __device__ __forceinline__ void bwd_in_b(const Raw<D>& qr, const Raw<D>& rr, con
 
 struct OutBwd {
   bf16 *dy2, *da1, *dx1, *dout;
+  float* delta;   // optional: delta[m] = rowsum(dout * o), the attention backward's row term (one head)
   const int64_t* ids;
   float drop_p;
   uint32_t s1, s2;
@@ -472,11 +473,12 @@ __device__ __forceinline__ void bwd_out_a(const Raw<D>& dr, const Raw<D>& hr, co
   round_act<D>(acc, dar);
   store_raw<D>(o.da1, D, T.m, T.ok, dar, g);
 }
-// part 2: dz = da1 W1 + dzres; dx1 = LN2'(x1, dz) [saved, + affine partials into red]; dout = dx1 Wo [saved]
+// part 2: dz = da1 W1 + dzres; dx1 = LN2'(x1, dz) [saved, + affine partials into red]; dout = dx1 Wo [saved];
+// with o.delta: delta = rowsum(dout * O) of the stored (bf16) values, O = the attention output (orr)
 template <int D>
-__device__ __forceinline__ void bwd_out_b(const Raw<D>& dar, const Raw<D>& xr, const Raw<D>& dzr, const Tile& T,
-                                          float mu, float rs, const bf16* w1, const bf16* wo, const float* lnw,
-                                          const OutBwd& o, float* red, int lane, int wave) {
+__device__ __forceinline__ void bwd_out_b(const Raw<D>& dar, const Raw<D>& xr, const Raw<D>& dzr, const Raw<D>& orr,
+                                          const Tile& T, float mu, float rs, const bf16* w1, const bf16* wo,
+                                          const float* lnw, const OutBwd& o, float* red, int lane, int wave) {
   const int g = lane >> 4;
   Raw<D> r;
   Act<D> dz;
@@ -491,6 +493,15 @@ __device__ __forceinline__ void bwd_out_b(const Raw<D>& dar, const Raw<D>& xr, c
   mm<D>(wo, r, acc, lane);
   round_act<D>(acc, r);
   store_raw<D>(o.dout, D, T.m, T.ok, r, g);
+  if (o.delta) {
+    float dl = 0.f;
+#pragma unroll
+    for (int s = 0; s < Lay<D>::S; ++s)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dl = __builtin_fmaf((float)r.v[s][e], (float)orr.v[s][e], dl);
+    dl = row_sum(dl);
+    if (T.ok && g == 0) o.delta[T.m] = dl;
+  }
 }
 
 // ------------------------------------------------------------------ single-block kernels
@@ -601,10 +612,11 @@ struct OutBwdArgs {
   const bf16* W2T; const bf16* W1T; const bf16* WoT;      // transposed [in][out] copies
   bf16* dy2; bf16* da1; bf16* dx1; bf16* dout; float* part;
   float drop_p; uint64_t salt1, salt2; const uint64_t* seed_base;
+  const bf16* o; float* delta;                              // optional (both or neither)
 };
 __device__ __forceinline__ OutBwd out_bwd_of(const OutBwdArgs& a) {
   const bool drop = a.drop_p > 0.f;
-  return OutBwd{a.dy2, a.da1, a.dx1, a.dout, a.ids, a.drop_p,
+  return OutBwd{a.dy2, a.da1, a.dx1, a.dout, a.delta, a.ids, a.drop_p,
                 drop ? seed32(eff_seed(a.salt1, a.seed_base)) : 0u, drop ? seed32(eff_seed(a.salt2, a.seed_base)) : 0u};
 }
 
@@ -644,14 +656,28 @@ __global__ __launch_bounds__(NT) void block_out_bwd_kernel(OutBwdArgs a) {
       load_raw<D>(dr, a.dxn, D, T.mc, g);
       load_raw<D>(hr, a.h1, D, T.mc, g);
     }
-    Raw<D> xr;
+    Raw<D> xr, orr;
     load_raw<D>(xr, a.x1, D, T.mc, g);
+    if (a.delta) load_raw<D>(orr, a.o, D, T.mc, g);
     const float mu = a.mean2[T.mc], rs = a.rstd2[T.mc];
     Raw<D> dzr, dar;
     bwd_out_a<D>(dr, hr, T, wslot(smem, 0, WB), ob, dzr, dar, lane);
-    bwd_out_b<D>(dar, xr, dzr, T, mu, rs, wslot(smem, 1, WB), wslot(smem, 2, WB), lv, ob, red, lane, wave);
+    bwd_out_b<D>(dar, xr, dzr, orr, T, mu, rs, wslot(smem, 1, WB), wslot(smem, 2, WB), lv, ob, red, lane, wave);
   }
   ln_partials<D>(red, a.part, tid);
+}
+
+// delta[m] = rowsum(a[m] * b[m]) over d bf16 columns, one wave per row (the row-fused fallback's delta)
+__global__ __launch_bounds__(256) void row_dot_kernel(const bf16* a, const bf16* b, int64_t M, int64_t d,
+                                                      float* delta) {
+  const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (m >= M) return;
+  float s = 0.f;
+  for (int64_t c = lane; c < d; c += 64) s = __builtin_fmaf((float)a[m * d + c], (float)b[m * d + c], s);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0) delta[m] = s;
 }
 
 struct InBwdArgs {
@@ -818,13 +844,28 @@ int rs_sas_block_out_bwd(int64_t M, int64_t d, const void* dxn, const int64_t* i
                          const float* mean2, const float* rstd2, const float* ln_w, const void* W2T, const void* W1T,
                          const void* WoT, void* dy2, void* da1, void* dx1, void* dout, float* part, float drop_p,
                          uint64_t salt1, uint64_t salt2, const uint64_t* seed_base, void* stream) {
-  if (!use_chain())
-    return rf_sas_block_out_bwd(M, d, dxn, ids, h1, x1, mean2, rstd2, ln_w, W2T, W1T, WoT, dy2, da1, dx1, dout, part,
-                                drop_p, salt1, salt2, seed_base, stream);
+  return rs_sas_block_out_bwd_delta(M, d, dxn, ids, h1, x1, mean2, rstd2, ln_w, W2T, W1T, WoT, dy2, da1, dx1, dout,
+                                    part, drop_p, salt1, salt2, seed_base, nullptr, nullptr, stream);
+}
+
+int rs_sas_block_out_bwd_delta(int64_t M, int64_t d, const void* dxn, const int64_t* ids, const void* h1,
+                               const void* x1, const float* mean2, const float* rstd2, const float* ln_w,
+                               const void* W2T, const void* W1T, const void* WoT, void* dy2, void* da1, void* dx1,
+                               void* dout, float* part, float drop_p, uint64_t salt1, uint64_t salt2,
+                               const uint64_t* seed_base, const void* o, float* delta, void* stream) {
+  if (!o != !delta) return RS_ERR_ARG;
+  if (!use_chain()) {
+    const int r = rf_sas_block_out_bwd(M, d, dxn, ids, h1, x1, mean2, rstd2, ln_w, W2T, W1T, WoT, dy2, da1, dx1, dout,
+                                       part, drop_p, salt1, salt2, seed_base, stream);
+    if (r || !delta) return r;
+    hipLaunchKernelGGL(rc::row_dot_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+                       (const __bf16*)dout, (const __bf16*)o, M, d, delta);
+    return (int)hipGetLastError();
+  }
   if (M <= 0) return RS_ERR_ARG;
   rc::OutBwdArgs a = {M, (const __bf16*)dxn, ids, (const __bf16*)h1, (const __bf16*)x1, mean2, rstd2, ln_w,
                       (const __bf16*)W2T, (const __bf16*)W1T, (const __bf16*)WoT, (__bf16*)dy2, (__bf16*)da1,
-                      (__bf16*)dx1, (__bf16*)dout, part, drop_p, salt1, salt2, seed_base};
+                      (__bf16*)dx1, (__bf16*)dout, part, drop_p, salt1, salt2, seed_base, (const __bf16*)o, delta};
   const dim3 grid((unsigned)rc::grid_for(M));
   hipStream_t s = (hipStream_t)stream;
   if (d == 64) {

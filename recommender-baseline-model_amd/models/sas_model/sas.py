@@ -488,10 +488,14 @@ class SASEngine:
         g = [dict(dy2=e("dy2", (M, d)), da1=e("da1", (M, d)), dx1=e("dx1", (M, d)), do=e("do", (M, d)),
                   dq=e("dq", (M, d)), dkv=e("dkv", (M, 2 * d))) for _ in range(L)]
 
+        # one head: the out-side backward also forms the attention backward's row term delta = rowsum(dO * O)
+        # (the attention kernels then read neither O nor recompute it)
+        dl = [self.ws.get(f"attn_delta{i}", (B * H * T,), torch.float32) for i in range(L)] if H == 1 else None
+
         def out_bwd_args(i):
             return (ids, s["h1"][i], s["x1"][i], s["mu2"][i], s["r2"][i], self.Wf(f"forward_layernorms.{i}.weight"),
                     wT[i, 5], wT[i, 4], wT[i, 3], g[i]["dy2"], g[i]["da1"], g[i]["dx1"], g[i]["do"], lnp[i, 0], p,
-                    self.salt[f"ffn1_{i}"], self.salt[f"ffn2_{i}"], sb)
+                    self.salt[f"ffn1_{i}"], self.salt[f"ffn2_{i}"], sb, s["o"][i] if dl else None, dl[i] if dl else None)
 
         def in_bwd_args(i):
             return (g[i]["dq"], g[i]["dkv"], g[i]["dx1"], s["x"][i], s["mu1"][i], s["r1"][i],
@@ -502,7 +506,8 @@ class SASEngine:
             pre, fw = f"attention_layers.{i}.", f"forward_layers.{i}."
             dq, dkv, kv = g[i]["dq"], g[i]["dkv"], s["kv"][i]
             ops.attn_bwd(B, T, H, Dh, s["q"][i], kv[:, :d], kv[:, d:], s["o"][i], g[i]["do"], s["lse"][i], dq,
-                         dkv[:, :d], dkv[:, d:], 1.0 / math.sqrt(Dh), 0, ids, p, self.salt[f"attn{i}"], sb, wat)
+                         dkv[:, :d], dkv[:, d:], 1.0 / math.sqrt(Dh), 0, ids, p, self.salt[f"attn{i}"], sb,
+                         dl[i] if dl else wat, delta_in=bool(dl))
             dxi = e("dxi", (M, d))
             ops.sas_block_in_bwd(*in_bwd_args(i), dxi, lnp[i, 1])
             if i > 0:

@@ -190,9 +190,15 @@ def attn_fwd(B, T, H, Dh, q, k, v, o, lse, scale, mask_kind, ids, drop_p, seed, 
          ptr(lse), scale, mask_kind, ptr(ids), drop_p, seed, ptr(seed_base), stream())
 
 
-def attn_bwd(B, T, H, Dh, q, k, v, o, do, lse, dq, dk, dv, scale, mask_kind, ids, drop_p, seed, seed_base, ws):
+RS_ATTN_DELTA_IN = 0x100
+
+
+def attn_bwd(B, T, H, Dh, q, k, v, o, do, lse, dq, dk, dv, scale, mask_kind, ids, drop_p, seed, seed_base, ws,
+             delta_in=False):
+    """delta_in: ws already holds delta = rowsum(dO * O) per (b, h, t) (sas_block_out_bwd with o=)."""
+    mk = mask_kind | (RS_ATTN_DELTA_IN if delta_in else 0)
     call("rs_attn_bwd", dtype_code(q), B, T, H, Dh, ptr(q), ld(q), ptr(k), ld(k), ptr(v), ld(v), ptr(o), ld(o),
-         ptr(do), ld(do), ptr(lse), ptr(dq), ld(dq), ptr(dk), ld(dk), ptr(dv), ld(dv), scale, mask_kind, ptr(ids),
+         ptr(do), ld(do), ptr(lse), ptr(dq), ld(dq), ptr(dk), ld(dk), ptr(dv), ld(dv), scale, mk, ptr(ids),
          drop_p, seed, ptr(seed_base), ptr(ws), stream())
 
 
@@ -416,12 +422,13 @@ def sas_block_out(o, Q, Wo, bo, x1, ln_w, ln_b, eps, z, mean, rstd, W1, b1, h1, 
 
 
 def sas_block_out_bwd(dxn, ids, h1, x1, mean2, rstd2, ln_w, W2T, W1T, WoT, dy2, da1, dx1, dout, part, drop_p, salt1,
-                      salt2, seed_base):
-    """part: fp32 >= 2*d*sas_block_parts(M), receives the LN2 affine partials (ln_partial_segments)."""
+                      salt2, seed_base, o=None, delta=None):
+    """part: fp32 >= 2*d*sas_block_parts(M), receives the LN2 affine partials (ln_partial_segments).  o, delta
+    (one-head attention output [M, d] bf16, fp32 [M]): also delta = rowsum(dout * o) for attn_bwd(delta_in=True)."""
     M, d = dxn.shape
-    call("rs_sas_block_out_bwd", M, d, ptr(dxn), ptr(ids), ptr(h1), ptr(x1), ptr(mean2), ptr(rstd2), ptr(ln_w),
-         ptr(W2T), ptr(W1T), ptr(WoT), ptr(dy2), ptr(da1), ptr(dx1), ptr(dout), ptr(part), drop_p, salt1, salt2,
-         ptr(seed_base), stream())
+    call("rs_sas_block_out_bwd_delta", M, d, ptr(dxn), ptr(ids), ptr(h1), ptr(x1), ptr(mean2), ptr(rstd2),
+         ptr(ln_w), ptr(W2T), ptr(W1T), ptr(WoT), ptr(dy2), ptr(da1), ptr(dx1), ptr(dout), ptr(part), drop_p, salt1,
+         salt2, ptr(seed_base), ptr(o), ptr(delta), stream())
 
 
 def sas_block_in_bwd(dq, dkv, dx1, x, mean1, rstd1, ln_w, WinT, dx, part):

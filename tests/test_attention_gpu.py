@@ -160,3 +160,37 @@ def test_attention_dropout_matches_torch_with_the_kernels_mask(dtype, mask_kind,
     assert rel(dq.float().cpu(), qr.grad.cpu()) < 2 * tol
     assert rel(dkv[:, :d].float().cpu(), kr.grad.cpu()) < 2 * tol
     assert rel(dkv[:, d:].float().cpu(), vr.grad.cpu()) < 2 * tol
+
+
+@pytest.mark.parametrize("mask_kind", [0, 1])
+@pytest.mark.parametrize("B,T,H,Dh,p", [(4, 200, 1, 128, 0.2), (3, 50, 2, 64, 0.0), (2, 37, 1, 32, 0.1)])
+def test_attention_bwd_with_given_delta(mask_kind, B, T, H, Dh, p):
+    """mask_kind | RS_ATTN_DELTA_IN: the backward takes delta = rowsum(dO * O) from the caller (the SAS out-side
+    backward forms it) instead of reading O; same gradients as forming it itself (delta's fp32 summation order is
+    the only difference) and still the torch reference's within the bf16 bound."""
+    import rbm_amd  # noqa: F401
+    from rbm_amd import ops
+    torch.manual_seed(7 + T)
+    d, dev, dt = H * Dh, "cuda", torch.bfloat16
+    ids = torch.randint(1, 50, (B, T), device=dev)
+    ids[0, : T // 3] = 0
+    q = torch.randn(B * T, d, device=dev).to(dt)
+    kv = torch.randn(B * T, 2 * d, device=dev).to(dt)
+    o = torch.empty(B * T, d, device=dev, dtype=dt)
+    lse = torch.empty(B * H * T, device=dev)
+    sc, sb = 1.0 / math.sqrt(Dh), torch.zeros(1, dtype=torch.int64, device=dev)
+    ops.attn_fwd(B, T, H, Dh, q, kv[:, :d], kv[:, d:], o, lse, sc, mask_kind, ids, p, 11, sb)
+    do = torch.randn(B * T, d, device=dev).to(dt)
+    outs = []
+    for given in (False, True):
+        dq, dkv = torch.empty_like(q), torch.empty_like(kv)
+        ws = (do.float() * o.float()).view(B, T, H, Dh).sum(-1).transpose(1, 2).reshape(-1).contiguous() if given \
+            else torch.empty(B * H * T, device=dev)
+        o_arg = torch.full_like(o, float("nan")) if given else o       # O must not be read
+        ops.attn_bwd(B, T, H, Dh, q, kv[:, :d], kv[:, d:], o_arg, do, lse, dq, dkv[:, :d], dkv[:, d:], sc, mask_kind,
+                     ids, p, 11, sb, ws, delta_in=given)
+        outs.append((dq.float(), dkv.float()))
+    torch.cuda.synchronize()
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.isfinite(b).all()
+        assert rel(b.cpu(), a.cpu()) < 1e-2

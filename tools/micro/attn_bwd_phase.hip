@@ -10,7 +10,7 @@
 
 KStamp kstamp_next(int) { return KStamp{nullptr, nullptr, 0}; }
 
-static void run(int B, int T) {
+static void run(int B, int T, float drop, int mk = 0) {
   const int H = 1, Dh = 128, d = 128;
   const size_t M = (size_t)B * T;
   void *q, *kv, *o, *dout, *dq, *dkv;
@@ -25,7 +25,7 @@ static void run(int B, int T) {
   for (int it = 0; it < 5; ++it) {
     hipMemcpyToSymbol(HIP_SYMBOL(g_attn_prof), p.data(), p.size() * 8);   // zero
     attn_lds_bwd(B, T, H, Dh, q, d, kv, 2 * d, (char*)kv + d * 2, 2 * d, o, d, dout, d, lse, dq, d, dkv, 2 * d,
-                 (char*)dkv + d * 2, 2 * d, 0.088f, 0, nullptr, 0.2f, 7, sb, delta, 0);
+                 (char*)dkv + d * 2, 2 * d, 0.088f, mk, nullptr, drop, 7, sb, delta, 0);
   }
   hipDeviceSynchronize();
   hipMemcpyFromSymbol(p.data(), HIP_SYMBOL(g_attn_prof), p.size() * 8);
@@ -44,7 +44,7 @@ static void run(int B, int T) {
       t1 = std::max(t1, f);
     }
   const double u = 0.01;   // 100 MHz ticks -> us
-  printf("B=%d T=%d nsplit=%d blocks=2x%d: span %.2f us\n", B, T, ns, nblk, (t1 - t0) * u);
+  printf("B=%d T=%d p=%.1f delta_in=%d nsplit=%d blocks=2x%d: span %.2f us\n", B, T, drop, mk != 0, ns, nblk, (t1 - t0) * u);
   for (int kind = 0; kind < 2; ++kind) {
     std::vector<double> ent, stg, cmp, fin;
     for (int b = kind * nblk; b < (kind + 1) * nblk; ++b)
@@ -62,7 +62,10 @@ static void run(int B, int T) {
 }
 
 int main() {
-  run(128, 200);
-  run(128, 50);
+  run(128, 200, 0.2f);
+  run(128, 200, 0.2f, RS_ATTN_DELTA_IN);
+  run(128, 200, 0.0f, RS_ATTN_DELTA_IN);
+  run(128, 50, 0.2f);
+  run(128, 50, 0.2f, RS_ATTN_DELTA_IN);
   return 0;
 }
