@@ -52,8 +52,8 @@ struct AttnLdsArgs {
   KStamp ks;                     // backward: dQ kernel stamps begin, dK/dV kernel end
   // backward work plan (causal): per (split, wave) up to PLAN_I items, 0 = none; unused (use_plan 0) -> one
   // tile per wave round robin.  Item = valid << 31 | slot << 26 | role << 24 | chunk end << 16 | chunk begin
-  // << 8 | tile; chunks are 32 keys (dQ) / 32 queries (dK/dV); role 0 = whole tile, 1 = upper half (its
-  // partial goes to LDS slot `slot`), 2 = lower half (adds that slot's partial, then writes the tile)
+  // << 8 | tile; chunks are 32 keys (dQ) / 32 queries (dK/dV); role 0 = whole tile, 1 = lower half (its
+  // partial goes to LDS slot `slot`), 2 = upper half (adds that slot's partial, then writes the tile)
   int use_plan;
   uint32_t plan[PLAN_S][8][PLAN_I];
 };
@@ -127,6 +127,93 @@ __device__ __forceinline__ bf16x8 gload8(const bf16* base, int64_t ld, int64_t r
   const unsigned keep = row < T ? 0xffffffffu : 0u;
   v &= keep;
   return __builtin_bit_cast(bf16x8, v);
+}
+
+// ------------------------------------------------------------------ progressive staging by LDS-DMA
+// The operand images are filled by LDS-DMA (global_load_lds_dwordx4: 64 lanes x 16 B to 1 KB of LDS,
+// lane-linear) in 32-row chunks by ONE loader wave (the workgroup's last), which keeps three chunks in flight
+// and publishes each chunk (an LDS flag) as soon as its own vmcnt says it has landed; the other waves start on
+// the first chunks while the rest stream in, and wait on the loader's flags only where they need a chunk.  The
+// loader issues every DMA itself, so one wave's in-order vmcnt covers them all (no cross-wave publication), and
+// the computing waves have no DMA in flight, so the compiler's vmcnt waits on their own loads stay exact.  The
+// padded image row (DH + 16 elements) is 16-byte granular and a 32-row chunk is a whole number of 1 KB pieces
+// (9 KB at DH = 128), so a piece's lanes that land on a row's pad just load some valid 16 B; rows past T load row
+// T - 1 (finite values; every product with them is masked to 0).  After its stream the loader computes the
+// smaller share the work plan gives it.
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)(lds_ptr_t)p; }
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(dst)
+               : "memory");
+}
+template <int N> __device__ __forceinline__ void vm_wait_n() { asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory"); }
+#define LOADER (NW - 1)   // the loader wave
+#define NCNT 16           // chunk flags (T <= 256: at most 8 chunks), ints, in LDS
+template <int DH> struct DmaStage {
+  static constexpr int ROWB = Img<DH>::LD * 2, CHB = 32 * ROWB, PPC = CHB / 1024, PP = 2 * PPC, WIN = 3;
+  static_assert(CHB % 1024 == 0, "a 32-row chunk is whole DMA pieces");
+  static_assert(WIN * PP <= 63, "chunks in flight fit vmcnt");
+  // all pieces of chunk c of both images (A -> LDS byte address la, B -> lb; head slices, row strides ldA / ldB)
+  static __device__ __forceinline__ void chunk(const bf16* A, int64_t ldA, uint32_t la, const bf16* B, int64_t ldB,
+                                               uint32_t lb, int T, int c, int lane) {
+#pragma unroll
+    for (int j = 0; j < PP; ++j) {
+      const bool second = j >= PPC;
+      const int pj = second ? j - PPC : j;
+      const int off = c * CHB + pj * 1024 + lane * 16;
+      const int row = off / ROWB, o = off - row * ROWB;
+      const int col = o < DH * 2 ? o >> 1 : 0;
+      const int64_t rr = row < T ? row : T - 1;
+      const bf16* src = second ? B + rr * ldB + col : A + rr * ldA + col;
+      dma16(src, __builtin_amdgcn_readfirstlane((second ? lb : la) + (uint32_t)(c * CHB + pj * 1024)));
+    }
+  }
+  // loader, before the prologue barrier: the first WIN chunks
+  static __device__ __forceinline__ void prime(const bf16* A, int64_t ldA, const bf16* imgA, const bf16* B,
+                                               int64_t ldB, const bf16* imgB, int T, int nch, int lane) {
+    const uint32_t la = lds_addr(imgA), lb = lds_addr(imgB);
+    for (int c = 0; c < min(nch, WIN); ++c) chunk(A, ldA, la, B, ldB, lb, T, c, lane);
+  }
+  // loader, after the barrier (the flags are zero): publish chunk c once landed, keep WIN chunks in flight
+  static __device__ __forceinline__ void stream(const bf16* A, int64_t ldA, const bf16* imgA, const bf16* B,
+                                                int64_t ldB, const bf16* imgB, int T, int nch, int* flag, int lane) {
+    const uint32_t la = lds_addr(imgA), lb = lds_addr(imgB);
+    for (int c = 0; c < nch; ++c) {
+      const int later = min(nch, c + WIN) - (c + 1);   // chunks issued after c, still allowed in flight
+      if (later >= 2) vm_wait_n<2 * PP>();
+      else if (later == 1) vm_wait_n<PP>();
+      else vm_wait_n<0>();
+      if (lane == 0) __hip_atomic_store(&flag[c], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (c + WIN < nch) chunk(A, ldA, la, B, ldB, lb, T, c + WIN, lane);
+    }
+  }
+};
+// a computing wave's view of the loader's flags
+struct ChunkWait {
+  const int* flag;
+  int nch, ready;
+  // chunk c (and every earlier one: the loader publishes in order) is in LDS
+  __device__ __forceinline__ void ensure(int c) {
+    c = min(c, nch - 1);
+    if (c <= ready) return;
+    // bounded: a missing flag (a bug) ends in wrong values, not a hung GPU
+    for (int spin = 0; spin < (1 << 22) &&
+                       __hip_atomic_load(&flag[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0;
+         ++spin)
+      __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+    ready = c;
+  }
+};
+// prologue barrier without a memory fence (the fence's vmcnt(0) would wait for the loader's DMAs): LDS writes
+// made before it (flags, key mask, lse / delta rows) are complete and visible after it
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 }
 
 // stage rows [0, rows) of a (T x DH) head slice into an LDS image (rows >= T zero).
@@ -242,7 +329,9 @@ __global__ __launch_bounds__(NT) void attn_fwd_lds_kernel(AttnLdsArgs a) {
   const bf16* Kg = a.k + b * a.T * a.ldk + h * DH;
   const bf16* Vg = a.v + b * a.T * a.ldv + h * DH;
   const bf16* Qg = a.q + b * a.T * a.ldq + h * DH;
-  // the first query tile's operands are requested before (and so arrive with) the K/V staging
+  // the first query tile's operands are requested before (and so arrive with) the K/V staging.  (The forward
+  // keeps all-wave register staging: its longest query tile needs every key chunk at once, so the loader-wave
+  // stream of the backward passes measured slower here: 14.7 vs 12.6 us at B = 128, T = 200.)
   bf16x8 qf[KC];
   {
     const int64_t qrow0 = (split + wave * a.nsplit) * 16 + cl;
@@ -371,7 +460,8 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnLdsArgs& a, int64_t l
   bf16* Ks = reinterpret_cast<bf16*>(smem);
   bf16* Vs = Ks + rows * LD;
   float* km = reinterpret_cast<float*>(Vs + rows * LD);
-  float* slots = km + rows;                            // plan: fp32 partial dQ tiles [slot][DT*4][64]
+  int* cnt = reinterpret_cast<int*>(km + rows);
+  float* slots = km + rows + NCNT;                     // plan: fp32 partial dQ tiles [slot][DT*4][64]
   int* flags = reinterpret_cast<int*>(slots + DQ_SLOTS * DT * 4 * 64);
   const bf16* Qg = a.q + b * a.T * a.ldq + h * DH;
   const bf16* Og = a.o + b * a.T * a.ldo + h * DH;
@@ -393,11 +483,16 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnLdsArgs& a, int64_t l
     return true;
   };
   if (a.use_plan && tid < DQ_SLOTS) flags[tid] = 0;
-  // the first item's q, dO, O rows are requested before (and arrive with) the K/V staging
+  if (tid < NCNT) cnt[tid] = 0;
+  const int nch = rows / 32;
   bf16x8 qf[KC], df[KC], of[KC];
   int qt0 = 0, cb0, ce0, role0, slot0;
   const bool any = item(0, qt0, cb0, ce0, role0, slot0);
-  {
+  const bf16* Kg = a.k + b * a.T * a.ldk + h * DH;
+  const bf16* Vg = a.v + b * a.T * a.ldv + h * DH;
+  if (wave == LOADER) {
+    DmaStage<DH>::prime(Kg, a.ldk, Ks, Vg, a.ldv, Vs, T, nch, lane);
+  } else {   // the first item's q, dO (, O) rows
     const int64_t qrow0 = (any ? qt0 : 0) * 16 + cl;
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
@@ -406,9 +501,10 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnLdsArgs& a, int64_t l
       if (!a.delta_in) of[kc] = gload8(Og, a.ldo, qrow0, a.T, kc * 32 + 8 * g);
     }
   }
-  stage2<DH>(Ks, a.k + b * a.T * a.ldk + h * DH, a.ldk, Vs, a.v + b * a.T * a.ldv + h * DH, a.ldv, a.T, rows, tid);
   stage_keymask(km, a, b, rows, tid);
-  __syncthreads();
+  lds_barrier();
+  if (wave == LOADER) DmaStage<DH>::stream(Kg, a.ldk, Ks, Vg, a.ldv, Vs, T, nch, cnt, lane);
+  ChunkWait ch{cnt, nch, wave == LOADER ? nch - 1 : -1};
   APROF(5);
   const uint64_t seed = eff_seed(a.seed, a.seed_base);
 
@@ -416,7 +512,7 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnLdsArgs& a, int64_t l
   for (int it = 0; item(it, qt, cb, ce, role, slot); ++it) {
     const int q0 = qt * 16;
     const int64_t qrow = q0 + cl;
-    if (it > 0) {
+    if (it > 0 || wave == LOADER) {
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc) {
         qf[kc] = gload8(Qg, a.ldq, qrow, a.T, kc * 32 + 8 * g);
@@ -498,10 +594,12 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnLdsArgs& a, int64_t l
       }
     };
     f32x4 sA, dA, sB, dB, dsA, dsB;
+    ch.ensure(cb);
     sdp(2 * cb, sA, dA);
     for (int c = cb; c < ce; ++c) {
       sdp(2 * c + 1, sB, dB);
       dsv(2 * c, sA, dA, dsA);
+      if (c + 1 < ce) ch.ensure(c + 1);   // the next chunk's rows (once per chunk: a scheduling fence)
       sdp(2 * c + 2, sA, dA);      // past the range on the last chunk: clamped, unused
       dsv(2 * c + 1, sB, dB, dsB);
       const bf16x8 bds = pack8(dsA, dsB);
@@ -515,14 +613,18 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnLdsArgs& a, int64_t l
       for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) sl[(dt * 4 + r) * 64 + lane] = acc[dt][r];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      // LDS-only hand-off: the slot writes precede the flag in this wave's in-order LDS stream (a release fence
+      // would also wait for this wave's DMAs still in flight)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (lane == 0) __hip_atomic_store(&flags[slot], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       continue;
     }
     if (role == 2) {
-      while (__hip_atomic_load(&flags[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+      for (int spin = 0; spin < (1 << 22) &&
+                         __hip_atomic_load(&flags[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0;
+           ++spin)
         __builtin_amdgcn_s_sleep(1);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      asm volatile("" ::: "memory");
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
@@ -596,7 +698,8 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnLdsArgs& a, int64_t 
   float* lse_s = reinterpret_cast<float*>(dOs + rows * LD);
   float* dl_s = lse_s + rows;
   float* km = dl_s + rows;
-  bf16* slots = reinterpret_cast<bf16*>(km + rows);     // plan: bf16 partial (dK, dV) tiles [slot][2][DT*4][64]
+  int* cnt = reinterpret_cast<int*>(km + rows);
+  bf16* slots = reinterpret_cast<bf16*>(km + rows + NCNT);   // plan: bf16 partial (dK, dV) tiles [slot][2][DT*4][64]
   int* flags = reinterpret_cast<int*>(slots + DKV_SLOTS * 2 * DT * 4 * 64);
   const bf16* Kg = a.k + b * a.T * a.ldk + h * DH;
   const bf16* Vg = a.v + b * a.T * a.ldv + h * DH;
@@ -618,46 +721,50 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnLdsArgs& a, int64_t 
     return true;
   };
   if (a.use_plan && tid < DKV_SLOTS) flags[tid] = 0;
-  // everything this workgroup reads before its first MFMA is requested in one batch: the first key
-  // tile's k/v rows, the per-query lse/delta (rows <= 256 <= NT: one per thread), the Q/dO images
+  if (tid < NCNT) cnt[tid] = 0;
+  const int nch = rows / 32;
   bf16x8 kf[KC], vf[KC];
   int kt0 = 0, cb0, ce0, role0, slot0;
   const bool any = item(0, kt0, cb0, ce0, role0, slot0);
-  {
+  const bf16* Qg = a.q + b * a.T * a.ldq + h * DH;
+  const bf16* dOg = a.dout + b * a.T * a.lddo + h * DH;
+  // own_delta: this wave's first two 16-row groups of O, requested with its first operands
+  const bf16* Og = a.o + b * a.T * a.ldo + h * DH;
+  bf16x8 op[2][KC];
+  if (wave == LOADER) {
+    DmaStage<DH>::prime(Qg, a.ldq, Qs, dOg, a.lddo, dOs, T, nch, lane);
+  } else {   // the first key tile's k/v rows
     const int64_t key0 = (any ? kt0 : 0) * 16 + cl;
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
       kf[kc] = gload8(Kg, a.ldk, key0, a.T, kc * 32 + 8 * g);
       vf[kc] = gload8(Vg, a.ldv, key0, a.T, kc * 32 + 8 * g);
     }
-  }
-  const int ti = min(tid, T - 1);            // branch-free: clamped load, masked value
-  float lse_v = a.lse[bh * a.T + ti] * LOG2E, dl_v = own_delta ? 0.f : a.delta[bh * a.T + ti];
-  if (tid >= T) lse_v = dl_v = 0.f;
-  // own_delta: this wave's first two 16-row groups of O, requested with the staging loads
-  const bf16* Og = a.o + b * a.T * a.ldo + h * DH;
-  bf16x8 op[2][KC];
-  if (own_delta) {
+    if (own_delta) {
 #pragma unroll
-    for (int k = 0; k < 2; ++k)
+      for (int k = 0; k < 2; ++k)
 #pragma unroll
-      for (int kc = 0; kc < KC; ++kc) op[k][kc] = gload8(Og, a.ldo, (wave + k * NW) * 16 + cl, a.T, kc * 32 + 8 * g);
+        for (int kc = 0; kc < KC; ++kc) op[k][kc] = gload8(Og, a.ldo, (wave + k * NW) * 16 + cl, a.T, kc * 32 + 8 * g);
+    }
   }
-  stage2<DH>(Qs, a.q + b * a.T * a.ldq + h * DH, a.ldq, dOs, a.dout + b * a.T * a.lddo + h * DH, a.lddo, a.T, rows,
-             tid);
-  if (tid < rows) {
-    lse_s[tid] = lse_v;
-    dl_s[tid] = dl_v;
+  if (tid < rows) {   // per-query lse / delta (rows <= 256: waves 0..3, never the loader)
+    const int ti = min(tid, T - 1);
+    const float lse_v = a.lse[bh * a.T + ti] * LOG2E, dl_v = own_delta ? 0.f : a.delta[bh * a.T + ti];
+    lse_s[tid] = tid < T ? lse_v : 0.f;
+    dl_s[tid] = tid < T ? dl_v : 0.f;
   }
   stage_keymask(km, a, b, rows, tid);
-  __syncthreads();
+  lds_barrier();
+  if (wave == LOADER) DmaStage<DH>::stream(Qg, a.ldq, Qs, dOg, a.lddo, dOs, T, nch, cnt, lane);
+  ChunkWait ch{cnt, nch, wave == LOADER ? nch - 1 : -1};
   if (own_delta) {
+    ch.ensure(nch - 1);   // the whole dO image
     for (int k = 0, rg = wave; rg * 16 < rows; ++k, rg += NW) {
       const int row = rg * 16 + cl;
       bf16x8 of[KC];
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc)
-        of[kc] = k == 0 ? op[0][kc] : k == 1 ? op[1][kc] : gload8(Og, a.ldo, row, a.T, kc * 32 + 8 * g);
+        of[kc] = (k < 2 && wave != LOADER) ? op[k][kc] : gload8(Og, a.ldo, row, a.T, kc * 32 + 8 * g);
       float dl = 0.f;
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc) {
@@ -680,7 +787,7 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnLdsArgs& a, int64_t 
   for (int it = 0; item(it, kt, cb, ce, role, slot); ++it) {
     const int64_t key = kt * 16 + cl;  // this lane's key
     const int ki = kt * 16 + cl;
-    if (it > 0) {
+    if (it > 0 || wave == LOADER) {
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc) {
         kf[kc] = gload8(Kg, a.ldk, key, a.T, kc * 32 + 8 * g);
@@ -743,10 +850,12 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnLdsArgs& a, int64_t 
       }
     };
     f32x4 sA, dA, sB, dB, pdA, dsA, pdB, dsB;
+    ch.ensure(cb);
     sdp(2 * cb, sA, dA);
     for (int c = cb; c < ce; ++c) {
       sdp(2 * c + 1, sB, dB);
       pds(2 * c, sA, dA, pdA, dsA);
+      if (c + 1 < ce) ch.ensure(c + 1);
       sdp(2 * c + 2, sA, dA);
       pds(2 * c + 1, sB, dB, pdB, dsB);
       const bf16x8 bp = pack8(pdA, pdB);
@@ -767,14 +876,16 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnLdsArgs& a, int64_t 
           sl[(dt * 4 + r) * 64 + lane] = (bf16)dk[dt][r];
           sl[(DT * 4 + dt * 4 + r) * 64 + lane] = (bf16)dv[dt][r];
         }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // LDS-only hand-off (see the dQ pass)
       if (lane == 0) __hip_atomic_store(&flags[slot], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       continue;
     }
     if (role == 2) {
-      while (__hip_atomic_load(&flags[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+      for (int spin = 0; spin < (1 << 22) &&
+                         __hip_atomic_load(&flags[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0;
+           ++spin)
         __builtin_amdgcn_s_sleep(1);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      asm volatile("" ::: "memory");
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
@@ -824,12 +935,12 @@ __global__ __launch_bounds__(NT) void attn_bwd_lds_kernel(AttnLdsArgs aq, AttnLd
 template <int DH>
 static size_t fwd_lds_bytes(int T) {
   const int rows = ((T + 31) / 32) * 32;
-  return (size_t)2 * rows * Img<DH>::LD * 2 + rows * 4;
+  return (size_t)2 * rows * Img<DH>::LD * 2 + rows * 4 + NCNT * 4;
 }
 template <int DH>
 static size_t dkv_lds_bytes(int T) {
   const int rows = ((T + 31) / 32) * 32;
-  return (size_t)2 * rows * Img<DH>::LD * 2 + 3 * rows * 4;
+  return (size_t)2 * rows * Img<DH>::LD * 2 + 3 * rows * 4 + NCNT * 4;
 }
 
 static int pick_split(int64_t BH, int ntiles) {
@@ -873,12 +984,13 @@ static hipError_t fwd_t(AttnLdsArgs& a, hipStream_t s) {
 // Causal backward work plan.  Round robin gives a wave one whole tile: the dQ tile of the last queries
 // scans every key (13 key tiles at T = 200) while the mean is half that, and the workgroup waits for its
 // longest wave.  Here the longest tiles (up to `slots` of them) are cut in two halves of their chunk range
-// -- the upper half's wave leaves a partial in an LDS slot for the lower half's wave, which adds it and
+// -- the lower half's wave leaves a partial in an LDS slot for the upper half's wave, which adds it and
 // writes the tile -- and the items are dealt longest-first to the least-loaded wave, writers first in each
 // wave's list (a reader only ever waits for a writer, so there is no cycle).  Measured at B = 128, T = 200
 // (tools/micro/attn_bwd_phase.hip): the slowest wave did ~2x the mean work; balanced, the dK/dV pass's
 // slowest wave went 14.5 -> 12.5 us, the dQ pass's barely moved -- with every wave busy the workgroup is
 // bound by the CU's LDS operand traffic (one 1 KB fragment read per MFMA), not by its longest wave.
+#define LOADER_HANDICAP 3   // plan chunks the loader's staging stream is worth
 struct PlanItem {
   int tile, cb, ce, role, slot;
 };
@@ -903,15 +1015,17 @@ static bool make_plan(AttnLdsArgs& a, int ntiles, bool dkv, int slots) {
       const int w = it.ce - it.cb;
       if (w < 2) break;
       const int hmid = it.cb + (w + 1) / 2;
-      items[n++] = PlanItem{it.tile, hmid, it.ce, 1, used};   // upper half: writer
+      // lower half: writer (its chunks are staged first, so it starts early); upper half: reader (dealt last)
+      items[n++] = PlanItem{it.tile, hmid, it.ce, 2, used};
       it.ce = hmid;
-      it.role = 2;                                              // lower half: reader
+      it.role = 1;
       it.slot = used++;
     }
     std::sort(items, items + n, [](const PlanItem& x, const PlanItem& y) {
       return x.ce - x.cb != y.ce - y.cb ? x.ce - x.cb > y.ce - y.cb : x.tile < y.tile;
     });
     int load[NW] = {0}, cnt[NW] = {0};
+    load[LOADER] = LOADER_HANDICAP;   // the loader wave streams the operand images first
     PlanItem lists[NW][PLAN_I];
     for (int k = 0; k < n; ++k) {
       int w = 0;

@@ -1,6 +1,6 @@
 """The causal attention backward's work plan (attention_lds.hip make_plan, read through the host-only
 rs_attn_bwd_plan; no GPU): every (tile, chunk) pair of every split is covered exactly once, each split tile's
-two halves share one LDS slot (writer = upper half, reader = lower half), writers precede whole tiles and
+two halves share one LDS slot (writer = lower half, reader = upper half), writers precede whole tiles and
 readers in every wave's list, and the slowest wave does less than the round-robin dealing's worst wave and at most
 2 chunks over the even share."""
 import ctypes as C
@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 PLAN_S, NW, PLAN_I = 4, 8, 6
+HANDICAP = 3   # attention_lds.hip LOADER_HANDICAP: plan chunks the loader wave's staging stream is worth
 
 
 def plan(B, T, H, dkv):
@@ -67,9 +68,10 @@ def test_plan_invariants(B, T, H, dkv):
             (_, t1, b1, e1), (_, t2, b2, e2) = sorted(items)
             assert t1 == t2 and (e2 == b1 or e1 == b2)            # two halves of one tile
             writer = [it for it in items if it[0] == 1][0]
-            assert writer[2] > min(b1, b2)                         # the writer holds the upper half
-        assert max(loads) < max(rr)                          # better than round robin's slowest wave
-        assert max(loads) <= -(-total // NW) + 2             # near the even share
+            assert writer[2] == min(b1, b2)                        # the writer holds the lower half
+        loads[NW - 1] += HANDICAP                            # the loader wave streams the operand images first
+        assert max(loads) < max(rr) + HANDICAP               # better than round robin's slowest wave
+        assert max(loads) <= -(-(total + HANDICAP) // NW) + 2   # near the even share
 
 
 def test_plan_falls_back_for_short_sequences():
