@@ -9,10 +9,12 @@
 //
 //   rs_item_index_build: keys (ids | pos | neg) -> stable counting sort of the entries by key:
 //                        per-512-entry-block key histograms (LDS), per-key exclusive prefix over
-//                        blocks, a scan over keys, then each block places its entries with a
-//                        block radix sort for the in-block rank.  When the per-block histogram
-//                        table would exceed 2^26 ints a device radix sort (rocPRIM) is used
-//                        instead.  -> start[v] for v <= V
+//                        blocks, a two-level scan over keys (group sums of 64 keys, one workgroup
+//                        scanning the groups, a wave scan per group), then each block places its
+//                        entries by a bitonic sort of (key, index) words in LDS for the in-block
+//                        rank -- all hand-written.  Only beyond the counting sort's reach (per-block
+//                        histogram table over 2^26 ints, or keys over 22 bits; no benchmarked shape)
+//                        is a library device radix sort (rocPRIM) used.  -> start[v] for v <= V
 //   rs_item_grad:        chunks of 64 sorted entries: contribution rows summed per key run in
 //                        LDS; a key wholly inside one chunk is written by that chunk (+=); a
 //                        key spanning chunks leaves per-chunk partials that the chunk holding
@@ -31,6 +33,9 @@ constexpr int CH = 64;          // sorted entries per gradient chunk
 constexpr int BE = 512;         // entries per counting-sort block (512: 150 blocks at cfg2, 1024 took 75)
 constexpr int VMAX_LDS = 32768;            // largest table for the LDS histogram
 constexpr int64_t HMAX = (int64_t)1 << 26;  // largest per-block histogram table (ints) for the counting sort
+constexpr int IBITS = 9;                    // BE = 2^IBITS: an entry's block index in the sort word's low bits
+constexpr int KBITS_MAX = 32 - IBITS - 1;   // key bits the counting-sort path's (key, index) sort word holds
+static_assert(BE == 1 << IBITS, "sort word layout");
 
 struct Layout {
   int64_t n, nchunks, nb, V;
@@ -51,7 +56,7 @@ static hipError_t layout(int nsrc, int64_t rows, int64_t table_rows, int64_t d, 
   L.nchunks = cdiv(L.n, CH);
   L.nb = cdiv(L.n, BE);
   L.V = table_rows;
-  L.cs = L.nb * table_rows <= HMAX;
+  L.cs = L.nb * table_rows <= HMAX && key_bits(table_rows) <= KBITS_MAX;
   size_t o = 0;
   L.sk = o; o = al256(o + L.n * 4);
   L.sv = o; o = al256(o + L.n * 4);
@@ -62,13 +67,9 @@ static hipError_t layout(int nsrc, int64_t rows, int64_t table_rows, int64_t d, 
     L.H = o; o = al256(o + L.nb * table_rows * 4);
     L.total = o; o = al256(o + (table_rows + 1) * 4);   // [V] = 0: the scan's last entry is the total
     L.keys_in = L.vals_in = 0;
-    L.temp = o;
-    size_t tb = 0;
-    const hipError_t e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const int*)nullptr, (int*)nullptr,
-                                                          (int)(table_rows + 1), (hipStream_t)0);
-    if (e != hipSuccess) return e;
-    L.temp_bytes = tb;
-    o = al256(o + tb);
+    L.temp = o;                                          // group sums of the key scan: cdiv(V, 64) + 1 ints
+    L.temp_bytes = (size_t)(cdiv(table_rows, 64) + 1) * 4;
+    o = al256(o + L.temp_bytes);
   } else {
     L.H = L.total = 0;
     L.keys_in = o; o = al256(o + L.n * 4);
@@ -136,7 +137,7 @@ __global__ __launch_bounds__(256) void hist_global_kernel(Keys K, int* __restric
 // H[b][v] <- sum_{b' < b} H[b'][v];  total[v] = sum_b H[b][v].  Workgroup = 64 keys (lanes) x 4
 // waves, wave w owning a contiguous quarter of the block range; quarters combined through LDS.
 __global__ __launch_bounds__(256) void prefix_blocks_kernel(int* __restrict__ H, int64_t nb, int64_t V,
-                                                            int* __restrict__ total) {
+                                                            int* __restrict__ total, int* __restrict__ gsum) {
   __shared__ int part[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t v = (int64_t)blockIdx.x * 64 + lane;
@@ -157,8 +158,14 @@ __global__ __launch_bounds__(256) void prefix_blocks_kernel(int* __restrict__ H,
   __syncthreads();
   int off = 0;
   for (int x = 0; x < w; ++x) off += part[x][lane];
+  if (w == 3) {   // this group of 64 keys: per-key totals and their sum (the key scan's group sums)
+    int t = v < V ? off + acc : 0;
+    if (v < V) total[v] = t;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+    if (lane == 0) gsum[blockIdx.x] = t;
+  }
   if (v >= V) return;
-  if (w == 3) total[v] = off + acc;
   for (int64_t b = b0; b < b1; b += U) {
 #pragma unroll
     for (int u = 0; u < U; ++u) h[u] = b + u < b1 ? H[(b + u) * V + v] : 0;
@@ -170,42 +177,84 @@ __global__ __launch_bounds__(256) void prefix_blocks_kernel(int* __restrict__ H,
   }
 }
 
-// start[v] = sum_{v' < v} total[v'] (v <= V): one workgroup
-// each block places its entries: rank inside the block by a stable block radix sort
+// exclusive scan of the group sums in place (G groups of 64 keys; gsum[G] = the grand total): one workgroup,
+// each thread a contiguous run of groups
+__global__ __launch_bounds__(1024) void scan_groups_kernel(int* __restrict__ gsum, int64_t G) {
+  __shared__ int ts[1024];
+  const int tid = threadIdx.x;
+  const int64_t per = cdiv(G, 1024), g0 = tid * per, g1 = min(G, g0 + per);
+  int s = 0;
+  for (int64_t g = g0; g < g1; ++g) s += gsum[g];
+  ts[tid] = s;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {     // inclusive Hillis-Steele scan of the thread sums
+    const int x = tid >= o ? ts[tid - o] : 0;
+    __syncthreads();
+    ts[tid] += x;
+    __syncthreads();
+  }
+  int off = ts[tid] - s;
+  for (int64_t g = g0; g < g1; ++g) {
+    const int x = gsum[g];
+    gsum[g] = off;
+    off += x;
+  }
+  if (tid == 1023) gsum[G] = ts[1023];
+}
+
+// start[v] = sum_{v' < v} total[v'] for v <= V: one wave per group of 64 keys, the group's offset plus an
+// exclusive wave scan of its totals (total[V] = 0, so start[V] is the grand total)
+__global__ __launch_bounds__(256) void start_kernel(const int* __restrict__ total, const int* __restrict__ gsum,
+                                                    int64_t V, int* __restrict__ start) {
+  const int lane = threadIdx.x & 63;
+  const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), v = g * 64 + lane;
+  if (g * 64 > V) return;
+  const int t = v < V ? total[v] : 0;
+  int x = t;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (v <= V) start[v] = gsum[g] + x - t;
+}
+
+// each block places its entries: the stable rank inside the block comes from a bitonic sort of the block's
+// (key << IBITS | index) words in LDS (keys <= KBITS_MAX bits; unused slots sort last)
 __global__ __launch_bounds__(256) void place_kernel(Keys K, const int* __restrict__ H, const int* __restrict__ start,
-                                                    int bits, uint32_t* __restrict__ sk, uint32_t* __restrict__ sv) {
-  typedef hipcub::BlockRadixSort<uint32_t, 256, BE / 256, uint32_t> BRS;
-  __shared__ typename BRS::TempStorage tmp;
-  __shared__ uint32_t sorted[BE];
+                                                    uint32_t* __restrict__ sk, uint32_t* __restrict__ sv) {
+  __shared__ uint32_t w[BE];
   const int tid = threadIdx.x;
   const int64_t e0 = (int64_t)blockIdx.x * BE;
   const int cnt = (int)min((int64_t)BE, K.n - e0);
-  uint32_t key[BE / 256], idx[BE / 256];
-#pragma unroll
-  for (int i = 0; i < BE / 256; ++i) {
-    const int l = tid * (BE / 256) + i;
-    idx[i] = (uint32_t)l;
-    key[i] = l < cnt ? K.get(e0 + l) : 0xffffffffu;
-  }
-  BRS(tmp).Sort(key, idx, 0, bits);
-#pragma unroll
-  for (int i = 0; i < BE / 256; ++i) sorted[tid * (BE / 256) + i] = key[i];
+  for (int l = tid; l < BE; l += 256) w[l] = l < cnt ? (K.get(e0 + l) << IBITS | (uint32_t)l) : 0xffffffffu;
+  for (int k = 2; k <= BE; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      __syncthreads();
+      for (int t = tid; t < BE; t += 256) {
+        const int u = t ^ j;
+        if (u > t) {
+          const uint32_t a = w[t], b = w[u];
+          if ((a > b) == ((t & k) == 0)) {
+            w[t] = b;
+            w[u] = a;
+          }
+        }
+      }
+    }
   __syncthreads();
   const int* h = H + (int64_t)blockIdx.x * K.V;
-#pragma unroll
-  for (int i = 0; i < BE / 256; ++i) {
-    const int j = tid * (BE / 256) + i;
-    if ((int)idx[i] >= cnt) continue;
-    const uint32_t k = key[i];
-    int lo = 0, hi = j;                       // first position of k in the sorted block
+  for (int j = tid; j < cnt; j += 256) {
+    const uint32_t x = w[j], k = x >> IBITS;
+    int lo = 0, hi = j;                       // first position of key k in the sorted block
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
-      if (sorted[mid] < k) lo = mid + 1;
+      if ((w[mid] >> IBITS) < k) lo = mid + 1;
       else hi = mid;
     }
     const int64_t pos = (int64_t)start[k] + h[k] + (j - lo);
     sk[pos] = k;
-    sv[pos] = (uint32_t)(e0 + idx[i]);
+    sv[pos] = (uint32_t)(e0 + (x & (BE - 1)));
   }
 }
 
@@ -467,14 +516,14 @@ int rs_item_index_build(int nsrc, const int64_t* keys0, const int64_t* keys1, co
       if ((e = hipMemsetAsync(H, 0, (size_t)L.nb * table_rows * 4, s)) != hipSuccess) return (int)e;
       hipLaunchKernelGGL(ig::hist_global_kernel, dim3((unsigned)L.nb), dim3(256), 0, s, K, H);
     }
-    hipLaunchKernelGGL(ig::prefix_blocks_kernel, dim3((unsigned)cdiv(table_rows, 64)), dim3(256), 0, s, H, L.nb,
-                       table_rows, total);
-    // start[v] = exclusive prefix of the per-key totals (a decoupled-lookback device scan over V+1 entries)
-    size_t tb = L.temp_bytes;
-    if ((e = hipcub::DeviceScan::ExclusiveSum((void*)(w + L.temp), tb, total, start, (int)(table_rows + 1), s)) !=
-        hipSuccess)
-      return (int)e;
-    hipLaunchKernelGGL(ig::place_kernel, dim3((unsigned)L.nb), dim3(256), 0, s, K, H, start, bits, sk, sv);
+    int* gsum = (int*)(w + L.temp);
+    const int64_t G = cdiv(table_rows, 64);
+    hipLaunchKernelGGL(ig::prefix_blocks_kernel, dim3((unsigned)G), dim3(256), 0, s, H, L.nb, table_rows, total, gsum);
+    // start[v] = exclusive prefix of the per-key totals: group offsets, then a wave scan per group of 64 keys
+    hipLaunchKernelGGL(ig::scan_groups_kernel, dim3(1), dim3(1024), 0, s, gsum, G);
+    hipLaunchKernelGGL(ig::start_kernel, dim3((unsigned)cdiv(G + 1, 4)), dim3(256), 0, s, total, gsum, table_rows,
+                       start);
+    hipLaunchKernelGGL(ig::place_kernel, dim3((unsigned)L.nb), dim3(256), 0, s, K, H, start, sk, sv);
     return (int)hipGetLastError();
   }
   uint32_t* kin = (uint32_t*)(w + L.keys_in);
