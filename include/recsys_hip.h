@@ -135,6 +135,11 @@ int rs_attn_fwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t Dh, const vo
  * already holds delta[(b*H+h)*T + t] = rowsum(dO * O) over the head's columns (rs_sas_block_out_bwd with o given
  * forms it); the bf16 LDS path then reads neither O nor recomputes it (other paths recompute it into ws). */
 #define RS_ATTN_DELTA_IN 0x100
+/* delta[(b*H+h)*T + t] = rowsum over head h's Dh columns of dout * o (values as stored; dtype as rs_attn_bwd) --
+ * the RS_ATTN_DELTA_IN input when no fused kernel forms it (BERT: after the output projection's input gradient,
+ * bert_modules/attention/multi_head.py + single.py reversed). */
+int rs_attn_row_delta(int dtype, int64_t B, int64_t T, int64_t H, int64_t Dh, const void* dout, int64_t lddo,
+                      const void* o, int64_t ldo, float* delta, void* stream);
 int rs_attn_bwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t Dh, const void* q, int64_t ldq,
                 const void* k, int64_t ldk, const void* v, int64_t ldv, const void* o, int64_t ldo,
                 const void* dout, int64_t lddo, const float* lse, void* dq, int64_t lddq, void* dk,

@@ -461,7 +461,72 @@ static int vec_ok(int dtype, int64_t Dh, const void* const* ptrs, int np, const 
   return 1;
 }
 
+// delta[(b*H + h)*T + t] = sum over the head's Dh columns of dO * O (the attention backward's row term), one wave
+// per (token row, head); the values as stored (bf16 or fp32)
+template <typename E>
+__global__ __launch_bounds__(256) void row_delta_kernel(int64_t M, int64_t T, int64_t H, int64_t Dh, const E* dout,
+                                                        int64_t lddo, const E* o, int64_t ldo, float* delta) {
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (w >= M * H) return;
+  const int64_t m = w / H, h = w % H;
+  const E* a = dout + m * lddo + h * Dh;
+  const E* b = o + m * ldo + h * Dh;
+  float s = 0.f;
+  for (int64_t c = lane; c < Dh; c += 64) s = __builtin_fmaf((float)a[c], (float)b[c], s);
+#pragma unroll
+  for (int x = 32; x > 0; x >>= 1) s += __shfl_xor(s, x, 64);
+  if (lane == 0) {
+    const int64_t bb = m / T, t = m % T;
+    delta[(bb * H + h) * T + t] = s;
+  }
+}
+
+// bf16, Dh a multiple of 8 and 16-byte aligned rows: 16 lanes per (row, head), 16 B per lane per step
+__global__ __launch_bounds__(256) void row_delta_v8_kernel(int64_t M, int64_t T, int64_t H, int64_t Dh,
+                                                           const __bf16* dout, int64_t lddo, const __bf16* o,
+                                                           int64_t ldo, float* delta) {
+  const int64_t w = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;   // (row, head) of this 16-lane group
+  const int l = threadIdx.x & 15;
+  const bool ok = w < M * H;
+  const int64_t ww = ok ? w : M * H - 1;
+  const int64_t m = ww / H, h = ww % H;
+  const __bf16* a = dout + m * lddo + h * Dh;
+  const __bf16* b = o + m * ldo + h * Dh;
+  float s = 0.f;
+  for (int64_t c = 8 * l; c < Dh; c += 128) {
+    const bf16x8 x = *reinterpret_cast<const bf16x8*>(a + c), y = *reinterpret_cast<const bf16x8*>(b + c);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s = __builtin_fmaf((float)x[j], (float)y[j], s);
+  }
+#pragma unroll
+  for (int x = 8; x > 0; x >>= 1) s += __shfl_xor(s, x, 64);
+  if (ok && l == 0) {
+    const int64_t bb = m / T, t = m % T;
+    delta[(bb * H + h) * T + t] = s;
+  }
+}
+
 extern "C" {
+
+int rs_attn_row_delta(int dtype, int64_t B, int64_t T, int64_t H, int64_t Dh, const void* dout, int64_t lddo,
+                      const void* o, int64_t ldo, float* delta, void* stream) {
+  if (B <= 0 || T <= 0 || H <= 0 || Dh <= 0 || !dout || !o || !delta) return RS_ERR_ARG;
+  const int64_t M = B * T;
+  const dim3 grid((unsigned)((M * H + 3) / 4));
+  hipStream_t s = (hipStream_t)stream;
+  const bool v8 = Dh % 8 == 0 && lddo % 8 == 0 && ldo % 8 == 0 && ((uintptr_t)dout & 15) == 0 && ((uintptr_t)o & 15) == 0;
+  if (dtype == RS_DTYPE_BF16 && v8)
+    hipLaunchKernelGGL(row_delta_v8_kernel, dim3((unsigned)((M * H * 16 + 255) / 256)), dim3(256), 0, s, M, T, H,
+                       Dh, (const __bf16*)dout, lddo, (const __bf16*)o, ldo, delta);
+  else if (dtype == RS_DTYPE_BF16)
+    hipLaunchKernelGGL(row_delta_kernel<__bf16>, grid, dim3(256), 0, s, M, T, H, Dh, (const __bf16*)dout, lddo,
+                       (const __bf16*)o, ldo, delta);
+  else
+    hipLaunchKernelGGL(row_delta_kernel<float>, grid, dim3(256), 0, s, M, T, H, Dh, (const float*)dout, lddo,
+                       (const float*)o, ldo, delta);
+  return (int)hipGetLastError();
+}
 
 int rs_attn_fwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t Dh, const void* q, int64_t ldq,
                 const void* k, int64_t ldk, const void* v, int64_t ldv, void* o, int64_t ldo, float* lse,

@@ -299,9 +299,12 @@ class BERTEngine:
             ops.linear_dgrad(dyo, self.W(pre + "attention.output_linear.weight"), do)
             qkv = a["qkv"]
             dqkv = e((M, 3 * d))
+            # the attention backward's row term delta = rowsum(dO * O) per head, formed once here: neither
+            # attention pass then reads O, and the dK/dV pass streams its Q/dO images while it computes
+            ops.attn_row_delta(B, T, H, Dh, do, a["o"], wat)
             ops.attn_bwd(B, T, H, Dh, qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], a["o"], do, a["lse"],
                          dqkv[:, :d], dqkv[:, d:2 * d], dqkv[:, 2 * d:], 1.0 / math.sqrt(Dh), 1, ids, s["p"],
-                         self.salt[f"attn{i}"], sb, wat)
+                         self.salt[f"attn{i}"], sb, wat, delta_in=True)
             dh = e((M, d))
             if self.qkv_fused:
                 wgrad(dqkv, a["h"], self.Wqkv(i, grad), self.bqkv(i, grad))

@@ -193,6 +193,11 @@ def attn_fwd(B, T, H, Dh, q, k, v, o, lse, scale, mask_kind, ids, drop_p, seed, 
 RS_ATTN_DELTA_IN = 0x100
 
 
+def attn_row_delta(B, T, H, Dh, do, o, delta):
+    """delta[(b*H+h)*T + t] = sum over head h's columns of do * o (the input of attn_bwd(delta_in=True))."""
+    call("rs_attn_row_delta", dtype_code(do), B, T, H, Dh, ptr(do), ld(do), ptr(o), ld(o), ptr(delta), stream())
+
+
 def attn_bwd(B, T, H, Dh, q, k, v, o, do, lse, dq, dk, dv, scale, mask_kind, ids, drop_p, seed, seed_base, ws,
              delta_in=False):
     """delta_in: ws already holds delta = rowsum(dO * O) per (b, h, t) (sas_block_out_bwd with o=)."""

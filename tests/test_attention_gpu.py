@@ -184,8 +184,11 @@ def test_attention_bwd_with_given_delta(mask_kind, B, T, H, Dh, p):
     outs = []
     for given in (False, True):
         dq, dkv = torch.empty_like(q), torch.empty_like(kv)
-        ws = (do.float() * o.float()).view(B, T, H, Dh).sum(-1).transpose(1, 2).reshape(-1).contiguous() if given \
-            else torch.empty(B * H * T, device=dev)
+        ws = torch.empty(B * H * T, device=dev)
+        if given:   # rs_attn_row_delta, checked against torch
+            ops.attn_row_delta(B, T, H, Dh, do, o, ws)
+            ref = (do.float() * o.float()).view(B, T, H, Dh).sum(-1).transpose(1, 2).reshape(-1)
+            assert rel(ws.cpu(), ref.cpu()) < 1e-5
         o_arg = torch.full_like(o, float("nan")) if given else o       # O must not be read
         ops.attn_bwd(B, T, H, Dh, q, kv[:, :d], kv[:, d:], o_arg, do, lse, dq, dkv[:, :d], dkv[:, d:], sc, mask_kind,
                      ids, p, 11, sb, ws, delta_in=given)
@@ -194,3 +197,19 @@ def test_attention_bwd_with_given_delta(mask_kind, B, T, H, Dh, p):
     for a, b in zip(outs[0], outs[1]):
         assert torch.isfinite(b).all()
         assert rel(b.cpu(), a.cpu()) < 1e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("B,T,H,Dh", [(2, 37, 2, 64), (3, 20, 1, 50), (2, 9, 3, 128)])
+def test_attn_row_delta_matches_torch(dtype, B, T, H, Dh):
+    """rs_attn_row_delta (the RS_ATTN_DELTA_IN input BERT forms after its output projection's input gradient):
+    vectorised (bf16, Dh % 8 == 0) and scalar forms against torch."""
+    import rbm_amd  # noqa: F401
+    from rbm_amd import ops
+    torch.manual_seed(B + T + H + Dh)
+    do = torch.randn(B * T, H * Dh, device="cuda").to(dtype)
+    o = torch.randn(B * T, H * Dh, device="cuda").to(dtype)
+    ws = torch.empty(B * H * T, device="cuda")
+    ops.attn_row_delta(B, T, H, Dh, do, o, ws)
+    ref = (do.double() * o.double()).view(B, T, H, Dh).sum(-1).transpose(1, 2).reshape(-1)
+    assert rel(ws.cpu(), ref.cpu()) < 1e-5
