@@ -12,7 +12,10 @@ import os
 import torch  # noqa: F401  (must be loaded before the HIP library)
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "librecsys_hip.so")
+# RS_LIB_VARIANT=x loads librecsys_hip.x.so from the package directory instead (A/B timing of two builds in one
+# GPU session; the default is the in-tree build)
+LIB_PATH = os.path.join(PKG, "librecsys_hip.so" if not os.environ.get("RS_LIB_VARIANT")
+                        else f"librecsys_hip.{os.environ['RS_LIB_VARIANT']}.so")
 
 F32, BF16 = 0, 1
 

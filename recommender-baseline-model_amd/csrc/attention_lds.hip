@@ -362,19 +362,26 @@ __global__ __launch_bounds__(NT) void attn_fwd_lds_kernel(AttnLdsArgs a) {
       if (kt < nkt) {
 #pragma unroll
         for (int kc = 0; kc < KC; ++kc) s[kt] = mfma16(row_frag(Ks, LD, kt * 16 + cl, kc * 32 + 8 * g), qf[kc], s[kt]);
-        // per-element masking only where a tile can hold masked scores (wave-uniform test)
+        // per-element masking only where a tile can hold masked scores (wave-uniform test); selects, not
+        // exec-mask branches (the key-padding flags are one vector load, 0 when causal)
         const bool need = a.mask_kind != 0 || kt == qt || kt * 16 + 16 > T;
         const int kb = kt * 16 + 4 * g;
+        if (need) {
+          const f32x4 kmv = *reinterpret_cast<const f32x4*>(km + kb);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float x = s[kt][r] * sl2;
-          if (need) {
+          for (int r = 0; r < 4; ++r) {
             const int k = kb + r;
-            if (k >= T || (a.mask_kind == 0 && k > qi)) x = NEG_INF;
-            else if (a.mask_kind == 1 && km[k] != 0.f) x = MASK2;
+            const bool dead = (k >= T) | ((a.mask_kind == 0) & (k > qi));
+            const float x = s[kt][r] * sl2;
+            s[kt][r] = dead ? NEG_INF : (kmv[r] != 0.f ? MASK2 : x);
+            mx = fmaxf(mx, s[kt][r]);
           }
-          s[kt][r] = x;
-          mx = fmaxf(mx, x);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            s[kt][r] *= sl2;
+            mx = fmaxf(mx, s[kt][r]);
+          }
         }
       }
     }
