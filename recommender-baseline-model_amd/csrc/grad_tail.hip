@@ -34,7 +34,7 @@ __global__ __launch_bounds__(256) void reduce_span_kernel(wg::RArgs r, int rblk,
   __shared__ float4 red[wg::RED_G][wg::RED_C];
   if ((int)blockIdx.x < rblk) {
     if (cols) wg::reduce_cols_block(r, blockIdx.x);
-    else wg::reduce_segments_block(r, blockIdx.x, red);
+    else wg::reduce_any_block(r, blockIdx.x, red);
   } else {
     ig::item_span<D>(g, nchunks, (int64_t)blockIdx.x - rblk);
   }
@@ -55,7 +55,7 @@ __global__ __launch_bounds__(256) void reduce_pos_kernel(wg::RArgs r, int rblk, 
   } else {
     const int b = (int)(blockIdx.x - T_);
     if (cols) wg::reduce_cols_block(r, b);
-    else wg::reduce_segments_block(r, b, red);
+    else wg::reduce_any_block(r, b, red);
   }
 }
 

@@ -168,7 +168,9 @@ struct Seg {
   int64_t stride;
   int splits, n;      // n floats (multiple of 4, 16-byte aligned src/out)
   float* out;
+  int cols;           // 1: column-per-thread form (few splits), 0: split groups + LDS tree
 };
+constexpr int COLS_MAX = 32;   // splits up to which a segment is summed column per thread
 struct RArgs {
   Seg s[MAXS];
   int blk0[MAXS + 1];
@@ -237,10 +239,21 @@ __device__ __forceinline__ void reduce_segments_block(const RArgs& a, int b, flo
   }
 }
 
+__device__ __forceinline__ void reduce_cols_block(const RArgs& a, int b);
+// a launch mixing both forms: each segment's blocks take its own (block-uniform branch)
+__device__ __forceinline__ void reduce_any_block(const RArgs& a, int b, float4 (*red2)[RED_C]) {
+  int si = 0;
+#pragma unroll 1
+  for (int q = 1; q < a.nseg; ++q)
+    if (b >= a.blk0[q]) si = q;
+  if (a.s[si].cols) reduce_cols_block(a, b);
+  else reduce_segments_block(a, b, red2);
+}
+
 __global__ __launch_bounds__(256) void reduce_segments_kernel(RArgs a) {
   KStampEnd stamp_(a.ks);
   __shared__ float4 red[RED_G][RED_C];
-  reduce_segments_block(a, blockIdx.x, red);
+  reduce_any_block(a, blockIdx.x, red);
 }
 
 // few splits (<= 32): one float4 column per thread, all splits summed in order by that thread (4 loads
@@ -288,21 +301,23 @@ __global__ __launch_bounds__(256) void reduce_cols_kernel(RArgs a) {
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 // one reduction launch's arguments for segs[0, nseg <= MAXS): RS_ERR_ARG on a bad segment; blk = workgroups,
-// cols = the column-per-thread form (few splits)
+// cols = every segment takes the column-per-thread form (reduce_cols_kernel; else the mixed launch).  Each
+// segment picks its form by its split count: the weight-gradient slabs (tens of splits) stream a column per
+// thread at HBM rate, the LayerNorm partial sets (one per row-chain workgroup: 256) take split groups + a tree
 static int reduce_args(int nseg, const rs_reduce_segment* segs, int accumulate, wg::RArgs& ra, int& blk, bool& cols) {
   ra = wg::RArgs{};
   ra.nseg = nseg;
   ra.accumulate = accumulate;
-  int64_t max_splits = 0;
-  for (int q = 0; q < nseg; ++q) max_splits = max(max_splits, segs[q].splits);
-  cols = max_splits <= 16;     // few splits: a column per thread (reduce_cols_kernel)
+  cols = true;
   blk = 0;
   for (int q = 0; q < nseg; ++q) {
     const rs_reduce_segment& g = segs[q];
     if (g.n <= 0 || g.n % 4 || g.stride % 4 || g.splits < 1 || !al16(g.src) || !al16(g.out)) return RS_ERR_ARG;
-    ra.s[q] = {g.src, g.stride, (int)g.splits, (int)g.n, g.out};
+    const int c = g.splits <= wg::COLS_MAX;
+    cols = cols && c;
+    ra.s[q] = {g.src, g.stride, (int)g.splits, (int)g.n, g.out, c};
     ra.blk0[q] = blk;
-    blk += (int)cdiv(g.n / 4, cols ? 256 : (g.splits > 64 ? 4 : wg::RED_C));
+    blk += (int)cdiv(g.n / 4, c ? 256 : (g.splits > 64 ? 4 : wg::RED_C));
   }
   ra.blk0[nseg] = blk;
   return 0;
