@@ -220,28 +220,56 @@ __global__ __launch_bounds__(256) void start_kernel(const int* __restrict__ tota
 }
 
 // each block places its entries: the stable rank inside the block comes from a bitonic sort of the block's
-// (key << IBITS | index) words in LDS (keys <= KBITS_MAX bits; unused slots sort last)
+// (key << IBITS | index) words (keys <= KBITS_MAX bits; unused slots sort last).  Thread t holds elements 2t, 2t+1:
+// partners 1 apart swap in registers, 2..64 apart across lanes of one wave (shuffles), only the stages 128 and 256
+// apart (3 of the 45) go through LDS with a barrier.
+__device__ __forceinline__ void bsort_cas(uint32_t& x, uint32_t y, bool lower, bool asc) {
+  // keep min when (this is the lower element) == (ascending), else max
+  const uint32_t lo = x < y ? x : y, hi = x < y ? y : x;
+  x = lower == asc ? lo : hi;
+}
 __global__ __launch_bounds__(256) void place_kernel(Keys K, const int* __restrict__ H, const int* __restrict__ start,
                                                     uint32_t* __restrict__ sk, uint32_t* __restrict__ sv) {
   __shared__ uint32_t w[BE];
   const int tid = threadIdx.x;
   const int64_t e0 = (int64_t)blockIdx.x * BE;
   const int cnt = (int)min((int64_t)BE, K.n - e0);
-  for (int l = tid; l < BE; l += 256) w[l] = l < cnt ? (K.get(e0 + l) << IBITS | (uint32_t)l) : 0xffffffffu;
-  for (int k = 2; k <= BE; k <<= 1)
+  uint32_t v[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int l = 2 * tid + i;
+    v[i] = l < cnt ? (K.get(e0 + l) << IBITS | (uint32_t)l) : 0xffffffffu;
+  }
+  for (int k = 2; k <= BE; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
-      __syncthreads();
-      for (int t = tid; t < BE; t += 256) {
-        const int u = t ^ j;
-        if (u > t) {
-          const uint32_t a = w[t], b = w[u];
-          if ((a > b) == ((t & k) == 0)) {
-            w[t] = b;
-            w[u] = a;
-          }
+      if (j == 1) {
+        const bool asc = ((2 * tid) & k) == 0;
+        const uint32_t a = v[0], b = v[1];
+        v[0] = asc ? (a < b ? a : b) : (a < b ? b : a);
+        v[1] = asc ? (a < b ? b : a) : (a < b ? a : b);
+      } else if (j <= 64) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int e = 2 * tid + i;
+          const uint32_t y = (uint32_t)__shfl_xor((int)v[i], j >> 1, 64);
+          bsort_cas(v[i], y, (e & j) == 0, (e & k) == 0);
+        }
+      } else {
+        __syncthreads();   // the previous cross-wave stage's reads are done
+        w[2 * tid] = v[0];
+        w[2 * tid + 1] = v[1];
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int e = 2 * tid + i;
+          bsort_cas(v[i], w[e ^ j], (e & j) == 0, (e & k) == 0);
         }
       }
     }
+  }
+  __syncthreads();
+  w[2 * tid] = v[0];
+  w[2 * tid + 1] = v[1];
   __syncthreads();
   const int* h = H + (int64_t)blockIdx.x * K.V;
   for (int j = tid; j < cnt; j += 256) {
