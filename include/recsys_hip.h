@@ -100,6 +100,14 @@ int rs_colsum(int dtype, const void* X, int64_t M, int64_t N, int64_t ldx, float
 int rs_embed_fwd(int dtype, int mode, const int64_t* ids, int64_t rows, int64_t T, const void* table,
                  const void* pos, int64_t d, float scale, float drop_p, uint64_t seed, const uint64_t* seed_base,
                  void* out, void* stream);
+/* rs_embed_fwd (vector layout: d a multiple of 8 bf16 / 4 fp32, 16-byte aligned buffers) that also counts, per
+ * wave of 64 lanes, the rows r with count_ids[r] != 0 into count_parts[rs_embed_count_parts(dtype, rows, d)] (int32;
+ * SAS: the valid positions pos != 0, the BCE divisor, for rs_sas_head_fused).  RS_ERR_UNSUPPORTED otherwise. */
+int64_t rs_embed_count_parts(int dtype, int64_t rows, int64_t d);
+int rs_embed_fwd_counted(int dtype, int mode, const int64_t* ids, int64_t rows, int64_t T, const void* table,
+                         const void* pos, int64_t d, float scale, float drop_p, uint64_t seed,
+                         const uint64_t* seed_base, void* out, const int64_t* count_ids, int* count_parts,
+                         void* stream);
 /* dtable[ids[r]] += dX*mask*scale (rows with id 0 skipped: padding_idx=0, fp32 atomics);
  * dpos[t] (+)= sum_b dX[b,t] * mask (deterministic; accumulate flag). */
 int rs_embed_bwd(int dtype, int mode, const int64_t* ids, int64_t rows, int64_t T, const void* dx,
@@ -431,6 +439,13 @@ int rs_wgrad_grouped_pos(int nprob, const rs_wgrad_problem* probs, int64_t M, in
                          int64_t slab_numel, int nextra, const rs_reduce_segment* extra, const int64_t* ids,
                          int64_t T, const void* dx, int64_t d, float drop_p, uint64_t salt,
                          const uint64_t* seed_base, float* dpos, void* stream);
+/* rs_wgrad_grouped_pos whose reduction launch also carries rs_sas_head_finish (one more workgroup): the SAS
+ * head's loss statistics loss_out[0..3] from rs_sas_head_fused's partials (head_part, M rows). */
+int rs_wgrad_grouped_pos_stats(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_t rows_per_split,
+                               float* slab, int64_t slab_numel, int nextra, const rs_reduce_segment* extra,
+                               const int64_t* ids, int64_t T, const void* dx, int64_t d, float drop_p, uint64_t salt,
+                               const uint64_t* seed_base, float* dpos, const float* head_part,
+                               const float* head_divisor, float* loss_out, void* stream);
 /* The reduction alone: out (+)= sum over splits, for nseg segments (any number, 64 per launch). */
 int rs_reduce_segments(int nseg, const rs_reduce_segment* segs, int accumulate, void* stream);
 
@@ -466,6 +481,15 @@ int rs_sas_head_bwd(int64_t M, int64_t d, const float* part, const float* diviso
                     const float* nl, const float* dpl_in, const float* dnl_in, float* dpl, float* dnl,
                     const int64_t* pos, const int64_t* neg, const void* E, const void* x, const float* ln_w,
                     const float* mean, const float* rstd, void* dx, float* lnpart, void* stream);
+/* Forward + backward of the head in one kernel for the fused training step (the BCE divisor c = *divisor or the
+ * sum of count_parts from rs_embed_fwd_counted, so no row waits for the others): writes f, pl, nl, dpl, dnl, dx,
+ * lnpart (as rs_sas_head_bwd) and part[b][3] (as rs_sas_head_fwd).  No mean/rstd.  rs_sas_head_finish then forms
+ * out[0..3] from part exactly as rs_sas_head_bwd does (one workgroup; may run on a side stream). */
+int rs_sas_head_fused(int64_t M, int64_t d, const void* x, const float* ln_w, const float* ln_b, float eps,
+                      const int* count_parts, int64_t ncount, const float* divisor, void* f, const void* E,
+                      const int64_t* pos, const int64_t* neg, float* pl, float* nl, float* dpl, float* dnl, void* dx,
+                      float* lnpart, float* part, void* stream);
+int rs_sas_head_finish(int64_t M, const float* part, const float* divisor, float* out, void* stream);
 
 /* ---- on-device SAS sampler and ranking metrics (sampler.hip) ----------------------------------
  * rs_sas_sample: one training batch as WarpSampler's workers build it (BS/dataloaders/sas.py:65-91):

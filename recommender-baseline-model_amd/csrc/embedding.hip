@@ -14,29 +14,42 @@
 #include "common.h"
 #include "../../include/recsys_hip.h"
 
+// count_ids (optional): wave w (global index) also writes count_parts[w] = the number of its rows r with
+// count_ids[r] != 0 (SAS: the valid positions, pos != 0, the loss's divisor -- known here, long before the fused
+// head needs it).  The id load is issued with the gathers and the count is a wave ballot: no barrier.
 template <typename T>
 __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restrict__ ids, int64_t rows, int64_t T_,
                                                         const T* __restrict__ table, const T* __restrict__ pos,
                                                         int64_t d, float scale, int mode, float drop_p,
-                                                        uint64_t salt, const uint64_t* seed_base, T* __restrict__ out) {
+                                                        uint64_t salt, const uint64_t* seed_base, T* __restrict__ out,
+                                                        const int64_t* __restrict__ count_ids,
+                                                        int* __restrict__ count_parts) {
   const uint64_t seed = eff_seed(salt, seed_base);
   constexpr int V = Vec<T>::N;
   const int64_t cpr = d / V;
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i >= rows * cpr) return;
-  const int64_t r = i / cpr, c = (i % cpr) * V, t = r % T_;
-  const int64_t id = ids[r];
-  float e[V], p[V], o[V];
-  load_chunk<T>(e, table + id * d + c);
-  load_chunk<T>(p, pos + t * d + c);
-  const float keep = (mode == 0 && id == 0) ? 0.f : 1.f;
+  const bool in = i < rows * cpr;
+  const bool head = count_ids && in && i % cpr == 0;
+  const int64_t cid = head ? count_ids[i / cpr] : 0;
+  if (in) {
+    const int64_t r = i / cpr, c = (i % cpr) * V, t = r % T_;
+    const int64_t id = ids[r];
+    float e[V], p[V], o[V];
+    load_chunk<T>(e, table + id * d + c);
+    load_chunk<T>(p, pos + t * d + c);
+    const float keep = (mode == 0 && id == 0) ? 0.f : 1.f;
 #pragma unroll
-  for (int j = 0; j < V; ++j) {
-    float x = mode == 0 ? e[j] * scale + p[j] : e[j] + p[j];
-    if (drop_p > 0.f) x *= drop_mul(drop_p, seed, (uint64_t)(r * d + c + j));
-    o[j] = x * keep;
+    for (int j = 0; j < V; ++j) {
+      float x = mode == 0 ? e[j] * scale + p[j] : e[j] + p[j];
+      if (drop_p > 0.f) x *= drop_mul(drop_p, seed, (uint64_t)(r * d + c + j));
+      o[j] = x * keep;
+    }
+    store_chunk<T>(out + r * d + c, o);
   }
-  store_chunk<T>(out + r * d + c, o);
+  if (count_ids) {   // grid-uniform
+    const int n = __popcll(__ballot(head && cid != 0));
+    if ((threadIdx.x & 63) == 0) count_parts[(blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6] = n;
+  }
 }
 
 // any width / alignment (e.g. the reference's default SAS d = 50): one element per thread, same math
@@ -215,16 +228,19 @@ __global__ __launch_bounds__(256) void sampled_logits_bwd_kernel(const T* __rest
 template <typename T>
 static hipError_t embed_fwd_t(int mode, const int64_t* ids, int64_t rows, int64_t T_, const void* table,
                               const void* pos, int64_t d, float scale, float drop_p, uint64_t seed,
-                              const uint64_t* seed_base, void* out, hipStream_t s) {
+                              const uint64_t* seed_base, void* out, hipStream_t s,
+                              const int64_t* count_ids = nullptr, int* count_parts = nullptr) {
   const bool vec = d % Vec<T>::N == 0 && ((uintptr_t)table | (uintptr_t)pos | (uintptr_t)out) % 16 == 0;
   if (!vec) {
+    if (count_ids) return hipErrorInvalidValue;
     hipLaunchKernelGGL((embed_fwd_any_kernel<T>), dim3((unsigned)cdiv(rows * d, 256)), dim3(256), 0, s, ids, rows, T_,
                        (const T*)table, (const T*)pos, d, scale, mode, drop_p, seed, seed_base, (T*)out);
     return hipGetLastError();
   }
   const int64_t n = rows * (d / Vec<T>::N);
   hipLaunchKernelGGL((embed_fwd_kernel<T>), dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, ids, rows, T_,
-                     (const T*)table, (const T*)pos, d, scale, mode, drop_p, seed, seed_base, (T*)out);
+                     (const T*)table, (const T*)pos, d, scale, mode, drop_p, seed, seed_base, (T*)out, count_ids,
+                     count_parts);
   return hipGetLastError();
 }
 
@@ -265,6 +281,26 @@ int rs_embed_fwd(int dtype, int mode, const int64_t* ids, int64_t rows, int64_t 
   return (int)(dtype == RS_DTYPE_BF16
                    ? embed_fwd_t<__bf16>(mode, ids, rows, T, table, pos, d, scale, drop_p, seed, seed_base, out, s)
                    : embed_fwd_t<float>(mode, ids, rows, T, table, pos, d, scale, drop_p, seed, seed_base, out, s));
+}
+
+int64_t rs_embed_count_parts(int dtype, int64_t rows, int64_t d) {
+  const int V = dtype == RS_DTYPE_BF16 ? Vec<__bf16>::N : Vec<float>::N;
+  return rows > 0 && d > 0 && d % V == 0 ? 4 * cdiv(rows * (d / V), 256) : 0;   // one per wave
+}
+
+int rs_embed_fwd_counted(int dtype, int mode, const int64_t* ids, int64_t rows, int64_t T, const void* table,
+                         const void* pos, int64_t d, float scale, float drop_p, uint64_t seed,
+                         const uint64_t* seed_base, void* out, const int64_t* count_ids, int* count_parts,
+                         void* stream) {
+  if (rows <= 0 || T <= 0 || rows % T || d <= 0 || !count_ids || !count_parts) return RS_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const hipError_t e =
+      dtype == RS_DTYPE_BF16
+          ? embed_fwd_t<__bf16>(mode, ids, rows, T, table, pos, d, scale, drop_p, seed, seed_base, out, s, count_ids,
+                                count_parts)
+          : embed_fwd_t<float>(mode, ids, rows, T, table, pos, d, scale, drop_p, seed, seed_base, out, s, count_ids,
+                               count_parts);
+  return e == hipErrorInvalidValue ? RS_ERR_UNSUPPORTED : (int)e;
 }
 
 int rs_embed_bwd(int dtype, int mode, const int64_t* ids, int64_t rows, int64_t T, const void* dx, int64_t d,

@@ -187,7 +187,10 @@ class SASEngine:
         return torch.empty(shape, dtype=dtype or self.dt, device=self.dev)
 
     # ---- forward -------------------------------------------------------------------
-    def forward(self, ids, pos, neg, training, need_logits=True, clone_seed=True):
+    def forward(self, ids, pos, neg, training, need_logits=True, clone_seed=True, fuse_head=False):
+        """fuse_head (the fused training step, whose backward forms the BCE gradient itself): the head's forward
+        is left to backward, which runs it and the head's backward as ONE kernel (rs_sas_head_fused); the
+        returned pl / nl are filled there.  The embedding forward counts the valid positions for it."""
         B, T = ids.shape
         M, d, H, Dh, L = B * T, self.d, self.H, self.Dh, self.L
         p = self.p if training else 0.0
@@ -206,8 +209,16 @@ class SASEngine:
             fork = torch.cuda.Event()
             fork.record()
         x = e("x0", (M, d))
-        ops.embed_fwd(0, ids, T, self.W("item_emb.weight"), self.W("pos_emb.weight"), math.sqrt(d), p,
-                      self.salt["emb"], sb, x)
+        fuse_head = fuse_head and side and need_logits and os.environ.get("RS_SAS_HEAD_FUSED", "1") != "0"
+        ncnt = ops.embed_count_parts(self.W("item_emb.weight"), M) if fuse_head else 0
+        if ncnt > 0:
+            cntp = self.ws.get("cntp", (ncnt,), torch.int32)
+            ops.embed_fwd_counted(0, ids, T, self.W("item_emb.weight"), self.W("pos_emb.weight"), math.sqrt(d), p,
+                                  self.salt["emb"], sb, x, pos, cntp)
+            s["cntp"] = cntp
+        else:
+            ops.embed_fwd(0, ids, T, self.W("item_emb.weight"), self.W("pos_emb.weight"), math.sqrt(d), p,
+                          self.salt["emb"], sb, x)
         if side:
             # issued after the first forward launch: in the captured graph the forward chain is then the
             # first child of the step's root and keeps the launch queue; the side branch gets the second
@@ -245,6 +256,10 @@ class SASEngine:
                 x = xn
         f, muf, rf = e("f", (M, d)), e("mu", (M,), torch.float32), e("r", (M,), torch.float32)
         s.update(xL=x, f=f, muf=muf, rf=rf)
+        if "cntp" in s:
+            pl, nl = e("pl", (B, T), torch.float32), e("nl", (B, T), torch.float32)
+            s.update(pl=pl, nl=nl, headp=e("headp", (3 * (-(-M // 64)),), torch.float32))
+            return pl, nl, s
         if fused and need_logits:
             # last LayerNorm + tied sampled logits + BCE partial sums in one kernel (head.hip)
             pl, nl = e("pl", (B, T), torch.float32), e("nl", (B, T), torch.float32)
@@ -335,7 +350,16 @@ class SASEngine:
             dx = e("dx", (M, d))
             lnh = self.ws.get("lnh", (2 * d * (-(-M // 64)),), torch.float32)
             E, gl = self.W("item_emb.weight"), self.Wf("last_layernorm.weight")
-            if dpl is None:
+            stats = ()
+            if dpl is None and "cntp" in s:
+                # the head's forward and backward in one kernel; the loss statistics (one workgroup) ride in the
+                # gradient tail's reduction launch
+                dpl, dnl = e("dpl", (B, T), torch.float32), e("dnl", (B, T), torch.float32)
+                ops.sas_head_fused(s["xL"], gl, self.Wf("last_layernorm.bias"), LN_EPS, s["cntp"], divisor, s["f"], E,
+                                   s["pos"], s["neg"], s["pl"], s["nl"], dpl, dnl, dx, lnh, s["headp"])
+                if loss_out is not None:
+                    stats = (s["headp"], divisor, loss_out)
+            elif dpl is None:
                 dpl, dnl = e("dpl", (B, T), torch.float32), e("dnl", (B, T), torch.float32)
                 ops.sas_head_bwd(s["headp"], divisor, loss_out, s["pl"], s["nl"], None, None, dpl, dnl, s["pos"],
                                  s["neg"], E, s["xL"], gl, s["muf"], s["rf"], dx, lnh)
@@ -365,11 +389,14 @@ class SASEngine:
             # the positional table's gradient rides in the grouped reduction's launch (RS_SAS_POS_MERGED=0: its
             # own launch after it)
             pos_merged = fused_items is None and os.environ.get("RS_SAS_POS_MERGED", "1") != "0"
-            pos_args = (lambda dx: (ids, T, dx, p, self.salt["emb"], sb, G("pos_emb.weight"))) if pos_merged else None
+            pos_args = ((lambda dx: (ids, T, dx, p, self.salt["emb"], sb, G("pos_emb.weight")) + stats) if pos_merged
+                        else None)
             dx = self._backward_blocks_fused(s, dx, grad, segs, tail=item_grads if side else None, items=fused_items,
                                              pos=pos_args)
             if not pos_merged:
                 ops.embed_bwd(0, ids, T, dx, math.sqrt(d), p, self.salt["emb"], sb, None, G("pos_emb.weight"))
+                if stats:
+                    ops.sas_head_finish(M, *stats)
             if side:
                 torch.cuda.current_stream().wait_event(self._tail_join)
             elif tail_mode != "fused":

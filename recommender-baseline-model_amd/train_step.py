@@ -196,7 +196,7 @@ class FusedTrainStep:
                 split(tag, action)
         if self.kind == "sas":
             seq, pos, neg = batch
-            pl, nl, saved = eng.forward(seq, pos, neg, True, clone_seed=False)
+            pl, nl, saved = eng.forward(seq, pos, neg, True, clone_seed=False, fuse_head=eng.fused_head)
             if eng.fused_head:
                 # BCE forward/backward inside the fused head kernels (head.hip)
                 eng.backward(saved, None, None, self.flat.grad, loss_out=self.loss_out,

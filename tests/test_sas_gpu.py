@@ -216,3 +216,43 @@ def test_sas_fused_block_matches_unfused(V, T, d, L, h, B, monkeypatch):
             u, v = np.concatenate([u[:d], u[2 * d:]]), np.concatenate([v[:d], v[2 * d:]])
         assert rel(u, v) < 1e-2, (n, rel(u, v))
     assert (sa["h1"][0] == 0).float().mean().item() > 0.5 * 0.2   # relu + dropout zeros present
+
+
+@pytest.mark.parametrize("V,T,d,L,h,B,dp", [(500, 37, 64, 2, 2, 3, False), (400, 200, 128, 2, 1, 5, False),
+                                            (400, 200, 128, 2, 1, 5, True), (300, 50, 64, 1, 2, 7, False)])
+def test_sas_fused_head_matches_split_head(V, T, d, L, h, B, dp):
+    """rs_sas_head_fused (forward + backward of the head in one kernel, divisor from the embedding forward's counts)
+    against rs_sas_head_fwd + rs_sas_head_bwd: the same per-row arithmetic in the same order, so the logits, the
+    features, every parameter gradient and the loss statistics are bit-identical (dropout on, padded positions,
+    ragged last row tile; dp: the data-parallel divisor 1)."""
+    import rbm_amd  # noqa: F401
+    import rbm_amd.data as synth
+    from rbm_amd import ops
+    from rbm_amd.models import model_factory
+    torch.manual_seed(V)
+    m = model_factory(sas_args(V, T, d, L, h, p=0.2, dtype="bf16"))
+    eng = m.sas.engine()
+    eng.sync_compute_weights()
+    assert eng.fused_head
+    rng = np.random.default_rng(T)
+    seq, pos, neg = (torch.from_numpy(a).cuda() for a in synth.sas_batch(rng, B, T, V))
+    pos[0, :9] = 0
+    pos[-1, -1] = 0
+    one = torch.ones(1, dtype=torch.float32, device="cuda") if dp else None
+    runs = []
+    for fuse in (False, True):
+        eng.seed_base.fill_(7)
+        pl, nl, s = eng.forward(seq, pos, neg, True, fuse_head=fuse)
+        assert ("cntp" in s) == fuse
+        grad = torch.zeros(eng.flat.numel, dtype=torch.float32, device="cuda")
+        lo = torch.full((4,), float("nan"), dtype=torch.float32, device="cuda")
+        eng.backward(s, None, None, grad, loss_out=lo, divisor=one)
+        torch.cuda.synchronize()
+        runs.append((pl.clone(), nl.clone(), s["f"].clone(), grad, lo))
+    # the separate finish kernel (rs_sas_head_finish) forms the same statistics from the fused kernel's partials
+    lo2 = torch.full((4,), float("nan"), dtype=torch.float32, device="cuda")
+    ops.sas_head_finish(B * T, s["headp"], one, lo2)
+    assert torch.equal(lo2, runs[1][4])
+    for a, b, what in zip(runs[0], runs[1], ("pl", "nl", "f", "grad", "loss")):
+        assert torch.equal(a, b), (what, (a.float() - b.float()).abs().max().item())
+    assert runs[1][4][1].item() == (pos != 0).sum().item()
