@@ -11,9 +11,9 @@ the global gradient sum, loss sum and count; the optimizer divides by the count
 different valid counts.
 
 Overlap with backward: the flat buffer is split into buckets that become final at
-different points of the backward -- SAS: the dense block / LayerNorm weights (+ aux) after the grouped
-weight-gradient launch, then the item / positional tables; BERT: the vocabulary head (out.weight,
-out.bias, + aux) right after its weight gradient, then everything else.  BucketedExchange starts each
+different points of the backward -- BERT: the vocabulary head (out.weight, out.bias, + aux) right after its
+weight gradient, then everything else.  (The fused SAS backward finishes all its gradients in its last launches,
+so it exchanges one bucket: see FusedTrainStep._buckets.)  BucketedExchange starts each
 bucket's all-reduce (async, on the backend's stream, ordered after the work already issued on the
 current stream) as soon as it is final, so it overlaps the rest of the backward; finish() makes the
 current stream wait for all of them before the optimizer.

@@ -139,11 +139,11 @@ class FusedTrainStep:
         final first (tag named by the engine's split call) and "final" (the rest, after the backward)."""
         f = self.flat
         if self.kind == "sas" and self.engine.fused_head:
-            # item_emb, pos_emb lead the buffer (reference parameter order); the block weights follow
-            cut = max(f.offsets["item_emb.weight"], f.offsets["pos_emb.weight"]) + \
-                -(-f.view("pos_emb.weight").numel() // 64) * 64
-            assert cut == min(o for n, o in f.offsets.items() if n not in ("item_emb.weight", "pos_emb.weight"))
-            return {"final": (0, cut), "dense": (cut, f.grad.numel())}
+            # ONE bucket: the fused SAS backward finishes every gradient in its last launches (the grouped weight
+            # gradients with the positional table's, the item table's beside them on the side queue, joined
+            # before the step ends), so a dense-block bucket cut there would go out back to back with the tables'
+            # -- two collectives' latency and a graph-segment boundary for no overlap (2.65 MB fp32 at cfg2)
+            return {"final": (0, f.grad.numel())}
         if self.kind == "bert" and getattr(self, "vshard", None) is not None:
             # the output layer's rows are rank-owned (complete gradients, no exchange); the loss is global already
             return {"final": (0, f.offsets["out.weight"])}
@@ -200,7 +200,8 @@ class FusedTrainStep:
             if eng.fused_head:
                 # BCE forward/backward inside the fused head kernels (head.hip)
                 eng.backward(saved, None, None, self.flat.grad, loss_out=self.loss_out,
-                             divisor=self.one if self.dp else None, split=sp)
+                             divisor=self.one if self.dp else None,
+                             split=sp if self.exchange is not None and "dense" in self.exchange.buckets else None)
                 write_aux()
                 return
             ws = eng.ws.get("bce", (3 * 256,), torch.float32)
