@@ -327,11 +327,14 @@ def main():
     if args.steps_per_graph == "auto":
         # the largest of 10 / 8 / 5 / 4 / 2 steps per replay that divides the timed count (a replay boundary costs
         # ~25 us); the warmup need not be a multiple: its remainder runs as eager steps (below)
-        S = next((u for u in (10, 8, 5, 4, 2) if args.steps % u == 0), 1) if world == 1 and not args.no_graph else 1
+        # (data parallel: when the trainer captures its all-reduce inside the step graph -- SAS)
+        unroll = (world == 1 or trainer.graph_collectives) and not args.no_graph
+        S = next((u for u in (10, 8, 5, 4, 2) if args.steps % u == 0), 1) if unroll else 1
     else:
         S = int(args.steps_per_graph)
-        if S > 1 and (world > 1 or args.no_graph or args.steps % S):
-            raise SystemExit("--steps-per-graph > 1 needs one GPU, graphs, and --steps a multiple of it")
+        if S > 1 and ((world > 1 and not trainer.graph_collectives) or args.no_graph or args.steps % S):
+            raise SystemExit("--steps-per-graph > 1 needs graphs (with the all-reduce inside them under DP) and "
+                             "--steps a multiple of it")
 
     if args.sampler == "device" and cfg["model"] == "sas":
         import rbm_amd.data as synth

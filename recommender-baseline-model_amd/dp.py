@@ -40,6 +40,11 @@ def world():
     return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
 
+def backend(group=None):
+    """The process group's backend name ("nccl" = RCCL on ROCm, "gloo"), None without torch.distributed."""
+    return str(dist.get_backend(group)).lower() if dist.is_available() and dist.is_initialized() else None
+
+
 def allreduce_grads(flat_grad, group=None, bucket_numel=None):
     """SUM all-reduce of the flat gradient buffer (parameters + aux tail), in place.
 

@@ -20,6 +20,8 @@ compute and optimizer graphs around the eager RCCL call under DP) and
 ``replay`` runs it on new batches copied into the graphs' static inputs; the
 dropout step-seed lives in device memory and is advanced inside the graph.
 """
+import os
+
 import torch
 
 from . import dp as dpx
@@ -124,6 +126,16 @@ class FusedTrainStep:
         self._stamps = None
         self.exchange = dpx.BucketedExchange(self.flat.grad, self._buckets(), self.pg, partial=self.vshard is not None) \
             if self.overlap else None
+        # SAS under DP: the gradient all-reduce is captured INSIDE the step graph (RCCL collectives are graph
+        # capturable; thread-local capture mode lets the process group's watchdog poll meanwhile), so a replay is
+        # forward + backward + all-reduce + Adam with no host round trip, and several steps unroll into one
+        # graph as on one device.  Measured on one GPU (world-1 group, tools/dp_overhead.py, cfg2): the segmented
+        # form -- step graph, all-reduce issued between replays, optimizer graph -- costs 0.355 against 0.308
+        # ms/step.  RCCL only (gloo's collectives on device tensors synchronise with the host: not capturable);
+        # RS_DP_GRAPH_COLLECTIVES=0: the segmented form.
+        self.graph_collectives = (self.dp and self.kind == "sas" and self.vshard is None
+                                  and os.environ.get("RS_DP_GRAPH_COLLECTIVES", "1") != "0"
+                                  and dpx.backend(self.pg) == "nccl")
         self.sparse_mode = sparse_rows
         self.sparse = None
         self._sparse_checked = False
@@ -388,8 +400,8 @@ class FusedTrainStep:
         S = int(steps_per_graph)
         if S < 1:
             raise ValueError("steps_per_graph must be >= 1")
-        if S > 1 and self.dp:
-            raise ValueError("steps_per_graph > 1 is single-device only (DP exchanges gradients between steps)")
+        if S > 1 and self.dp and not self.graph_collectives:
+            raise ValueError("steps_per_graph > 1 under DP needs the all-reduce inside the graph (graph_collectives)")
         self.steps_per_graph = S
         # one loss-statistics row per unrolled step: the step's kernels write its own row (a copy node between
         # Adam and the next step's first kernel cost ~9 us of idle per step in the graph)
@@ -400,7 +412,7 @@ class FusedTrainStep:
     def _unrolled(self, inputs, sample=None):
         """compute() for an unrolled graph: S x (sample, forward + backward, Adam, keep the loss)."""
         def compute(split=None):
-            base = self.loss_out
+            base, base_val = self.loss_out, self.loss_val
             try:
                 for k in range(self.steps_per_graph):
                     if k and self._stamps is not None:
@@ -408,13 +420,26 @@ class FusedTrainStep:
                         # marks numbered from 0, so every step's launches fit the per-step mark capacity
                         ops.kernel_stamps(self._stamps[0], self.opt.state, self._stamps[1])
                     self.loss_out = self.loss_rows[k]
+                    self.loss_val = self.loss_rows[k, 2:3]    # DP: the global mean loss lands in the step's row
                     if sample is not None:
                         sample()
                     self._compute(*inputs(k))
+                    self._graph_exchange()
                     self._update()
             finally:
-                self.loss_out = base
+                self.loss_out, self.loss_val = base, base_val
         return compute
+
+    def _graph_exchange(self):
+        """DP with graph collectives: the whole-buffer all-reduce, issued inside the step being captured."""
+        if not self.dp:
+            return
+        if self.exchange is not None:
+            for tag in self.exchange.buckets:
+                self.exchange.launch(tag)
+            self.exchange.finish()
+        else:
+            self._exchange()
 
     def _capture_graphs(self, compute, stamps=None, unrolled=False):
         """The compute graph (+ the optimizer in the same graph on one device).  DP: the compute graph is cut at
@@ -424,7 +449,17 @@ class FusedTrainStep:
         if stamps is not None:
             ops.kernel_stamps(stamps[0], self.opt.state, stamps[1])
         try:
-            if self.overlap:
+            if self.graph_collectives:
+                # one graph: compute, the all-reduce, the optimizer (unrolled: S of those)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
+                    compute()
+                    if not unrolled:
+                        self._graph_exchange()
+                        self._update()
+                self.g_compute = g
+                self.g_segments = None
+            elif self.overlap:
                 self.g_segments = self._capture_segments(compute)
                 self.g_compute = None
             else:
@@ -440,6 +475,9 @@ class FusedTrainStep:
                 ops.kernel_stamps(None, None)
             self._stamps = None
         self.g_update = None
+        if self.graph_collectives:
+            self.graphs = (self.g_compute,)
+            return
         if self.dp:
             self.g_update = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g_update, capture_error_mode=CAPTURE_MODE):
@@ -480,6 +518,9 @@ class FusedTrainStep:
             self.exchange.launch(tag)
 
     def _replay_graphs(self):
+        if self.graph_collectives:
+            self.g_compute.replay()
+            return self.loss_steps if self.steps_per_graph > 1 else self.loss_val
         if self.overlap:
             for g, tag, action in self.g_segments:
                 g.replay()

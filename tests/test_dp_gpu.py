@@ -110,3 +110,35 @@ def test_dp_overlap_bitwise_equals_single_allreduce_bf16(nccl_group, kind):
         res.append((losses, tr.flat.data.detach().cpu().clone()))
     assert res[0][0] == res[1][0]
     assert torch.equal(res[0][1], res[1][1])
+
+
+def test_dp_graph_collectives_equal_segmented(nccl_group, monkeypatch):
+    """SAS under DP with the all-reduce captured inside the step graph (one step per replay, and two steps
+    unrolled into one replay) against the segmented form (step graph, all-reduce between replays, optimizer
+    graph): bit-identical parameters and losses (bf16 fused step, dropout on)."""
+    import rbm_amd  # noqa: F401
+    from rbm_amd.models import model_factory
+    from rbm_amd.train_step import FusedTrainStep
+    batches = _batches("sas", 4)
+    res = []
+    for mode, S in (("0", 1), ("1", 1), ("1", 2)):
+        monkeypatch.setenv("RS_DP_GRAPH_COLLECTIVES", mode)
+        torch.manual_seed(5)
+        a = argparse.Namespace(model_code="sas", num_items=500, max_len=50, device="cuda", sas_hidden_units=128,
+                               sas_num_blocks=2, sas_heads=1, sas_dropout=0.1, l2_emb=0.0, rs_dtype="bf16")
+        tr = FusedTrainStep(model_factory(a), lr=1e-3, dp=True)
+        assert tr.graph_collectives == (mode == "1")
+        tr.capture(*batches[0], steps_per_graph=S)
+        assert len(tr.graphs) == (1 if mode == "1" else 2)
+        if S == 1:
+            losses = [float(tr.replay(*b).item()) for b in batches]
+        else:
+            losses = []
+            for j in range(0, len(batches), S):
+                packed = torch.stack([torch.stack(b) for b in batches[j:j + S]])
+                losses += [float(x) for x in tr.replay_packed(packed).cpu()]
+        torch.cuda.synchronize()
+        res.append((losses, tr.flat.data.detach().cpu().clone()))
+    for losses, params in res[1:]:
+        assert losses == res[0][0], (losses, res[0][0])
+        assert torch.equal(params, res[0][1])
