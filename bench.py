@@ -336,13 +336,30 @@ def main():
             raise SystemExit("--steps-per-graph > 1 needs graphs (with the all-reduce inside them under DP) and "
                              "--steps a multiple of it")
 
+    def capture(fn):
+        """fn(S) captures the step graphs; under DP, an all-reduce that refuses capture in an unrolled graph falls
+        back to one step per replay with the collectives between segment graphs (every rank alike)."""
+        nonlocal S
+        try:
+            fn(S)
+        except Exception as e:
+            if world == 1 or S == 1:
+                raise
+            print(f"rank {rank}: unrolled DP capture failed ({e}); one step per replay", file=sys.stderr)
+            torch.cuda.synchronize()
+            trainer.graph_collectives = False
+            if trainer.exchange is not None:
+                trainer.exchange.works, trainer.exchange.sent = [], []
+            S = 1
+            fn(S)
+
     if args.sampler == "device" and cfg["model"] == "sas":
         import rbm_amd.data as synth
         from rbm_amd.dataloaders import DeviceWarpSampler
         users = synth.user_histories(np.random.default_rng(77 + rank), cfg.get("users", 6040), cfg["T"], cfg["V"],
                                      shape=cfg["shape"])
         sampler = DeviceWarpSampler(users, cfg["V"], B, cfg["T"], seed=5 + rank)
-        trainer.capture_sampled(sampler, stamps=stamps, steps_per_graph=S)
+        capture(lambda s: trainer.capture_sampled(sampler, stamps=stamps, steps_per_graph=s))
         batches = [()]
         run = trainer.replay_sampled
         eager = lambda i: (sampler.sample_into(*trainer.static), trainer.step(*trainer.static))  # noqa: E731
@@ -362,7 +379,7 @@ def main():
     elif args.no_graph:
         run = trainer.step
     else:
-        trainer.capture(*batches[0], stamps=stamps, steps_per_graph=S)
+        capture(lambda s: trainer.capture(*batches[0], stamps=stamps, steps_per_graph=s))
         step_batches = batches
         eager = lambda i: trainer.step(*step_batches[i % len(step_batches)])  # noqa: E731
         batches = [torch.stack(b) for b in batches]     # one device copy per replay (replay_packed)

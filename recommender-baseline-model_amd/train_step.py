@@ -451,12 +451,23 @@ class FusedTrainStep:
         try:
             if self.graph_collectives:
                 # one graph: compute, the all-reduce, the optimizer (unrolled: S of those)
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
-                    compute()
-                    if not unrolled:
-                        self._graph_exchange()
-                        self._update()
+                try:
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
+                        compute()
+                        if not unrolled:
+                            self._graph_exchange()
+                            self._update()
+                except Exception as e:   # the collective refused capture: every rank takes the same branch
+                    if self.steps_per_graph > 1:
+                        raise
+                    import warnings
+                    warnings.warn(f"all-reduce capture failed ({e}); falling back to segmented DP graphs")
+                    torch.cuda.synchronize()
+                    self.graph_collectives = False
+                    if self.exchange is not None:
+                        self.exchange.works, self.exchange.sent = [], []
+                    return self._capture_graphs(compute, stamps, unrolled)
                 self.g_compute = g
                 self.g_segments = None
             elif self.overlap:
