@@ -340,6 +340,17 @@ int rs_seed_advance(uint64_t* seed_base, void* stream);
 int rs_sas_block_in(int64_t M, int64_t d, const void* x, int64_t ldx, const float* ln_w, const float* ln_b,
                     float eps, void* Q, float* mean, float* rstd, const void* Wq, const float* bq, void* q,
                     const void* Wkv, const float* bkv, void* kv, void* stream);
+/* The first block's input side with the embedding stage folded in (rowchain: one launch instead of two): x0 =
+ * (item_emb[ids]*scale + pos_emb[t]) -> dropout(p, salt) -> *(ids != 0), exactly as rs_embed_fwd mode 0, stored
+ * to x0 [M][d] and fed to rs_sas_block_in's chain; with count_ids, count_parts[rs_sas_block_in_count_parts(M)]
+ * (int32) receives per-wave counts of count_ids != 0 (the BCE divisor for rs_sas_head_fused).  Other shapes or
+ * the non-chain build: rs_embed_fwd(_counted) then rs_sas_block_in (same results). */
+int64_t rs_sas_block_in_count_parts(int64_t M);
+int rs_sas_block_in_embed(int64_t M, int64_t d, const int64_t* ids, int64_t T, const void* item_emb, const void* pos_emb,
+                          float scale, float drop_p, uint64_t salt, const uint64_t* seed_base, void* x0,
+                          const int64_t* count_ids, int* count_parts, const float* ln_w, const float* ln_b, float eps,
+                          void* Q, float* mean, float* rstd, const void* Wq, const float* bq, void* q, const void* Wkv,
+                          const float* bkv, void* kv, void* stream);
 /* The output side (sas.py:75-84, PointWiseFeedForward sas.py:8-24):
  *   x1 = Q + o Wo^T + bo;  z = LN2(x1);  h1 = relu(drop(z W1^T + b1, salt1));
  *   xn = (drop(h1 W2^T + b2, salt2) + z) * (ids != 0)

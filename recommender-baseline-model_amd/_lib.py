@@ -95,6 +95,9 @@ SIGNATURES = {
     "rs_rows_pack": [vp, i64, i64, vp, vp, vp, i64, vp],
     "rs_rows_unpack": [vp, i64, i64, vp, vp, vp],
     "rs_sas_block_in": [i64, i64, vp, i64, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
+    "rs_sas_block_in_count_parts": [i64],
+    "rs_sas_block_in_embed": [i64, i64, vp, i64, vp, vp, f32, f32, u64, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp,
+                              vp, vp, vp, vp, vp, vp],
     "rs_sas_block_out": [i64, i64, vp, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32,
                          u64, u64, vp, vp],
     "rs_sas_block_out_bwd": [i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32, u64, u64,
@@ -134,7 +137,7 @@ SIGNATURES = {
 RESTYPES = {"rs_wgrad_grouped_slab_numel": C.c_int64, "rs_sas_block_parts": C.c_int64,
             "rs_touched_rows_ws_numel": C.c_int64, "rs_item_index_ws_bytes": C.c_int64,
             "rs_vocab_ce_ws_numel": C.c_int64,
-            "rs_embed_count_parts": C.c_int64}
+            "rs_embed_count_parts": C.c_int64, "rs_sas_block_in_count_parts": C.c_int64}
 
 _lib = None
 

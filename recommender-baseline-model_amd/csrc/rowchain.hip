@@ -505,6 +505,15 @@ __device__ __forceinline__ void bwd_out_b(const Raw<D>& dar, const Raw<D>& xr, c
 }
 
 // ------------------------------------------------------------------ single-block kernels
+// The SAS embedding stage folded into the first block's input kernel (rs_sas_block_in_embed): the tile's
+// x = (item_emb[ids]·scale + pos_emb[t]) → dropout → ·(ids != 0) is formed in registers exactly as
+// embed_fwd_kernel forms it (same expression, same hash index r·d + c), stored (x0, the backward's LN1 input) and
+// fed to the chain; each wave also counts its tiles' valid positions (count_ids != 0) into count_parts[wave].
+struct EmbIn {
+  const int64_t* ids; const bf16* etab; const bf16* ptab; int64_t T;
+  float scale, drop_p; uint64_t salt; const uint64_t* seed_base;
+  bf16* xout; const int64_t* cnt_ids; int* cnt_parts;
+};
 struct InArgs {
   int64_t M;
   const bf16* x; int64_t ldx;
@@ -512,7 +521,36 @@ struct InArgs {
   bf16* Q; float* mean; float* rstd;
   const bf16* Wq; const float* bq; bf16* q;
   const bf16* Wkv; const float* bkv; bf16* kv;
+  EmbIn e;                                                  // e.etab == nullptr: x is read
 };
+template <int D>
+__device__ __forceinline__ void embed_tile(Raw<D>& xr, const EmbIn& e, const Tile& T, uint32_t s32, int g) {
+  const int64_t id = e.ids[T.mc], t = T.mc % e.T;
+  const bf16* ep = e.etab + id * D + 8 * g;
+  const bf16* pp = e.ptab + t * D + 8 * g;
+  bf16x8 ev[Lay<D>::S], pv[Lay<D>::S];
+#pragma unroll
+  for (int s = 0; s < Lay<D>::S; ++s) {
+    ev[s] = *reinterpret_cast<const bf16x8*>(ep + 32 * s);
+    pv[s] = *reinterpret_cast<const bf16x8*>(pp + 32 * s);
+  }
+  const float keep = id == 0 ? 0.f : 1.f;
+#pragma unroll
+  for (int s = 0; s < Lay<D>::S; ++s)
+#pragma unroll
+    for (int k = 0; k < 8; k += 2) {
+      float x0 = (float)ev[s][k] * e.scale + (float)pv[s][k];
+      float x1 = (float)ev[s][k + 1] * e.scale + (float)pv[s][k + 1];
+      if (e.drop_p > 0.f) {
+        float m0, m1;
+        drop_mul2(e.drop_p, s32, (uint64_t)(T.mc * D + 32 * s + 8 * g + k), m0, m1);
+        x0 *= m0;
+        x1 *= m1;
+      }
+      xr.v[s][k] = (bf16)(x0 * keep);
+      xr.v[s][k + 1] = (bf16)(x1 * keep);
+    }
+}
 
 // X -> Q = LN1(X) [saved], q = Q Wq^T + bq, kv = X Wkv^T + bkv
 template <int D>
@@ -525,8 +563,20 @@ __global__ __launch_bounds__(NT) void block_in_kernel(InArgs a) {
             cl = lane & 15;
   const int64_t G = gridDim.x, nt = n_tiles(a.M);
   int64_t t = blockIdx.x + G * wave;
+  const bool emb = a.e.etab != nullptr;
+  const uint32_t es32 = emb && a.e.drop_p > 0.f ? seed32(eff_seed(a.e.salt, a.e.seed_base)) : 0u;
+  int cnt = 0;
+  auto load_x = [&](Raw<D>& xr, const Tile& T) {
+    if (!emb) {
+      load_raw<D>(xr, a.x, a.ldx, T.mc, g);
+      return;
+    }
+    embed_tile<D>(xr, a.e, T, es32, g);
+    store_raw<D>(a.e.xout, D, T.m, T.ok, xr, g);
+    if (a.e.cnt_ids) cnt += __popcll(__ballot(T.ok && g == 0 && a.e.cnt_ids[T.mc] != 0));
+  };
   Raw<D> xr;
-  if (t < nt) load_raw<D>(xr, a.x, a.ldx, tile_of(t, a.M, cl).mc, g);
+  if (t < nt) load_x(xr, tile_of(t, a.M, cl));
   {
     const bf16* const W[3] = {a.Wq, a.Wkv, a.Wkv + (int64_t)D * D};
     const int64_t ldw[3] = {D, D, D};
@@ -538,10 +588,11 @@ __global__ __launch_bounds__(NT) void block_in_kernel(InArgs a) {
   for (; t < nt; t += G * NW) {
     asm volatile("" ::: "memory");   // no hoisting of the loop-invariant weight fragment reads
     const Tile T = tile_of(t, a.M, cl);
-    if (t != blockIdx.x + G * wave) load_raw<D>(xr, a.x, a.ldx, T.mc, g);
+    if (t != blockIdx.x + G * wave) load_x(xr, T);
     fwd_in_q<D>(xr, T, wslot(smem, 0, WB), lv, a.eps, a.Q, a.mean, a.rstd, a.q, lane);
     fwd_in_kv<D>(xr, T, wslot(smem, 1, WB), wslot(smem, 2, WB), lv, a.kv, lane);
   }
+  if (emb && a.e.cnt_parts && lane == 0) a.e.cnt_parts[blockIdx.x * NW + wave] = cnt;
 }
 
 struct OutArgs {
@@ -810,6 +861,43 @@ int rs_sas_block_in(int64_t M, int64_t d, const void* x, int64_t ldx, const floa
     hipLaunchKernelGGL(rc::block_in_kernel<128>, grid, dim3(rc::NT), rc::lds_fwd<128>(), s, a);
   } else {
     return RS_ERR_UNSUPPORTED;
+  }
+  return (int)hipGetLastError();
+}
+
+int64_t rs_sas_block_in_count_parts(int64_t M) { return M > 0 ? rc::grid_for(M) * rc::NW : 0; }
+
+int rs_sas_block_in_embed(int64_t M, int64_t d, const int64_t* ids, int64_t T, const void* item_emb, const void* pos_emb,
+                          float scale, float drop_p, uint64_t salt, const uint64_t* seed_base, void* x0,
+                          const int64_t* count_ids, int* count_parts, const float* ln_w, const float* ln_b, float eps,
+                          void* Q, float* mean, float* rstd, const void* Wq, const float* bq, void* q, const void* Wkv,
+                          const float* bkv, void* kv, void* stream) {
+  if (M <= 0 || T <= 0 || M % T || !ids || !item_emb || !pos_emb || !x0 || !count_ids != !count_parts)
+    return RS_ERR_ARG;
+  const bool vec = ((uintptr_t)item_emb | (uintptr_t)pos_emb | (uintptr_t)x0) % 16 == 0;
+  if (!use_chain() || !vec || (d != 64 && d != 128)) {   // the two stages one after the other (same results)
+    if (count_ids) {
+      if (int e = rs_embed_fwd_counted(RS_DTYPE_BF16, 0, ids, M, T, item_emb, pos_emb, d, scale, drop_p, salt,
+                                       seed_base, x0, count_ids, count_parts, stream))
+        return e;
+    } else if (int e = rs_embed_fwd(RS_DTYPE_BF16, 0, ids, M, T, item_emb, pos_emb, d, scale, drop_p, salt, seed_base,
+                                    x0, stream)) {
+      return e;
+    }
+    return rs_sas_block_in(M, d, x0, d, ln_w, ln_b, eps, Q, mean, rstd, Wq, bq, q, Wkv, bkv, kv, stream);
+  }
+  rc::InArgs a = {M, (const __bf16*)x0, d, ln_w, ln_b, eps, (__bf16*)Q, mean, rstd, (const __bf16*)Wq, bq,
+                  (__bf16*)q, (const __bf16*)Wkv, bkv, (__bf16*)kv,
+                  rc::EmbIn{ids, (const __bf16*)item_emb, (const __bf16*)pos_emb, T, scale, drop_p, salt, seed_base,
+                            (__bf16*)x0, count_ids, count_parts}};
+  const dim3 grid((unsigned)rc::grid_for(M));
+  hipStream_t s = (hipStream_t)stream;
+  if (d == 64) {
+    rc::set_lds(rc::block_in_kernel<64>, rc::lds_fwd<64>());
+    hipLaunchKernelGGL(rc::block_in_kernel<64>, grid, dim3(rc::NT), rc::lds_fwd<64>(), s, a);
+  } else {
+    rc::set_lds(rc::block_in_kernel<128>, rc::lds_fwd<128>());
+    hipLaunchKernelGGL(rc::block_in_kernel<128>, grid, dim3(rc::NT), rc::lds_fwd<128>(), s, a);
   }
   return (int)hipGetLastError();
 }

@@ -210,21 +210,33 @@ class SASEngine:
             fork.record()
         x = e("x0", (M, d))
         fuse_head = fuse_head and side and need_logits and os.environ.get("RS_SAS_HEAD_FUSED", "1") != "0"
-        ncnt = ops.embed_count_parts(self.W("item_emb.weight"), M) if fuse_head else 0
+        # the embedding stage inside the first block's input kernel (rs_sas_block_in_embed, one launch)
+        emb_in = fused and os.environ.get("RS_SAS_EMBED_FUSED", "1") != "0"
+        ncnt = (ops.sas_block_in_count_parts(M) if emb_in else ops.embed_count_parts(self.W("item_emb.weight"), M)) \
+            if fuse_head else 0
+        cntp = None
         if ncnt > 0:
             cntp = self.ws.get("cntp", (ncnt,), torch.int32)
+            s["cntp"] = cntp
+        if emb_in:
+            emb = (ids, T, self.W("item_emb.weight"), self.W("pos_emb.weight"), math.sqrt(d), p, self.salt["emb"], sb,
+                   x, pos if cntp is not None else None, cntp)
+        elif cntp is not None:
             ops.embed_fwd_counted(0, ids, T, self.W("item_emb.weight"), self.W("pos_emb.weight"), math.sqrt(d), p,
                                   self.salt["emb"], sb, x, pos, cntp)
-            s["cntp"] = cntp
         else:
             ops.embed_fwd(0, ids, T, self.W("item_emb.weight"), self.W("pos_emb.weight"), math.sqrt(d), p,
                           self.salt["emb"], sb, x)
-        if side:
-            # issued after the first forward launch: in the captured graph the forward chain is then the
-            # first child of the step's root and keeps the launch queue; the side branch gets the second
-            s["side"] = self._side_prologue(ids, pos, neg, after=fork)
+
+        def after_first():
+            if side:
+                # issued after the first forward launch: in the captured graph the forward chain is then the
+                # first child of the step's root and keeps the launch queue; the side branch gets the second
+                s["side"] = self._side_prologue(ids, pos, neg, after=fork)
+        if not emb_in:
+            after_first()
         if fused:
-            x = self._forward_blocks_fused(s, x)
+            x = self._forward_blocks_fused(s, x, emb=emb if emb_in else None, after_first=after_first)
         else:
             for i in range(L):
                 pre = f"attention_layers.{i}."
@@ -275,10 +287,11 @@ class SASEngine:
         ops.sampled_logits_fwd(f, self.W("item_emb.weight"), pos, neg, pl, nl)
         return pl, nl, s
 
-    def _forward_blocks_fused(self, s, x):
+    def _forward_blocks_fused(self, s, x, emb=None, after_first=None):
         """SAS blocks' forward with the row-chain kernels (rowchain.hip) on each side of the attention core
         (rs_sas_block_in, rs_attn_fwd, rs_sas_block_out per block).  Fills s's per-block saved tensors; returns the
-        last block's output."""
+        last block's output.  emb: sas_block_in_embed's embedding arguments (x is then its x0 output, formed by the
+        first launch); after_first(): called after the first launch."""
         B, T, p, ids, sb = s["B"], s["T"], s["p"], s["ids"], s["sb"]
         M, d, H, Dh, L = B * T, self.d, self.H, self.Dh, self.L
         e = self._buf
@@ -304,7 +317,12 @@ class SASEngine:
                     self.salt[f"ffn1_{i}"], self.salt[f"ffn2_{i}"], sb)
 
         ln_w, ln_b, Q, mu1, r1, Wq, bq, q, Wkv, bkv, kv = in_args(0)
-        ops.sas_block_in(x, ln_w, ln_b, LN_EPS, Q, mu1, r1, Wq, bq, q, Wkv, bkv, kv)
+        if emb is not None:
+            ops.sas_block_in_embed(*emb, ln_w, ln_b, LN_EPS, Q, mu1, r1, Wq, bq, q, Wkv, bkv, kv)
+        else:
+            ops.sas_block_in(x, ln_w, ln_b, LN_EPS, Q, mu1, r1, Wq, bq, q, Wkv, bkv, kv)
+        if after_first is not None:
+            after_first()
         xs = [x]
         for i in range(L):
             b = lay[i]

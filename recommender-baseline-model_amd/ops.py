@@ -432,6 +432,22 @@ def sas_block_in(x, ln_w, ln_b, eps, Q, mean, rstd, Wq, bq, q, Wkv, bkv, kv):
          ptr(Wq), ptr(bq), ptr(q), ptr(Wkv), ptr(bkv), ptr(kv), stream())
 
 
+def sas_block_in_count_parts(M):
+    return int(_lib.lib().rs_sas_block_in_count_parts(M))
+
+
+def sas_block_in_embed(ids, T, item_emb, pos_emb, scale, drop_p, salt, seed_base, x0, count_ids, count_parts,
+                       ln_w, ln_b, eps, Q, mean, rstd, Wq, bq, q, Wkv, bkv, kv):
+    """embed_fwd(_counted) (mode 0) + sas_block_in in one launch (rowchain); x0 receives the embedding output."""
+    M, d = x0.shape
+    assert ids.numel() == M and item_emb.dtype == torch.bfloat16 and x0.dtype == torch.bfloat16
+    if count_parts is not None:
+        assert count_parts.dtype == torch.int32 and count_parts.numel() >= sas_block_in_count_parts(M)
+    call("rs_sas_block_in_embed", M, d, ptr(ids), T, ptr(item_emb), ptr(pos_emb), scale, drop_p, salt,
+         ptr(seed_base), ptr(x0), ptr(count_ids), ptr(count_parts), ptr(ln_w), ptr(ln_b), eps, ptr(Q), ptr(mean),
+         ptr(rstd), ptr(Wq), ptr(bq), ptr(q), ptr(Wkv), ptr(bkv), ptr(kv), stream())
+
+
 def sas_block_out(o, Q, Wo, bo, x1, ln_w, ln_b, eps, z, mean, rstd, W1, b1, h1, W2, b2, xn, ids, drop_p,
                   salt1, salt2, seed_base):
     M, d = o.shape

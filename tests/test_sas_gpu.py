@@ -256,3 +256,34 @@ def test_sas_fused_head_matches_split_head(V, T, d, L, h, B, dp):
     for a, b, what in zip(runs[0], runs[1], ("pl", "nl", "f", "grad", "loss")):
         assert torch.equal(a, b), (what, (a.float() - b.float()).abs().max().item())
     assert runs[1][4][1].item() == (pos != 0).sum().item()
+
+
+@pytest.mark.parametrize("V,T,d,L,h,B", [(500, 37, 64, 2, 2, 3), (400, 200, 128, 2, 1, 5), (3416, 200, 128, 2, 1, 9)])
+def test_sas_embed_fused_block_in_matches_separate(V, T, d, L, h, B, monkeypatch):
+    """rs_sas_block_in_embed (the embedding stage inside the first block's input kernel, valid positions counted
+    per wave) against rs_embed_fwd_counted + rs_sas_block_in: the same expression and dropout hash per element,
+    so x0, the logits, every gradient and the loss statistics are bit-identical (dropout on, padded rows)."""
+    import rbm_amd  # noqa: F401
+    import rbm_amd.data as synth
+    from rbm_amd.models import model_factory
+    torch.manual_seed(V)
+    m = model_factory(sas_args(V, T, d, L, h, p=0.2, dtype="bf16"))
+    eng = m.sas.engine()
+    eng.sync_compute_weights()
+    rng = np.random.default_rng(T + 1)
+    seq, pos, neg = (torch.from_numpy(a).cuda() for a in synth.sas_batch(rng, B, T, V))
+    seq[0, :11] = 0
+    pos[0, :10] = 0
+    runs = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("RS_SAS_EMBED_FUSED", fused)
+        eng.seed_base.fill_(9)
+        pl, nl, s = eng.forward(seq, pos, neg, True, fuse_head=True)
+        grad = torch.zeros(eng.flat.numel, dtype=torch.float32, device="cuda")
+        lo = torch.full((4,), float("nan"), dtype=torch.float32, device="cuda")
+        eng.backward(s, None, None, grad, loss_out=lo)
+        torch.cuda.synchronize()
+        runs.append((s["x"][0].clone(), s["q"][0].clone(), pl.clone(), nl.clone(), grad, lo))
+    for a, b, what in zip(runs[0], runs[1], ("x0", "q0", "pl", "nl", "grad", "loss")):
+        assert torch.equal(a, b), (what, (a.float() - b.float()).abs().max().item())
+    assert runs[1][5][1].item() == (pos != 0).sum().item()
