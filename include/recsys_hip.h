@@ -360,6 +360,22 @@ int rs_sas_block_out(int64_t M, int64_t d, const void* o, const void* Q, const v
                      const void* W1, const float* b1, void* h1, const void* W2, const float* b2, void* xn,
                      const int64_t* ids, float drop_p, uint64_t salt1, uint64_t salt2, const uint64_t* seed_base,
                      void* stream);
+/* rs_sas_block_out for the LAST block with the SAS head riding in the same kernel (token-local once the BCE
+ * divisor c = *divisor or the sum of count_parts[ncount] from rs_sas_block_in_embed is known): per token, after
+ * xn: f = LN_last(xn) [saved], pl/nl = <f, E[pos]>/<f, E[neg]>, dpl = (sigmoid(pl)-1)/c, dnl = sigmoid(nl)/c on
+ * pos != 0 [saved], dx = LN_last'(xn, dpl E[pos] + dnl E[neg]) [saved, bf16].  Per workgroup
+ * (rs_sas_block_grid(M) of them): lnpart[b][2][d] LN affine partials, part[b][3] BCE partials (sum softplus(-pl),
+ * sum softplus(nl), count) for rs_sas_head_finish / rs_wgrad_grouped_pos_stats.  RS_ERR_UNSUPPORTED off the
+ * row-chain build or d not in {64, 128} (callers use rs_sas_block_out + rs_sas_head_fused). */
+int64_t rs_sas_block_grid(int64_t M);
+int rs_sas_block_out_head(int64_t M, int64_t d, const void* o, const void* Q, const void* Wo, const float* bo,
+                          void* x1, const float* ln_w, const float* ln_b, float eps, void* z, float* mean, float* rstd,
+                          const void* W1, const float* b1, void* h1, const void* W2, const float* b2, void* xn,
+                          const int64_t* ids, float drop_p, uint64_t salt1, uint64_t salt2,
+                          const uint64_t* seed_base, const void* E, const int64_t* pos, const int64_t* neg,
+                          const float* lnl_w, const float* lnl_b, const int* count_parts, int64_t ncount,
+                          const float* divisor, void* f, float* pl, float* nl, float* dpl, float* dnl, void* dx,
+                          float* lnpart, float* part, void* stream);
 
 /* Union-of-touched-rows exchange of an embedding-table gradient (sparse_rows.hip; data parallel,
  * replaces the dense all-reduce of the token / item table gradient -- the reference has no
@@ -412,7 +428,7 @@ int rs_transpose_bf16(int64_t nmat, const int64_t* desc, int64_t max_tiles, cons
 /* ---- grouped weight gradients (wgrad.hip) ---------------------------------------------------
  * Every Linear / Conv1d(k=1) weight gradient of a backward pass, dW[N][K] += dY^T X and
  * db[N] += colsum(dY) over the M token rows (the autograd accumulation of nn.Linear's backward,
- * BS/models/sas_model/sas.py:8-24,67-84; bert_modules/*), in ONE GEMM launch (problems x output
+ * BS/models/sas_model/sas.py:8-24,67-84; bert_modules/...), in ONE GEMM launch (problems x output
  * tiles x row splits) followed by ONE deterministic grouped reduction of the split partials.
  * bf16 dY/X (16-byte aligned, ld % 8 == 0), fp32 dW/db accumulated; N, K multiples of 64. */
 typedef struct {
@@ -451,11 +467,11 @@ int rs_wgrad_grouped_pos(int nprob, const rs_wgrad_problem* probs, int64_t M, in
                          int64_t T, const void* dx, int64_t d, float drop_p, uint64_t salt,
                          const uint64_t* seed_base, float* dpos, void* stream);
 /* rs_wgrad_grouped_pos whose reduction launch also carries rs_sas_head_finish (one more workgroup): the SAS
- * head's loss statistics loss_out[0..3] from rs_sas_head_fused's partials (head_part, M rows). */
+ * head's loss statistics loss_out[0..3] from the head's partials (head_part[head_blocks][3]). */
 int rs_wgrad_grouped_pos_stats(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_t rows_per_split,
                                float* slab, int64_t slab_numel, int nextra, const rs_reduce_segment* extra,
                                const int64_t* ids, int64_t T, const void* dx, int64_t d, float drop_p, uint64_t salt,
-                               const uint64_t* seed_base, float* dpos, const float* head_part,
+                               const uint64_t* seed_base, float* dpos, const float* head_part, int64_t head_blocks,
                                const float* head_divisor, float* loss_out, void* stream);
 /* The reduction alone: out (+)= sum over splits, for nseg segments (any number, 64 per launch). */
 int rs_reduce_segments(int nseg, const rs_reduce_segment* segs, int accumulate, void* stream);
@@ -494,13 +510,14 @@ int rs_sas_head_bwd(int64_t M, int64_t d, const float* part, const float* diviso
                     const float* mean, const float* rstd, void* dx, float* lnpart, void* stream);
 /* Forward + backward of the head in one kernel for the fused training step (the BCE divisor c = *divisor or the
  * sum of count_parts from rs_embed_fwd_counted, so no row waits for the others): writes f, pl, nl, dpl, dnl, dx,
- * lnpart (as rs_sas_head_bwd) and part[b][3] (as rs_sas_head_fwd).  No mean/rstd.  rs_sas_head_finish then forms
- * out[0..3] from part exactly as rs_sas_head_bwd does (one workgroup; may run on a side stream). */
+ * lnpart (as rs_sas_head_bwd) and part[b][3] (as rs_sas_head_fwd), b < ceil(M/64).  No mean/rstd.
+ * rs_sas_head_finish(nblk = ceil(M/64), ...) then forms out[0..3] from part exactly as rs_sas_head_bwd does (one
+ * workgroup; may run on a side stream). */
 int rs_sas_head_fused(int64_t M, int64_t d, const void* x, const float* ln_w, const float* ln_b, float eps,
                       const int* count_parts, int64_t ncount, const float* divisor, void* f, const void* E,
                       const int64_t* pos, const int64_t* neg, float* pl, float* nl, float* dpl, float* dnl, void* dx,
                       float* lnpart, float* part, void* stream);
-int rs_sas_head_finish(int64_t M, const float* part, const float* divisor, float* out, void* stream);
+int rs_sas_head_finish(int64_t nblk, const float* part, const float* divisor, float* out, void* stream);
 
 /* ---- on-device SAS sampler and ranking metrics (sampler.hip) ----------------------------------
  * rs_sas_sample: one training batch as WarpSampler's workers build it (BS/dataloaders/sas.py:65-91):

@@ -96,6 +96,9 @@ SIGNATURES = {
     "rs_rows_unpack": [vp, i64, i64, vp, vp, vp],
     "rs_sas_block_in": [i64, i64, vp, i64, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "rs_sas_block_in_count_parts": [i64],
+    "rs_sas_block_grid": [i64],
+    "rs_sas_block_out_head": [i64, i64, vp, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32,
+                              u64, u64, vp, vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "rs_sas_block_in_embed": [i64, i64, vp, i64, vp, vp, f32, f32, u64, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp,
                               vp, vp, vp, vp, vp, vp],
     "rs_sas_block_out": [i64, i64, vp, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32,
@@ -118,7 +121,7 @@ SIGNATURES = {
     "rs_wgrad_grouped_pos": [i32, C.POINTER(WgradProblem), i64, i64, vp, i64, i32, C.POINTER(ReduceSegment),
                              vp, i64, vp, i64, f32, u64, vp, vp, vp],
     "rs_wgrad_grouped_pos_stats": [i32, C.POINTER(WgradProblem), i64, i64, vp, i64, i32, C.POINTER(ReduceSegment),
-                                   vp, i64, vp, i64, f32, u64, vp, vp, vp, vp, vp, vp],
+                                   vp, i64, vp, i64, f32, u64, vp, vp, vp, i64, vp, vp, vp],
     "rs_wgrad_grouped_items": [i32, C.POINTER(WgradProblem), i64, i64, vp, i64, i32, C.POINTER(ReduceSegment),
                                vp, i32, i64, i64, i64, vp, f32, f32, u64, vp, vp, vp, vp, vp, vp],
     "rs_transpose_bf16": [i64, vp, i64, vp, vp, vp],
@@ -137,7 +140,8 @@ SIGNATURES = {
 RESTYPES = {"rs_wgrad_grouped_slab_numel": C.c_int64, "rs_sas_block_parts": C.c_int64,
             "rs_touched_rows_ws_numel": C.c_int64, "rs_item_index_ws_bytes": C.c_int64,
             "rs_vocab_ce_ws_numel": C.c_int64,
-            "rs_embed_count_parts": C.c_int64, "rs_sas_block_in_count_parts": C.c_int64}
+            "rs_embed_count_parts": C.c_int64, "rs_sas_block_in_count_parts": C.c_int64,
+            "rs_sas_block_grid": C.c_int64}
 
 _lib = None
 

@@ -132,15 +132,16 @@ int rs_wgrad_grouped_pos(int nprob, const rs_wgrad_problem* probs, int64_t M, in
                          int64_t T_, const void* dx, int64_t d, float drop_p, uint64_t salt,
                          const uint64_t* seed_base, float* dpos, void* stream) {
   return rs_wgrad_grouped_pos_stats(nprob, probs, M, rows_per_split, slab, slab_numel, nextra, extra, ids, T_, dx, d,
-                                    drop_p, salt, seed_base, dpos, nullptr, nullptr, nullptr, stream);
+                                    drop_p, salt, seed_base, dpos, nullptr, 0, nullptr, nullptr, stream);
 }
 
 int rs_wgrad_grouped_pos_stats(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_t rows_per_split,
                                float* slab, int64_t slab_numel, int nextra, const rs_reduce_segment* extra,
                                const int64_t* ids, int64_t T_, const void* dx, int64_t d, float drop_p, uint64_t salt,
-                               const uint64_t* seed_base, float* dpos, const float* head_part,
+                               const uint64_t* seed_base, float* dpos, const float* head_part, int64_t head_blocks,
                                const float* head_divisor, float* loss_out, void* stream) {
-  if (!ids || !dx || !dpos || T_ <= 0 || M % T_ || !head_part != !loss_out) return RS_ERR_ARG;
+  if (!ids || !dx || !dpos || T_ <= 0 || M % T_ || !head_part != !loss_out || (loss_out && head_blocks <= 0))
+    return RS_ERR_ARG;
   wg::Args a;
   int T, ns;
   rs_reduce_segment segs[2 * wg::MAXP + wg::MAXS];
@@ -152,7 +153,7 @@ int rs_wgrad_grouped_pos_stats(int nprob, const rs_wgrad_problem* probs, int64_t
     if (int e = rs_embed_bwd(RS_DTYPE_BF16, 0, ids, M, T_, dx, d, 1.f, drop_p, salt, seed_base, nullptr, dpos, 1,
                              stream))
       return e;
-    return loss_out ? rs_sas_head_finish(M, head_part, head_divisor, loss_out, stream) : 0;
+    return loss_out ? rs_sas_head_finish(head_blocks, head_part, head_divisor, loss_out, stream) : 0;
   }
   wg::RArgs r;
   int rblk;
@@ -166,7 +167,7 @@ int rs_wgrad_grouped_pos_stats(int nprob, const rs_wgrad_problem* probs, int64_t
   else hipLaunchKernelGGL(wg::wgrad_group_kernel<64>, grid, dim3(256), 0, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  const gt::HeadStats hs{(int)cdiv(M, hd::RB), head_part, head_divisor, loss_out};
+  const gt::HeadStats hs{(int)head_blocks, head_part, head_divisor, loss_out};
   hipLaunchKernelGGL(gt::reduce_pos_kernel, dim3((unsigned)(rblk + T_ + (loss_out ? 1 : 0))), dim3(256), 0, s, r, rblk,
                      (int)cols, ids, M, T_, (const __bf16*)dx, d, drop_p, salt, seed_base, dpos, hs);
   return (int)hipGetLastError();

@@ -460,9 +460,9 @@ int rs_sas_head_fused(int64_t M, int64_t d, const void* x, const float* ln_w, co
   return (int)hipGetLastError();
 }
 
-int rs_sas_head_finish(int64_t M, const float* part, const float* divisor, float* out, void* stream) {
-  if (M <= 0 || !part || !out) return RS_ERR_ARG;
-  hipLaunchKernelGGL(hd::head_finish_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, (int)cdiv(M, hd::RB), part,
+int rs_sas_head_finish(int64_t nblk, const float* part, const float* divisor, float* out, void* stream) {
+  if (nblk <= 0 || !part || !out) return RS_ERR_ARG;
+  hipLaunchKernelGGL(hd::head_finish_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, (int)nblk, part,
                      divisor, out);
   return (int)hipGetLastError();
 }

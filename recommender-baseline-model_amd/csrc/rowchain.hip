@@ -39,6 +39,10 @@ __device__ unsigned long long g_rc_prof[4096 * 8 * 16];
   } while (0)
 #endif
 
+#ifndef RC_HEAD_PREFETCH
+#define RC_HEAD_PREFETCH 1   // where the head's item-row loads are issued: 0 tile start, 1 mid-chain (A/B: 0.2999 vs 0.3020 ms at cfg2), 2 after it
+#endif
+
 #ifndef RC_NOSTORE
 #define RC_NOSTORE 0   // tools/micro/rowchain_phase.hip: 1 = skip block_out's saved-tensor stores (cost probe)
 #endif
@@ -595,6 +599,18 @@ __global__ __launch_bounds__(NT) void block_in_kernel(InArgs a) {
   if (emb && a.e.cnt_parts && lane == 0) a.e.cnt_parts[blockIdx.x * NW + wave] = cnt;
 }
 
+// The SAS output head riding in the LAST block's output kernel (rs_sas_block_out_head): every quantity of the head
+// is token-local once the BCE divisor is known (the valid-position count, summed from the first block's per-wave
+// counts), so each tile's x_L = x' goes on, in registers, through the last LayerNorm (f saved), the tied sampled
+// logits <f, E[pos]>, <f, E[neg]>, the BCE gradient (dpl, dnl saved), df = dpl E[pos] + dnl E[neg] and the last
+// LayerNorm's backward (dx_L saved for the blocks' backward; affine partials per workgroup, BCE partials sp, sn,
+// count per workgroup for the loss statistics).  Same math as head.hip's kernels (sums in this layout's order).
+struct HeadArgs {
+  const bf16* E; const int64_t* pos; const int64_t* neg;
+  const float* gl; const float* bl; float eps;
+  const int* cnt_parts; int ncnt; const float* divisor;
+  bf16* f; float* pl; float* nl; float* dpl; float* dnl; bf16* dx; float* lnpart; float* part;
+};
 struct OutArgs {
   int64_t M;
   const bf16* o; const bf16* Q;
@@ -604,7 +620,66 @@ struct OutArgs {
   const bf16* W2; const float* b2; bf16* xn;
   const int64_t* ids;
   float drop_p; uint64_t salt1, salt2; const uint64_t* seed_base;
+  HeadArgs h;                                               // h.E == nullptr: no head
 };
+__device__ __forceinline__ float h_softplus(float z) { return fmaxf(z, 0.f) + log1pf(__expf(-fabsf(z))); }
+__device__ __forceinline__ float h_sigmoid(float z) { return 1.f / (1.f + __expf(-z)); }
+
+// the tile's item rows E[pos], E[neg] (issued at the tile's start: their latency hides behind the block's chain)
+template <int D>
+__device__ __forceinline__ int64_t head_rows(const HeadArgs& h, const Tile& T, Raw<D>& er, Raw<D>& nr, int g) {
+  const int64_t ip = h.pos[T.mc], in = h.neg[T.mc];
+  load_raw<D>(er, h.E, D, ip, g);
+  load_raw<D>(nr, h.E, D, in, g);
+  return ip;
+}
+template <int D>
+__device__ __forceinline__ void head_tile(const Raw<D>& xr, const Raw<D>& er, const Raw<D>& nr, int64_t ip,
+                                          const Tile& T, const float* gl, const float* bl, const HeadArgs& h,
+                                          float scale, float* red, float (&acc)[3], int lane, int wave) {
+  const int g = lane >> 4;
+  Act<D> y;
+  to_act<D>(y, xr);
+  float mu, rs;
+  ln_fwd<D>(y, gl, bl, h.eps, g, mu, rs);
+  Raw<D> fr;
+  round_act<D>(y, fr);                       // the logits read the stored (bf16) features
+  store_raw<D>(h.f, D, T.m, T.ok, fr, g);
+  float dp = 0.f, dn = 0.f;
+#pragma unroll
+  for (int j = 0; j < Lay<D>::J; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      dp += y.v[j][e] * (float)er.v[j >> 1][4 * (j & 1) + e];
+      dn += y.v[j][e] * (float)nr.v[j >> 1][4 * (j & 1) + e];
+    }
+  dp = row_sum(dp);
+  dn = row_sum(dn);
+  const bool valid = T.ok && ip != 0;
+  const float gp = valid ? (h_sigmoid(dp) - 1.f) * scale : 0.f;
+  const float gn = valid ? h_sigmoid(dn) * scale : 0.f;
+  if (T.ok && g == 0) {
+    h.pl[T.m] = dp;
+    h.nl[T.m] = dn;
+    h.dpl[T.m] = gp;
+    h.dnl[T.m] = gn;
+    if (ip != 0) {
+      acc[0] += h_softplus(-dp);
+      acc[1] += h_softplus(dn);
+      acc[2] += 1.f;
+    }
+  }
+  Act<D> df;
+#pragma unroll
+  for (int j = 0; j < Lay<D>::J; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      df.v[j][e] = gp * (float)er.v[j >> 1][4 * (j & 1) + e] + gn * (float)nr.v[j >> 1][4 * (j & 1) + e];
+  ln_bwd<D>(df, xr, T.ok, gl, mu, rs, red, lane, wave);
+  Raw<D> dr;
+  round_act<D>(df, dr);
+  store_raw<D>(h.dx, D, T.m, T.ok, dr, g);
+}
 __device__ __forceinline__ OutFwd out_fwd_of(const OutArgs& a) {
   const bool drop = a.drop_p > 0.f;
   return OutFwd{a.x1, a.z, a.h1, a.xn, a.mean, a.rstd, a.ids, a.drop_p, a.eps,
@@ -613,12 +688,15 @@ __device__ __forceinline__ OutFwd out_fwd_of(const OutArgs& a) {
 
 // O -> x1 = Q + O Wo^T + bo [saved], z = LN2(x1) [saved], h1 = relu(drop(z W1^T + b1)) [saved],
 // x' = (drop(h1 W2^T + b2) + z) * (ids != 0)
-template <int D>
+template <int D, bool HEAD>
 __global__ __launch_bounds__(NT) void block_out_kernel(OutArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  typedef Smem<D, 3, 5, 0> L;
+  typedef Smem<D, 3, 7, 1> L;
   constexpr int WB = Lay<D>::WBYTES;
-  const float* lv = reinterpret_cast<const float*>(smem + L::W);   // bo, ln_w, ln_b, b1, b2
+  const float* lv = reinterpret_cast<const float*>(smem + L::W);   // bo, ln_w, ln_b, b1, b2 (+ head: gl, bl)
+  float* red = reinterpret_cast<float*>(smem + L::V);
+  constexpr bool head = HEAD;
+  __shared__ float hred[4][NW];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
             cl = lane & 15;
   RCPROF(0);
@@ -635,10 +713,31 @@ __global__ __launch_bounds__(NT) void block_out_kernel(OutArgs a) {
     const bf16* const W[3] = {a.Wo, a.W1, a.W2};
     const int64_t ldw[3] = {D, D, D};
     stage_w<D, 3>(smem, W, ldw, wave, lane);
-    const float* const V[5] = {a.bo, a.ln_w, a.ln_b, a.b1, a.b2};
-    stage_v<D, 5>(reinterpret_cast<float*>(smem + L::W), V, tid);
+    if (head) {
+      const float* const V[7] = {a.bo, a.ln_w, a.ln_b, a.b1, a.b2, a.h.gl, a.h.bl};
+      stage_v<D, 7>(reinterpret_cast<float*>(smem + L::W), V, tid);
+    } else {
+      const float* const V[5] = {a.bo, a.ln_w, a.ln_b, a.b1, a.b2};
+      stage_v<D, 5>(reinterpret_cast<float*>(smem + L::W), V, tid);
+    }
+  }
+  // head: the loss's divisor (the valid count: integer partials, any order is exact) and zeroed LN partial rows
+  float hscale = 0.f;
+  float hacc[3] = {0.f, 0.f, 0.f};
+  if (head) {
+    ln_zero(red, D, lane, wave);
+    int c = 0;
+    for (int i = tid; i < a.h.ncnt; i += NT) c += a.h.cnt_parts[i];
+    c = (int)wave_sum((float)c);   // exact: counts < 2^24
+    if (lane == 0) hred[3][wave] = (float)c;
   }
   __syncthreads();
+  if (head) {
+    float c = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) c += hred[3][w];
+    hscale = 1.f / (a.h.divisor ? *a.h.divisor : c);
+  }
   RCPROF(1);
   for (; t < nt; t += G * NW) {
     asm volatile("" ::: "memory");
@@ -647,13 +746,33 @@ __global__ __launch_bounds__(NT) void block_out_kernel(OutArgs a) {
       load_raw<D>(orr, a.o, D, T.mc, g);
       load_raw<D>(Qr, a.Q, D, T.mc, g);
     }
-    Raw<D> zr, hr, xr;
+    Raw<D> zr, hr, xr, er, nr;
+    int64_t ip = 0;
+    if (head && RC_HEAD_PREFETCH == 0) ip = head_rows<D>(a.h, T, er, nr, g);
     fwd_out_a<D>(orr, Qr, T, wslot(smem, 0, WB), wslot(smem, 1, WB), lv, of, zr, hr, lane);
     RCPROF(2);
+    if (head && RC_HEAD_PREFETCH == 1) ip = head_rows<D>(a.h, T, er, nr, g);
     fwd_out_b<D>(hr, zr, T, wslot(smem, 2, WB), lv, of, xr, lane);
     RCPROF(4);
+    if (head && RC_HEAD_PREFETCH == 2) ip = head_rows<D>(a.h, T, er, nr, g);
+    if (head) head_tile<D>(xr, er, nr, ip, T, lv + 5 * D, lv + 6 * D, a.h, hscale, red, hacc, lane, wave);
   }
   RCPROF(5);
+  if (head) {
+    // BCE partials: lanes -> waves -> the workgroup's row (fixed order); LN affine partials likewise
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const float v = wave_sum(hacc[k]);
+      if (lane == 0) hred[k][wave] = v;
+    }
+    ln_partials<D>(red, a.h.lnpart, tid);   // begins with a barrier
+    if (tid < 3) {
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) v += hred[tid][w];
+      a.h.part[blockIdx.x * 3 + tid] = v;
+    }
+  }
 }
 
 struct OutBwdArgs {
@@ -801,11 +920,29 @@ static int64_t grid_for(int64_t M) {
   return nt < g_ncu ? nt : g_ncu;
 }
 template <int D> static size_t lds_fwd() { return Smem<D, 3, 5, 0>::BYTES; }
+template <int D, bool HEAD> static size_t lds_out() {
+  return HEAD ? Smem<D, 3, 7, 1>::BYTES : Smem<D, 3, 5, 0>::BYTES;
+}
 template <int D> static size_t lds_bwd() { return Smem<D, 3, 1, 1>::BYTES; }
 
 template <typename K>
 static void set_lds(K kern, size_t bytes) {
-  hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+template <int D, bool HEAD>
+static void launch_out_t(const OutArgs& a, hipStream_t s) {
+  constexpr auto k = block_out_kernel<D, HEAD>;
+  const size_t lds = lds_out<D, HEAD>();
+  set_lds(k, lds);
+  hipLaunchKernelGGL(k, dim3((unsigned)grid_for(a.M)), dim3(NT), lds, s, a);
+}
+static int launch_out(const OutArgs& a, int64_t d, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const bool head = a.h.E != nullptr;
+  if (d == 64) head ? launch_out_t<64, true>(a, s) : launch_out_t<64, false>(a, s);
+  else if (d == 128) head ? launch_out_t<128, true>(a, s) : launch_out_t<128, false>(a, s);
+  else return RS_ERR_UNSUPPORTED;
+  return (int)hipGetLastError();
 }
 
 }  // namespace rc
@@ -914,18 +1051,27 @@ int rs_sas_block_out(int64_t M, int64_t d, const void* o, const void* Q, const v
   rc::OutArgs a = {M, (const __bf16*)o, (const __bf16*)Q, (const __bf16*)Wo, bo, (__bf16*)x1, ln_w, ln_b, eps,
                    (__bf16*)z, mean, rstd, (const __bf16*)W1, b1, (__bf16*)h1, (const __bf16*)W2, b2, (__bf16*)xn,
                    ids, drop_p, salt1, salt2, seed_base};
-  const dim3 grid((unsigned)rc::grid_for(M));
-  hipStream_t s = (hipStream_t)stream;
-  if (d == 64) {
-    rc::set_lds(rc::block_out_kernel<64>, rc::lds_fwd<64>());
-    hipLaunchKernelGGL(rc::block_out_kernel<64>, grid, dim3(rc::NT), rc::lds_fwd<64>(), s, a);
-  } else if (d == 128) {
-    rc::set_lds(rc::block_out_kernel<128>, rc::lds_fwd<128>());
-    hipLaunchKernelGGL(rc::block_out_kernel<128>, grid, dim3(rc::NT), rc::lds_fwd<128>(), s, a);
-  } else {
-    return RS_ERR_UNSUPPORTED;
-  }
-  return (int)hipGetLastError();
+  return rc::launch_out(a, d, stream);
+}
+
+int64_t rs_sas_block_grid(int64_t M) { return M > 0 ? rc::grid_for(M) : 0; }
+
+int rs_sas_block_out_head(int64_t M, int64_t d, const void* o, const void* Q, const void* Wo, const float* bo,
+                          void* x1, const float* ln_w, const float* ln_b, float eps, void* z, float* mean, float* rstd,
+                          const void* W1, const float* b1, void* h1, const void* W2, const float* b2, void* xn,
+                          const int64_t* ids, float drop_p, uint64_t salt1, uint64_t salt2,
+                          const uint64_t* seed_base, const void* E, const int64_t* pos, const int64_t* neg,
+                          const float* lnl_w, const float* lnl_b, const int* count_parts, int64_t ncount,
+                          const float* divisor, void* f, float* pl, float* nl, float* dpl, float* dnl, void* dx,
+                          float* lnpart, float* part, void* stream) {
+  if (M <= 0 || !E || !pos || !neg || !count_parts || ncount <= 0 || !f || !dx || !lnpart || !part) return RS_ERR_ARG;
+  if (!use_chain() || (d != 64 && d != 128)) return RS_ERR_UNSUPPORTED;
+  rc::OutArgs a = {M, (const __bf16*)o, (const __bf16*)Q, (const __bf16*)Wo, bo, (__bf16*)x1, ln_w, ln_b, eps,
+                   (__bf16*)z, mean, rstd, (const __bf16*)W1, b1, (__bf16*)h1, (const __bf16*)W2, b2, (__bf16*)xn,
+                   ids, drop_p, salt1, salt2, seed_base,
+                   rc::HeadArgs{(const __bf16*)E, pos, neg, lnl_w, lnl_b, eps, count_parts, (int)ncount, divisor,
+                                (__bf16*)f, pl, nl, dpl, dnl, (__bf16*)dx, lnpart, part}};
+  return rc::launch_out(a, d, stream);
 }
 
 int rs_sas_block_out_bwd(int64_t M, int64_t d, const void* dxn, const int64_t* ids, const void* h1, const void* x1,

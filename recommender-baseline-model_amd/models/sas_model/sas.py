@@ -187,10 +187,13 @@ class SASEngine:
         return torch.empty(shape, dtype=dtype or self.dt, device=self.dev)
 
     # ---- forward -------------------------------------------------------------------
-    def forward(self, ids, pos, neg, training, need_logits=True, clone_seed=True, fuse_head=False):
+    def forward(self, ids, pos, neg, training, need_logits=True, clone_seed=True, fuse_head=False,
+                head_divisor=None):
         """fuse_head (the fused training step, whose backward forms the BCE gradient itself): the head's forward
-        is left to backward, which runs it and the head's backward as ONE kernel (rs_sas_head_fused); the
-        returned pl / nl are filled there.  The embedding forward counts the valid positions for it."""
+        and backward run as one pass per token -- inside the last block's output kernel (rs_sas_block_out_head),
+        or else as one kernel in backward (rs_sas_head_fused); the returned pl / nl are filled by then.  The
+        embedding stage counts the valid positions (the BCE divisor) for it; head_divisor (device scalar, data
+        parallel: 1) replaces that count and must be the divisor later passed to backward."""
         B, T = ids.shape
         M, d, H, Dh, L = B * T, self.d, self.H, self.Dh, self.L
         p = self.p if training else 0.0
@@ -235,8 +238,21 @@ class SASEngine:
                 s["side"] = self._side_prologue(ids, pos, neg, after=fork)
         if not emb_in:
             after_first()
+        head = None
+        if cntp is not None and os.environ.get("RS_ROWCHAIN", "1") != "0" and \
+                os.environ.get("RS_SAS_HEAD_IN_BLOCK", "1") != "0":
+            # the head inside the last block's output kernel: its outputs, per-workgroup partials
+            Gb = ops.sas_block_grid(M)
+            f32 = torch.float32
+            s.update(head_in_block=True, hdiv=head_divisor, f=e("f", (M, d)), pl=e("pl", (B, T), f32),
+                     nl=e("nl", (B, T), f32), dpl=e("dpl", (B, T), f32), dnl=e("dnl", (B, T), f32),
+                     hdx=e("dx", (M, d)), lnh=self.ws.get("lnh_blk", (2 * d * Gb,), f32),
+                     headp=e("headp", (3 * Gb,), f32))
+            head = (self.W("item_emb.weight"), pos, neg, self.Wf("last_layernorm.weight"),
+                    self.Wf("last_layernorm.bias"), cntp, head_divisor, s["f"], s["pl"], s["nl"], s["dpl"], s["dnl"],
+                    s["hdx"], s["lnh"], s["headp"])
         if fused:
-            x = self._forward_blocks_fused(s, x, emb=emb if emb_in else None, after_first=after_first)
+            x = self._forward_blocks_fused(s, x, emb=emb if emb_in else None, after_first=after_first, head=head)
         else:
             for i in range(L):
                 pre = f"attention_layers.{i}."
@@ -266,6 +282,9 @@ class SASEngine:
                                ("lse", lse), ("x1", x1), ("z", z), ("mu2", mu2), ("r2", r2), ("h1", h1)):
                     s[k_].append(v_)
                 x = xn
+        if "head_in_block" in s:
+            s.update(xL=x)
+            return s["pl"], s["nl"], s
         f, muf, rf = e("f", (M, d)), e("mu", (M,), torch.float32), e("r", (M,), torch.float32)
         s.update(xL=x, f=f, muf=muf, rf=rf)
         if "cntp" in s:
@@ -287,11 +306,12 @@ class SASEngine:
         ops.sampled_logits_fwd(f, self.W("item_emb.weight"), pos, neg, pl, nl)
         return pl, nl, s
 
-    def _forward_blocks_fused(self, s, x, emb=None, after_first=None):
+    def _forward_blocks_fused(self, s, x, emb=None, after_first=None, head=None):
         """SAS blocks' forward with the row-chain kernels (rowchain.hip) on each side of the attention core
         (rs_sas_block_in, rs_attn_fwd, rs_sas_block_out per block).  Fills s's per-block saved tensors; returns the
         last block's output.  emb: sas_block_in_embed's embedding arguments (x is then its x0 output, formed by the
-        first launch); after_first(): called after the first launch."""
+        first launch); after_first(): called after the first launch; head: sas_block_out_head's head arguments
+        (the last block's output kernel then also runs the SAS head)."""
         B, T, p, ids, sb = s["B"], s["T"], s["p"], s["ids"], s["sb"]
         M, d, H, Dh, L = B * T, self.d, self.H, self.Dh, self.L
         e = self._buf
@@ -328,7 +348,10 @@ class SASEngine:
             b = lay[i]
             ops.attn_fwd(B, T, H, Dh, b["q"], b["kv"][:, :d], b["kv"][:, d:], b["o"], b["lse"], 1.0 / math.sqrt(Dh),
                          0, ids, p, self.salt[f"attn{i}"], sb)
-            ops.sas_block_out(*out_args(i))
+            if head is not None and i == L - 1:
+                ops.sas_block_out_head(out_args(i), *head)
+            else:
+                ops.sas_block_out(*out_args(i))
             if i + 1 < L:
                 ln_w, ln_b, Q, mu1, r1, Wq, bq, q, Wkv, bkv, kv = in_args(i + 1)
                 ops.sas_block_in(b["xn"], ln_w, ln_b, LN_EPS, Q, mu1, r1, Wq, bq, q, Wkv, bkv, kv)
@@ -369,7 +392,15 @@ class SASEngine:
             lnh = self.ws.get("lnh", (2 * d * (-(-M // 64)),), torch.float32)
             E, gl = self.W("item_emb.weight"), self.Wf("last_layernorm.weight")
             stats = ()
-            if dpl is None and "cntp" in s:
+            nb = -(-M // 64)
+            if dpl is None and "head_in_block" in s:
+                # the head ran inside the last block's output kernel (forward)
+                assert s["hdiv"] is divisor, "backward's divisor must be the one forward's head used"
+                dx, dpl, dnl, lnh = s["hdx"], s["dpl"], s["dnl"], s["lnh"]
+                nb = s["headp"].numel() // 3
+                if loss_out is not None:
+                    stats = (s["headp"], divisor, loss_out)
+            elif dpl is None and "cntp" in s:
                 # the head's forward and backward in one kernel; the loss statistics (one workgroup) ride in the
                 # gradient tail's reduction launch
                 dpl, dnl = e("dpl", (B, T), torch.float32), e("dnl", (B, T), torch.float32)
@@ -384,8 +415,7 @@ class SASEngine:
             else:
                 ops.sas_head_bwd(None, None, None, None, None, dpl, dnl, None, None, s["pos"], s["neg"], E, s["xL"],
                                  gl, s["muf"], s["rf"], dx, lnh)
-            segs = ops.ln_partial_segments(lnh, M, d, G("last_layernorm.weight"), G("last_layernorm.bias"),
-                                           nb=-(-M // 64))
+            segs = ops.ln_partial_segments(lnh, M, d, G("last_layernorm.weight"), G("last_layernorm.bias"), nb=nb)
             # the item table's gradient: "side" (default) = rs_item_grad on the side queue beside the grouped
             # weight gradients; "fused" = inside those launches on this queue (rs_wgrad_grouped_items; measured
             # 0.367 vs 0.356 ms/step at cfg2: the item chunks queue behind the weight-gradient tiles); "serial"
@@ -414,7 +444,7 @@ class SASEngine:
             if not pos_merged:
                 ops.embed_bwd(0, ids, T, dx, math.sqrt(d), p, self.salt["emb"], sb, None, G("pos_emb.weight"))
                 if stats:
-                    ops.sas_head_finish(M, *stats)
+                    ops.sas_head_finish(*stats)
             if side:
                 torch.cuda.current_stream().wait_event(self._tail_join)
             elif tail_mode != "fused":

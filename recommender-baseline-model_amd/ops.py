@@ -448,6 +448,25 @@ def sas_block_in_embed(ids, T, item_emb, pos_emb, scale, drop_p, salt, seed_base
          ptr(rstd), ptr(Wq), ptr(bq), ptr(q), ptr(Wkv), ptr(bkv), ptr(kv), stream())
 
 
+def sas_block_grid(M):
+    return int(_lib.lib().rs_sas_block_grid(M))
+
+
+def sas_block_out_head(out_args, E, pos, neg, lnl_w, lnl_b, count_parts, divisor, f, pl, nl, dpl, dnl, dx, lnpart,
+                       part):
+    """sas_block_out(*out_args) for the last block with the SAS head in the same launch (rowchain);
+    lnpart [G][2][d], part [G][3] with G = sas_block_grid(M)."""
+    (o, Q, Wo, bo, x1, ln_w, ln_b, eps, z, mean, rstd, W1, b1, h1, W2, b2, xn, ids, drop_p, salt1, salt2,
+     seed_base) = out_args
+    M, d = o.shape
+    G = sas_block_grid(M)
+    assert part.numel() == 3 * G and lnpart.numel() >= 2 * d * G and count_parts.dtype == torch.int32
+    call("rs_sas_block_out_head", M, d, ptr(o), ptr(Q), ptr(Wo), ptr(bo), ptr(x1), ptr(ln_w), ptr(ln_b), eps, ptr(z),
+         ptr(mean), ptr(rstd), ptr(W1), ptr(b1), ptr(h1), ptr(W2), ptr(b2), ptr(xn), ptr(ids), drop_p, salt1, salt2,
+         ptr(seed_base), ptr(E), ptr(pos), ptr(neg), ptr(lnl_w), ptr(lnl_b), ptr(count_parts), count_parts.numel(),
+         ptr(divisor), ptr(f), ptr(pl), ptr(nl), ptr(dpl), ptr(dnl), ptr(dx), ptr(lnpart), ptr(part), stream())
+
+
 def sas_block_out(o, Q, Wo, bo, x1, ln_w, ln_b, eps, z, mean, rstd, W1, b1, h1, W2, b2, xn, ids, drop_p,
                   salt1, salt2, seed_base):
     M, d = o.shape
@@ -534,7 +553,7 @@ def wgrad_grouped(problems, M, rows_per_split, slab, extra=(), items=None, pos=N
             hp, hdiv, lout = st
             call("rs_wgrad_grouped_pos_stats", len(problems), arr, M, rows_per_split, ptr(slab), slab.numel(),
                  len(extra), segs, ptr(ids), T, ptr(dx), dx.shape[-1], drop_p, salt, ptr(seed_base), ptr(dpos),
-                 ptr(hp), ptr(hdiv), ptr(lout), stream())
+                 ptr(hp), hp.numel() // 3, ptr(hdiv), ptr(lout), stream())
             return
         call("rs_wgrad_grouped_pos", len(problems), arr, M, rows_per_split, ptr(slab), slab.numel(), len(extra),
              segs, ptr(ids), T, ptr(dx), dx.shape[-1], drop_p, salt, ptr(seed_base), ptr(dpos), stream())
@@ -611,8 +630,9 @@ def sas_head_fused(x, ln_w, ln_b, eps, count_parts, divisor, f, E, pos, neg, pl,
          ptr(part), stream())
 
 
-def sas_head_finish(M, part, divisor, out, stream_=None):
-    call("rs_sas_head_finish", M, ptr(part), ptr(divisor), ptr(out), stream_ if stream_ is not None else stream())
+def sas_head_finish(part, divisor, out):
+    """Loss statistics out[0..3] from the head's BCE partials part[nblk][3] (one workgroup)."""
+    call("rs_sas_head_finish", part.numel() // 3, ptr(part), ptr(divisor), ptr(out), stream())
 
 
 # ---- on-device sampler and ranking metrics (sampler.hip) -----------------------------------

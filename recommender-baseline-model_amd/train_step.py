@@ -208,7 +208,8 @@ class FusedTrainStep:
                 split(tag, action)
         if self.kind == "sas":
             seq, pos, neg = batch
-            pl, nl, saved = eng.forward(seq, pos, neg, True, clone_seed=False, fuse_head=eng.fused_head)
+            pl, nl, saved = eng.forward(seq, pos, neg, True, clone_seed=False, fuse_head=eng.fused_head,
+                                        head_divisor=self.one if self.dp else None)
             if eng.fused_head:
                 # BCE forward/backward inside the fused head kernels (head.hip)
                 eng.backward(saved, None, None, self.flat.grad, loss_out=self.loss_out,

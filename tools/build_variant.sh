@@ -1,0 +1,14 @@
+#!/bin/bash
+# Build librecsys_hip.$NAME.so: SRC (a csrc/*.hip translation unit) recompiled with extra FLAGS, linked with the
+# other in-tree objects (run the normal build first).  For A/B timing with RS_LIB_VARIANT=$NAME (tools/ab_bench.sh).
+#   NAME=p1 SRC=rowchain.hip FLAGS="-DRC_HEAD_PREFETCH=1" bash tools/build_variant.sh
+set -e
+cd "$(dirname "$0")/.."
+PKG=recommender-baseline-model_amd
+OBJ=$PKG/csrc/build
+mkdir -p /tmp/rsvar
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -I include -I $PKG/csrc $FLAGS \
+  -c $PKG/csrc/$SRC -o /tmp/rsvar/$SRC.$NAME.o
+objs=$(ls $OBJ/*.o | grep -v "/$SRC.o$")
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 $objs /tmp/rsvar/$SRC.$NAME.o -o $PKG/librecsys_hip.$NAME.so
+echo $PKG/librecsys_hip.$NAME.so
