@@ -25,7 +25,7 @@ for c in ${CONFIGS:-cfg2 cfg3 cfg4 cfg5}; do
   timeout -k 10 900 python bench.py --config $c $CB $ST > $OUT/bench_$c.log 2>&1; rc=$?; tail -1 $OUT/bench_$c.log | cut -c1-160
   [ $rc -eq 0 ] || exit $rc
   tail -1 $OUT/bench_$c.log > $OUT/bench_$c.json
-  PS="--steps 50 --warmup 10"; [ "$c" = "cfg5" ] && PS="--steps 10 --warmup 3"
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_$c -o prof --output-format csv -- python3 bench.py --config $c $PS --cpu-baseline-seconds 0 > $OUT/rocprof_$c.log 2>&1 || { tail -20 $OUT/rocprof_$c.log; exit 1; }
 done
+# rocprof kernel stats + one step's timeline per config (raw traces deleted: gpurun copies back <= 64 MiB)
+CONFIGS="${CONFIGS:-cfg2 cfg3 cfg4 cfg5}" TAG=${TAG:-art} bash tools/gpu_profile.sh || exit 1
 echo done
