@@ -126,6 +126,11 @@ int rs_layernorm_bwd(int dtype, int variant, const void* X, int64_t ldx, const v
                      int64_t M, int64_t d, const float* gamma, const float* mean, const float* rinv, float eps,
                      void* dX, int64_t lddx, int accumulate_dx, float* dgamma, float* dbeta, float* ws,
                      void* stream);
+/* The affine-gradient partial count of rs_layernorm_bwd's vectorised path (d a multiple of 8 bf16 / 4 fp32 with
+ * 16-byte aligned rows and leading dimensions): with dgamma = dbeta = NULL it leaves ws[nparts][2][d] (gamma
+ * terms, then beta terms) unreduced, for a later grouped reduction (rs_reduce_segments / rs_wgrad_grouped's extra
+ * segments).  0 = the shape takes the other path (pass dgamma/dbeta). */
+int64_t rs_layernorm_bwd_nparts(int dtype, int64_t M, int64_t d);
 
 /* Fused scaled-dot-product attention per (sequence, head), T keys, head dim Dh.
  * q/k/v/o rows are tokens (b*T + t); head h occupies columns [h*Dh, (h+1)*Dh).

@@ -58,6 +58,7 @@ SIGNATURES = {
     "rs_embed_count_parts": [i32, i64, i64],
     "rs_embed_bwd": [i32, i32, vp, i64, i64, vp, i64, f32, f32, u64, vp, vp, vp, i32, vp],
     "rs_layernorm_fwd": [i32, i32, vp, i64, i64, i64, vp, vp, f32, vp, i64, vp, vp, vp],
+    "rs_layernorm_bwd_nparts": [i32, i64, i64],
     "rs_layernorm_bwd": [i32, i32, vp, i64, vp, i64, i64, i64, vp, vp, vp, f32, vp, i64, i32, vp, vp, vp, vp],
     "rs_attn_fwd": [i32, i64, i64, i64, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp, f32, i32, vp, f32, u64, vp, vp],
     "rs_attn_row_delta": [i32, i64, i64, i64, i64, vp, i64, vp, i64, vp, vp],
@@ -141,7 +142,7 @@ RESTYPES = {"rs_wgrad_grouped_slab_numel": C.c_int64, "rs_sas_block_parts": C.c_
             "rs_touched_rows_ws_numel": C.c_int64, "rs_item_index_ws_bytes": C.c_int64,
             "rs_vocab_ce_ws_numel": C.c_int64,
             "rs_embed_count_parts": C.c_int64, "rs_sas_block_in_count_parts": C.c_int64,
-            "rs_sas_block_grid": C.c_int64}
+            "rs_sas_block_grid": C.c_int64, "rs_layernorm_bwd_nparts": C.c_int64}
 
 _lib = None
 

@@ -408,6 +408,16 @@ int rs_layernorm_fwd(int dtype, int variant, const void* X, int64_t ldx, int64_t
                    : ln_fwd_t<float>(X, ldx, M, (int)d, gamma, beta, eps, variant, Y, ldy, mean, rinv, s));
 }
 
+int64_t rs_layernorm_bwd_nparts(int dtype, int64_t M, int64_t d) {
+  const int V = dtype == RS_DTYPE_BF16 ? Vec<__bf16>::N : Vec<float>::N;
+  if (M <= 0 || d <= 1 || d % V) return 0;
+  const int64_t cpr = d / V;
+  const int64_t lpr = (cpr == 4 || cpr == 8 || cpr == 16 || cpr == 32 || cpr == 64) ? cpr : cpr == 128 ? 64 : 0;
+  if (!lpr) return 0;
+  const int64_t rpb = 4 * (64 / lpr);
+  return std::min<int64_t>(LN_BWD_BLOCKS / 2, cdiv(M, rpb * 4));
+}
+
 int rs_layernorm_bwd(int dtype, int variant, const void* X, int64_t ldx, const void* dY, int64_t lddy,
                      int64_t M, int64_t d, const float* gamma, const float* mean, const float* rinv, float eps,
                      void* dX, int64_t lddx, int accumulate_dx, float* dgamma, float* dbeta, float* ws,

@@ -260,6 +260,19 @@ class BERTEngine:
         grouped = (self.dt == torch.bfloat16 and self.qkv_fused and d % 64 == 0 and Fd % 64 == 0
                    and os.environ.get("RS_BERT_UNGROUPED", "0") != "1")
         probs = []
+        ln_segs = []
+
+        def ln_bwd(X, dY, gname, bname, mean, rstd, dX, tag):
+            """LayerNorm backward; grouped: its affine partials are summed by the grouped launch's reduction (no
+            reduction launch per LayerNorm on the backward's critical path)"""
+            nparts = ops.layernorm_bwd_nparts(X) if grouped else 0
+            if nparts:
+                part = self.ws.get(f"lnpart_{tag}", (2 * d * nparts,), torch.float32)
+                ops.layernorm_bwd(X, dY, self.Wf(gname), mean, rstd, LN_EPS, dX, None, None, part, 1, accumulate=True)
+                ln_segs.extend(ops.ln_partial_segments(part, M, d, G(gname), G(bname), nb=nparts))
+            else:
+                ops.layernorm_bwd(X, dY, self.Wf(gname), mean, rstd, LN_EPS, dX, G(gname), G(bname), wln, 1,
+                                  accumulate=True)
 
         def wgrad(dY, X, dW, db):
             if grouped:
@@ -285,9 +298,8 @@ class BERTEngine:
             wgrad(da, a["h2"], G(pre + "feed_forward.w_1.weight"), G(pre + "feed_forward.w_1.bias"))
             dh2 = e((M, d))
             ops.linear_dgrad(da, self.W(pre + "feed_forward.w_1.weight"), dh2)
-            ops.layernorm_bwd(a["x1"], dh2, self.Wf(pre + "output_sublayer.norm.a_2"), a["mu2"], a["r2"], LN_EPS, dx2,
-                              G(pre + "output_sublayer.norm.a_2"), G(pre + "output_sublayer.norm.b_2"), wln, 1,
-                              accumulate=True)
+            ln_bwd(a["x1"], dh2, pre + "output_sublayer.norm.a_2", pre + "output_sublayer.norm.b_2", a["mu2"], a["r2"],
+                   dx2, f"{i}o")
             # x1 = x + drop_res1(o Wo^T + bo)
             if hp > 0 or grouped:
                 dyo = e((M, d))
@@ -315,9 +327,8 @@ class BERTEngine:
                                      db=G(self._qkv(i, j, "bias")))
                     ops.linear_dgrad(dqkv[:, j * d:(j + 1) * d], self.W(self._qkv(i, j, "weight")), dh,
                                      accumulate=j > 0)
-            ops.layernorm_bwd(a["x"], dh, self.Wf(pre + "input_sublayer.norm.a_2"), a["mu1"], a["r1"], LN_EPS, dx2,
-                              G(pre + "input_sublayer.norm.a_2"), G(pre + "input_sublayer.norm.b_2"), wln, 1,
-                              accumulate=True)
+            ln_bwd(a["x"], dh, pre + "input_sublayer.norm.a_2", pre + "input_sublayer.norm.b_2", a["mu1"], a["r1"],
+                   dx2, f"{i}i")
             dx = dx2
         if self._det_table():
             # token-table gradient by inverted index (rs_item_grad: sorted keys, per-row sums, no float
@@ -343,7 +354,7 @@ class BERTEngine:
             shapes = [(p[0].shape[1], p[1].shape[1]) for p in chunk]
             rows = self._wgrad_rows(M, sum(-(-n // 128) * -(-k // 128) for n, k in shapes))
             wslab = self.ws.get(f"wslab{c}", (ops.wgrad_grouped_slab_numel(shapes, M, rows),), torch.float32)
-            ops.wgrad_grouped(chunk, M, rows, wslab)
+            ops.wgrad_grouped(chunk, M, rows, wslab, extra=ln_segs if c == 0 else ())
 
     def _det_table(self):
         return self.dt == torch.bfloat16 and self.d in (64, 128, 256) and os.environ.get("RS_BERT_ATOMIC_TABLE") != "1"

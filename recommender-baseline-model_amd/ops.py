@@ -165,6 +165,13 @@ def layernorm_fwd(X, gamma, beta, eps, Y, mean, rinv, variant):
          ptr(Y), ld(Y), ptr(mean), ptr(rinv), stream())
 
 
+def layernorm_bwd_nparts(X):
+    """Partial count layernorm_bwd leaves in ws when called with dgamma = dbeta = None (0: not deferrable)."""
+    M, d = X.shape
+    ok = X.data_ptr() % 16 == 0 and ld(X) % (8 if X.dtype == torch.bfloat16 else 4) == 0
+    return int(_lib.lib().rs_layernorm_bwd_nparts(dtype_code(X), M, d)) if ok else 0
+
+
 def layernorm_bwd(X, dY, gamma, mean, rinv, eps, dX, dgamma, dbeta, ws, variant, accumulate=False):
     M, d = X.shape
     call("rs_layernorm_bwd", dtype_code(X), variant, ptr(X), ld(X), ptr(dY), ld(dY), M, d, ptr(gamma),

@@ -112,3 +112,27 @@ def test_sparse_token_exchange_equals_dense(tmp_path, graph):
     r1 = torch.load(tmp_path / "on_r1.pt", weights_only=True)
     for k in r0["sd"]:
         assert torch.equal(r0["sd"][k], r1["sd"][k]), k        # the replicas stay identical
+
+
+@pytest.mark.parametrize("n,cap,frac", [(1, 4, 1.0), (1000, 1000, 0.2), (12800, 12800, 0.2), (12800, 1000, 0.2),
+                                        (70001, 70001, 0.5), (5000, 6000, 0.0)])
+def test_compact_rows_matches_numpy(n, cap, frac):
+    """rs_compact_rows (one 1024-row block per workgroup, wave ballots): the ordered labelled-row list capped at
+    cap, the rank of every row (-1 unlabelled or past the cap), the capped count, -1 in the unused list slots."""
+    from rbm_amd import ops
+    rng = np.random.default_rng(n)
+    lab = np.where(rng.random(n) < frac, rng.integers(1, 100, n), 0).astype(np.int64)
+    labels = torch.from_numpy(lab).cuda()
+    idx = torch.full((cap,), 7, dtype=torch.int32, device="cuda")
+    rank = torch.full((n,), 7, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ops.compact_rows(labels, cap, idx, rank, cnt)
+    torch.cuda.synchronize()
+    rows = np.nonzero(lab)[0]
+    k = min(len(rows), cap)
+    want_rank = np.full(n, -1, dtype=np.int32)
+    want_rank[rows[:k]] = np.arange(k)
+    assert int(cnt.item()) == k
+    assert np.array_equal(idx.cpu().numpy()[:k], rows[:k])
+    assert (idx.cpu().numpy()[len(rows):] == -1).all()
+    assert np.array_equal(rank.cpu().numpy(), want_rank)
