@@ -29,7 +29,10 @@
 
 namespace ig {
 
-constexpr int CH = 64;          // sorted entries per gradient chunk
+#ifndef IG_CH
+#define IG_CH 32   // A/B against 64: cfg2 0.2962 vs 0.2991, cfg4 0.2258 vs 0.2322 ms/step (more, shorter chunk workgroups beside the weight-gradient tiles); 128 slower
+#endif
+constexpr int CH = IG_CH;       // sorted entries per gradient chunk
 constexpr int BE = 512;         // entries per counting-sort block (512: 150 blocks at cfg2, 1024 took 75)
 constexpr int VMAX_LDS = 32768;            // largest table for the LDS histogram
 constexpr int64_t HMAX = (int64_t)1 << 26;  // largest per-block histogram table (ints) for the counting sort
