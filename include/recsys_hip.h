@@ -131,6 +131,16 @@ int rs_layernorm_bwd(int dtype, int variant, const void* X, int64_t ldx, const v
  * terms, then beta terms) unreduced, for a later grouped reduction (rs_reduce_segments / rs_wgrad_grouped's extra
  * segments).  0 = the shape takes the other path (pass dgamma/dbeta). */
 int64_t rs_layernorm_bwd_nparts(int dtype, int64_t M, int64_t d);
+/* rs_layernorm_bwd followed by the dropout site(s) that consume dX, in one launch (vectorised path; other shapes
+ * run the two launches): out2 == NULL -- out1 = drop(dX; salt1) as rs_dropout_rowmask without a row mask;
+ * else out1 = drop(dX; salt1), out2 = drop(out1; salt2) as rs_dropout2.  dX as stored (accumulated) is the
+ * input; hash index row * d + column; out1/out2 dense [M][d].  (BERT: bert_modules/utils/sublayer.py:18 and
+ * transformer.py:32 backward.) */
+int rs_layernorm_bwd_drop(int dtype, int variant, const void* X, int64_t ldx, const void* dY, int64_t lddy,
+                          int64_t M, int64_t d, const float* gamma, const float* mean, const float* rinv, float eps,
+                          void* dX, int64_t lddx, int accumulate_dx, float* dgamma, float* dbeta, float* ws,
+                          float drop_p, uint64_t salt1, uint64_t salt2, const uint64_t* seed_base, void* out1,
+                          void* out2, void* stream);
 
 /* Fused scaled-dot-product attention per (sequence, head), T keys, head dim Dh.
  * q/k/v/o rows are tokens (b*T + t); head h occupies columns [h*Dh, (h+1)*Dh).

@@ -59,6 +59,8 @@ SIGNATURES = {
     "rs_embed_bwd": [i32, i32, vp, i64, i64, vp, i64, f32, f32, u64, vp, vp, vp, i32, vp],
     "rs_layernorm_fwd": [i32, i32, vp, i64, i64, i64, vp, vp, f32, vp, i64, vp, vp, vp],
     "rs_layernorm_bwd_nparts": [i32, i64, i64],
+    "rs_layernorm_bwd_drop": [i32, i32, vp, i64, vp, i64, i64, i64, vp, vp, vp, f32, vp, i64, i32, vp, vp, vp, f32,
+                              u64, u64, vp, vp, vp, vp],
     "rs_layernorm_bwd": [i32, i32, vp, i64, vp, i64, i64, i64, vp, vp, vp, f32, vp, i64, i32, vp, vp, vp, vp],
     "rs_attn_fwd": [i32, i64, i64, i64, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp, f32, i32, vp, f32, u64, vp, vp],
     "rs_attn_row_delta": [i32, i64, i64, i64, i64, vp, i64, vp, i64, vp, vp],

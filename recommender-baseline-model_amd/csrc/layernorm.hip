@@ -199,15 +199,32 @@ __global__ __launch_bounds__(256) void ln_fwd_v_kernel(const T* __restrict__ X, 
 // backward; the affine partials of each lane's columns are accumulated over all rows the lane
 // group visits (grid-stride), combined over the block's row groups in LDS (fixed order) and
 // written to part[block][2][d] for the deterministic slab reduce.
-template <typename T, int LPR, int NCH, int VAR, bool ACC>
+// DROP (BERT's backward): the dropout site(s) that consume dX, applied to dX as stored -- 1: out1 = drop(dX; s1)
+// (rs_dropout_rowmask without row mask), 2: out1 = drop(dX; s1), out2 = drop(out1; s2) (rs_dropout2) -- with the
+// same hash indices (row * d + column) and roundings as those kernels: one launch instead of two.
+struct LnDrop {
+  float p;
+  uint64_t salt1, salt2;
+  const uint64_t* seed_base;   // the device step word (graph replays advance it): seeds formed in the kernel
+  void* out1;
+  void* out2;
+};
+template <typename T, int LPR, int NCH, int VAR, bool ACC, int DROP = 0>
 __global__ __launch_bounds__(256) void ln_bwd_v_kernel(const T* __restrict__ X, int64_t ldx, const T* __restrict__ dY,
                                                        int64_t lddy, int64_t M, int d, const float* __restrict__ gamma,
                                                        const float* __restrict__ mean, const float* __restrict__ rinv,
                                                        float eps, T* __restrict__ dX, int64_t lddx,
-                                                       float* __restrict__ part) {
+                                                       float* __restrict__ part, LnDrop dr = LnDrop{}) {
   constexpr int V = Vec<T>::N, RPW = 64 / LPR, RPB = 4 * RPW;
   const int lane = threadIdx.x & 63, sub = lane % LPR;
   const int rgrp = (threadIdx.x >> 6) * RPW + lane / LPR;  // row group within the block
+  uint32_t ds1 = 0u, ds2 = 0u;
+  if constexpr (DROP > 0) {
+    if (dr.p > 0.f) {
+      ds1 = seed32(eff_seed(dr.salt1, dr.seed_base));
+      if constexpr (DROP == 2) ds2 = seed32(eff_seed(dr.salt2, dr.seed_base));
+    }
+  }
   float pg[NCH][V], pb[NCH][V], gm[NCH][V];
 #pragma unroll
   for (int i = 0; i < NCH; ++i)
@@ -277,6 +294,33 @@ __global__ __launch_bounds__(256) void ln_bwd_v_kernel(const T* __restrict__ X, 
             else o[j] = t;
           }
           store_chunk<T>(dX + row * lddx + c0, o);
+          if constexpr (DROP > 0) {
+            const uint64_t base = (uint64_t)(row * d + c0);
+#pragma unroll
+            for (int j = 0; j < V; ++j) o[j] = to_f(from_f<T>(o[j]));   // dX as stored
+            if (dr.p > 0.f) {
+#pragma unroll
+              for (int j = 0; j < V; j += 2) {
+                float m0, m1;
+                drop_mul2(dr.p, ds1, base + j, m0, m1);
+                o[j] = to_f(from_f<T>(o[j] * m0));
+                o[j + 1] = to_f(from_f<T>(o[j + 1] * m1));
+              }
+            }
+            store_chunk<T>(reinterpret_cast<T*>(dr.out1) + row * d + c0, o);
+            if constexpr (DROP == 2) {
+              if (dr.p > 0.f) {
+#pragma unroll
+                for (int j = 0; j < V; j += 2) {
+                  float m0, m1;
+                  drop_mul2(dr.p, ds2, base + j, m0, m1);
+                  o[j] *= m0;
+                  o[j + 1] *= m1;
+                }
+              }
+              store_chunk<T>(reinterpret_cast<T*>(dr.out2) + row * d + c0, o);
+            }
+          }
         }
       }
     }
@@ -341,7 +385,8 @@ static hipError_t ln_fwd_t(const void* X, int64_t ldx, int64_t M, int d, const f
 template <typename T>
 static hipError_t ln_bwd_t(const void* X, int64_t ldx, const void* dY, int64_t lddy, int64_t M, int d,
                            const float* gamma, const float* mean, const float* rinv, float eps, int variant,
-                           void* dX, int64_t lddx, int acc, float* dgamma, float* dbeta, float* ws, hipStream_t s) {
+                           void* dX, int64_t lddx, int acc, float* dgamma, float* dbeta, float* ws, hipStream_t s,
+                           int drop = 0, LnDrop dr = LnDrop{}) {
   const T* x = (const T*)X;
   const T* dy = (const T*)dY;
   T* dx = (T*)dX;
@@ -358,9 +403,15 @@ static hipError_t ln_bwd_t(const void* X, int64_t ldx, const void* dY, int64_t l
     if (lpr) {
       const int64_t rpb = 4 * (64 / lpr);
       const int nb = (int)std::min<int64_t>(LN_BWD_BLOCKS / 2, cdiv(M, rpb * 4));
-#define LNBV1(LPR, NCH, VAR, ACC)                                                                          \
-  hipLaunchKernelGGL((ln_bwd_v_kernel<T, LPR, NCH, VAR, ACC>), dim3(nb), dim3(256), 0, s, x, ldx, dy, lddy, M, d, \
-                     gamma, mean, rinv, eps, dx, lddx, ws)
+#define LNBV1D(LPR, NCH, VAR, ACC, DR)                                                                      \
+  hipLaunchKernelGGL((ln_bwd_v_kernel<T, LPR, NCH, VAR, ACC, DR>), dim3(nb), dim3(256), 0, s, x, ldx, dy, lddy, M, \
+                     d, gamma, mean, rinv, eps, dx, lddx, ws, dr)
+#define LNBV1(LPR, NCH, VAR, ACC)                     \
+  do {                                                \
+    if (drop == 0) LNBV1D(LPR, NCH, VAR, ACC, 0);     \
+    else if (drop == 1) LNBV1D(LPR, NCH, VAR, ACC, 1); \
+    else LNBV1D(LPR, NCH, VAR, ACC, 2);               \
+  } while (0)
 #define LNBV(LPR, NCH)                                                \
   do {                                                                \
     if (variant == 0) {                                               \
@@ -377,11 +428,13 @@ static hipError_t ln_bwd_t(const void* X, int64_t ldx, const void* dY, int64_t l
       else LNBV(64, 2);
 #undef LNBV
 #undef LNBV1
+#undef LNBV1D
       hipError_t e = hipGetLastError();
       if (e != hipSuccess || !(dgamma || dbeta)) return e;
       return launch_reduce_slabs(ws, nb, 2 * (int64_t)d, d, dgamma, dbeta, 1, s);
     }
   }
+  if (drop) return hipErrorInvalidValue;   // the dropout epilogue is the vectorised path's (callers fall back)
   const int nblk = (int)std::min<int64_t>(LN_BWD_BLOCKS, cdiv(M, 4));
   dim3 grid(nblk), block(256);
 #define LNB(NV) hipLaunchKernelGGL((ln_bwd_kernel<T, NV>), grid, block, 0, s, x, ldx, dy, lddy, M, d, gamma, mean, rinv, eps, variant, dx, lddx, acc, ws)
@@ -416,6 +469,34 @@ int64_t rs_layernorm_bwd_nparts(int dtype, int64_t M, int64_t d) {
   if (!lpr) return 0;
   const int64_t rpb = 4 * (64 / lpr);
   return std::min<int64_t>(LN_BWD_BLOCKS / 2, cdiv(M, rpb * 4));
+}
+
+int rs_layernorm_bwd_drop(int dtype, int variant, const void* X, int64_t ldx, const void* dY, int64_t lddy,
+                          int64_t M, int64_t d, const float* gamma, const float* mean, const float* rinv, float eps,
+                          void* dX, int64_t lddx, int accumulate_dx, float* dgamma, float* dbeta, float* ws,
+                          float drop_p, uint64_t salt1, uint64_t salt2, const uint64_t* seed_base, void* out1,
+                          void* out2, void* stream) {
+  if (M <= 0 || d <= 1 || d > 64 * LN_MAXV || !out1) return RS_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int drop = out2 ? 2 : 1;
+  const int V = dtype == RS_DTYPE_BF16 ? 8 : 4;
+  const bool al = ((uintptr_t)out1 | (uintptr_t)(out2 ? out2 : out1)) % 16 == 0 && d % V == 0;
+  if (al) {
+    const LnDrop dr{drop_p, salt1, salt2, seed_base, out1, out2};
+    const hipError_t e =
+        dtype == RS_DTYPE_BF16
+            ? ln_bwd_t<__bf16>(X, ldx, dY, lddy, M, (int)d, gamma, mean, rinv, eps, variant, dX, lddx, accumulate_dx,
+                               dgamma, dbeta, ws, s, drop, dr)
+            : ln_bwd_t<float>(X, ldx, dY, lddy, M, (int)d, gamma, mean, rinv, eps, variant, dX, lddx, accumulate_dx,
+                              dgamma, dbeta, ws, s, drop, dr);
+    if (e != hipErrorInvalidValue) return (int)e;
+  }
+  // not the vectorised path: the two launches (same results)
+  if (int r = rs_layernorm_bwd(dtype, variant, X, ldx, dY, lddy, M, d, gamma, mean, rinv, eps, dX, lddx,
+                               accumulate_dx, dgamma, dbeta, ws, stream))
+    return r;
+  return out2 ? rs_dropout2(dtype, dX, M, d, lddx, drop_p, salt1, salt2, seed_base, d, out1, out2, stream)
+              : rs_dropout_rowmask(dtype, dX, M, d, lddx, drop_p, salt1, seed_base, d, nullptr, out1, nullptr, stream);
 }
 
 int rs_layernorm_bwd(int dtype, int variant, const void* X, int64_t ldx, const void* dY, int64_t lddy,

@@ -262,17 +262,21 @@ class BERTEngine:
         probs = []
         ln_segs = []
 
-        def ln_bwd(X, dY, gname, bname, mean, rstd, dX, tag):
+        def ln_bwd(X, dY, gname, bname, mean, rstd, dX, tag, drop=None):
             """LayerNorm backward; grouped: its affine partials are summed by the grouped launch's reduction (no
-            reduction launch per LayerNorm on the backward's critical path)"""
+            reduction launch per LayerNorm on the backward's critical path).  drop = (salt1, salt2 | None, out1,
+            out2 | None): the dropout site(s) consuming dX, in the same launch (rs_layernorm_bwd_drop)."""
             nparts = ops.layernorm_bwd_nparts(X) if grouped else 0
-            if nparts:
-                part = self.ws.get(f"lnpart_{tag}", (2 * d * nparts,), torch.float32)
-                ops.layernorm_bwd(X, dY, self.Wf(gname), mean, rstd, LN_EPS, dX, None, None, part, 1, accumulate=True)
-                ln_segs.extend(ops.ln_partial_segments(part, M, d, G(gname), G(bname), nb=nparts))
+            part = self.ws.get(f"lnpart_{tag}", (2 * d * nparts,), torch.float32) if nparts else wln
+            dg, db = (None, None) if nparts else (G(gname), G(bname))
+            if drop is not None:
+                s1, s2, o1, o2 = drop
+                ops.layernorm_bwd_drop(X, dY, self.Wf(gname), mean, rstd, LN_EPS, dX, dg, db, part, 1, hp, s1,
+                                       s2 if s2 is not None else 0, sb, o1, o2, accumulate=True)
             else:
-                ops.layernorm_bwd(X, dY, self.Wf(gname), mean, rstd, LN_EPS, dX, G(gname), G(bname), wln, 1,
-                                  accumulate=True)
+                ops.layernorm_bwd(X, dY, self.Wf(gname), mean, rstd, LN_EPS, dX, dg, db, part, 1, accumulate=True)
+            if nparts:
+                ln_segs.extend(ops.ln_partial_segments(part, M, d, G(gname), G(bname), nb=nparts))
 
         def wgrad(dY, X, dW, db):
             if grouped:
@@ -280,13 +284,17 @@ class BERTEngine:
             else:
                 ops.linear_wgrad(dY, X, dW, slab, db=db)
 
+        pending = None
         for i in reversed(range(L)):
             a = s["blocks"][i]
             pre = f"bert.transformer_blocks.{i}."
             # x_out = drop_blk(x1 + drop_res2(g W2^T + b2))
             # (the deferred weight gradients need dy / dyo to outlive the in-place LayerNorm-backward
             # accumulations into dx2: separate buffers even without dropout)
-            if hp > 0 or grouped:
+            if pending is not None:
+                dx2, dy = pending        # formed by the block above's input LayerNorm backward
+                pending = None
+            elif hp > 0 or grouped:
                 dx2, dy = e((M, d)), e((M, d))
                 ops.dropout2(dx, hp, self.salt[f"blk{i}"], self.salt[f"res2{i}"], sb, dx2, dy)
             else:
@@ -298,14 +306,19 @@ class BERTEngine:
             wgrad(da, a["h2"], G(pre + "feed_forward.w_1.weight"), G(pre + "feed_forward.w_1.bias"))
             dh2 = e((M, d))
             ops.linear_dgrad(da, self.W(pre + "feed_forward.w_1.weight"), dh2)
-            ln_bwd(a["x1"], dh2, pre + "output_sublayer.norm.a_2", pre + "output_sublayer.norm.b_2", a["mu2"], a["r2"],
-                   dx2, f"{i}o")
-            # x1 = x + drop_res1(o Wo^T + bo)
-            if hp > 0 or grouped:
+            # x1 = x + drop_res1(o Wo^T + bo): dyo = drop_res1(dx2) formed by the LayerNorm backward's launch
+            if grouped:
                 dyo = e((M, d))
-                ops.dropout_rowmask(dx2, hp, self.salt[f"res1{i}"], sb, None, dyo)
+                ln_bwd(a["x1"], dh2, pre + "output_sublayer.norm.a_2", pre + "output_sublayer.norm.b_2", a["mu2"],
+                       a["r2"], dx2, f"{i}o", drop=(self.salt[f"res1{i}"], None, dyo, None))
             else:
-                dyo = dx2
+                ln_bwd(a["x1"], dh2, pre + "output_sublayer.norm.a_2", pre + "output_sublayer.norm.b_2", a["mu2"],
+                       a["r2"], dx2, f"{i}o")
+                if hp > 0:
+                    dyo = e((M, d))
+                    ops.dropout_rowmask(dx2, hp, self.salt[f"res1{i}"], sb, None, dyo)
+                else:
+                    dyo = dx2
             wgrad(dyo, a["o"], G(pre + "attention.output_linear.weight"), G(pre + "attention.output_linear.bias"))
             do = e((M, d))
             ops.linear_dgrad(dyo, self.W(pre + "attention.output_linear.weight"), do)
@@ -327,8 +340,15 @@ class BERTEngine:
                                      db=G(self._qkv(i, j, "bias")))
                     ops.linear_dgrad(dqkv[:, j * d:(j + 1) * d], self.W(self._qkv(i, j, "weight")), dh,
                                      accumulate=j > 0)
-            ln_bwd(a["x"], dh, pre + "input_sublayer.norm.a_2", pre + "input_sublayer.norm.b_2", a["mu1"], a["r1"],
-                   dx2, f"{i}i")
+            if grouped and i > 0:
+                # the block below starts with dropout2 of this dX (its blk and res2 sites): same launch
+                pending = (e((M, d)), e((M, d)))
+                ln_bwd(a["x"], dh, pre + "input_sublayer.norm.a_2", pre + "input_sublayer.norm.b_2", a["mu1"],
+                       a["r1"], dx2, f"{i}i",
+                       drop=(self.salt[f"blk{i - 1}"], self.salt[f"res2{i - 1}"], pending[0], pending[1]))
+            else:
+                ln_bwd(a["x"], dh, pre + "input_sublayer.norm.a_2", pre + "input_sublayer.norm.b_2", a["mu1"],
+                       a["r1"], dx2, f"{i}i")
             dx = dx2
         if self._det_table():
             # token-table gradient by inverted index (rs_item_grad: sorted keys, per-row sums, no float

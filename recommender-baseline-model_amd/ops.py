@@ -172,6 +172,16 @@ def layernorm_bwd_nparts(X):
     return int(_lib.lib().rs_layernorm_bwd_nparts(dtype_code(X), M, d)) if ok else 0
 
 
+def layernorm_bwd_drop(X, dY, gamma, mean, rinv, eps, dX, dgamma, dbeta, ws, variant, drop_p, salt1, salt2, seed_base,
+                       out1, out2=None, accumulate=False):
+    """layernorm_bwd, then out1 = drop(dX; salt1) (and out2 = drop(out1; salt2)) in the same launch."""
+    M, d = X.shape
+    assert out1.shape == (M, d) and out1.is_contiguous() and (out2 is None or out2.is_contiguous())
+    call("rs_layernorm_bwd_drop", dtype_code(X), variant, ptr(X), ld(X), ptr(dY), ld(dY), M, d, ptr(gamma),
+         ptr(mean), ptr(rinv), eps, ptr(dX), ld(dX), int(accumulate), ptr(dgamma), ptr(dbeta), ptr(ws), drop_p, salt1,
+         salt2, ptr(seed_base), ptr(out1), ptr(out2), stream())
+
+
 def layernorm_bwd(X, dY, gamma, mean, rinv, eps, dX, dgamma, dbeta, ws, variant, accumulate=False):
     M, d = X.shape
     call("rs_layernorm_bwd", dtype_code(X), variant, ptr(X), ld(X), ptr(dY), ld(dY), M, d, ptr(gamma),
