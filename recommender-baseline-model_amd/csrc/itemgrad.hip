@@ -130,6 +130,11 @@ __global__ __launch_bounds__(256) void hist_kernel(Keys K, int* __restrict__ H) 
 __global__ __launch_bounds__(256) void hist_global_kernel(Keys K, int* __restrict__ H) {
   const int64_t e0 = (int64_t)blockIdx.x * BE;
   int* h = H + (int64_t)blockIdx.x * K.V;
+  // the block zeroes its own histogram row first (no memset node in the step graph: at cfg4 the runtime's fill
+  // kernels of that node ran ~50 us late and held the whole index branch back into the backward)
+  for (int64_t v = threadIdx.x; v < K.V; v += 256) h[v] = 0;
+  __threadfence_block();
+  __syncthreads();
 #pragma unroll
   for (int i = 0; i < BE / 256; ++i) {
     const int64_t e = e0 + threadIdx.x + i * 256;
@@ -544,7 +549,6 @@ int rs_item_index_build(int nsrc, const int64_t* keys0, const int64_t* keys1, co
       if (!attr) return RS_ERR_UNSUPPORTED;
       hipLaunchKernelGGL(ig::hist_kernel, dim3((unsigned)L.nb), dim3(256), (size_t)L.V * sizeof(int), s, K, H);
     } else {
-      if ((e = hipMemsetAsync(H, 0, (size_t)L.nb * table_rows * 4, s)) != hipSuccess) return (int)e;
       hipLaunchKernelGGL(ig::hist_global_kernel, dim3((unsigned)L.nb), dim3(256), 0, s, K, H);
     }
     int* gsum = (int*)(w + L.temp);
