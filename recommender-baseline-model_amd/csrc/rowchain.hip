@@ -40,7 +40,7 @@ __device__ unsigned long long g_rc_prof[4096 * 8 * 16];
 #endif
 
 #ifndef RC_HEAD_PREFETCH
-#define RC_HEAD_PREFETCH 1   // where the head's item-row loads are issued: 0 tile start, 1 mid-chain (A/B: 0.2999 vs 0.3020 ms at cfg2), 2 after it
+#define RC_HEAD_PREFETCH 1   // head item-row loads: 0 tile start, 1 mid-chain (A/B 0.2999 vs 0.3020 ms at cfg2), 2 after the chain, 3 ids at the start + rows mid-chain (18 VGPRs spilled: 0.2975 vs 0.2953)
 #endif
 
 #ifndef RC_NOSTORE
@@ -575,9 +575,12 @@ __global__ __launch_bounds__(NT) void block_in_kernel(InArgs a) {
       load_raw<D>(xr, a.x, a.ldx, T.mc, g);
       return;
     }
+    // the count's id load goes out with the gathers and is consumed before the x0 store: vmcnt retires in order
+    // and counts stores too on gfx950, so a load consumed after a store waits for that store
+    const int64_t cid = a.e.cnt_ids && T.ok && g == 0 ? a.e.cnt_ids[T.mc] : 0;
     embed_tile<D>(xr, a.e, T, es32, g);
+    if (a.e.cnt_ids) cnt += __popcll(__ballot(cid != 0));
     store_raw<D>(a.e.xout, D, T.m, T.ok, xr, g);
-    if (a.e.cnt_ids) cnt += __popcll(__ballot(T.ok && g == 0 && a.e.cnt_ids[T.mc] != 0));
   };
   Raw<D> xr;
   if (t < nt) load_x(xr, tile_of(t, a.M, cl));
@@ -632,6 +635,12 @@ __device__ __forceinline__ int64_t head_rows(const HeadArgs& h, const Tile& T, R
   load_raw<D>(er, h.E, D, ip, g);
   load_raw<D>(nr, h.E, D, in, g);
   return ip;
+}
+template <int D>
+__device__ __forceinline__ void head_rows_at(const HeadArgs& h, int64_t ip, int64_t in, Raw<D>& er, Raw<D>& nr,
+                                             int g) {
+  load_raw<D>(er, h.E, D, ip, g);
+  load_raw<D>(nr, h.E, D, in, g);
 }
 template <int D>
 __device__ __forceinline__ void head_tile(const Raw<D>& xr, const Raw<D>& er, const Raw<D>& nr, int64_t ip,
@@ -747,11 +756,18 @@ __global__ __launch_bounds__(NT) void block_out_kernel(OutArgs a) {
       load_raw<D>(Qr, a.Q, D, T.mc, g);
     }
     Raw<D> zr, hr, xr, er, nr;
-    int64_t ip = 0;
+    int64_t ip = 0, in = 0;
     if (head && RC_HEAD_PREFETCH == 0) ip = head_rows<D>(a.h, T, er, nr, g);
+    // 3: the tile's item ids at its start (before any store: vmcnt retires in order and counts stores, so an
+    // index load issued after the chain's stores would wait for them), the item rows mid-chain
+    if (head && RC_HEAD_PREFETCH == 3) {
+      ip = a.h.pos[T.mc];
+      in = a.h.neg[T.mc];
+    }
     fwd_out_a<D>(orr, Qr, T, wslot(smem, 0, WB), wslot(smem, 1, WB), lv, of, zr, hr, lane);
     RCPROF(2);
     if (head && RC_HEAD_PREFETCH == 1) ip = head_rows<D>(a.h, T, er, nr, g);
+    if (head && RC_HEAD_PREFETCH == 3) head_rows_at<D>(a.h, ip, in, er, nr, g);
     fwd_out_b<D>(hr, zr, T, wslot(smem, 2, WB), lv, of, xr, lane);
     RCPROF(4);
     if (head && RC_HEAD_PREFETCH == 2) ip = head_rows<D>(a.h, T, er, nr, g);
