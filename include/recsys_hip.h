@@ -482,12 +482,13 @@ int rs_wgrad_grouped_pos(int nprob, const rs_wgrad_problem* probs, int64_t M, in
                          int64_t T, const void* dx, int64_t d, float drop_p, uint64_t salt,
                          const uint64_t* seed_base, float* dpos, void* stream);
 /* rs_wgrad_grouped_pos whose reduction launch also carries rs_sas_head_finish (one more workgroup): the SAS
- * head's loss statistics loss_out[0..3] from the head's partials (head_part[head_blocks][3]). */
+ * head's loss statistics loss_out[0..3] from the head's partials (head_part[head_blocks][3]); aux_out (optional,
+ * data parallel): (loss sum, count) written there too -- the all-reduced tail of the gradient buffer. */
 int rs_wgrad_grouped_pos_stats(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_t rows_per_split,
                                float* slab, int64_t slab_numel, int nextra, const rs_reduce_segment* extra,
                                const int64_t* ids, int64_t T, const void* dx, int64_t d, float drop_p, uint64_t salt,
                                const uint64_t* seed_base, float* dpos, const float* head_part, int64_t head_blocks,
-                               const float* head_divisor, float* loss_out, void* stream);
+                               const float* head_divisor, float* loss_out, float* aux_out, void* stream);
 /* The reduction alone: out (+)= sum over splits, for nseg segments (any number, 64 per launch). */
 int rs_reduce_segments(int nseg, const rs_reduce_segment* segs, int accumulate, void* stream);
 

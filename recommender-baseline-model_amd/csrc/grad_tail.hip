@@ -49,6 +49,7 @@ struct HeadStats {
   const float* part;
   const float* divisor;
   float* out;
+  float* aux;   // optional second copy of (loss sum, count)
 };
 __global__ __launch_bounds__(256) void reduce_pos_kernel(wg::RArgs r, int rblk, int cols, const int64_t* ids,
                                                          int64_t rows, int64_t T_, const __bf16* dx, int64_t d,
@@ -59,7 +60,7 @@ __global__ __launch_bounds__(256) void reduce_pos_kernel(wg::RArgs r, int rblk, 
   const int h = hs.out ? 1 : 0;
   if (h && blockIdx.x == 0) {
     static_assert(sizeof(red) >= 3 * 256 * sizeof(float), "head_stats scratch");
-    hd::head_stats(hs.nblk, hs.part, hs.divisor, hs.out, reinterpret_cast<float(*)[256]>(&red[0][0]));
+    hd::head_stats(hs.nblk, hs.part, hs.divisor, hs.out, reinterpret_cast<float(*)[256]>(&red[0][0]), hs.aux);
     return;
   }
   // the positions' workgroups (long: a 128-row column sum each) are dispatched first, the many short
@@ -132,14 +133,14 @@ int rs_wgrad_grouped_pos(int nprob, const rs_wgrad_problem* probs, int64_t M, in
                          int64_t T_, const void* dx, int64_t d, float drop_p, uint64_t salt,
                          const uint64_t* seed_base, float* dpos, void* stream) {
   return rs_wgrad_grouped_pos_stats(nprob, probs, M, rows_per_split, slab, slab_numel, nextra, extra, ids, T_, dx, d,
-                                    drop_p, salt, seed_base, dpos, nullptr, 0, nullptr, nullptr, stream);
+                                    drop_p, salt, seed_base, dpos, nullptr, 0, nullptr, nullptr, nullptr, stream);
 }
 
 int rs_wgrad_grouped_pos_stats(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_t rows_per_split,
                                float* slab, int64_t slab_numel, int nextra, const rs_reduce_segment* extra,
                                const int64_t* ids, int64_t T_, const void* dx, int64_t d, float drop_p, uint64_t salt,
                                const uint64_t* seed_base, float* dpos, const float* head_part, int64_t head_blocks,
-                               const float* head_divisor, float* loss_out, void* stream) {
+                               const float* head_divisor, float* loss_out, float* aux_out, void* stream) {
   if (!ids || !dx || !dpos || T_ <= 0 || M % T_ || !head_part != !loss_out || (loss_out && head_blocks <= 0))
     return RS_ERR_ARG;
   wg::Args a;
@@ -153,7 +154,11 @@ int rs_wgrad_grouped_pos_stats(int nprob, const rs_wgrad_problem* probs, int64_t
     if (int e = rs_embed_bwd(RS_DTYPE_BF16, 0, ids, M, T_, dx, d, 1.f, drop_p, salt, seed_base, nullptr, dpos, 1,
                              stream))
       return e;
-    return loss_out ? rs_sas_head_finish(head_blocks, head_part, head_divisor, loss_out, stream) : 0;
+    if (!loss_out) return 0;
+    if (int e = rs_sas_head_finish(head_blocks, head_part, head_divisor, loss_out, stream)) return e;
+    return aux_out ? (int)hipMemcpyAsync(aux_out, loss_out, 2 * sizeof(float), hipMemcpyDeviceToDevice,
+                                         (hipStream_t)stream)
+                   : 0;
   }
   wg::RArgs r;
   int rblk;
@@ -167,7 +172,7 @@ int rs_wgrad_grouped_pos_stats(int nprob, const rs_wgrad_problem* probs, int64_t
   else hipLaunchKernelGGL(wg::wgrad_group_kernel<64>, grid, dim3(256), 0, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  const gt::HeadStats hs{(int)head_blocks, head_part, head_divisor, loss_out};
+  const gt::HeadStats hs{(int)head_blocks, head_part, head_divisor, loss_out, aux_out};
   hipLaunchKernelGGL(gt::reduce_pos_kernel, dim3((unsigned)(rblk + T_ + (loss_out ? 1 : 0))), dim3(256), 0, s, r, rblk,
                      (int)cols, ids, M, T_, (const __bf16*)dx, d, drop_p, salt, seed_base, dpos, hs);
   return (int)hipGetLastError();

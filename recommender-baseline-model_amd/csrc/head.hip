@@ -239,7 +239,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(int64_t M, int nblk, cons
 // the loss statistics of the head's block partials (as head_bwd_kernel's workgroup 0 forms them), by one workgroup:
 // out = [sum of the BCE terms, valid count, loss = mean pos term + mean neg term, neg sum]
 __device__ void head_stats(int nblk, const float* __restrict__ part, const float* __restrict__ divisor,
-                           float* __restrict__ out, float (*red)[256]) {
+                           float* __restrict__ out, float (*red)[256], float* __restrict__ aux = nullptr) {
   const int tid = threadIdx.x;
   float c = 0.f, a = 0.f, b = 0.f;
   for (int i = tid; i < nblk; i += 256) {
@@ -265,6 +265,10 @@ __device__ void head_stats(int nblk, const float* __restrict__ part, const float
     out[1] = red[2][0];
     out[2] = red[0][0] / cc + red[1][0] / cc;
     out[3] = red[1][0];
+    if (aux) {   // data parallel: (loss sum, count) straight into the gradient buffer's all-reduced tail
+      aux[0] = out[0];
+      aux[1] = out[1];
+    }
   }
 }
 

@@ -369,10 +369,11 @@ class SASEngine:
         return ops.sas_block_fused_ok(self.d, self.dt)
 
     # ---- backward ------------------------------------------------------------------
-    def backward(self, s, dpl, dnl, grad, loss_out=None, divisor=None, split=None):
+    def backward(self, s, dpl, dnl, grad, loss_out=None, divisor=None, split=None, aux_out=None):
         """Accumulates every parameter gradient into the flat fp32 buffer ``grad``.  dpl/dnl: the
         logits' gradients; None (fused path only) = form the BCE gradient of the forward's logits here,
-        writing the loss statistics to loss_out (divisor: device count, None = this batch's)."""
+        writing the loss statistics to loss_out (divisor: device count, None = this batch's).  aux_out (data
+        parallel, fused head): (loss sum, count) also written there by the same launch; returns True if it was."""
         B, T, p, ids = s["B"], s["T"], s["p"], s["ids"]
         M, d, H, Dh, L = B * T, self.d, self.H, self.Dh, self.L
         sb = s["sb"]
@@ -399,7 +400,7 @@ class SASEngine:
                 dx, dpl, dnl, lnh = s["hdx"], s["dpl"], s["dnl"], s["lnh"]
                 nb = s["headp"].numel() // 3
                 if loss_out is not None:
-                    stats = (s["headp"], divisor, loss_out)
+                    stats = (s["headp"], divisor, loss_out) + ((aux_out,) if aux_out is not None else ())
             elif dpl is None and "cntp" in s:
                 # the head's forward and backward in one kernel; the loss statistics (one workgroup) ride in the
                 # gradient tail's reduction launch
@@ -407,7 +408,7 @@ class SASEngine:
                 ops.sas_head_fused(s["xL"], gl, self.Wf("last_layernorm.bias"), LN_EPS, s["cntp"], divisor, s["f"], E,
                                    s["pos"], s["neg"], s["pl"], s["nl"], dpl, dnl, dx, lnh, s["headp"])
                 if loss_out is not None:
-                    stats = (s["headp"], divisor, loss_out)
+                    stats = (s["headp"], divisor, loss_out) + ((aux_out,) if aux_out is not None else ())
             elif dpl is None:
                 dpl, dnl = e("dpl", (B, T), torch.float32), e("dnl", (B, T), torch.float32)
                 ops.sas_head_bwd(s["headp"], divisor, loss_out, s["pl"], s["nl"], None, None, dpl, dnl, s["pos"],
@@ -444,14 +445,16 @@ class SASEngine:
             if not pos_merged:
                 ops.embed_bwd(0, ids, T, dx, math.sqrt(d), p, self.salt["emb"], sb, None, G("pos_emb.weight"))
                 if stats:
-                    ops.sas_head_finish(*stats)
+                    ops.sas_head_finish(*stats[:3])
+                    if len(stats) > 3:
+                        stats[3].copy_(stats[2][0:2])
             if side:
                 torch.cuda.current_stream().wait_event(self._tail_join)
             elif tail_mode != "fused":
                 item_grads(dx)
             if split is not None:
                 split("dense")          # every parameter gradient is final (data-parallel overlap)
-            return
+            return len(stats) > 3
         df = e("df", (M, d))
         ops.sampled_logits_bwd(s["f"], self.W("item_emb.weight"), s["pos"], s["neg"], dpl, dnl, df,
                                G("item_emb.weight"))

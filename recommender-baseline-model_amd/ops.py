@@ -567,10 +567,10 @@ def wgrad_grouped(problems, M, rows_per_split, slab, extra=(), items=None, pos=N
         assert items is None
         ids, T, dx, drop_p, salt, seed_base, dpos, *st = pos
         if st:
-            hp, hdiv, lout = st
+            hp, hdiv, lout, *aux = st
             call("rs_wgrad_grouped_pos_stats", len(problems), arr, M, rows_per_split, ptr(slab), slab.numel(),
                  len(extra), segs, ptr(ids), T, ptr(dx), dx.shape[-1], drop_p, salt, ptr(seed_base), ptr(dpos),
-                 ptr(hp), hp.numel() // 3, ptr(hdiv), ptr(lout), stream())
+                 ptr(hp), hp.numel() // 3, ptr(hdiv), ptr(lout), ptr(aux[0] if aux else None), stream())
             return
         call("rs_wgrad_grouped_pos", len(problems), arr, M, rows_per_split, ptr(slab), slab.numel(), len(extra),
              segs, ptr(ids), T, ptr(dx), dx.shape[-1], drop_p, salt, ptr(seed_base), ptr(dpos), stream())

@@ -212,9 +212,12 @@ class FusedTrainStep:
                                         head_divisor=self.one if self.dp else None)
             if eng.fused_head:
                 # BCE forward/backward inside the fused head kernels (head.hip)
-                eng.backward(saved, None, None, self.flat.grad, loss_out=self.loss_out,
-                             divisor=self.one if self.dp else None,
-                             split=sp if self.exchange is not None and "dense" in self.exchange.buckets else None)
+                # DP: the loss sum and count go to the buffer's tail in the tail's reduction launch (no copy node)
+                if eng.backward(saved, None, None, self.flat.grad, loss_out=self.loss_out,
+                                divisor=self.one if self.dp else None,
+                                split=sp if self.exchange is not None and "dense" in self.exchange.buckets else None,
+                                aux_out=self.flat.aux[dpx.LOSS_SUM:dpx.COUNT + 1] if self.dp else None):
+                    aux_written[0] = True
                 write_aux()
                 return
             ws = eng.ws.get("bce", (3 * 256,), torch.float32)
