@@ -242,6 +242,12 @@ int rs_adam_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16
 int rs_adam_prepare_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, double* state,
                          const float* hyper, int zero_grad, const float* grad_divisor, uint64_t* seed_base,
                          const int64_t* tdesc, int ntd, int64_t tbase, void* wT, void* stream);
+/* rs_adam_prepare_step that also writes *loss_out = *loss_sum / *grad_divisor (data parallel: the step's mean
+ * loss from the all-reduced gradient tail) in the same launch. */
+int rs_adam_prepare_step_loss(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, double* state,
+                              const float* hyper, int zero_grad, const float* grad_divisor, uint64_t* seed_base,
+                              const int64_t* tdesc, int ntd, int64_t tbase, void* wT, const float* loss_sum,
+                              float* loss_out, void* stream);
 
 /* SASRec's parameter-norm regulariser, BS/trainers/sas.py:51-52 (loss += l2_emb * torch.norm(p) for every
  * parameter p): *loss += l2 * sum_seg ||p_seg||_2 and g += scale * l2 * p / ||p_seg|| (0 where the norm is 0,

@@ -78,6 +78,7 @@ SIGNATURES = {
     "rs_adam_prepare": [vp, vp, vp, vp, vp],
     "rs_adam_step": [i64, vp, vp, vp, vp, vp, vp, vp, i32, vp],
     "rs_adam_prepare_step": [i64, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, i32, i64, vp, vp],
+    "rs_adam_prepare_step_loss": [i64, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, i32, i64, vp, vp, vp, vp],
     "rs_cast_bf16": [i64, vp, vp, vp],
     "rs_l2_penalty": [vp, vp, vp, i64, f32, vp, vp, vp, vp],
     "rs_dropout_rowmask": [i32, vp, i64, i64, i64, f32, u64, vp, i64, vp, vp, vp, vp],

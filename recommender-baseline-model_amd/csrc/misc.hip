@@ -89,8 +89,12 @@ __global__ __launch_bounds__(256) void adam_step_kernel(int64_t n, float* __rest
                                                         const float* __restrict__ hyper, int zero_grad,
                                                         const float* __restrict__ divisor, uint64_t* seed_base,
                                                         const int64_t* __restrict__ tdesc, int ntd, int64_t tbase,
-                                                        __bf16* __restrict__ wT) {
+                                                        __bf16* __restrict__ wT, const float* __restrict__ lsum,
+                                                        float* __restrict__ lout) {
   const float b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
+  // data parallel: the step's reported loss = all-reduced loss sum / all-reduced count (the division torch.div did
+  // in its own launch), by one thread: both inputs are final before this launch
+  if (PREP && lout && blockIdx.x == 0 && threadIdx.x == 0) *lout = lsum[0] / divisor[0];
   float step_size, bc2s, gs;
   double t = 0.0;
   AdamScalars c;
@@ -347,29 +351,38 @@ int rs_adam_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16
   if (p_bf16)
     ADAM_LAUNCH(true, false, dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
                        (__bf16*)p_bf16, st, hyper, zero_grad, nullptr, nullptr, nullptr, 0, 0,
-                       nullptr);
+                       nullptr, nullptr, nullptr);
   else
     ADAM_LAUNCH(false, false, dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
                        (__bf16*)nullptr, st, hyper, zero_grad, nullptr, nullptr, nullptr, 0, 0,
-                       nullptr);
+                       nullptr, nullptr, nullptr);
   return (int)hipGetLastError();
 }
 
 int rs_adam_prepare_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, double* state,
                          const float* hyper, int zero_grad, const float* grad_divisor, uint64_t* seed_base,
                          const int64_t* tdesc, int ntd, int64_t tbase, void* wT, void* stream) {
+  return rs_adam_prepare_step_loss(n, p, g, m, v, p_bf16, state, hyper, zero_grad, grad_divisor, seed_base, tdesc, ntd,
+                                   tbase, wT, nullptr, nullptr, stream);
+}
+
+int rs_adam_prepare_step_loss(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, double* state,
+                              const float* hyper, int zero_grad, const float* grad_divisor, uint64_t* seed_base,
+                              const int64_t* tdesc, int ntd, int64_t tbase, void* wT, const float* loss_sum,
+                              float* loss_out, void* stream) {
   if (n <= 0 || !state || ((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16) return RS_ERR_ARG;
+  if (!loss_out != !loss_sum || (loss_out && !grad_divisor)) return RS_ERR_ARG;
   if (ntd < 0 || (ntd > 0 && (!tdesc || !wT || !p_bf16))) return RS_ERR_ARG;
   const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(cdiv(n / 4, 256), 8192));
   hipStream_t s = (hipStream_t)stream;
   if (p_bf16)
     ADAM_LAUNCH(true, true, dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
                        (__bf16*)p_bf16, state, hyper, zero_grad, grad_divisor, seed_base, tdesc, ntd,
-                       tbase, (__bf16*)wT);
+                       tbase, (__bf16*)wT, loss_sum, loss_out);
   else
     ADAM_LAUNCH(false, true, dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
                        (__bf16*)nullptr, state, hyper, zero_grad, grad_divisor, seed_base, nullptr, 0,
-                       0, nullptr);
+                       0, nullptr, loss_sum, loss_out);
   return (int)hipGetLastError();
 }
 

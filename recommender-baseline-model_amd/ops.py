@@ -309,7 +309,7 @@ def adam_step(p, g, m, v, p_bf16, state, hyper, zero_grad=False):
 
 
 def adam_prepare_step(p, g, m, v, p_bf16, state, hyper, zero_grad=False, grad_divisor=None, seed_base=None,
-                      transposed=None):
+                      transposed=None, loss_sum=None, loss_out=None):
     """adam_prepare + adam_step in one launch (state: double[144]; state[7], state[16 + 16 k] arrival counters).
     transposed: (desc int64 device [n][6] as transpose_bf16's, its host copy, dst bf16 tensor) -- the bf16
     result of those matrices is also written transposed (p[0] is element 0 of the flat buffer)."""
@@ -324,6 +324,11 @@ def adam_prepare_step(p, g, m, v, p_bf16, state, hyper, zero_grad=False, grad_di
                 raise ValueError("adam_prepare_step: transposed matrix outside the buffers or misaligned")
         if p_bf16 is None:
             raise ValueError("adam_prepare_step: transposed copies need the bf16 output")
+    if loss_out is not None:   # + loss_out = loss_sum / grad_divisor in the same launch
+        call("rs_adam_prepare_step_loss", p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), ptr(p_bf16), ptr(state),
+             ptr(hyper), int(zero_grad), ptr(grad_divisor), ptr(seed_base), ptr(td), nt, 0, ptr(wt), ptr(loss_sum),
+             ptr(loss_out), stream())
+        return
     call("rs_adam_prepare_step", p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), ptr(p_bf16), ptr(state), ptr(hyper),
          int(zero_grad), ptr(grad_divisor), ptr(seed_base), ptr(td), nt, 0, ptr(wt), stream())
 

@@ -50,17 +50,19 @@ class FusedAdam:
         """StepLR hook (BS/trainers/base.py:40,87): lives on the device, so graph replays see it."""
         self.hyper[0] = lr
 
-    def step(self, grad_divisor=None, seed_base=None, ranges=None, transposed=None):
+    def step(self, grad_divisor=None, seed_base=None, ranges=None, transposed=None, loss=None):
         """One Adam update; also clears the gradient buffer (the next step accumulates from zero) and
         advances the dropout step seed when given.  ranges: [(lo, hi)] flat slices to update (default all; a
-        vocabulary-sharded rank skips the output rows other ranks own)."""
+        vocabulary-sharded rank skips the output rows other ranks own).  loss = (sum, out): out = sum / grad_divisor
+        in the first launch."""
         f = self.flat
         for k, (lo, hi) in enumerate(ranges or [(0, f.numel)]):
             bf = f.bf16[lo:hi] if f.bf16 is not None else None
             if k == 0:   # the first range's launch also prepares the step's scalars (rs_adam_prepare_step)
                 ops.adam_prepare_step(f.data[lo:hi], f.grad[lo:hi], self.m[lo:hi], self.v[lo:hi], bf, self.state,
                                       self.hyper, zero_grad=True, grad_divisor=grad_divisor, seed_base=seed_base,
-                                      transposed=transposed if lo == 0 else None)
+                                      transposed=transposed if lo == 0 else None,
+                                      loss_sum=loss[0] if loss else None, loss_out=loss[1] if loss else None)
             else:
                 ops.adam_step(f.data[lo:hi], f.grad[lo:hi], self.m[lo:hi], self.v[lo:hi], bf, self.state,
                               self.hyper, zero_grad=True)
@@ -264,10 +266,13 @@ class FusedTrainStep:
         else:
             tr = self.engine.transposed_spec() if hasattr(self.engine, "transposed_spec") else None
             if self.dp:
-                torch.div(self.flat.aux[dpx.LOSS_SUM:dpx.LOSS_SUM + 1], self.flat.aux[dpx.COUNT:dpx.COUNT + 1],
-                          out=self.loss_val)
-                self._l2(self.loss_val, scale=self.flat.aux[dpx.COUNT:dpx.COUNT + 1])
-                self.opt.step(grad_divisor=self.flat.aux[dpx.COUNT:dpx.COUNT + 1], seed_base=sb, transposed=tr)
+                lsum, cnt = self.flat.aux[dpx.LOSS_SUM:dpx.LOSS_SUM + 1], self.flat.aux[dpx.COUNT:dpx.COUNT + 1]
+                if self.l2:
+                    torch.div(lsum, cnt, out=self.loss_val)
+                    self._l2(self.loss_val, scale=cnt)
+                    self.opt.step(grad_divisor=cnt, seed_base=sb, transposed=tr)
+                else:   # the loss division rides in the optimizer's launch
+                    self.opt.step(grad_divisor=cnt, seed_base=sb, transposed=tr, loss=(lsum, self.loss_val))
             else:
                 self._l2(self.loss_out[2:3])
                 self.opt.step(seed_base=sb, transposed=tr)
