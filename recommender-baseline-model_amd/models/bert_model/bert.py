@@ -400,12 +400,13 @@ class BERTEngine:
 
     @staticmethod
     def _wgrad_rows(M, tiles):
-        """rows per split of the grouped weight-gradient launch: about three 128x128-tile workgroups per
-        CU in total (one resident at a time), so the row ranges balance over the 256 CUs."""
+        """rows per split of the grouped weight-gradient launch: about one and a half 128x128-tile workgroups
+        per CU in total (cfg3: 192 tiles x 2 splits; 4 splits measured 156 against 153 us for the launch, 1 split
+        219 us)."""
         env = os.environ.get("RS_WGRAD_ROWS")
         if env:
             return int(env)
-        splits = max(1, round(768 / tiles))
+        splits = max(1, round(384 / tiles))
         return max(64, -(-(-(-M // splits)) // 64) * 64)
 
     # ---- full-vocabulary logits (the reference forward API) ---------------------------
