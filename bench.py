@@ -73,6 +73,10 @@ def parse():
                     help="training steps unrolled into one graph replay (single GPU; 'auto' = the largest of "
                          "10/8/5/4/2 dividing --steps, else 1); every step still runs on its own batch with its own "
                          "Adam update; warmup steps beyond a multiple of it run as eager steps")
+    ap.add_argument("--roofline-replays", type=int, default=20,
+                    help="eager training steps after the timed ones with HIP timing events around the dominant "
+                         "kernel's launches (0 = none: the in-kernel stamps of the timed steps then give "
+                         "avg_launch_us)")
     ap.add_argument("--nbatches", type=int, default=8, help="distinct synthetic batches cycled through")
     ap.add_argument("--sampler", default="host", choices=["host", "device"],
                     help="SAS: 'device' = batches drawn each step by the on-device WarpSampler "
@@ -128,13 +132,22 @@ def _time_on_stream(fn, reps, stream):
     return e0.elapsed_time(e1) * 1e3 / reps
 
 
-def _roof(kernel, us, flops, nbytes, dtype, note, live_us=None, live_expected=None):
+def _roof(kernel, us, flops, nbytes, dtype, note, live_us=None, live_expected=None, event_us=None):
     iso_us = us
-    if live_us:
-        us = sum(live_us) / len(live_us)
+    stamp_us = sum(live_us) / len(live_us) if live_us else None
+    if event_us:
+        us = sum(event_us) / len(event_us)
+        note += (f"; avg_launch_us = mean of {len(event_us)} launches inside training steps of the same trainer run "
+                 f"after the timed ones, each bracketed by HIP timing events on the stream it runs on, minus the "
+                 f"median time of an empty event pair queued the same way (event_pair_cost_us)")
+        if live_us:
+            note += (f"; stamp_launch_us = mean of {len(live_us)} launches of the timed steps themselves (in-kernel "
+                     f"s_memrealtime stamps: first wave in to last wave out, so without dispatch ramp and drain)")
+    elif live_us:
+        us = stamp_us
         note += (f"; avg_launch_us = mean of {len(live_us)} launches timed inside the timed steps (in-kernel "
-                 f"s_memrealtime stamps: first wave in to last wave out of the launch), isolated_launch_us = the "
-                 f"same launch re-timed alone with HIP events")
+                 f"s_memrealtime stamps: first wave in to last wave out of the launch)")
+    note += "; isolated_launch_us = the same launch re-timed alone, back to back, with HIP events"
     ai = flops / nbytes if nbytes else float("inf")
     peak_f = MI355X_BF16_TFLOPS if dtype == "bf16" else MI355X_F32_TFLOPS
     # both utilisations of the same live launch time, whichever bound the arithmetic intensity selects
@@ -149,14 +162,18 @@ def _roof(kernel, us, flops, nbytes, dtype, note, live_us=None, live_expected=No
         ach = nbytes / (us * 1e-6) / 1e9
         return {"kernel": kernel, "bound": "hbm", "achieved": round(ach, 1), "peak": MI355X_HBM_GBS, "unit": "GB/s",
                 "frac": round(ach / MI355X_HBM_GBS, 4), "traffic": traffic, "avg_launch_us": round(us, 2),
-                "isolated_launch_us": round(iso_us, 2), "live_samples": len(live_us or ()),
+                "isolated_launch_us": round(iso_us, 2),
+                "stamp_launch_us": round(stamp_us, 2) if stamp_us else None, "event_samples": len(event_us or ()),
+                "live_samples": len(live_us or ()),
                 "live_samples_expected": live_expected,
                 "algorithmic_bytes_per_launch": int(nbytes), "algorithmic_flops_per_launch": int(flops),
                 "arith_intensity": round(ai, 1), **util, "note": note}
     ach = flops / (us * 1e-6) / 1e12
     return {"kernel": kernel, "bound": "mfma", "achieved": round(ach, 2), "peak": peak_f, "unit": "TFLOP/s",
             "frac": round(ach / peak_f, 4), "traffic": traffic, "avg_launch_us": round(us, 2),
-            "isolated_launch_us": round(iso_us, 2), "live_samples": len(live_us or ()),
+            "isolated_launch_us": round(iso_us, 2),
+            "stamp_launch_us": round(stamp_us, 2) if stamp_us else None, "event_samples": len(event_us or ()),
+            "live_samples": len(live_us or ()),
             "live_samples_expected": live_expected,
             "algorithmic_bytes_per_launch": int(nbytes), "algorithmic_flops_per_launch": int(flops),
             "arith_intensity": round(ai, 1), **util, "note": note}
@@ -171,7 +188,7 @@ def dominant(cfg):
     return "vocab_ce_fwd" if cfg["V"] >= 100000 else "wgrad_grouped"
 
 
-def roofline(cfg, B, dtype, live_us=None, reps=50, labelled=None, live_expected=None):
+def roofline(cfg, B, dtype, live_us=None, reps=50, labelled=None, live_expected=None, event_us=None):
     """Dominant kernel of the step (by rocprof device time).  SAS: the attention backward (rs_attn_bwd:
     dQ+delta and dK/dV kernels); BERT: the grouped block weight gradients (rs_wgrad_grouped).
     live_us: its launch durations measured INSIDE the timed step replays (in-kernel begin/end stamps of
@@ -199,16 +216,20 @@ def roofline(cfg, B, dtype, live_us=None, reps=50, labelled=None, live_expected=
         ws = torch.empty(B * H * T, device="cuda")
         with torch.cuda.stream(stream):
             ops.attn_fwd(B, T, H, Dh, q, kv[:, :d], kv[:, d:], o, lse, 1 / math.sqrt(Dh), 0, ids, cfg["p"], 5, sb)
+            # the step's variant: delta = rowsum(dO*O) handed in by the out-side backward (sas.py, delta_in=True),
+            # so the launch timed here reads neither O nor forms delta, exactly like the live-stamped one
+            ops.attn_row_delta(B, T, H, Dh, do, o, ws)
         us = _time_on_stream(lambda: ops.attn_bwd(B, T, H, Dh, q, kv[:, :d], kv[:, d:], o, do, lse, dq, dkv[:, :d],
-                                                  dkv[:, d:], 1 / math.sqrt(Dh), 0, ids, cfg["p"], 5, sb, ws),
+                                                  dkv[:, d:], 1 / math.sqrt(Dh), 0, ids, cfg["p"], 5, sb, ws,
+                                                  delta_in=True),
                              reps, stream)
         # algorithmic: dV, dP, dQ, dK products over the causal triangle (2 flop/MAC); bytes: read
-        # q,k,v,o,dO + lse, write dq,dk,dv once
+        # q, k, v, dO + lse, delta, write dq, dk, dv once (7 activation tensors of M x d)
         flops = 4 * 2.0 * (T * (T + 1) / 2) * Dh * B * H
-        nbytes = 8 * M * d * es + B * H * T * 4 * 2
+        nbytes = 7 * M * d * es + B * H * T * 4 * 2
         return _roof("rs_attn_bwd (attn_bwd_lds: dQ + dK/dV workgroups)", us, flops, nbytes, dtype,
-                     f"causal attention backward, B={B} T={T} Dh={Dh} dropout {cfg['p']}; one launch, both passes",
-                     live_us, live_expected)
+                     f"causal attention backward (delta_in: no O read), B={B} T={T} Dh={Dh} dropout {cfg['p']}; "
+                     f"one launch, both passes", live_us, live_expected, event_us)
     if dominant(cfg) == "vocab_ce_fwd":
         # BERT, 1M-item vocabulary: h[R,d] . E^T + b with the online-softmax partial epilogue over the labelled
         # rows (R = the batches' mean labelled count), E = out.weight [V+1, d] bf16
@@ -223,7 +244,7 @@ def roofline(cfg, B, dtype, live_us=None, reps=50, labelled=None, live_expected=
         flops = 2.0 * R * V1 * d
         nbytes = (V1 * d + R * d) * es + R * -(-V1 // 128) * 2 * 4     # E, h once; (max, sum) partials
         return _roof("rs_vocab_head_fwd (E-tile-stationary logits + online-softmax partials)", us, flops, nbytes, dtype,
-                     f"R={R} labelled rows (batch mean) x V+1={V1} x d={d}", live_us, live_expected)
+                     f"R={R} labelled rows (batch mean) x V+1={V1} x d={d}", live_us, live_expected, event_us)
     # BERT: the grouped weight-gradient launch of all block weights (rs_wgrad_grouped: GEMM + reduction),
     # the largest single kernel of the step
     from rbm_amd.models.bert_model.bert import BERTEngine
@@ -239,7 +260,7 @@ def roofline(cfg, B, dtype, live_us=None, reps=50, labelled=None, live_expected=
     nbytes = sum(M * (n + k) * es + (n * k + n) * 4 * 2 for n, k in shapes)   # dY, X once; dW, db read+write
     return _roof("rs_wgrad_grouped (wgrad_group_kernel + reduce_cols_kernel)", us, flops, nbytes, dtype,
                  f"{len(shapes)} block weight gradients of M={M} token rows (d={d}, ff={Fd}, L={L}), "
-                 f"{-(-M // rows)} row splits; 2 kernels per launch", live_us, live_expected)
+                 f"{-(-M // rows)} row splits; 2 kernels per launch", live_us, live_expected, event_us)
 
 
 # ------------------------------------------------------------------------------------ CPU baseline
@@ -400,6 +421,10 @@ def main():
         loss = eager(i)
     torch.cuda.synchronize()
     if world > 1:
+        # the replicas must hold the same parameter bits after the warmup steps (one all-reduced gradient per
+        # step): checks the exchange -- in-graph or segmented -- end to end before anything is timed
+        if not trainer.replicas_equal():
+            raise SystemExit(f"rank {rank}: data-parallel replicas diverged during warmup")
         dist.barrier()
     torch.cuda.synchronize()
     if sbuf is not None:
@@ -424,10 +449,38 @@ def main():
         live = [us for _, _, us in ops.read_kernel_stamps(sbuf, ops.wall_clock_khz())]
         live_expected = args.steps * marks_per_step
         del sbuf
+    # the dominant kernel's launch time by HIP events: after the timed steps, training steps of the same trainer run
+    # eagerly with a pair of timing events recorded around each of its launches on the stream it runs on (event nodes
+    # inside a ROCm graph cost the step a few us each, so they stay out of the timed replays, whose own launches
+    # carry the in-kernel stamps above).  A spin kernel first holds the queue while the host issues the whole step,
+    # so its launches then run back to back as in a replay and the events see device time only.  Every rank alike
+    # (under DP the steps hold the collectives).
+    event_us, ev_cost, event_raw = None, None, None
+    if not args.no_graph and args.roofline_replays > 0:
+        pairs = ops.event_timing((dominant(cfg),))
+        empty = []
+        try:
+            for i in range(args.roofline_replays):
+                torch.cuda._sleep(5_000_000)
+                # an empty event pair queued the same way: the events' own cost, subtracted from every bracket
+                c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                c0.record()
+                c1.record()
+                empty.append((c0, c1))
+                eager(i)
+                torch.cuda.synchronize()
+        finally:
+            ops.event_timing(())
+        ev_cost = sorted(c0.elapsed_time(c1) * 1e3 for c0, c1 in empty)[len(empty) // 2]
+        event_us = [e0.elapsed_time(e1) * 1e3 - ev_cost for _, e0, e1 in pairs]
+        event_raw = sum(e0.elapsed_time(e1) * 1e3 for _, e0, e1 in pairs) / max(1, len(pairs))
     labelled = (sum(float((lab != 0).sum()) for _, lab in host_batches) / len(host_batches)
                 if cfg["model"] == "bert" else None)
-    roof = roofline(cfg, B, args.dtype, live_us=live, labelled=labelled, live_expected=live_expected) \
-        if rank == 0 else None
+    roof = roofline(cfg, B, args.dtype, live_us=live, labelled=labelled, live_expected=live_expected,
+                    event_us=event_us) if rank == 0 else None
+    if roof is not None and event_us:
+        roof["event_pair_raw_us"] = round(event_raw, 2)
+        roof["event_pair_cost_us"] = round(ev_cost, 2)
     if rank == 0:
         cpu = cpu_baseline(cfg, B, args.cpu_baseline_seconds) if world == 1 and args.cpu_baseline_seconds > 0 \
             else None

@@ -252,7 +252,7 @@ int rs_adam_prepare_step_loss(int64_t n, float* p, float* g, float* m, float* v,
 /* SASRec's parameter-norm regulariser, BS/trainers/sas.py:51-52 (loss += l2_emb * torch.norm(p) for every
  * parameter p): *loss += l2 * sum_seg ||p_seg||_2 and g += scale * l2 * p / ||p_seg|| (0 where the norm is 0,
  * as torch's norm backward).  desc: device int64 [nchunk][4] = {lo, hi, first chunk of the segment, chunks of
- * the segment} over the flat parameter buffer (chunks of one segment consecutive); ws: fp32 [nchunk]; scale:
+ * the segment} over the flat parameter buffer (chunks of one segment consecutive); ws: fp32 [2 * nchunk]; scale:
  * device float or null (= 1; the data-parallel step passes the global count its optimizer divides by);
  * g and loss nullable.  Deterministic. */
 int rs_l2_penalty(const float* p, float* g, const int64_t* desc, int64_t nchunk, float l2, const float* scale,

@@ -10,8 +10,10 @@
 // of the segment}, segments in order, chunks of one segment consecutive.
 //
 //   pass 1 (one workgroup per chunk): ws[c] = sum_{i in chunk c} p[i]^2          (fp32, fixed order)
-//   pass 2 (one workgroup per chunk): ||p_seg|| = sqrt(sum of the segment's ws, in chunk order);
-//          g[i] += scale * l2 * p[i] / ||p_seg||; workgroup 0 also adds l2 * sum_seg ||p_seg|| to *loss.
+//   pass 2 (one workgroup): per segment ||p_seg|| = sqrt(block sum of its chunk sums) -> ws[nchunk + first
+//          chunk]; adds l2 * sum_seg ||p_seg|| (segments in order) to *loss
+//   pass 3 (one workgroup per chunk): g[i] += scale * l2 * p[i] / ||p_seg||  (one norm read per chunk)
+// ws holds 2 * nchunk floats.
 // Deterministic (no atomics).  scale: a device float (the data-parallel step's global count: the
 // optimizer divides the summed gradient by it, so the penalty's gradient is pre-multiplied) or null = 1.
 #include "common.h"
@@ -52,32 +54,33 @@ __global__ __launch_bounds__(NT) void sumsq_kernel(const float* __restrict__ p, 
   if (threadIdx.x == 0) ws[c] = s;
 }
 
-__device__ __forceinline__ float seg_norm(const int64_t* desc, const float* ws, int64_t c) {
-  const int64_t c0 = desc[4 * c + 2], nc = desc[4 * c + 3];
-  float s = 0.f;
-  for (int64_t k = 0; k < nc; ++k) s += ws[c0 + k];
-  return sqrtf(s);
+// one workgroup: every segment's norm (its chunk sums reduced by the whole workgroup, fixed order) and the loss
+__global__ __launch_bounds__(NT) void norm_kernel(const int64_t* __restrict__ desc, int64_t nchunk,
+                                                  float* __restrict__ ws, float l2, float* __restrict__ loss) {
+  __shared__ float red[NT / 64 + 1];
+  float tot = 0.f;
+  for (int64_t c0 = 0; c0 < nchunk;) {
+    const int64_t nc = desc[4 * c0 + 3];
+    float s = 0.f;
+    for (int64_t k = threadIdx.x; k < nc; k += NT) s += ws[c0 + k];
+    s = block_sum(s, red);
+    const float nrm = sqrtf(s);
+    tot += nrm;
+    if (threadIdx.x == 0) ws[nchunk + c0] = nrm;
+    c0 += nc > 0 ? nc : 1;
+  }
+  if (threadIdx.x == 0 && loss) *loss += l2 * tot;
 }
 
 __global__ __launch_bounds__(NT) void apply_kernel(const float* __restrict__ p, float* __restrict__ g,
                                                    const int64_t* __restrict__ desc, int64_t nchunk,
                                                    const float* __restrict__ ws, float l2,
-                                                   const float* __restrict__ scale, float* __restrict__ loss) {
-  __shared__ float red[NT / 64 + 1];
+                                                   const float* __restrict__ scale) {
   const int64_t c = blockIdx.x;
   const int64_t lo = desc[4 * c], hi = desc[4 * c + 1];
-  const float nrm = seg_norm(desc, ws, c);
+  const float nrm = ws[nchunk + desc[4 * c + 2]];
   const float k = nrm > 0.f ? l2 * (scale ? *scale : 1.f) / nrm : 0.f;
-  if (g)
-    for (int64_t i = lo + threadIdx.x; i < hi; i += NT) g[i] = __builtin_fmaf(k, p[i], g[i]);
-  if (c == 0 && loss) {
-    // sum of the segment norms, segments in order (each counted at its first chunk)
-    float s = 0.f;
-    for (int64_t j = threadIdx.x; j < nchunk; j += NT)
-      if (desc[4 * j + 2] == j) s += seg_norm(desc, ws, j);
-    s = block_sum(s, red);
-    if (threadIdx.x == 0) *loss += l2 * s;
-  }
+  for (int64_t i = lo + threadIdx.x; i < hi; i += NT) g[i] = __builtin_fmaf(k, p[i], g[i]);
 }
 
 }  // namespace pen
@@ -89,8 +92,10 @@ int rs_l2_penalty(const float* p, float* g, const int64_t* desc, int64_t nchunk,
   if (!p || !desc || !ws || nchunk <= 0 || nchunk > (int64_t)1 << 30) return RS_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(pen::sumsq_kernel, dim3((unsigned)nchunk), dim3(pen::NT), 0, s, p, desc, ws);
-  hipLaunchKernelGGL(pen::apply_kernel, dim3((unsigned)nchunk), dim3(pen::NT), 0, s, p, g, desc, nchunk, ws, l2,
-                     scale, loss);
+  hipLaunchKernelGGL(pen::norm_kernel, dim3(1), dim3(pen::NT), 0, s, desc, nchunk, ws, l2, loss);
+  if (g)
+    hipLaunchKernelGGL(pen::apply_kernel, dim3((unsigned)nchunk), dim3(pen::NT), 0, s, p, g, desc, nchunk, ws, l2,
+                       scale);
   return (int)hipGetLastError();
 }
 

@@ -36,13 +36,42 @@ import torch.distributed as dist
 LOSS_SUM, COUNT = 0, 1   # aux slots
 
 
-def world():
-    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+def world(group=None):
+    """World size of `group` (default: the global group); 1 without torch.distributed."""
+    return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
 
 
 def backend(group=None):
     """The process group's backend name ("nccl" = RCCL on ROCm, "gloo"), None without torch.distributed."""
     return str(dist.get_backend(group)).lower() if dist.is_available() and dist.is_initialized() else None
+
+
+def agree(ok, group=None):
+    """True on every rank iff `ok` is true on every rank (an eager MIN all-reduce of one flag; a no-op without
+    torch.distributed).  Used where a rank-local outcome (a graph capture that may refuse a collective) decides
+    which collectives every rank issues next: the ranks must take the same branch or the next collective hangs."""
+    if world(group) == 1:
+        return bool(ok)
+    dev = "cuda" if backend(group) == "nccl" else "cpu"
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(t.item())
+
+
+def replicas_equal(t, group=None):
+    """True iff the tensor `t` holds the same bits on every rank (the data-parallel replicas' parameters after a
+    step): MAX and MIN all-reduces of an exact integer checksum of its bits."""
+    if world(group) == 1:
+        return True
+    x = t.detach().reshape(-1).view(torch.int32).to(torch.int64)
+    w = torch.arange(1, x.numel() + 1, device=x.device, dtype=torch.int64) % 65521 + 1
+    c = torch.stack([(x * w).sum(), x.sum()])
+    if backend(group) != "nccl":
+        c = c.cpu()
+    hi, lo = c.clone(), c.clone()
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
+    return bool(torch.equal(hi, lo))
 
 
 def allreduce_grads(flat_grad, group=None, bucket_numel=None):
@@ -134,7 +163,7 @@ class SparseRowExchange:
         self.ops = ops
         self.g = grad_rows
         self.rows, self.d = grad_rows.shape
-        self.W = world()
+        self.W = world(group)
         self.n_local = int(n_local)
         self.group = group
         self.cap = min(self.rows, self.W * self.n_local)

@@ -52,6 +52,32 @@ def kernel_stamp_kinds():
     return [STAMP_KINDS.get(arr[i], "?") for i in range(n)]
 
 
+# ------------------------------------------------------------------ HIP-event launch timing
+_EVENTS = {"kinds": (), "pairs": []}
+
+
+def event_timing(kinds=()):
+    """Bracket every launch of the named kinds (STAMP_KINDS names) with a pair of timing HIP events on the current
+    stream (eager launches; bench.py's roofline leg).  Returns the list collecting (kind, begin event, end event);
+    kinds=() disables."""
+    _EVENTS["kinds"], _EVENTS["pairs"] = tuple(kinds), []
+    return _EVENTS["pairs"]
+
+
+def _ev_begin(kind):
+    if kind not in _EVENTS["kinds"]:
+        return None
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    _EVENTS["pairs"].append((kind, e0, e1))
+    return e1
+
+
+def _ev_end(e1):
+    if e1 is not None:
+        e1.record()
+
+
 def wall_clock_khz():
     k = C.c_int()
     call("rs_wall_clock_khz", C.byref(k))
@@ -233,9 +259,11 @@ def attn_bwd(B, T, H, Dh, q, k, v, o, do, lse, dq, dk, dv, scale, mask_kind, ids
              delta_in=False):
     """delta_in: ws already holds delta = rowsum(dO * O) per (b, h, t) (sas_block_out_bwd with o=)."""
     mk = mask_kind | (RS_ATTN_DELTA_IN if delta_in else 0)
+    ev = _ev_begin("attn_bwd")
     call("rs_attn_bwd", dtype_code(q), B, T, H, Dh, ptr(q), ld(q), ptr(k), ld(k), ptr(v), ld(v), ptr(o), ld(o),
          ptr(do), ld(do), ptr(lse), ptr(dq), ld(dq), ptr(dk), ld(dk), ptr(dv), ld(dv), scale, mk, ptr(ids),
          drop_p, seed, ptr(seed_base), ptr(ws), stream())
+    _ev_end(ev)
 
 
 def sampled_logits_fwd(f, E, pos, neg, pl, nl):
@@ -353,7 +381,7 @@ def l2_chunk_desc(flat, device):
 
 def l2_penalty(p, g, desc, l2, ws, loss=None, scale=None):
     """loss += l2 * sum ||p_seg||, g += scale * l2 * p / ||p_seg|| (BS/trainers/sas.py:51-52; rs_l2_penalty)."""
-    assert ws.numel() >= desc.shape[0] and ws.dtype == torch.float32
+    assert ws.numel() >= 2 * desc.shape[0] and ws.dtype == torch.float32   # chunk sums + segment norms
     call("rs_l2_penalty", ptr(p), ptr(g), ptr(desc), desc.shape[0], float(l2), ptr(scale), ptr(ws), ptr(loss),
          stream())
 
@@ -400,8 +428,10 @@ def vocab_head_fwd(h, E, bias, labels, ws, out, rows_dev=None, count_override=No
     """vocab_ce_fwd's result from the vocabulary-tile-stationary kernel (rs_vocab_head_fwd)."""
     R, d = h.shape
     V1 = E.shape[0]
+    ev = _ev_begin("vocab_ce_fwd")
     call("rs_vocab_head_fwd", R, V1, d, ptr(h), ld(h), ptr(E), ld(E), ptr(bias), ptr(labels), ptr(rows_dev),
          ptr(count_override), ptr(ws), ptr(out), stream())
+    _ev_end(ev)
 
 
 def vocab_head_bwd(h, E, bias, labels, ws, count, dl, rows_dev=None, dloss=None, voff=0):
@@ -556,6 +586,12 @@ def _segments(segs):
 
 
 def wgrad_grouped(problems, M, rows_per_split, slab, extra=(), items=None, pos=None):
+    ev = _ev_begin("wgrad_grouped")
+    _wgrad_grouped(problems, M, rows_per_split, slab, extra, items, pos)
+    _ev_end(ev)
+
+
+def _wgrad_grouped(problems, M, rows_per_split, slab, extra=(), items=None, pos=None):
     """problems: [(dY, X, dW, db|None)] with dW [N][K] fp32 (+=); extra: reduce segments
     (src, stride, splits, n, out) summed (+=) in the same reduction launch.  items: item_grad's arguments
     (ws, nsrc, rows, dx, scale, drop_p, salt, seed_base, f, w1, w2, dtable) -- that gradient then shares the two

@@ -117,7 +117,7 @@ class FusedTrainStep:
         self.l2 = float(getattr(model.sas, "l2_emb", 0.0)) if self.kind == "sas" else 0.0
         if self.l2:
             self.l2_desc = ops.l2_chunk_desc(self.flat, dev)
-            self.l2_ws = torch.zeros(self.l2_desc.shape[0], dtype=torch.float32, device=dev)
+            self.l2_ws = torch.zeros(2 * self.l2_desc.shape[0], dtype=torch.float32, device=dev)
         self.loss_out = torch.zeros(4, dtype=torch.float32, device=dev)
         self.count = torch.zeros(1, dtype=torch.float32, device=dev)
         self.one = torch.ones(1, dtype=torch.float32, device=dev)
@@ -179,7 +179,7 @@ class FusedTrainStep:
         name = "bert.embedding.token.weight"
         rows, d = self.flat.shapes[name]
         n = tokens.numel()
-        if self.sparse_mode == "auto" and not dpx.SparseRowExchange.worthwhile(rows, n, dpx.world()):
+        if self.sparse_mode == "auto" and not dpx.SparseRowExchange.worthwhile(rows, n, dpx.world(self.pg)):
             return
         self.sparse = dpx.SparseRowExchange(self.flat.view(name, self.flat.grad), n, self.pg)
         self.engine.sparse_tok = self.sparse
@@ -290,6 +290,12 @@ class FusedTrainStep:
             self._exchange()
         self._update()
         return self.loss_val if self.dp else self.loss_out[2:3]
+
+    def replicas_equal(self):
+        """Data parallel: True iff every rank holds the same parameter bits (collective; call on every rank).  The
+        replicas start equal and every step applies the same all-reduced gradient, so a difference means an
+        exchange went wrong (bench.py checks it after its warmup)."""
+        return dpx.replicas_equal(self.flat.data, self.pg) if self.dp else True
 
     # ---------------------------------------------------------------- checkpoints
     def _param_slices(self):
@@ -460,6 +466,7 @@ class FusedTrainStep:
         try:
             if self.graph_collectives:
                 # one graph: compute, the all-reduce, the optimizer (unrolled: S of those)
+                err = None
                 try:
                     g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
@@ -467,15 +474,20 @@ class FusedTrainStep:
                         if not unrolled:
                             self._graph_exchange()
                             self._update()
-                except Exception as e:   # the collective refused capture: every rank takes the same branch
-                    if self.steps_per_graph > 1:
-                        raise
-                    import warnings
-                    warnings.warn(f"all-reduce capture failed ({e}); falling back to segmented DP graphs")
-                    torch.cuda.synchronize()
+                except Exception as e:   # the collective refused capture on this rank
+                    err = e
+                torch.cuda.synchronize()
+                if self.exchange is not None:
+                    self.exchange.works, self.exchange.sent = [], []
+                # the ranks agree on the outcome (eager MIN of a flag) before anything else is issued: a rank that
+                # fell back alone would run eager / segmented collectives against the others' captured ones
+                if not dpx.agree(err is None, self.pg):
                     self.graph_collectives = False
-                    if self.exchange is not None:
-                        self.exchange.works, self.exchange.sent = [], []
+                    if self.steps_per_graph > 1:   # every rank raises alike; the caller re-captures with S = 1
+                        raise RuntimeError(f"all-reduce capture failed on some rank ({err or 'not this one'})")
+                    import warnings
+                    warnings.warn(f"all-reduce capture failed on some rank ({err or 'not this one'}); falling back "
+                                  f"to segmented DP graphs on every rank")
                     return self._capture_graphs(compute, stamps, unrolled)
                 self.g_compute = g
                 self.g_segments = None

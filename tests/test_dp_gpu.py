@@ -115,7 +115,7 @@ def test_dp_overlap_bitwise_equals_single_allreduce_bf16(nccl_group, kind):
 def test_dp_graph_collectives_equal_segmented(nccl_group, monkeypatch):
     """SAS under DP with the all-reduce captured inside the step graph (one step per replay, and two steps
     unrolled into one replay) against the segmented form (step graph, all-reduce between replays, optimizer
-    graph): bit-identical parameters and losses (bf16 fused step, dropout on)."""
+    graph): bit-identical parameters and losses (bf16 fused step, dropout on, l2_emb > 0)."""
     import rbm_amd  # noqa: F401
     from rbm_amd.models import model_factory
     from rbm_amd.train_step import FusedTrainStep
@@ -125,7 +125,7 @@ def test_dp_graph_collectives_equal_segmented(nccl_group, monkeypatch):
         monkeypatch.setenv("RS_DP_GRAPH_COLLECTIVES", mode)
         torch.manual_seed(5)
         a = argparse.Namespace(model_code="sas", num_items=500, max_len=50, device="cuda", sas_hidden_units=128,
-                               sas_num_blocks=2, sas_heads=1, sas_dropout=0.1, l2_emb=0.0, rs_dtype="bf16")
+                               sas_num_blocks=2, sas_heads=1, sas_dropout=0.1, l2_emb=0.01, rs_dtype="bf16")
         tr = FusedTrainStep(model_factory(a), lr=1e-3, dp=True)
         assert tr.graph_collectives == (mode == "1")
         tr.capture(*batches[0], steps_per_graph=S)

@@ -64,7 +64,7 @@ def test_l2_zero_norm_parameter_gets_zero_gradient():
     fl = eng.flat
     fl.view("last_layernorm.bias").zero_()
     desc = ops.l2_chunk_desc(fl, fl.device)
-    ws = torch.zeros(desc.shape[0], device="cuda")
+    ws = torch.zeros(2 * desc.shape[0], device="cuda")
     g = torch.zeros(fl.numel, device="cuda")
     loss = torch.zeros(1, device="cuda")
     ops.l2_penalty(fl.data, g, desc, 0.1, ws, loss=loss)
