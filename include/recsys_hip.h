@@ -100,14 +100,6 @@ int rs_colsum(int dtype, const void* X, int64_t M, int64_t N, int64_t ldx, float
 int rs_embed_fwd(int dtype, int mode, const int64_t* ids, int64_t rows, int64_t T, const void* table,
                  const void* pos, int64_t d, float scale, float drop_p, uint64_t seed, const uint64_t* seed_base,
                  void* out, void* stream);
-/* rs_embed_fwd (vector layout: d a multiple of 8 bf16 / 4 fp32, 16-byte aligned buffers) that also counts, per
- * wave of 64 lanes, the rows r with count_ids[r] != 0 into count_parts[rs_embed_count_parts(dtype, rows, d)] (int32;
- * SAS: the valid positions pos != 0, the BCE divisor, for rs_sas_head_fused).  RS_ERR_UNSUPPORTED otherwise. */
-int64_t rs_embed_count_parts(int dtype, int64_t rows, int64_t d);
-int rs_embed_fwd_counted(int dtype, int mode, const int64_t* ids, int64_t rows, int64_t T, const void* table,
-                         const void* pos, int64_t d, float scale, float drop_p, uint64_t seed,
-                         const uint64_t* seed_base, void* out, const int64_t* count_ids, int* count_parts,
-                         void* stream);
 /* dtable[ids[r]] += dX*mask*scale (rows with id 0 skipped: padding_idx=0, fp32 atomics);
  * dpos[t] (+)= sum_b dX[b,t] * mask (deterministic; accumulate flag). */
 int rs_embed_bwd(int dtype, int mode, const int64_t* ids, int64_t rows, int64_t T, const void* dx,
@@ -364,8 +356,8 @@ int rs_sas_block_in(int64_t M, int64_t d, const void* x, int64_t ldx, const floa
 /* The first block's input side with the embedding stage folded in (rowchain: one launch instead of two): x0 =
  * (item_emb[ids]*scale + pos_emb[t]) -> dropout(p, salt) -> *(ids != 0), exactly as rs_embed_fwd mode 0, stored
  * to x0 [M][d] and fed to rs_sas_block_in's chain; with count_ids, count_parts[rs_sas_block_in_count_parts(M)]
- * (int32) receives per-wave counts of count_ids != 0 (the BCE divisor for rs_sas_head_fused).  Other shapes or
- * the non-chain build: rs_embed_fwd(_counted) then rs_sas_block_in (same results). */
+ * (int32) receives per-wave counts of count_ids != 0 (the BCE divisor for rs_sas_block_out_head).  d in {64, 128}
+ * and 16-byte aligned tables / x0, else RS_ERR_ARG. */
 int64_t rs_sas_block_in_count_parts(int64_t M);
 int rs_sas_block_in_embed(int64_t M, int64_t d, const int64_t* ids, int64_t T, const void* item_emb, const void* pos_emb,
                           float scale, float drop_p, uint64_t salt, const uint64_t* seed_base, void* x0,
@@ -386,8 +378,7 @@ int rs_sas_block_out(int64_t M, int64_t d, const void* o, const void* Q, const v
  * xn: f = LN_last(xn) [saved], pl/nl = <f, E[pos]>/<f, E[neg]>, dpl = (sigmoid(pl)-1)/c, dnl = sigmoid(nl)/c on
  * pos != 0 [saved], dx = LN_last'(xn, dpl E[pos] + dnl E[neg]) [saved, bf16].  Per workgroup
  * (rs_sas_block_grid(M) of them): lnpart[b][2][d] LN affine partials, part[b][3] BCE partials (sum softplus(-pl),
- * sum softplus(nl), count) for rs_sas_head_finish / rs_wgrad_grouped_pos_stats.  RS_ERR_UNSUPPORTED off the
- * row-chain build or d not in {64, 128} (callers use rs_sas_block_out + rs_sas_head_fused). */
+ * sum softplus(nl), count) for rs_wgrad_grouped_pos_stats.  RS_ERR_UNSUPPORTED for d not in {64, 128}. */
 int64_t rs_sas_block_grid(int64_t M);
 int rs_sas_block_out_head(int64_t M, int64_t d, const void* o, const void* Q, const void* Wo, const float* bo,
                           void* x1, const float* ln_w, const float* ln_b, float eps, void* z, float* mean, float* rstd,
@@ -472,15 +463,6 @@ int64_t rs_wgrad_grouped_slab_numel(int nprob, const rs_wgrad_problem* probs, in
 int rs_wgrad_grouped(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_t rows_per_split, float* slab,
                      int64_t slab_numel, int nextra, const rs_reduce_segment* extra, void* stream);
 
-/* rs_wgrad_grouped followed by rs_item_grad (same arguments, same results bit for bit) in two launches on one
- * stream: the weight-gradient tiles and the item-gradient chunks share the first launch, the slab reduction
- * and the item-gradient span pass the second (grad_tail.hip; the SAS step's backward tail). */
-int rs_wgrad_grouped_items(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_t rows_per_split, float* slab,
-                           int64_t slab_numel, int nextra, const rs_reduce_segment* extra, const void* ws, int nsrc,
-                           int64_t rows, int64_t table_rows, int64_t d, const void* dx, float scale, float drop_p,
-                           uint64_t salt, const uint64_t* seed_base, const void* f, const float* w1, const float* w2,
-                           float* dtable, void* stream);
-
 /* rs_wgrad_grouped followed by rs_embed_bwd's positional part (bf16, SAS mode 0, scale 1, dpos +=): the
  * positional table's gradient rides in the grouped reduction's launch as T extra workgroups (grad_tail.hip). */
 int rs_wgrad_grouped_pos(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_t rows_per_split, float* slab,
@@ -530,15 +512,8 @@ int rs_sas_head_bwd(int64_t M, int64_t d, const float* part, const float* diviso
                     const float* nl, const float* dpl_in, const float* dnl_in, float* dpl, float* dnl,
                     const int64_t* pos, const int64_t* neg, const void* E, const void* x, const float* ln_w,
                     const float* mean, const float* rstd, void* dx, float* lnpart, void* stream);
-/* Forward + backward of the head in one kernel for the fused training step (the BCE divisor c = *divisor or the
- * sum of count_parts from rs_embed_fwd_counted, so no row waits for the others): writes f, pl, nl, dpl, dnl, dx,
- * lnpart (as rs_sas_head_bwd) and part[b][3] (as rs_sas_head_fwd), b < ceil(M/64).  No mean/rstd.
- * rs_sas_head_finish(nblk = ceil(M/64), ...) then forms out[0..3] from part exactly as rs_sas_head_bwd does (one
- * workgroup; may run on a side stream). */
-int rs_sas_head_fused(int64_t M, int64_t d, const void* x, const float* ln_w, const float* ln_b, float eps,
-                      const int* count_parts, int64_t ncount, const float* divisor, void* f, const void* E,
-                      const int64_t* pos, const int64_t* neg, float* pl, float* nl, float* dpl, float* dnl, void* dx,
-                      float* lnpart, float* part, void* stream);
+/* out[0..3] from a head's BCE partials part[nblk][3] exactly as rs_sas_head_bwd forms them (one workgroup; the
+ * unfused form of rs_wgrad_grouped_pos_stats' statistics). */
 int rs_sas_head_finish(int64_t nblk, const float* part, const float* divisor, float* out, void* stream);
 
 /* ---- on-device SAS sampler and ranking metrics (sampler.hip) ----------------------------------

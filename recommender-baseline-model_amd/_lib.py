@@ -54,8 +54,6 @@ SIGNATURES = {
     "rs_linear_wgrad": [i32, i64, i64, i64, vp, i64, vp, i64, vp, vp, i32, i32, vp, vp, vp],
     "rs_colsum": [i32, vp, i64, i64, i64, vp, vp, i32, vp],
     "rs_embed_fwd": [i32, i32, vp, i64, i64, vp, vp, i64, f32, f32, u64, vp, vp, vp],
-    "rs_embed_fwd_counted": [i32, i32, vp, i64, i64, vp, vp, i64, f32, f32, u64, vp, vp, vp, vp, vp],
-    "rs_embed_count_parts": [i32, i64, i64],
     "rs_embed_bwd": [i32, i32, vp, i64, i64, vp, i64, f32, f32, u64, vp, vp, vp, i32, vp],
     "rs_layernorm_fwd": [i32, i32, vp, i64, i64, i64, vp, vp, f32, vp, i64, vp, vp, vp],
     "rs_layernorm_bwd_nparts": [i32, i64, i64],
@@ -118,7 +116,6 @@ SIGNATURES = {
     "rs_item_index_ws_bytes": [i32, i64, i64, i64],
     "rs_item_index_build": [i32, vp, vp, vp, i64, i64, i64, vp, i64, vp],
     "rs_sas_head_fwd": [i64, i64, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
-    "rs_sas_head_fused": [i64, i64, vp, vp, vp, f32, vp, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "rs_sas_head_finish": [i64, vp, vp, vp, vp],
     "rs_sas_head_bwd": [i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "rs_item_grad": [vp, i32, i64, i64, i64, vp, f32, f32, u64, vp, vp, vp, vp, vp, vp],
@@ -126,8 +123,6 @@ SIGNATURES = {
                              vp, i64, vp, i64, f32, u64, vp, vp, vp],
     "rs_wgrad_grouped_pos_stats": [i32, C.POINTER(WgradProblem), i64, i64, vp, i64, i32, C.POINTER(ReduceSegment),
                                    vp, i64, vp, i64, f32, u64, vp, vp, vp, i64, vp, vp, vp, vp],
-    "rs_wgrad_grouped_items": [i32, C.POINTER(WgradProblem), i64, i64, vp, i64, i32, C.POINTER(ReduceSegment),
-                               vp, i32, i64, i64, i64, vp, f32, f32, u64, vp, vp, vp, vp, vp, vp],
     "rs_transpose_bf16": [i64, vp, i64, vp, vp, vp],
     "rs_sas_sample": [vp, vp, i64, i64, i64, i64, vp, u64, vp, vp, vp, vp],
     "rs_bert_mask": [vp, vp, i64, i64, i64, i64, f32, vp, vp, u64, vp, vp, vp],
@@ -144,7 +139,7 @@ SIGNATURES = {
 RESTYPES = {"rs_wgrad_grouped_slab_numel": C.c_int64, "rs_sas_block_parts": C.c_int64,
             "rs_touched_rows_ws_numel": C.c_int64, "rs_item_index_ws_bytes": C.c_int64,
             "rs_vocab_ce_ws_numel": C.c_int64,
-            "rs_embed_count_parts": C.c_int64, "rs_sas_block_in_count_parts": C.c_int64,
+            "rs_sas_block_in_count_parts": C.c_int64,
             "rs_sas_block_grid": C.c_int64, "rs_layernorm_bwd_nparts": C.c_int64}
 
 _lib = None

@@ -432,17 +432,11 @@ hipError_t attn_lds_bwd(int64_t B, int64_t T, int64_t H, int64_t Dh, const void*
                         const uint64_t* seed_base, float* delta, hipStream_t s);
 
 // bf16 storage with T <= 256 takes the LDS-resident kernels (attention_lds.hip); fp32 (the
-// parity mode) and anything else the register/LDS-chunk kernels above.  RS_ATTN_LEGACY=1 forces
-// the latter (A/B testing).
+// parity mode) and anything else the register/LDS-chunk kernels above.
 static bool use_lds_path(int dtype, int64_t BH, int64_t T, int64_t Dh) {
-  static int legacy = -1;
-  if (legacy < 0) {
-    const char* e = getenv("RS_ATTN_LEGACY");
-    legacy = (e && e[0] == '1') ? 1 : 0;
-  }
   // the LDS kernels form the dropout-mask element index in 32 bits
   const bool idx32 = BH * T * (T + (T & 1)) < ((int64_t)1 << 32);
-  return !legacy && dtype == RS_DTYPE_BF16 && idx32 && attn_lds_supported(T, Dh);
+  return dtype == RS_DTYPE_BF16 && idx32 && attn_lds_supported(T, Dh);
 }
 
 static int check(int64_t B, int64_t T, int64_t H, int64_t Dh) {

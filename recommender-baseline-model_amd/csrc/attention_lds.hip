@@ -650,12 +650,6 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnLdsArgs& a, int64_t l
   APROF(6);
 }
 
-template <int DH>
-__global__ __launch_bounds__(NT) void attn_bwd_dq_lds_kernel(AttnLdsArgs a) {
-  KStampBegin stamp_(a.ks);
-  attn_bwd_dq_body<DH>(a, blockIdx.x + (int64_t)a.nsplit * blockIdx.y);
-}
-
 // ------------------------------------------------------------------ backward: dK, dV
 // Dropout multipliers of P[q0 + r*... ] for this lane's key ki and its 4 queries (row indices rq0 + r*Tp): the
 // pair hash of (query, key pair) is shared by the lanes of keys ki and ki^1 (lanes l and l^1), so each lane hashes
@@ -920,12 +914,6 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnLdsArgs& a, int64_t 
   APROF(9);
 }
 
-template <int DH>
-__global__ __launch_bounds__(NT) void attn_bwd_dkv_lds_kernel(AttnLdsArgs a) {
-  KStampEnd stamp_(a.ks);
-  attn_bwd_dkv_body<DH>(a, blockIdx.x + (int64_t)a.nsplit * blockIdx.y, false);
-}
-
 // both backward passes in one launch: workgroups [0, n_dq) are dQ ones (dispatched first), the rest dK/dV
 // ones, which take CUs as dQ workgroups retire -- their Q/dO staging overlaps other CUs' dQ compute instead
 // of following a launch boundary with the whole chip loading at once
@@ -959,12 +947,7 @@ static int pick_split(int64_t BH, int ntiles) {
 
 // backward: the merged launch runs 2 * nsplit * BH workgroups (dQ + dK/dV); keep them to one round on the
 // chip's 256 CUs (one workgroup each) so every dK/dV workgroup runs BESIDE the dQ ones, not after them
-static bool bwd_merged() {
-  static const bool m = [] { const char* e = getenv("RS_ATTN_BWD_MERGED"); return !e || e[0] != '0'; }();
-  return m;
-}
 static int pick_split_bwd(int64_t BH, int ntiles) {
-  if (!bwd_merged()) return pick_split(BH, ntiles);
   int s = 1;
   while (2 * BH * s * 2 <= 256 && s * 2 <= std::max(1, ntiles / 4)) s *= 2;
   return s;
@@ -1084,25 +1067,14 @@ static hipError_t bwd_t(AttnLdsArgs& a, hipStream_t s) {
   aq.use_plan = want && lds_q + ext_q <= 160 * 1024 && make_plan(aq, nq, false, DQ_SLOTS);
   akv.use_plan = want && lds_kv + ext_kv <= 160 * 1024 && make_plan(akv, nq, true, DKV_SLOTS);
   const size_t bq = lds_q + (aq.use_plan ? ext_q : 0), bkv = lds_kv + (akv.use_plan ? ext_kv : 0);
-  if (bwd_merged()) {
-    hipLaunchKernelGGL((attn_bwd_lds_kernel<DH>), dim3((unsigned)(2 * a.nsplit * a.B * a.H)), dim3(NT),
-                       std::max(bq, bkv), s, aq, akv);
-    return hipGetLastError();
-  }
-  hipLaunchKernelGGL((attn_bwd_dq_lds_kernel<DH>), dim3((unsigned)a.nsplit, (unsigned)(a.B * a.H)), dim3(NT), bq, s,
-                     aq);
-  hipLaunchKernelGGL((attn_bwd_dkv_lds_kernel<DH>), dim3((unsigned)a.nsplit, (unsigned)(a.B * a.H)), dim3(NT), bkv,
-                     s, akv);
+  hipLaunchKernelGGL((attn_bwd_lds_kernel<DH>), dim3((unsigned)(2 * a.nsplit * a.B * a.H)), dim3(NT),
+                     std::max(bq, bkv), s, aq, akv);
   return hipGetLastError();
 }
 
 template <int DH>
 static void set_lds_limits() {
   hipFuncSetAttribute((const void*)attn_fwd_lds_kernel<DH>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipFuncSetAttribute((const void*)attn_bwd_dq_lds_kernel<DH>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                      160 * 1024);
-  hipFuncSetAttribute((const void*)attn_bwd_dkv_lds_kernel<DH>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                      160 * 1024);
   hipFuncSetAttribute((const void*)attn_bwd_lds_kernel<DH>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 

@@ -283,26 +283,6 @@ int rs_embed_fwd(int dtype, int mode, const int64_t* ids, int64_t rows, int64_t 
                    : embed_fwd_t<float>(mode, ids, rows, T, table, pos, d, scale, drop_p, seed, seed_base, out, s));
 }
 
-int64_t rs_embed_count_parts(int dtype, int64_t rows, int64_t d) {
-  const int V = dtype == RS_DTYPE_BF16 ? Vec<__bf16>::N : Vec<float>::N;
-  return rows > 0 && d > 0 && d % V == 0 ? 4 * cdiv(rows * (d / V), 256) : 0;   // one per wave
-}
-
-int rs_embed_fwd_counted(int dtype, int mode, const int64_t* ids, int64_t rows, int64_t T, const void* table,
-                         const void* pos, int64_t d, float scale, float drop_p, uint64_t seed,
-                         const uint64_t* seed_base, void* out, const int64_t* count_ids, int* count_parts,
-                         void* stream) {
-  if (rows <= 0 || T <= 0 || rows % T || d <= 0 || !count_ids || !count_parts) return RS_ERR_ARG;
-  hipStream_t s = (hipStream_t)stream;
-  const hipError_t e =
-      dtype == RS_DTYPE_BF16
-          ? embed_fwd_t<__bf16>(mode, ids, rows, T, table, pos, d, scale, drop_p, seed, seed_base, out, s, count_ids,
-                                count_parts)
-          : embed_fwd_t<float>(mode, ids, rows, T, table, pos, d, scale, drop_p, seed, seed_base, out, s, count_ids,
-                               count_parts);
-  return e == hipErrorInvalidValue ? RS_ERR_UNSUPPORTED : (int)e;
-}
-
 int rs_embed_bwd(int dtype, int mode, const int64_t* ids, int64_t rows, int64_t T, const void* dx, int64_t d,
                  float scale, float drop_p, uint64_t seed, const uint64_t* seed_base, float* dtable, float* dpos,
                  int accumulate_pos, void* stream) {

@@ -5,8 +5,6 @@
 
 namespace gbf {
 
-int tile_override();
-
 int epi_class(const GemmArgs& a) {
   const rs_epilogue& e = a.epi;
   if (!a.vec_ok || e.alpha != 1.0f) return EC_GENERIC;
@@ -23,29 +21,8 @@ int epi_class(const GemmArgs& a) {
   return ec | (e.act << 8);
 }
 
-int tile_override() {
-  // RS_GEMM_TILE=<bm>x<bn> forces a tile for the generic / slab kernels (micro-benchmarking only)
-  static int t = -1;
-  if (t < 0) {
-    const char* env = getenv("RS_GEMM_TILE");
-    t = 0;
-    if (env) {
-      int bm = 0, bn = 0;
-      if (sscanf(env, "%dx%d", &bm, &bn) == 2) t = bm * 1000 + bn;
-    }
-  }
-  return t;
-}
-
 template <bool AK, bool BK, int EC>
 hipError_t launch_any(GemmArgs& a, hipStream_t s) {
-  switch (tile_override()) {
-    case 128128: return launch_cfg<AK, BK, 128, 128, EC>(a, s);
-    case 64128: return launch_cfg<AK, BK, 64, 128, EC>(a, s);
-    case 128064: return launch_cfg<AK, BK, 128, 64, EC>(a, s);
-    case 64064: return launch_cfg<AK, BK, 64, 64, EC>(a, s);
-    default: break;
-  }
   auto blocks = [&](int bm, int bn) { return cdiv(a.M, bm) * cdiv(a.N, bn) * a.split_k; };
   if (blocks(128, 128) >= 512) return launch_cfg<AK, BK, 128, 128, EC>(a, s);
   if (a.N >= 128 && blocks(64, 128) >= 512) return launch_cfg<AK, BK, 64, 128, EC>(a, s);

@@ -278,191 +278,9 @@ __global__ __launch_bounds__(256) void head_finish_kernel(int nblk, const float*
   head_stats(nblk, part, divisor, out, red);
 }
 
-// Forward and backward in ONE kernel (the fused training step): the loss's divisor -- the valid-position count --
-// is a function of the batch alone, counted by the embedding forward (count_parts, one int per workgroup), so each
-// row's gradient needs nothing from the other rows: f = LN(x) [saved: f], pl / nl, dpl = (sigmoid(pl) - 1) / div,
-// dnl = sigmoid(nl) / div on valid rows [saved], df = dpl E[pos] + dnl E[neg], dx = LN'(x, df), the LN affine
-// partials and the BCE partials (sp, sn, count) of the block.  The loss statistics are formed from those later by
-// one workgroup riding in the gradient tail's reduction launch (rs_wgrad_grouped_pos_stats) or by
-// head_finish_kernel.  (Measured alternatives: a last-workgroup-done form inside this kernel, 57 vs 15 us -- the
-// device-scope fences write back each XCD's L2; the finish kernel on the side queue, +4 us on the item chain.)  div = *divisor when given (data parallel: 1, the optimizer divides by the
-// all-reduced count) else the count.  Same math, same order per row as head_fwd_kernel + head_bwd_kernel.
-template <int D>
-__global__ __launch_bounds__(256) void head_fused_kernel(int64_t M, const bf16* __restrict__ x,
-                                                         const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                         float eps, const int* __restrict__ cnt_parts, int ncnt,
-                                                         const float* __restrict__ divisor, bf16* __restrict__ f,
-                                                         const bf16* __restrict__ E, const int64_t* __restrict__ pos,
-                                                         const int64_t* __restrict__ neg, float* __restrict__ pl,
-                                                         float* __restrict__ nl, float* __restrict__ dpl,
-                                                         float* __restrict__ dnl, bf16* __restrict__ dx,
-                                                         float* __restrict__ lnpart, float* __restrict__ part) {
-  constexpr int LPR = D / 8, RPP = 256 / LPR, NP = RB / RPP;
-  const int tid = threadIdx.x, sub = tid % LPR, c0 = sub * 8;
-  const int64_t row0 = (int64_t)blockIdx.x * RB;
-  __shared__ float red[8][256];
-  __shared__ float redl[3][4];
-  __shared__ int cw[4];
-  float gm[8], bt[8];
-  load_chunk<float>(gm, gamma + c0);
-  load_chunk<float>(gm + 4, gamma + c0 + 4);
-  load_chunk<float>(bt, beta + c0);
-  load_chunk<float>(bt + 4, beta + c0 + 4);
-  float xv[NP][8], ep[NP][8], en[NP][8];
-  bool vrow[NP];
-#pragma unroll
-  for (int k = 0; k < NP; ++k) {
-    const int64_t m0 = row0 + k * RPP + tid / LPR;
-    const int64_t m = m0 < M ? m0 : M - 1;
-    const int64_t ipos = pos[m];
-    vrow[k] = ipos != 0;
-    load_chunk<bf16>(xv[k], x + m * D + c0);
-    load_chunk<bf16>(ep[k], E + ipos * D + c0);
-    load_chunk<bf16>(en[k], E + neg[m] * D + c0);
-  }
-  // the divisor: the valid count from the embedding forward's parts (integers: any order, exact), or the caller's
-  float scale;
-  {
-    int c = 0;
-    const int n4 = ncnt >> 2;
-    for (int i = tid; i < n4; i += 256) {
-      const int4 v = reinterpret_cast<const int4*>(cnt_parts)[i];
-      c += v.x + v.y + v.z + v.w;
-    }
-    for (int i = 4 * n4 + tid; i < ncnt; i += 256) c += cnt_parts[i];
-    c = (int)wave_sum((float)c);   // exact: counts < 2^24
-    if ((tid & 63) == 0) cw[tid >> 6] = c;
-    __syncthreads();
-    const float cc = divisor ? *divisor : (float)(cw[0] + cw[1] + cw[2] + cw[3]);
-    scale = 1.f / cc;
-  }
-  float sp = 0.f, sn = 0.f, cnt = 0.f;
-  float pg[8], pb[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) pg[j] = pb[j] = 0.f;
-#pragma unroll
-  for (int k = 0; k < NP; ++k) {
-    const int64_t m = row0 + k * RPP + tid / LPR;
-    const bool valid = m < M;
-    // forward: last LayerNorm, the stored (bf16) features, tied logits
-    float s = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) s += xv[k][j];
-#pragma unroll
-    for (int o = LPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-    const float mu = s / (float)D;
-    float q = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float u = xv[k][j] - mu;
-      q += u * u;
-    }
-#pragma unroll
-    for (int o = LPR / 2; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
-    const float a = 1.0f / sqrtf(q / (float)D + eps);
-    float y[8];
-    float dp = 0.f, dn = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      y[j] = (xv[k][j] - mu) * a * gm[j] + bt[j];
-      y[j] = (float)(bf16)y[j];                // the logits read the stored (bf16) features
-      dp += y[j] * ep[k][j];
-      dn += y[j] * en[k][j];
-    }
-#pragma unroll
-    for (int o = LPR / 2; o > 0; o >>= 1) {
-      dp += __shfl_xor(dp, o, 64);
-      dn += __shfl_xor(dn, o, 64);
-    }
-    const float gp = valid && vrow[k] ? (sigmoidf(dp) - 1.f) * scale : 0.f;
-    const float gn = valid && vrow[k] ? sigmoidf(dn) * scale : 0.f;
-    if (valid) {
-      store_chunk<bf16>(f + m * D + c0, y);
-      if (sub == 0) {
-        pl[m] = dp;
-        nl[m] = dn;
-        dpl[m] = gp;
-        dnl[m] = gn;
-        if (vrow[k]) {
-          sp += softplus(-dp);
-          sn += softplus(dn);
-          cnt += 1.f;
-        }
-      }
-    }
-    // backward: df, LayerNorm backward (x as stored, the statistics just formed)
-    float u[8], gq[8], sg = 0.f, sgu = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float g = valid ? gp * ep[k][j] + gn * en[k][j] : 0.f;   // df
-      u[j] = xv[k][j] - mu;
-      gq[j] = g * gm[j];
-      pg[j] += g * (u[j] * a);
-      pb[j] += g;
-      sg += gq[j];
-      sgu += gq[j] * u[j];
-    }
-#pragma unroll
-    for (int o = LPR / 2; o > 0; o >>= 1) {
-      sg += __shfl_xor(sg, o, 64);
-      sgu += __shfl_xor(sgu, o, 64);
-    }
-    const float mg = sg / (float)D;
-    const float coef = a * a * a * sgu / (float)D;
-    float t[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) t[j] = a * (gq[j] - mg) - coef * u[j];
-    if (valid) store_chunk<bf16>(dx + m * D + c0, t);
-  }
-  // BCE partials of the block (lanes -> waves -> fixed sum)
-  sp = wave_sum(sp);
-  sn = wave_sum(sn);
-  cnt = wave_sum(cnt);
-  const int w = tid >> 6;
-  if ((tid & 63) == 0) {
-    redl[0][w] = sp;
-    redl[1][w] = sn;
-    redl[2][w] = cnt;
-  }
-  // affine partials of the block: RPP row groups combined in a fixed order
-  float* r = &red[0][0];   // [RPP][D] = 2048 floats
-  const int grp = tid / LPR;
-  for (int which = 0; which < 2; ++which) {
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 8; ++j) r[grp * D + c0 + j] = which == 0 ? pg[j] : pb[j];
-    __syncthreads();
-    if (tid < D) {
-      float s2 = 0.f;
-      for (int g = 0; g < RPP; ++g) s2 += r[g * D + tid];
-      lnpart[((int64_t)blockIdx.x * 2 + which) * D + tid] = s2;
-    }
-  }
-  if (tid < 3) part[blockIdx.x * 3 + tid] = redl[tid][0] + redl[tid][1] + redl[tid][2] + redl[tid][3];
-}
-
 }  // namespace hd
 
 extern "C" {
-
-int rs_sas_head_fused(int64_t M, int64_t d, const void* x, const float* ln_w, const float* ln_b, float eps,
-                      const int* count_parts, int64_t ncount, const float* divisor, void* f, const void* E,
-                      const int64_t* pos, const int64_t* neg, float* pl, float* nl, float* dpl, float* dnl, void* dx,
-                      float* lnpart, float* part, void* stream) {
-  if (M <= 0 || !count_parts || ncount <= 0) return RS_ERR_ARG;
-  const dim3 grid((unsigned)cdiv(M, hd::RB));
-  hipStream_t s = (hipStream_t)stream;
-#define HU(D)                                                                                                    \
-  hipLaunchKernelGGL(hd::head_fused_kernel<D>, grid, dim3(256), 0, s, M, (const __bf16*)x, ln_w, ln_b, eps,      \
-                     count_parts, (int)ncount, divisor, (__bf16*)f, (const __bf16*)E, pos, neg, pl, nl, dpl, dnl, \
-                     (__bf16*)dx, lnpart, part)
-  if (d == 64) HU(64);
-  else if (d == 128) HU(128);
-  else if (d == 256) HU(256);
-  else return RS_ERR_UNSUPPORTED;
-#undef HU
-  return (int)hipGetLastError();
-}
 
 int rs_sas_head_finish(int64_t nblk, const float* part, const float* divisor, float* out, void* stream) {
   if (nblk <= 0 || !part || !out) return RS_ERR_ARG;

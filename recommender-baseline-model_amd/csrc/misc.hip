@@ -324,23 +324,8 @@ int rs_adam_prepare(double* state, const float* hyper, const float* grad_divisor
   return (int)hipGetLastError();
 }
 
-// float4 groups in flight per thread (RS_ADAM_UNROLL, default 2) and the grid cap
-static int adam_unroll() {
-  static int u = -1;
-  if (u < 0) {
-    const char* e = getenv("RS_ADAM_UNROLL");
-    u = e ? atoi(e) : 2;
-    if (u != 1 && u != 2 && u != 4) u = 2;
-  }
-  return u;
-}
-#define ADAM_LAUNCH(BO, PR, ...)                                                                       \
-  do {                                                                                                 \
-    const int u_ = adam_unroll();                                                                      \
-    if (u_ == 1) hipLaunchKernelGGL((adam_step_kernel<BO, PR, 1>), __VA_ARGS__);                       \
-    else if (u_ == 4) hipLaunchKernelGGL((adam_step_kernel<BO, PR, 4>), __VA_ARGS__);                  \
-    else hipLaunchKernelGGL((adam_step_kernel<BO, PR, 2>), __VA_ARGS__);                               \
-  } while (0)
+// two float4 groups in flight per thread (1 and 4 measured slower)
+#define ADAM_LAUNCH(BO, PR, ...) hipLaunchKernelGGL((adam_step_kernel<BO, PR, 2>), __VA_ARGS__)
 
 int rs_adam_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, const double* state,
                  const float* hyper, int zero_grad, void* stream) {

@@ -1,9 +1,11 @@
 // Wave-resident row chains for the SASRec sublayers (bf16, gfx950): the kernels behind
 // rs_sas_block_in / rs_sas_block_out / rs_sas_block_out_bwd / rs_sas_block_in_bwd.
 //
-// Same math, saved tensors and dropout indices as rowfused.hip (the reference lines are
-// listed there: sas.py:73-76 and sas.py:75-84 with PointWiseFeedForward sas.py:8-24), laid
-// out for the CDNA4 execution model instead of a 64-row workgroup tile:
+// Everything in a SAS block except the attention core is row-local (BS/models/sas_model/sas.py:73-76 before the
+// core: Q = LN1(x), q = Q Wq^T + bq, kv = x Wkv^T + bkv; sas.py:75-84 after it: x1 = Q + O Wo^T + bo, z = LN2(x1),
+// h1 = relu(drop(z W1^T + b1)), x' = (drop(h1 W2^T + b2) + z) * (ids != 0), PointWiseFeedForward sas.py:8-24).
+// The saved tensors, their layout and every dropout index (m*d + n per site salt) are those of the generic
+// kernels (fp32 parity mode, other widths).  Laid out for the CDNA4 execution model:
 //
 //  * one workgroup per CU (NW = 8 waves) stages the block's three d x d weight matrices ONCE
 //    into LDS (110 KB at d = 128), then every wave runs its own 16-token chain with no
@@ -853,19 +855,6 @@ __global__ __launch_bounds__(NT) void block_out_bwd_kernel(OutBwdArgs a) {
   ln_partials<D>(red, a.part, tid);
 }
 
-// delta[m] = rowsum(a[m] * b[m]) over d bf16 columns, one wave per row (the row-fused fallback's delta)
-__global__ __launch_bounds__(256) void row_dot_kernel(const bf16* a, const bf16* b, int64_t M, int64_t d,
-                                                      float* delta) {
-  const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (m >= M) return;
-  float s = 0.f;
-  for (int64_t c = lane; c < d; c += 64) s = __builtin_fmaf((float)a[m * d + c], (float)b[m * d + c], s);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-  if (lane == 0) delta[m] = s;
-}
-
 struct InBwdArgs {
   int64_t M;
   const bf16* dq; const bf16* dkv; const bf16* dx1; const bf16* x;
@@ -961,46 +950,45 @@ static int launch_out(const OutArgs& a, int64_t d, void* stream) {
   return (int)hipGetLastError();
 }
 
-}  // namespace rc
-
-// rowfused.hip's 64-row-tile kernels (RS_ROWCHAIN=0)
-int rf_sas_block_in(int64_t M, int64_t d, const void* x, int64_t ldx, const float* ln_w, const float* ln_b, float eps,
-                    void* Q, float* mean, float* rstd, const void* Wq, const float* bq, void* q, const void* Wkv,
-                    const float* bkv, void* kv, void* stream);
-int rf_sas_block_out(int64_t M, int64_t d, const void* o, const void* Q, const void* Wo, const float* bo, void* x1,
-                     const float* ln_w, const float* ln_b, float eps, void* z, float* mean, float* rstd,
-                     const void* W1, const float* b1, void* h1, const void* W2, const float* b2, void* xn,
-                     const int64_t* ids, float drop_p, uint64_t salt1, uint64_t salt2, const uint64_t* seed_base,
-                     void* stream);
-int rf_sas_block_out_bwd(int64_t M, int64_t d, const void* dxn, const int64_t* ids, const void* h1, const void* x1,
-                         const float* mean2, const float* rstd2, const float* ln_w, const void* W2T, const void* W1T,
-                         const void* WoT, void* dy2, void* da1, void* dx1, void* dout, float* part, float drop_p,
-                         uint64_t salt1, uint64_t salt2, const uint64_t* seed_base, void* stream);
-int rf_sas_block_in_bwd(int64_t M, int64_t d, const void* dq, const void* dkv, const void* dx1, const void* x,
-                        const float* mean1, const float* rstd1, const float* ln_w, const void* WinT, void* dx,
-                        float* part, void* stream);
-
-static bool use_chain() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("RS_ROWCHAIN");
-    v = (e && e[0] == '0') ? 0 : 1;
+// ------------------------------------------------------------------ batched bf16 transpose
+// dst[m][c][r] = src[m][r][c] for the SAS block weight matrices (desc: rows, cols, src_off, lds, dst_off, ldd in
+// elements; 64x64 tiles through LDS): the [in][out] copies the backward kernels stage as their A operands
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const int64_t* __restrict__ desc, const __bf16* src,
+                                                             __bf16* dst) {
+  __shared__ __bf16 t[64][66];
+  const int64_t* dsc = desc + 6 * blockIdx.y;
+  const int64_t rows = dsc[0], cols = dsc[1];
+  const int64_t tc = cdiv(cols, 64);
+  const int64_t tr = blockIdx.x / tc, tcc = blockIdx.x % tc;
+  if (tr * 64 >= rows) return;
+  const __bf16* sp = src + dsc[2];
+  __bf16* dp = dst + dsc[4];
+  const int64_t lds = dsc[3], ldd = dsc[5];
+  for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+    const int r = e / 64, c = e % 64;
+    const int64_t gr = tr * 64 + r, gc = tcc * 64 + c;
+    t[r][c] = (gr < rows && gc < cols) ? sp[gr * lds + gc] : (__bf16)0.f;
   }
-  return v == 1;
+  __syncthreads();
+  for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+    const int c = e / 64, r = e % 64;
+    const int64_t gr = tr * 64 + r, gc = tcc * 64 + c;
+    if (gr < rows && gc < cols) dp[gc * ldd + gr] = t[r][c];
+  }
 }
+
+}  // namespace rc
 
 extern "C" {
 
 int64_t rs_sas_block_parts(int64_t M) {
   if (M <= 0) return 0;
-  return use_chain() ? rc::grid_for(M) : cdiv(M, 64);
+  return rc::grid_for(M);
 }
 
 int rs_sas_block_in(int64_t M, int64_t d, const void* x, int64_t ldx, const float* ln_w, const float* ln_b, float eps,
                     void* Q, float* mean, float* rstd, const void* Wq, const float* bq, void* q, const void* Wkv,
                     const float* bkv, void* kv, void* stream) {
-  if (!use_chain())
-    return rf_sas_block_in(M, d, x, ldx, ln_w, ln_b, eps, Q, mean, rstd, Wq, bq, q, Wkv, bkv, kv, stream);
   if (M <= 0 || ldx % 8) return RS_ERR_ARG;
   rc::InArgs a = {M, (const __bf16*)x, ldx, ln_w, ln_b, eps, (__bf16*)Q, mean, rstd, (const __bf16*)Wq, bq,
                   (__bf16*)q, (const __bf16*)Wkv, bkv, (__bf16*)kv};
@@ -1027,18 +1015,7 @@ int rs_sas_block_in_embed(int64_t M, int64_t d, const int64_t* ids, int64_t T, c
                           const float* bkv, void* kv, void* stream) {
   if (M <= 0 || T <= 0 || M % T || !ids || !item_emb || !pos_emb || !x0 || !count_ids != !count_parts)
     return RS_ERR_ARG;
-  const bool vec = ((uintptr_t)item_emb | (uintptr_t)pos_emb | (uintptr_t)x0) % 16 == 0;
-  if (!use_chain() || !vec || (d != 64 && d != 128)) {   // the two stages one after the other (same results)
-    if (count_ids) {
-      if (int e = rs_embed_fwd_counted(RS_DTYPE_BF16, 0, ids, M, T, item_emb, pos_emb, d, scale, drop_p, salt,
-                                       seed_base, x0, count_ids, count_parts, stream))
-        return e;
-    } else if (int e = rs_embed_fwd(RS_DTYPE_BF16, 0, ids, M, T, item_emb, pos_emb, d, scale, drop_p, salt, seed_base,
-                                    x0, stream)) {
-      return e;
-    }
-    return rs_sas_block_in(M, d, x0, d, ln_w, ln_b, eps, Q, mean, rstd, Wq, bq, q, Wkv, bkv, kv, stream);
-  }
+  if (((uintptr_t)item_emb | (uintptr_t)pos_emb | (uintptr_t)x0) % 16 || (d != 64 && d != 128)) return RS_ERR_ARG;
   rc::InArgs a = {M, (const __bf16*)x0, d, ln_w, ln_b, eps, (__bf16*)Q, mean, rstd, (const __bf16*)Wq, bq,
                   (__bf16*)q, (const __bf16*)Wkv, bkv, (__bf16*)kv,
                   rc::EmbIn{ids, (const __bf16*)item_emb, (const __bf16*)pos_emb, T, scale, drop_p, salt, seed_base,
@@ -1060,9 +1037,6 @@ int rs_sas_block_out(int64_t M, int64_t d, const void* o, const void* Q, const v
                      const void* W1, const float* b1, void* h1, const void* W2, const float* b2, void* xn,
                      const int64_t* ids, float drop_p, uint64_t salt1, uint64_t salt2, const uint64_t* seed_base,
                      void* stream) {
-  if (!use_chain())
-    return rf_sas_block_out(M, d, o, Q, Wo, bo, x1, ln_w, ln_b, eps, z, mean, rstd, W1, b1, h1, W2, b2, xn, ids,
-                            drop_p, salt1, salt2, seed_base, stream);
   if (M <= 0) return RS_ERR_ARG;
   rc::OutArgs a = {M, (const __bf16*)o, (const __bf16*)Q, (const __bf16*)Wo, bo, (__bf16*)x1, ln_w, ln_b, eps,
                    (__bf16*)z, mean, rstd, (const __bf16*)W1, b1, (__bf16*)h1, (const __bf16*)W2, b2, (__bf16*)xn,
@@ -1081,7 +1055,7 @@ int rs_sas_block_out_head(int64_t M, int64_t d, const void* o, const void* Q, co
                           const float* divisor, void* f, float* pl, float* nl, float* dpl, float* dnl, void* dx,
                           float* lnpart, float* part, void* stream) {
   if (M <= 0 || !E || !pos || !neg || !count_parts || ncount <= 0 || !f || !dx || !lnpart || !part) return RS_ERR_ARG;
-  if (!use_chain() || (d != 64 && d != 128)) return RS_ERR_UNSUPPORTED;
+  if (d != 64 && d != 128) return RS_ERR_UNSUPPORTED;
   rc::OutArgs a = {M, (const __bf16*)o, (const __bf16*)Q, (const __bf16*)Wo, bo, (__bf16*)x1, ln_w, ln_b, eps,
                    (__bf16*)z, mean, rstd, (const __bf16*)W1, b1, (__bf16*)h1, (const __bf16*)W2, b2, (__bf16*)xn,
                    ids, drop_p, salt1, salt2, seed_base,
@@ -1104,14 +1078,6 @@ int rs_sas_block_out_bwd_delta(int64_t M, int64_t d, const void* dxn, const int6
                                void* dout, float* part, float drop_p, uint64_t salt1, uint64_t salt2,
                                const uint64_t* seed_base, const void* o, float* delta, void* stream) {
   if (!o != !delta) return RS_ERR_ARG;
-  if (!use_chain()) {
-    const int r = rf_sas_block_out_bwd(M, d, dxn, ids, h1, x1, mean2, rstd2, ln_w, W2T, W1T, WoT, dy2, da1, dx1, dout,
-                                       part, drop_p, salt1, salt2, seed_base, stream);
-    if (r || !delta) return r;
-    hipLaunchKernelGGL(rc::row_dot_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
-                       (const __bf16*)dout, (const __bf16*)o, M, d, delta);
-    return (int)hipGetLastError();
-  }
   if (M <= 0) return RS_ERR_ARG;
   rc::OutBwdArgs a = {M, (const __bf16*)dxn, ids, (const __bf16*)h1, (const __bf16*)x1, mean2, rstd2, ln_w,
                       (const __bf16*)W2T, (const __bf16*)W1T, (const __bf16*)WoT, (__bf16*)dy2, (__bf16*)da1,
@@ -1133,8 +1099,6 @@ int rs_sas_block_out_bwd_delta(int64_t M, int64_t d, const void* dxn, const int6
 int rs_sas_block_in_bwd(int64_t M, int64_t d, const void* dq, const void* dkv, const void* dx1, const void* x,
                         const float* mean1, const float* rstd1, const float* ln_w, const void* WinT, void* dx,
                         float* part, void* stream) {
-  if (!use_chain())
-    return rf_sas_block_in_bwd(M, d, dq, dkv, dx1, x, mean1, rstd1, ln_w, WinT, dx, part, stream);
   if (M <= 0) return RS_ERR_ARG;
   rc::InBwdArgs a = {M, (const __bf16*)dq, (const __bf16*)dkv, (const __bf16*)dx1, (const __bf16*)x, mean1, rstd1,
                      ln_w, (const __bf16*)WinT, 3 * d, (__bf16*)dx, part};
@@ -1149,6 +1113,14 @@ int rs_sas_block_in_bwd(int64_t M, int64_t d, const void* dq, const void* dkv, c
   } else {
     return RS_ERR_UNSUPPORTED;
   }
+  return (int)hipGetLastError();
+}
+
+int rs_transpose_bf16(int64_t nmat, const int64_t* desc, int64_t max_tiles, const void* src, void* dst,
+                      void* stream) {
+  if (nmat <= 0 || max_tiles <= 0) return RS_ERR_ARG;
+  hipLaunchKernelGGL(rc::transpose_bf16_kernel, dim3((unsigned)max_tiles, (unsigned)nmat), dim3(256), 0,
+                     (hipStream_t)stream, desc, (const __bf16*)src, (__bf16*)dst);
   return (int)hipGetLastError();
 }
 

@@ -22,7 +22,6 @@ rs_gather_rows), runs the vocabulary GEMM + CE on those rows only, and scatters
 the hidden-state gradient back (rs_scatter_rows).
 """
 import math
-import os
 import random
 
 import numpy as np
@@ -257,8 +256,7 @@ class BERTEngine:
         wat = self.ws.get("attn", (B * H * T,), torch.float32)
         # bf16: every block weight gradient is deferred into ONE grouped launch + ONE reduction
         # (rs_wgrad_grouped, wgrad.hip) after the last block's input gradient
-        grouped = (self.dt == torch.bfloat16 and self.qkv_fused and d % 64 == 0 and Fd % 64 == 0
-                   and os.environ.get("RS_BERT_UNGROUPED", "0") != "1")
+        grouped = self.dt == torch.bfloat16 and self.qkv_fused and d % 64 == 0 and Fd % 64 == 0
         probs = []
         ln_segs = []
 
@@ -377,7 +375,7 @@ class BERTEngine:
             ops.wgrad_grouped(chunk, M, rows, wslab, extra=ln_segs if c == 0 else ())
 
     def _det_table(self):
-        return self.dt == torch.bfloat16 and self.d in (64, 128, 256) and os.environ.get("RS_BERT_ATOMIC_TABLE") != "1"
+        return self.dt == torch.bfloat16 and self.d in (64, 128, 256)
 
     def _token_index(self, ids, side=True):
         """rs_item_index_build over the batch's token ids (the token-table gradient's inverted index); on a
@@ -403,9 +401,6 @@ class BERTEngine:
         """rows per split of the grouped weight-gradient launch: about one and a half 128x128-tile workgroups
         per CU in total (cfg3: 192 tiles x 2 splits; 4 splits measured 156 against 153 us for the launch, 1 split
         219 us)."""
-        env = os.environ.get("RS_WGRAD_ROWS")
-        if env:
-            return int(env)
         splits = max(1, round(384 / tiles))
         return max(64, -(-(-(-M // splits)) // 64) * 64)
 
@@ -455,16 +450,16 @@ class BERTEngine:
         if getattr(self, "vocab_shard", None) is not None:
             return self._sharded_head_and_backward(s, xL, hl, lab, idx, rank, cnt, labels, cap, loss_out, grad, split)
         ops.gather_rows(xL, idx, cnt, cap, hl, labels, lab)
-        head = os.environ.get("RS_BERT_VOCAB_HEAD", "tile")
-        if self.dt == torch.bfloat16 and head == "tile" and ops.vocab_head_supported(d):
+        if self.dt == torch.bfloat16 and ops.vocab_head_supported(d):
             # vocabulary-tile-stationary kernels (vocab_head.hip): logits never materialised
             wce = self.ws.get("vce", (ops.vocab_ce_ws_numel(cap, self.V1),), torch.float32)
             ops.vocab_head_fwd(hl, self.W("out.weight"), self.Wf("out.bias"), lab, wce, loss_out, rows_dev=cnt)
             count = global_count(loss_out[1:2])
             dl = self.ws.get("dlogits", (cap, self.V1p), self.dt)[:, :self.V1]
             ops.vocab_head_bwd(hl, self.W("out.weight"), self.Wf("out.bias"), lab, wce, count, dl, rows_dev=cnt)
-        elif self.dt == torch.bfloat16 and head != "materialised":
-            # logits never materialised: GEMM + online-softmax partials, then GEMM + dlogits (vocab_ce.hip)
+        elif self.dt == torch.bfloat16:
+            # widths the tile head does not cover: logits never materialised either -- GEMM + online-softmax
+            # partials, then GEMM + dlogits (vocab_ce.hip)
             wce = self.ws.get("vce", (ops.vocab_ce_ws_numel(cap, self.V1),), torch.float32)
             ops.vocab_ce_fwd(hl, self.W("out.weight"), self.Wf("out.bias"), lab, wce, loss_out, rows_dev=cnt)
             count = global_count(loss_out[1:2])

@@ -19,7 +19,6 @@ forward (per step)                      kernels (include/recsys_hip.h)
 backward: the mirror image (rs_*_bwd, dgrad/wgrad GEMMs, split-K slabs).
 """
 import math
-import os
 
 import torch
 import torch.nn as nn
@@ -190,10 +189,10 @@ class SASEngine:
     def forward(self, ids, pos, neg, training, need_logits=True, clone_seed=True, fuse_head=False,
                 head_divisor=None):
         """fuse_head (the fused training step, whose backward forms the BCE gradient itself): the head's forward
-        and backward run as one pass per token -- inside the last block's output kernel (rs_sas_block_out_head),
-        or else as one kernel in backward (rs_sas_head_fused); the returned pl / nl are filled by then.  The
-        embedding stage counts the valid positions (the BCE divisor) for it; head_divisor (device scalar, data
-        parallel: 1) replaces that count and must be the divisor later passed to backward."""
+        and backward run as one pass per token inside the last block's output kernel (rs_sas_block_out_head); the
+        returned pl / nl are filled by then.  The first block's input kernel counts the valid positions (the BCE
+        divisor) for it; head_divisor (device scalar, data parallel: 1) replaces that count and must be the divisor
+        later passed to backward."""
         B, T = ids.shape
         M, d, H, Dh, L = B * T, self.d, self.H, self.Dh, self.L
         p = self.p if training else 0.0
@@ -212,21 +211,17 @@ class SASEngine:
             fork = torch.cuda.Event()
             fork.record()
         x = e("x0", (M, d))
-        fuse_head = fuse_head and side and need_logits and os.environ.get("RS_SAS_HEAD_FUSED", "1") != "0"
-        # the embedding stage inside the first block's input kernel (rs_sas_block_in_embed, one launch)
-        emb_in = fused and os.environ.get("RS_SAS_EMBED_FUSED", "1") != "0"
-        ncnt = (ops.sas_block_in_count_parts(M) if emb_in else ops.embed_count_parts(self.W("item_emb.weight"), M)) \
-            if fuse_head else 0
+        # the fused training step: the head's forward and backward inside the last block's output kernel, the
+        # embedding stage inside the first block's input kernel, which counts the valid positions (the BCE divisor)
+        fuse_head = fuse_head and side and need_logits
         cntp = None
-        if ncnt > 0:
-            cntp = self.ws.get("cntp", (ncnt,), torch.int32)
+        if fuse_head:
+            cntp = self.ws.get("cntp", (ops.sas_block_in_count_parts(M),), torch.int32)
             s["cntp"] = cntp
-        if emb_in:
+        emb = None
+        if fused:
             emb = (ids, T, self.W("item_emb.weight"), self.W("pos_emb.weight"), math.sqrt(d), p, self.salt["emb"], sb,
                    x, pos if cntp is not None else None, cntp)
-        elif cntp is not None:
-            ops.embed_fwd_counted(0, ids, T, self.W("item_emb.weight"), self.W("pos_emb.weight"), math.sqrt(d), p,
-                                  self.salt["emb"], sb, x, pos, cntp)
         else:
             ops.embed_fwd(0, ids, T, self.W("item_emb.weight"), self.W("pos_emb.weight"), math.sqrt(d), p,
                           self.salt["emb"], sb, x)
@@ -236,11 +231,8 @@ class SASEngine:
                 # issued after the first forward launch: in the captured graph the forward chain is then the
                 # first child of the step's root and keeps the launch queue; the side branch gets the second
                 s["side"] = self._side_prologue(ids, pos, neg, after=fork)
-        if not emb_in:
-            after_first()
         head = None
-        if cntp is not None and os.environ.get("RS_ROWCHAIN", "1") != "0" and \
-                os.environ.get("RS_SAS_HEAD_IN_BLOCK", "1") != "0":
+        if cntp is not None:
             # the head inside the last block's output kernel: its outputs, per-workgroup partials
             Gb = ops.sas_block_grid(M)
             f32 = torch.float32
@@ -252,7 +244,7 @@ class SASEngine:
                     self.Wf("last_layernorm.bias"), cntp, head_divisor, s["f"], s["pl"], s["nl"], s["dpl"], s["dnl"],
                     s["hdx"], s["lnh"], s["headp"])
         if fused:
-            x = self._forward_blocks_fused(s, x, emb=emb if emb_in else None, after_first=after_first, head=head)
+            x = self._forward_blocks_fused(s, x, emb=emb, after_first=after_first, head=head)
         else:
             for i in range(L):
                 pre = f"attention_layers.{i}."
@@ -287,10 +279,6 @@ class SASEngine:
             return s["pl"], s["nl"], s
         f, muf, rf = e("f", (M, d)), e("mu", (M,), torch.float32), e("r", (M,), torch.float32)
         s.update(xL=x, f=f, muf=muf, rf=rf)
-        if "cntp" in s:
-            pl, nl = e("pl", (B, T), torch.float32), e("nl", (B, T), torch.float32)
-            s.update(pl=pl, nl=nl, headp=e("headp", (3 * (-(-M // 64)),), torch.float32))
-            return pl, nl, s
         if fused and need_logits:
             # last LayerNorm + tied sampled logits + BCE partial sums in one kernel (head.hip)
             pl, nl = e("pl", (B, T), torch.float32), e("nl", (B, T), torch.float32)
@@ -401,14 +389,6 @@ class SASEngine:
                 nb = s["headp"].numel() // 3
                 if loss_out is not None:
                     stats = (s["headp"], divisor, loss_out) + ((aux_out,) if aux_out is not None else ())
-            elif dpl is None and "cntp" in s:
-                # the head's forward and backward in one kernel; the loss statistics (one workgroup) ride in the
-                # gradient tail's reduction launch
-                dpl, dnl = e("dpl", (B, T), torch.float32), e("dnl", (B, T), torch.float32)
-                ops.sas_head_fused(s["xL"], gl, self.Wf("last_layernorm.bias"), LN_EPS, s["cntp"], divisor, s["f"], E,
-                                   s["pos"], s["neg"], s["pl"], s["nl"], dpl, dnl, dx, lnh, s["headp"])
-                if loss_out is not None:
-                    stats = (s["headp"], divisor, loss_out) + ((aux_out,) if aux_out is not None else ())
             elif dpl is None:
                 dpl, dnl = e("dpl", (B, T), torch.float32), e("dnl", (B, T), torch.float32)
                 ops.sas_head_bwd(s["headp"], divisor, loss_out, s["pl"], s["nl"], None, None, dpl, dnl, s["pos"],
@@ -417,41 +397,23 @@ class SASEngine:
                 ops.sas_head_bwd(None, None, None, None, None, dpl, dnl, None, None, s["pos"], s["neg"], E, s["xL"],
                                  gl, s["muf"], s["rf"], dx, lnh)
             segs = ops.ln_partial_segments(lnh, M, d, G("last_layernorm.weight"), G("last_layernorm.bias"), nb=nb)
-            # the item table's gradient: "side" (default) = rs_item_grad on the side queue beside the grouped
-            # weight gradients; "fused" = inside those launches on this queue (rs_wgrad_grouped_items; measured
-            # 0.367 vs 0.356 ms/step at cfg2: the item chunks queue behind the weight-gradient tiles); "serial"
-            tail_mode = os.environ.get("RS_SAS_GRAD_TAIL", "side")
-            side = tail_mode == "side"
-            if self._side_refreshed or not side:
+            # the item table's gradient (rs_item_grad, ~40 us) runs on the side stream beside the grouped weight
+            # gradients (both latency-bound; measured: inside those launches on one queue 0.367 vs 0.356 ms/step at
+            # cfg2, the item chunks queue behind the weight-gradient tiles); the positional table's gradient and the
+            # head's loss statistics ride in the grouped reduction's launch on the main one, so both branches end
+            # together and the join's cross-queue latency is hidden
+            if self._side_refreshed:
                 # the blocks' backward reads the transposed weights the side branch wrote this step (otherwise
-                # the previous step's optimizer wrote them), the item gradient on the main stream the index
+                # the previous step's optimizer wrote them)
                 torch.cuda.current_stream().wait_event(ev)
 
             def item_grads(dx):
                 ops.item_grad(iws, 3, M, dx, math.sqrt(d), p, self.salt["emb"], sb, s["f"], dpl, dnl,
                               G("item_emb.weight"))
-            # the item table's gradient (rs_item_grad, ~42 us beside the weight gradients) on the side stream;
-            # the positional table's (10 us) after the weight gradients on the main one: the two branches then
-            # end together and the join's cross-queue latency is hidden
-            fused_items = (lambda dx: (iws, 3, M, dx, math.sqrt(d), p, self.salt["emb"], sb, s["f"], dpl, dnl,
-                                       G("item_emb.weight"))) if tail_mode == "fused" else None
-            # the positional table's gradient rides in the grouped reduction's launch (RS_SAS_POS_MERGED=0: its
-            # own launch after it)
-            pos_merged = fused_items is None and os.environ.get("RS_SAS_POS_MERGED", "1") != "0"
-            pos_args = ((lambda dx: (ids, T, dx, p, self.salt["emb"], sb, G("pos_emb.weight")) + stats) if pos_merged
-                        else None)
-            dx = self._backward_blocks_fused(s, dx, grad, segs, tail=item_grads if side else None, items=fused_items,
-                                             pos=pos_args)
-            if not pos_merged:
-                ops.embed_bwd(0, ids, T, dx, math.sqrt(d), p, self.salt["emb"], sb, None, G("pos_emb.weight"))
-                if stats:
-                    ops.sas_head_finish(*stats[:3])
-                    if len(stats) > 3:
-                        stats[3].copy_(stats[2][0:2])
-            if side:
-                torch.cuda.current_stream().wait_event(self._tail_join)
-            elif tail_mode != "fused":
-                item_grads(dx)
+            dx = self._backward_blocks_fused(s, dx, grad, segs, tail=item_grads,
+                                             pos=lambda dx: (ids, T, dx, p, self.salt["emb"], sb,
+                                                             G("pos_emb.weight")) + stats)
+            torch.cuda.current_stream().wait_event(self._tail_join)
             if split is not None:
                 split("dense")          # every parameter gradient is final (data-parallel overlap)
             return len(stats) > 3
@@ -545,14 +507,14 @@ class SASEngine:
         ops.transpose_bf16(self._wT_desc, self._wT_tiles, self.flat.bf16, self._wT)
         return self._wT
 
-    def _backward_blocks_fused(self, s, dx, grad, extra_segs=(), tail=None, items=None, pos=None):
+    def _backward_blocks_fused(self, s, dx, grad, extra_segs=(), tail=None, pos=None):
         """SAS blocks' backward with rs_sas_block_out_bwd / rs_sas_block_in_bwd (rowfused.hip) for the
         row-local chains; then ALL ten weight gradients and the four LayerNorm affine partial sets in
         one grouped GEMM launch + one grouped reduction (rs_wgrad_grouped, wgrad.hip).  Returns the
         gradient at the embedding output.  tail(dx): work on that gradient alone (the item table's
         gradient), issued on the side stream so it runs beside the grouped weight-gradient launch (both are
-        latency-bound); the caller joins self._tail_join.  items(dx): item_grad's arguments, run inside the grouped
-        weight-gradient launches instead (ops.wgrad_grouped items=)."""
+        latency-bound); the caller joins self._tail_join.  pos(dx): the positional table's gradient (and the head's
+        loss statistics) in the grouped reduction's launch (ops.wgrad_grouped pos=)."""
         B, T, p, ids, sb = s["B"], s["T"], s["p"], s["ids"], s["sb"]
         M, d, H, Dh, L = B * T, self.d, self.H, self.Dh, self.L
         e = self._buf
@@ -611,8 +573,7 @@ class SASEngine:
         # the grouped launch is captured BEFORE the side branch: a HIP graph keeps a node's first child on its
         # queue, so the weight gradients follow the blocks' backward with no cross-queue hop (side branch
         # first: 11 us of fork latency before rs_wgrad_grouped and 11 us of join latency before Adam)
-        ops.wgrad_grouped(probs, M, rows, wslab, extra=segs, items=items(dx) if items is not None else None,
-                          pos=pos(dx) if pos is not None else None)
+        ops.wgrad_grouped(probs, M, rows, wslab, extra=segs, pos=pos(dx) if pos is not None else None)
         if tail is not None:
             self._side.wait_event(fork)
             with torch.cuda.stream(self._side):
@@ -626,9 +587,6 @@ class SASEngine:
     def _wgrad_rows(M, tiles):
         """rows per split of the grouped weight-gradient launch: ~256 workgroups (the 128x128-tile kernel
         runs one per CU), fewer splits also shrink the partial slab the reduction reads."""
-        env = os.environ.get("RS_WGRAD_ROWS")
-        if env:
-            return int(env)
         splits = max(1, 256 // tiles)
         return max(64, -(-(-(-M // splits)) // 64) * 64)
 

@@ -221,20 +221,6 @@ def embed_fwd(mode, ids, T, table, pos, scale, drop_p, seed, seed_base, out):
          seed, ptr(seed_base), ptr(out), stream())
 
 
-def embed_count_parts(table, rows):
-    """int32 partial counts rs_embed_fwd_counted writes for `rows` ids of width table.shape[1] (0: unsupported)."""
-    return int(_lib.lib().rs_embed_count_parts(dtype_code(table), rows, table.shape[1]))
-
-
-def embed_fwd_counted(mode, ids, T, table, pos, scale, drop_p, seed, seed_base, out, count_ids, count_parts):
-    rows = ids.numel()
-    d = table.shape[1]
-    assert count_parts.dtype == torch.int32 and count_parts.numel() >= embed_count_parts(table, rows)
-    assert count_ids.dtype == torch.int64 and count_ids.numel() == rows
-    call("rs_embed_fwd_counted", dtype_code(table), mode, ptr(ids), rows, T, ptr(table), ptr(pos), d, scale, drop_p,
-         seed, ptr(seed_base), ptr(out), ptr(count_ids), ptr(count_parts), stream())
-
-
 def embed_bwd(mode, ids, T, dx, scale, drop_p, seed, seed_base, dtable, dpos, accumulate_pos=True):
     rows = ids.numel()
     d = dx.shape[-1]
@@ -475,7 +461,7 @@ def seed_advance(seed_base):
 # ---- fused SAS sublayers (rowfused.hip) ----------------------------------------------------
 def sas_block_fused_ok(d, dtype):
     """rs_sas_block_in/out cover bf16 with d in {64, 128}; anything else runs the unfused kernels."""
-    return dtype == torch.bfloat16 and d in (64, 128) and os.environ.get("RS_SAS_UNFUSED", "0") != "1"
+    return dtype == torch.bfloat16 and d in (64, 128)
 
 
 def sas_block_in(x, ln_w, ln_b, eps, Q, mean, rstd, Wq, bq, q, Wkv, bkv, kv):
@@ -585,17 +571,15 @@ def _segments(segs):
     return arr
 
 
-def wgrad_grouped(problems, M, rows_per_split, slab, extra=(), items=None, pos=None):
+def wgrad_grouped(problems, M, rows_per_split, slab, extra=(), pos=None):
     ev = _ev_begin("wgrad_grouped")
-    _wgrad_grouped(problems, M, rows_per_split, slab, extra, items, pos)
+    _wgrad_grouped(problems, M, rows_per_split, slab, extra, pos)
     _ev_end(ev)
 
 
-def _wgrad_grouped(problems, M, rows_per_split, slab, extra=(), items=None, pos=None):
+def _wgrad_grouped(problems, M, rows_per_split, slab, extra=(), pos=None):
     """problems: [(dY, X, dW, db|None)] with dW [N][K] fp32 (+=); extra: reduce segments
-    (src, stride, splits, n, out) summed (+=) in the same reduction launch.  items: item_grad's arguments
-    (ws, nsrc, rows, dx, scale, drop_p, salt, seed_base, f, w1, w2, dtable) -- that gradient then shares the two
-    launches (rs_wgrad_grouped_items).  pos: (ids, T, dx, drop_p, salt, seed_base, dpos) -- the SAS positional
+    (src, stride, splits, n, out) summed (+=) in the same reduction launch.  pos: (ids, T, dx, drop_p, salt, seed_base, dpos) -- the SAS positional
     table's gradient (embed_bwd mode 0, scale 1, +=) then rides in the reduction launch (rs_wgrad_grouped_pos);
     pos + (head_part, divisor, loss_out): the SAS head's loss statistics too (rs_wgrad_grouped_pos_stats)."""
     arr = (_lib.WgradProblem * len(problems))()
@@ -605,7 +589,6 @@ def _wgrad_grouped(problems, M, rows_per_split, slab, extra=(), items=None, pos=
         arr[i] = _lib.WgradProblem(ptr(dY), ld(dY), ptr(X), ld(X), N, K, ptr(dW), ptr(db) if db is not None else None)
     segs = _segments(list(extra))
     if pos is not None:
-        assert items is None
         ids, T, dx, drop_p, salt, seed_base, dpos, *st = pos
         if st:
             hp, hdiv, lout, *aux = st
@@ -615,14 +598,6 @@ def _wgrad_grouped(problems, M, rows_per_split, slab, extra=(), items=None, pos=
             return
         call("rs_wgrad_grouped_pos", len(problems), arr, M, rows_per_split, ptr(slab), slab.numel(), len(extra),
              segs, ptr(ids), T, ptr(dx), dx.shape[-1], drop_p, salt, ptr(seed_base), ptr(dpos), stream())
-        return
-    if items is not None:
-        ws, nsrc, rows, dx, scale, drop_p, salt, seed_base, f, w1, w2, dtable = items
-        table_rows, d = dtable.shape
-        call("rs_wgrad_grouped_items", len(problems), arr, M, rows_per_split, ptr(slab), slab.numel(), len(extra),
-             segs, ptr(ws), nsrc, rows, table_rows, d, ptr(dx), scale, drop_p, salt, ptr(seed_base),
-             ptr(f) if f is not None else None, ptr(w1) if w1 is not None else None,
-             ptr(w2) if w2 is not None else None, ptr(dtable), stream())
         return
     call("rs_wgrad_grouped", len(problems), arr, M, rows_per_split, ptr(slab), slab.numel(), len(extra), segs,
          stream())
@@ -677,15 +652,6 @@ def sas_head_bwd(part, divisor, out, pl, nl, dpl_in, dnl_in, dpl, dnl, pos, neg,
     call("rs_sas_head_bwd", M, d, ptr(part), ptr(divisor), ptr(out), ptr(pl), ptr(nl), ptr(dpl_in), ptr(dnl_in),
          ptr(dpl), ptr(dnl), ptr(pos), ptr(neg), ptr(E), ptr(x), ptr(ln_w), ptr(mean), ptr(rstd), ptr(dx),
          ptr(lnpart), stream())
-
-
-def sas_head_fused(x, ln_w, ln_b, eps, count_parts, divisor, f, E, pos, neg, pl, nl, dpl, dnl, dx, lnpart, part):
-    M, d = x.shape
-    assert part.numel() >= 3 * ((M + 63) // 64) and lnpart.numel() >= 2 * d * ((M + 63) // 64)
-    assert count_parts.dtype == torch.int32 and count_parts.data_ptr() % 16 == 0
-    call("rs_sas_head_fused", M, d, ptr(x), ptr(ln_w), ptr(ln_b), eps, ptr(count_parts), count_parts.numel(),
-         ptr(divisor), ptr(f), ptr(E), ptr(pos), ptr(neg), ptr(pl), ptr(nl), ptr(dpl), ptr(dnl), ptr(dx), ptr(lnpart),
-         ptr(part), stream())
 
 
 def sas_head_finish(part, divisor, out):

@@ -36,23 +36,25 @@ def golden():
 
 
 # bf16 fused path: two bars per gradient tensor (norm-relative).
-#  * vs the bf16-storage emulation of the same math (oracle.sas.BF16Storage: fp64 arithmetic, bf16 rounding where
-#    the kernels store bf16): the KERNELS' own error -- accumulation order, fp32 vs fp64 -- held to EMU_TOL;
-#  * vs the exact math: the bf16 FORMAT's error on top.  tools/diag/bf16_budget.py shows it is forward-rounding
-#    sensitivity of a few ill-conditioned gradients (the FFN conv1 weight of a randomly initialised model moves
-#    3-7 % when ANY single forward tensor -- even just the weights -- is rounded to bf16); no fp32 accumulation in
-#    the backward changes it.  Bound: max(BF16_ABS_TOL, 2 x the emulation's own distance to the exact math).
+#  * PASS CRITERION -- vs the bf16-storage emulation of the same math (oracle.sas.BF16Storage: fp64 arithmetic, bf16
+#    rounding exactly where the kernels store bf16): the KERNELS' own error (accumulation order, fp32 vs fp64),
+#    held to EMU_TOL = 2e-2 (measured <= 1.3 %);
+#  * a fixed cap vs the exact math: the bf16 FORMAT's error on top of that.  tools/diag/bf16_budget.py shows it is
+#    forward-rounding sensitivity of a few ill-conditioned gradients (the FFN conv1 weight of a randomly initialised
+#    model moves 3-9 % when ANY single forward tensor -- even just the weights -- is rounded to bf16; 9.3 % measured
+#    for the emulation itself at cfg1's d = 50), so the cap is a stated constant, BF16_EXACT_CAP = 0.15, independent
+#    of the measurement it bounds.
 EMU_TOL = 2e-2
-BF16_ABS_TOL = 3e-2
+BF16_EXACT_CAP = 0.15
 
 
 def check_bf16_grads(get, g_emu, g_exact, d, kbias=lambda n: False, strip="", emu_tol=EMU_TOL):
     """get(name) -> the HIP gradient (numpy); g_emu / g_exact: oracle gradient dicts keyed like the state dict.
-    Returns {name: (err vs emulation, err vs exact, bound vs exact)}.  emu_tol: EMU_TOL for the fused kernels
-    (whose storage points the emulation models).  The unfused generic bf16 kernels round at other points (e.g.
-    the online-softmax attention packs the unnormalised P, the dropout/residual gradient splits are stored), and
-    one extra rounding anywhere in the forward moves the ill-conditioned FFN weight gradients by ~5 % (tools/diag/
-    bf16_budget.py), so there the emulation is only a coarse check (0.1) and the bound vs the exact math decides."""
+    Returns {name: (err vs emulation, err vs exact, the emulation's own distance to the exact math)}.  emu_tol:
+    EMU_TOL for the fused kernels (whose storage points the emulation models).  The unfused generic bf16 kernels
+    round at other points (e.g. the online-softmax attention packs the unnormalised P, the dropout/residual
+    gradient splits are stored), and one extra rounding anywhere in the forward moves the ill-conditioned FFN
+    weight gradients by ~5 % (tools/diag/bf16_budget.py), so there the emulation is only a coarse check (0.1)."""
     out, bad = {}, {}
     scale = max(float(np.linalg.norm(v.numpy())) for v in g_exact.values())
     for k in g_exact:
@@ -66,9 +68,8 @@ def check_bf16_grads(get, g_emu, g_exact, d, kbias=lambda n: False, strip="", em
                 continue
             g, e, x = (np.concatenate([t[:d], t[2 * d:]]) for t in (g, e, x))
         r_emu, r_ex, fmt = rel(g, e), rel(g, x), rel(e, x)
-        bound = max(BF16_ABS_TOL, 2 * fmt)
-        out[name] = (r_emu, r_ex, bound)
-        if r_emu >= emu_tol or r_ex >= bound:
+        out[name] = (r_emu, r_ex, fmt)
+        if r_emu >= emu_tol or r_ex >= BF16_EXACT_CAP:
             bad[name] = out[name]
     assert not bad, bad
     return out
