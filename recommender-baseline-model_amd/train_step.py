@@ -128,15 +128,17 @@ class FusedTrainStep:
         self._stamps = None
         self.exchange = dpx.BucketedExchange(self.flat.grad, self._buckets(), self.pg, partial=self.vshard is not None) \
             if self.overlap else None
-        # SAS under DP: the gradient all-reduce is captured INSIDE the step graph (RCCL collectives are graph
+        # Under DP over RCCL the collectives are captured INSIDE the step graph (RCCL collectives are graph
         # capturable; thread-local capture mode lets the process group's watchdog poll meanwhile), so a replay is
-        # forward + backward + all-reduce + Adam with no host round trip, and several steps unroll into one
-        # graph as on one device.  Measured on one GPU (world-1 group, tools/dp_overhead.py, cfg2): the segmented
-        # form -- step graph, all-reduce issued between replays, optimizer graph -- costs 0.355 against 0.308
-        # ms/step.  RCCL only (gloo's collectives on device tensors synchronise with the host: not capturable);
-        # RS_DP_GRAPH_COLLECTIVES=0: the segmented form.
-        self.graph_collectives = (self.dp and self.kind == "sas" and self.vshard is None
-                                  and os.environ.get("RS_DP_GRAPH_COLLECTIVES", "1") != "0"
+        # forward + backward + exchange + Adam with no host round trip, and several steps unroll into one graph as
+        # on one device.  A bucket the backward finishes early (BERT's vocabulary head), the vocabulary-sharded
+        # head's collectives and the sparse token-table exchange are issued at their point of the captured
+        # backward: the collective runs on the process group's stream, forked from the capture stream there and
+        # joined before the optimizer, so it overlaps the rest of the backward inside the graph.  Measured on one
+        # GPU (world-1 group, tools/dp_overhead.py, SAS cfg2): the segmented form -- step graph, all-reduce issued
+        # between replays, optimizer graph -- costs 0.355 against 0.308 ms/step.  RCCL only (gloo's collectives on
+        # device tensors synchronise with the host: not capturable); RS_DP_GRAPH_COLLECTIVES=0: the segmented form.
+        self.graph_collectives = (self.dp and os.environ.get("RS_DP_GRAPH_COLLECTIVES", "1") != "0"
                                   and dpx.backend(self.pg) == "nccl")
         self.sparse_mode = sparse_rows
         self.sparse = None
@@ -438,20 +440,27 @@ class FusedTrainStep:
                     self.loss_val = self.loss_rows[k, 2:3]    # DP: the global mean loss lands in the step's row
                     if sample is not None:
                         sample()
-                    self._compute(*inputs(k))
+                    self._compute(*inputs(k), split=self._inline_split())
                     self._graph_exchange()
                     self._update()
             finally:
                 self.loss_out, self.loss_val = base, base_val
         return compute
 
+    def _inline_split(self):
+        """split() for a step whose collectives are captured with it: a bucket's all-reduce (or the computation's
+        own collective) is issued right where the backward finishes it (None: no mid-backward exchange)."""
+        return self._eager_split if self.graph_collectives and self.overlap else None
+
     def _graph_exchange(self):
-        """DP with graph collectives: the whole-buffer all-reduce, issued inside the step being captured."""
+        """DP with graph collectives: the buckets not yet launched mid-backward, then the join, issued inside the
+        step being captured."""
         if not self.dp:
             return
         if self.exchange is not None:
             for tag in self.exchange.buckets:
-                self.exchange.launch(tag)
+                if tag not in self.exchange.sent:
+                    self.exchange.launch(tag)
             self.exchange.finish()
         else:
             self._exchange()
@@ -470,7 +479,7 @@ class FusedTrainStep:
                 try:
                     g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
-                        compute()
+                        compute(self._inline_split()) if not unrolled else compute()
                         if not unrolled:
                             self._graph_exchange()
                             self._update()

@@ -142,3 +142,43 @@ def test_dp_graph_collectives_equal_segmented(nccl_group, monkeypatch):
     for losses, params in res[1:]:
         assert losses == res[0][0], (losses, res[0][0])
         assert torch.equal(params, res[0][1])
+
+
+@pytest.mark.parametrize("variant", ["buckets", "sparse", "vocab_shard"])
+def test_dp_graph_collectives_equal_segmented_bert(nccl_group, monkeypatch, variant):
+    """BERT under DP with every collective captured inside the step graph -- the vocabulary head's bucket issued at
+    its point of the backward (forked onto the process group's stream, joined before Adam), the sparse token-table
+    exchange's id gather and compact all-reduce, or the vocabulary-sharded head's gathers / reductions -- one step
+    per replay and two steps unrolled, against the segmented form (collectives issued between segment graphs):
+    bit-identical losses and parameters (bf16 fused step, dropout on)."""
+    import rbm_amd  # noqa: F401
+    from rbm_amd.models import model_factory
+    from rbm_amd.train_step import FusedTrainStep
+    batches = _batches("bert", 4)
+    res = []
+    for mode, S in (("0", 1), ("1", 1), ("1", 2)):
+        monkeypatch.setenv("RS_DP_GRAPH_COLLECTIVES", mode)
+        torch.manual_seed(5)
+        a = argparse.Namespace(model_code="bert", num_items=500, max_len=50, device="cuda", bert_hidden_units=64,
+                               bert_num_blocks=2, bert_num_heads=2, bert_dropout=0.1, bert_hidden_dropout=0.1,
+                               bert_mask_prob=0.2, model_init_seed=5, rs_dtype="bf16")
+        tr = FusedTrainStep(model_factory(a), lr=1e-3, dp=True, vocab_shard=variant == "vocab_shard",
+                            sparse_rows="on" if variant == "sparse" else "off")
+        assert tr.graph_collectives == (mode == "1")
+        tr.capture(*batches[0], steps_per_graph=S)
+        if variant == "sparse":
+            assert tr.sparse is not None
+        if mode == "1":
+            assert len(tr.graphs) == 1
+        if S == 1:
+            losses = [float(tr.replay(*b).item()) for b in batches]
+        else:
+            losses = []
+            for j in range(0, len(batches), S):
+                packed = torch.stack([torch.stack(b) for b in batches[j:j + S]])
+                losses += [float(x) for x in tr.replay_packed(packed).cpu()]
+        torch.cuda.synchronize()
+        res.append((losses, tr.flat.data.detach().cpu().clone()))
+    for losses, params in res[1:]:
+        assert losses == res[0][0], (losses, res[0][0])
+        assert torch.equal(params, res[0][1])

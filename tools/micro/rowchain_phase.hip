@@ -3,7 +3,6 @@
 //   hipcc --offload-arch=gfx950 -O3 -DRC_PROF -I include -I recommender-baseline-model_amd/csrc \
 //         tools/micro/rowchain_phase.hip -o tools/micro/rowchain_phase
 #include "../../recommender-baseline-model_amd/csrc/rowchain.hip"
-#include "../../recommender-baseline-model_amd/csrc/rowfused.hip"
 
 #include <algorithm>
 #include <cstdio>
@@ -56,7 +55,7 @@ int main(int argc, char** argv) {
   const double u = 0.01;   // 100 MHz ticks -> us
   printf("block_out M=%lld grid=%d: event %.2f us, first entry -> last exit %.2f us\n", (long long)M, G, ms * 1e3,
          (t1 - t0) * u);
-  std::vector<double> ent, stg, g1, x1s, rest, ex, tot, ln2, mm1, ep1, mm2;
+  std::vector<double> ent, stg, ga, gb, ex, tot;
   for (int b_ = 0; b_ < G; ++b_)
     for (int w = 0; w < 8; ++w) {
       const unsigned long long* x = &p[((size_t)b_ * 8 + w) * 16];
@@ -64,26 +63,16 @@ int main(int argc, char** argv) {
       ent.push_back((x[0] - t0) * u);
       stg.push_back((x[1] - x[0]) * u);
       if (x[2]) {
-        g1.push_back((x[2] - x[1]) * u);
-        x1s.push_back((x[3] - x[2]) * u);
-        rest.push_back((x[4] - x[3]) * u);
-        ln2.push_back((x[6] - x[3]) * u);
-        mm1.push_back((x[7] - x[6]) * u);
-        ep1.push_back((x[8] - x[7]) * u);
-        mm2.push_back((x[9] - x[8]) * u);
+        ga.push_back((x[2] - x[1]) * u);
+        gb.push_back((x[4] - x[2]) * u);
       }
       ex.push_back((x[5] - t0) * u);
       tot.push_back((x[5] - x[0]) * u);
     }
   pct("entry after first", ent);
-  pct("weight staging", stg);
-  pct("inputs + first GEMM", g1);
-  pct("x1 epilogue + store", x1s);
-  pct("LN2 + FFN (2 GEMMs)", rest);
-  pct(" .. LN2 + z store", ln2);
-  pct(" .. GEMM W1", mm1);
-  pct(" .. h1 epilogue + store", ep1);
-  pct(" .. GEMM W2", mm2);
+  pct("weight staging (+barrier)", stg);
+  pct("x1, LN2, GEMM W1 (tile 1)", ga);
+  pct("GEMM W2 + stores (tile 1)", gb);
   pct("exit after first entry", ex);
   pct("wave lifetime", tot);
   return 0;
