@@ -210,10 +210,10 @@ int rs_splitk_scatter_rows(int dtype, const float* slab, int splits, int64_t cap
                            int64_t n, void* dst, int64_t ldd, void* stream);
 
 /* torch.optim.Adam step (BS/trainers/base.py:225-228; amsgrad=False) over a
- * flat fp32 buffer.  hyper (device fp32[5]) = {lr, beta1, beta2, eps, weight_decay}.
+ * flat fp32 buffer.  hyper (device double[5]) = {lr, beta1, beta2, eps, weight_decay} (doubles, as torch's Python
+ * floats: the scalars are formed in double and cast to float where they meet the tensors, like torch's).
  * state (device double[8]; double[144] for rs_adam_prepare_step; zero-initialised): rs_adam_prepare does state[0] += 1 (the step count t)
- * and forms state[1] = lr/(1-beta1^t), state[2] = sqrt(1-beta2^t) (1-b^t as -expm1(t*log1p(b-1)) in
- * fp32: no cancellation at beta2 near 1), state[3] = 1/(*grad_divisor) (1 when null: the
+ * and forms state[1] = float(lr/(1-beta1^t)), state[2] = float(sqrt(1-beta2^t)) (double math), state[3] = 1/(*grad_divisor) (1 when null: the
  * data-parallel step all-reduces UNnormalised gradients plus the valid-position count and
  * divides here, so the summed gradient equals the single-device mean's).  rs_adam_step then
  * updates (grad scaled by state[3])
@@ -227,17 +227,17 @@ int rs_splitk_scatter_rows(int dtype, const float* slab, int splits, int64_t cap
  * cols, src_off (element offset of the matrix in the flat buffer whose element tbase is p[0]), lds
  * (% 4 == 0), dst_off, ldd: wT[dst_off + c*ldd + r] = bf16(p[src_off + r*lds + c]) (rs_transpose_bf16's
  * output, so the SAS backward's transposed weights need no separate launch).  Same results bit for bit. */
-int rs_adam_prepare(double* state, const float* hyper, const float* grad_divisor, uint64_t* seed_base,
+int rs_adam_prepare(double* state, const double* hyper, const float* grad_divisor, uint64_t* seed_base,
                     void* stream);
 int rs_adam_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16,
-                 const double* state, const float* hyper, int zero_grad, void* stream);
+                 const double* state, const double* hyper, int zero_grad, void* stream);
 int rs_adam_prepare_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, double* state,
-                         const float* hyper, int zero_grad, const float* grad_divisor, uint64_t* seed_base,
+                         const double* hyper, int zero_grad, const float* grad_divisor, uint64_t* seed_base,
                          const int64_t* tdesc, int ntd, int64_t tbase, void* wT, void* stream);
 /* rs_adam_prepare_step that also writes *loss_out = *loss_sum / *grad_divisor (data parallel: the step's mean
  * loss from the all-reduced gradient tail) in the same launch. */
 int rs_adam_prepare_step_loss(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, double* state,
-                              const float* hyper, int zero_grad, const float* grad_divisor, uint64_t* seed_base,
+                              const double* hyper, int zero_grad, const float* grad_divisor, uint64_t* seed_base,
                               const int64_t* tdesc, int ntd, int64_t tbase, void* wT, const float* loss_sum,
                               float* loss_out, void* stream);
 

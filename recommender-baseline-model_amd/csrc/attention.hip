@@ -58,6 +58,14 @@ __device__ __forceinline__ float masked_score(const AttnArgs& a, int64_t b, int6
 }
 
 // 8 elements of row `row`, columns [col, col+8) (zero past rlim rows / dh columns)
+// exp / log of the generic kernels: the fp32 (parity) instantiations use the accurate libm forms, as the reference's
+// torch softmax does (the fast forms' argument rounding -- exp2(x * log2 e) -- adds noise that a 1000-step training
+// curve amplifies); bf16 keeps the fast hardware forms
+template <typename T> __device__ __forceinline__ float aexp(float x) { return __expf(x); }
+template <> __device__ __forceinline__ float aexp<float>(float x) { return expf(x); }
+template <typename T> __device__ __forceinline__ float alog(float x) { return __logf(x); }
+template <> __device__ __forceinline__ float alog<float>(float x) { return logf(x); }
+
 template <typename T>
 __device__ __forceinline__ void load_frag_rows(Frag<T>& f, const T* base, int64_t ld, int64_t row, int64_t rlim,
                                                int col, int dh, int vec) {
@@ -155,12 +163,12 @@ __global__ __launch_bounds__(64) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float nm = fmaxf(mx[r], cm[r]);
-      alpha[r] = (mx[r] == NEG_INF) ? 0.f : __expf(mx[r] - nm);
+      alpha[r] = (mx[r] == NEG_INF) ? 0.f : aexp<T>(mx[r] - nm);
       mx[r] = nm;
       float rs = 0.f;
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
-        const float e = (s[hf][r] == NEG_INF || nm == NEG_INF) ? 0.0f : __expf(s[hf][r] - nm);
+        const float e = (s[hf][r] == NEG_INF || nm == NEG_INF) ? 0.0f : aexp<T>(s[hf][r] - nm);
         s[hf][r] = e;
         rs += e;
       }
@@ -196,7 +204,7 @@ __global__ __launch_bounds__(64) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t qrow = q0 + 4 * g + r;
-      if (qrow < a.T) a.lse[bh * a.T + qrow] = mx[r] + __logf(sm[r]);
+      if (qrow < a.T) a.lse[bh * a.T + qrow] = mx[r] + alog<T>(sm[r]);
     }
   }
   T* O = reinterpret_cast<T*>(a.o) + b * a.T * a.ldo + h * Dh;
@@ -280,7 +288,7 @@ __global__ __launch_bounds__(64) void attn_bwd_dq_kernel(AttnArgs a) {
       for (int r = 0; r < 4; ++r) {
         const int64_t qrow = q0 + 4 * g + r, key = kbase + cl;
         float x = masked_score(a, b, qrow, key, s[r] * a.scale);
-        float p = (x == NEG_INF || qrow >= a.T) ? 0.f : __expf(x - lse[r]);
+        float p = (x == NEG_INF || qrow >= a.T) ? 0.f : aexp<T>(x - lse[r]);
         float dpe = dp[r];
         if (a.drop_p > 0.f) dpe *= drop_mul(a.drop_p, seed, (uint64_t)((bh * a.T + qrow) * tp + key));
         dSs[(4 * g + r) * SLD + half * 16 + cl] = from_f<T>(p * (dpe - dl[r]) * a.scale);
@@ -360,7 +368,7 @@ __global__ __launch_bounds__(64) void attn_bwd_dkv_kernel(AttnArgs a) {
       for (int r = 0; r < 4; ++r) {
         const int64_t key = k0 + 4 * g + r;
         float x = masked_score(a, b, qrow, key, st[r] * a.scale);
-        float p = (x == NEG_INF || qrow >= a.T || key >= a.T) ? 0.f : __expf(x - lq);
+        float p = (x == NEG_INF || qrow >= a.T || key >= a.T) ? 0.f : aexp<T>(x - lq);
         float dm = a.drop_p > 0.f ? drop_mul(a.drop_p, seed, (uint64_t)((bh * a.T + qrow) * tp + key)) : 1.f;
         Pt[(4 * g + r) * SLD + half * 16 + cl] = from_f<T>(p * dm);
         dSt[(4 * g + r) * SLD + half * 16 + cl] = from_f<T>(p * (dpt[r] * dm - dq) * a.scale);

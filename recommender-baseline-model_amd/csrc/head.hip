@@ -21,8 +21,8 @@ namespace hd {
 typedef __bf16 bf16;
 constexpr int RB = 64;   // rows per workgroup
 
-__device__ __forceinline__ float softplus(float z) { return fmaxf(z, 0.f) + log1pf(__expf(-fabsf(z))); }
-__device__ __forceinline__ float sigmoidf(float z) { return 1.f / (1.f + __expf(-z)); }
+__device__ __forceinline__ float softplus(float z) { return fmaxf(z, 0.f) + log1pf(expf(-fabsf(z))); }
+__device__ __forceinline__ float sigmoidf(float z) { return 1.f / (1.f + expf(-z)); }
 
 template <int D>
 __global__ __launch_bounds__(256) void head_fwd_kernel(int64_t M, const bf16* __restrict__ x,

@@ -13,8 +13,8 @@
 #include "common.h"
 #include "../../include/recsys_hip.h"
 
-__device__ __forceinline__ float softplus(float z) { return fmaxf(z, 0.f) + log1pf(__expf(-fabsf(z))); }
-__device__ __forceinline__ float sigmoidf(float z) { return 1.f / (1.f + __expf(-z)); }
+__device__ __forceinline__ float softplus(float z) { return fmaxf(z, 0.f) + log1pf(expf(-fabsf(z))); }
+__device__ __forceinline__ float sigmoidf(float z) { return 1.f / (1.f + expf(-z)); }
 
 #define BCE_BLOCKS 256
 
@@ -81,8 +81,8 @@ __global__ __launch_bounds__(256) void ce_row_kernel(const float* __restrict__ l
   if (lab != 0) {
     for (int64_t j = threadIdx.x; j < V1; j += blockDim.x) {
       const float v = x[j];
-      if (v > m) { s = s * __expf(m - v) + 1.f; m = v; }
-      else s += __expf(v - m);
+      if (v > m) { s = s * expf(m - v) + 1.f; m = v; }
+      else s += expf(v - m);
     }
   }
   // combine (m, s) across the block
@@ -94,13 +94,13 @@ __global__ __launch_bounds__(256) void ce_row_kernel(const float* __restrict__ l
       const float m1 = sm[threadIdx.x], m2 = sm[threadIdx.x + o];
       const float s1 = ss[threadIdx.x], s2 = ss[threadIdx.x + o];
       const float mm = fmaxf(m1, m2);
-      const float t = (mm == -__builtin_inff()) ? 0.f : s1 * __expf(m1 - mm) + s2 * __expf(m2 - mm);
+      const float t = (mm == -__builtin_inff()) ? 0.f : s1 * expf(m1 - mm) + s2 * expf(m2 - mm);
       sm[threadIdx.x] = mm; ss[threadIdx.x] = t;
     }
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    const float lse = lab != 0 ? sm[0] + __logf(ss[0]) : 0.f;
+    const float lse = lab != 0 ? sm[0] + logf(ss[0]) : 0.f;
     lse_out[r] = lse;
     part[r * 2 + 0] = lab != 0 ? lse - x[lab] : 0.f;
     part[r * 2 + 1] = lab != 0 ? 1.f : 0.f;
@@ -137,7 +137,7 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const float* __restrict__ l
   const float L = lse[r];
   for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < V1; j += (int64_t)gridDim.x * blockDim.x) {
     float g = 0.f;
-    if (lab != 0) g = (__expf(logits[r * ldl + j] - L) - (j == lab ? 1.f : 0.f)) * sc;
+    if (lab != 0) g = (expf(logits[r * ldl + j] - L) - (j == lab ? 1.f : 0.f)) * sc;
     dl[r * lddl + j] = from_f<T>(g);
   }
 }

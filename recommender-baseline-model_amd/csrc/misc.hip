@@ -10,15 +10,23 @@
 #include "common.h"
 #include "../../include/recsys_hip.h"
 
-// Bias corrections of step t, torch.optim.Adam (bias_correction1 = 1 - b1^t, step_size = lr / bc1,
-// bias_correction2_sqrt = sqrt(1 - b2^t)).  1 - b^t is formed as -expm1(t * log1p(b - 1)): no cancellation
-// for b2 near 1 (the float pow form loses ~3 digits at b2 = 0.999, t = 1).
+// Bias corrections of step t exactly as torch.optim.Adam forms them (BS/trainers/base.py:225-228; the
+// single-tensor path, torch/optim/adam.py): the hyperparameters are Python doubles there, bias_correction1 =
+// 1 - beta1 ** step, step_size = lr / bias_correction1, bias_correction2_sqrt = sqrt(1 - beta2 ** step) in double,
+// each cast to float where it meets the fp32 tensors.  hyper is double[5] for that reason: with fp32 betas,
+// 1 - 0.999f is 1.3e-5 (relative) off torch's float(1 - 0.999) -- a systematic bias in every v update and in
+// sqrt(bc2) that a 1000-step curve amplified.
 struct AdamScalars { float step_size, bc2s, gs; };
-__device__ __forceinline__ AdamScalars adam_scalars(double t, const float* hyper, const float* divisor) {
-  const float tf = (float)t, lr = hyper[0], b1 = hyper[1], b2 = hyper[2];
-  const float bc1 = -expm1f(tf * log1pf(b1 - 1.f));
-  const float bc2 = -expm1f(tf * log1pf(b2 - 1.f));
-  return {lr / bc1, sqrtf(bc2), divisor ? 1.f / divisor[0] : 1.f};
+__device__ __forceinline__ AdamScalars adam_scalars(double t, const double* hyper, const float* divisor) {
+  const double lr = hyper[0], b1 = hyper[1], b2 = hyper[2];
+  const double bc1 = 1.0 - pow(b1, t), bc2 = 1.0 - pow(b2, t);
+  return {(float)(lr / bc1), (float)sqrt(bc2), divisor ? 1.f / divisor[0] : 1.f};
+}
+// the per-element scalars: float(beta2) (exp_avg_sq.mul_(beta2)), float(1 - beta1) (lerp weight), float(1 - beta2)
+// (addcmul value), float(eps), float(weight_decay)
+struct AdamElem { float b2, omb1, omb2, eps, wd; };
+__device__ __forceinline__ AdamElem adam_elem(const double* hyper) {
+  return {(float)hyper[2], (float)(1.0 - hyper[1]), (float)(1.0 - hyper[2]), (float)hyper[3], (float)hyper[4]};
 }
 
 __device__ __forceinline__ void adam_commit(double* state, double t, AdamScalars c, uint64_t* seed_base) {
@@ -29,7 +37,7 @@ __device__ __forceinline__ void adam_commit(double* state, double t, AdamScalars
   state[3] = c.gs;
 }
 
-__global__ void adam_prepare_kernel(double* state, const float* hyper, const float* divisor, uint64_t* seed_base) {
+__global__ void adam_prepare_kernel(double* state, const double* hyper, const float* divisor, uint64_t* seed_base) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const double t = state[0] + 1.0;
   adam_commit(state, t, adam_scalars(t, hyper, divisor), seed_base);
@@ -43,7 +51,7 @@ __global__ void adam_prepare_kernel(double* state, const float* hyper, const flo
 template <bool BF16OUT>
 __device__ __forceinline__ void adam4(int64_t i, float4 pp, float4 gg, float4 mm, float4 vv, float* __restrict__ p,
                                       float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
-                                      __bf16* __restrict__ pb, float b1, float b2, float eps, float wd,
+                                      __bf16* __restrict__ pb, AdamElem h,
                                       float step_size, float bc2s, float gs, int zero_grad,
                                       const int64_t* __restrict__ tdesc, int ntd, int64_t tbase,
                                       __bf16* __restrict__ wT) {
@@ -51,10 +59,10 @@ __device__ __forceinline__ void adam4(int64_t i, float4 pp, float4 gg, float4 mm
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     float gj = gs == 1.f ? G[j] : G[j] * gs;
-    if (wd != 0.f) gj = gj + wd * P[j];
-    Mv[j] = Mv[j] + (1.f - b1) * (gj - Mv[j]);            // exp_avg.lerp_(grad, 1-beta1)
-    Vv[j] = Vv[j] * b2 + (1.f - b2) * gj * gj;            // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
-    const float denom = sqrtf(Vv[j]) / bc2s + eps;
+    if (h.wd != 0.f) gj = gj + h.wd * P[j];
+    Mv[j] = Mv[j] + h.omb1 * (gj - Mv[j]);                // exp_avg.lerp_(grad, 1-beta1)
+    Vv[j] = Vv[j] * h.b2 + h.omb2 * gj * gj;              // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
+    const float denom = sqrtf(Vv[j]) / bc2s + h.eps;
     P[j] = P[j] - step_size * (Mv[j] / denom);            // param.addcdiv_(exp_avg, denom, -step_size)
   }
   reinterpret_cast<float4*>(p)[i] = pp;
@@ -86,12 +94,12 @@ template <bool BF16OUT, bool PREP, int U>
 __global__ __launch_bounds__(256) void adam_step_kernel(int64_t n, float* __restrict__ p, float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v,
                                                         __bf16* __restrict__ pb, double* __restrict__ state,
-                                                        const float* __restrict__ hyper, int zero_grad,
+                                                        const double* __restrict__ hyper, int zero_grad,
                                                         const float* __restrict__ divisor, uint64_t* seed_base,
                                                         const int64_t* __restrict__ tdesc, int ntd, int64_t tbase,
                                                         __bf16* __restrict__ wT, const float* __restrict__ lsum,
                                                         float* __restrict__ lout) {
-  const float b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
+  const AdamElem h = adam_elem(hyper);
   // data parallel: the step's reported loss = all-reduced loss sum / all-reduced count (the division torch.div did
   // in its own launch), by one thread: both inputs are final before this launch
   if (PREP && lout && blockIdx.x == 0 && threadIdx.x == 0) *lout = lsum[0] / divisor[0];
@@ -122,7 +130,7 @@ __global__ __launch_bounds__(256) void adam_step_kernel(int64_t n, float* __rest
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      adam4<BF16OUT>(i + u * stride, pq[u], gq[u], mq[u], vq[u], p, g, m, v, pb, b1, b2, eps, wd, step_size, bc2s, gs,
+      adam4<BF16OUT>(i + u * stride, pq[u], gq[u], mq[u], vq[u], p, g, m, v, pb, h, step_size, bc2s, gs,
                      zero_grad, tdesc, ntd, tbase, wT);
   }
   for (; i < n4; i += stride) {
@@ -130,17 +138,17 @@ __global__ __launch_bounds__(256) void adam_step_kernel(int64_t n, float* __rest
     float4 gg = reinterpret_cast<const float4*>(g)[i];
     float4 mm = reinterpret_cast<float4*>(m)[i];
     float4 vv = reinterpret_cast<float4*>(v)[i];
-    adam4<BF16OUT>(i, pp, gg, mm, vv, p, g, m, v, pb, b1, b2, eps, wd, step_size, bc2s, gs, zero_grad, tdesc, ntd,
+    adam4<BF16OUT>(i, pp, gg, mm, vv, p, g, m, v, pb, h, step_size, bc2s, gs, zero_grad, tdesc, ntd,
                    tbase, wT);
   }
   // tail
   if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
     const int64_t j = n4 * 4 + threadIdx.x;
     float gj = gs == 1.f ? g[j] : g[j] * gs;
-    if (wd != 0.f) gj = gj + wd * p[j];
-    m[j] = m[j] + (1.f - b1) * (gj - m[j]);
-    v[j] = v[j] * b2 + (1.f - b2) * gj * gj;
-    const float denom = sqrtf(v[j]) / bc2s + eps;
+    if (h.wd != 0.f) gj = gj + h.wd * p[j];
+    m[j] = m[j] + h.omb1 * (gj - m[j]);
+    v[j] = v[j] * h.b2 + h.omb2 * gj * gj;
+    const float denom = sqrtf(v[j]) / bc2s + h.eps;
     p[j] = p[j] - step_size * (m[j] / denom);
     if (BF16OUT) pb[j] = (__bf16)p[j];
     if (zero_grad) g[j] = 0.f;
@@ -317,7 +325,7 @@ __global__ __launch_bounds__(256) void dropout_v8_kernel(const T* __restrict__ x
 
 extern "C" {
 
-int rs_adam_prepare(double* state, const float* hyper, const float* grad_divisor, uint64_t* seed_base,
+int rs_adam_prepare(double* state, const double* hyper, const float* grad_divisor, uint64_t* seed_base,
                     void* stream) {
   hipLaunchKernelGGL(adam_prepare_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, state, hyper, grad_divisor,
                      seed_base);
@@ -328,7 +336,7 @@ int rs_adam_prepare(double* state, const float* hyper, const float* grad_divisor
 #define ADAM_LAUNCH(BO, PR, ...) hipLaunchKernelGGL((adam_step_kernel<BO, PR, 2>), __VA_ARGS__)
 
 int rs_adam_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, const double* state,
-                 const float* hyper, int zero_grad, void* stream) {
+                 const double* hyper, int zero_grad, void* stream) {
   if (n <= 0 || ((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16) return RS_ERR_ARG;
   const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(cdiv(n / 4, 256), 8192));
   hipStream_t s = (hipStream_t)stream;
@@ -345,14 +353,14 @@ int rs_adam_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16
 }
 
 int rs_adam_prepare_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, double* state,
-                         const float* hyper, int zero_grad, const float* grad_divisor, uint64_t* seed_base,
+                         const double* hyper, int zero_grad, const float* grad_divisor, uint64_t* seed_base,
                          const int64_t* tdesc, int ntd, int64_t tbase, void* wT, void* stream) {
   return rs_adam_prepare_step_loss(n, p, g, m, v, p_bf16, state, hyper, zero_grad, grad_divisor, seed_base, tdesc, ntd,
                                    tbase, wT, nullptr, nullptr, stream);
 }
 
 int rs_adam_prepare_step_loss(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, double* state,
-                              const float* hyper, int zero_grad, const float* grad_divisor, uint64_t* seed_base,
+                              const double* hyper, int zero_grad, const float* grad_divisor, uint64_t* seed_base,
                               const int64_t* tdesc, int ntd, int64_t tbase, void* wT, const float* loss_sum,
                               float* loss_out, void* stream) {
   if (n <= 0 || !state || ((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16) return RS_ERR_ARG;

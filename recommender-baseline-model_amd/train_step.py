@@ -44,7 +44,7 @@ class FusedAdam:
         # [t, lr/bc1, sqrt(bc2), grad scale, -, -, -, arrival counters of rs_adam_prepare_step (state[7],
         # state[16 + 16 k], k < 8)]
         self.state = torch.zeros(144, dtype=torch.float64, device=dev)
-        self.hyper = torch.tensor([lr, betas[0], betas[1], eps, weight_decay], dtype=torch.float32, device=dev)
+        self.hyper = torch.tensor([lr, betas[0], betas[1], eps, weight_decay], dtype=torch.float64, device=dev)
 
     def set_lr(self, lr):
         """StepLR hook (BS/trainers/base.py:40,87): lives on the device, so graph replays see it."""
@@ -333,7 +333,7 @@ class FusedTrainStep:
         """Resume from a torch.optim.Adam state_dict (e.g. a reference checkpoint's 'optimizer_state_dict')."""
         g = sd["param_groups"][0]
         self.opt.hyper.copy_(torch.tensor([g["lr"], g["betas"][0], g["betas"][1], g["eps"], g["weight_decay"]],
-                                          dtype=torch.float32))
+                                          dtype=torch.float64))
         slices = self._param_slices()
         steps = set()
         self.opt.m.zero_()

@@ -18,7 +18,7 @@ def test_fused_prepare_step_matches_two_launches_and_torch(n, wd):
     from rbm_amd import ops
     g0 = torch.Generator().manual_seed(n)
     p0 = torch.randn(n, generator=g0)
-    hyper = torch.tensor([1e-3, 0.9, 0.999, 1e-8, wd], dtype=torch.float32, device="cuda")
+    hyper = torch.tensor([1e-3, 0.9, 0.999, 1e-8, wd], dtype=torch.float64, device="cuda")
     div = torch.tensor([3.0], device="cuda")
     runs = []
     for fused in (False, True):
@@ -48,6 +48,46 @@ def test_fused_prepare_step_matches_two_launches_and_torch(n, wd):
         opt.step()
     err = (runs[1][0].cpu().double() - tp.detach()).abs().max().item()
     assert err < 2e-6, err
+
+
+@pytest.mark.parametrize("wd", [0.0, 0.01])
+def test_fused_step_matches_torch_adam_in_float32(wd):
+    """The same five steps against torch.optim.Adam on float32 tensors (CPU, the reference's dtype) fed the very
+    gradients the kernel uses (g * float(1/divisor)): the moments and the parameters agree to a few float32 ulps.
+    The bias corrections and (1 - beta) factors are formed in double and cast to float as torch does with its
+    Python-float hyperparameters (fp32 betas put 1 - 0.999f 1.3e-5 relative off torch's float(1 - 0.999): a bias
+    in every exp_avg_sq update this bound rejects)."""
+    import rbm_amd  # noqa: F401
+    from rbm_amd import ops
+    n = 100_003
+    g0 = torch.Generator().manual_seed(5)
+    p0 = torch.randn(n, generator=g0)
+    hyper = torch.tensor([1e-3, 0.9, 0.999, 1e-8, wd], dtype=torch.float64, device="cuda")
+    div = torch.tensor([3.0], device="cuda")
+    p, m, v = p0.cuda().clone(), torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
+    st, seed = _state(), torch.zeros(1, dtype=torch.int64, device="cuda")
+    tp = torch.nn.Parameter(p0.clone())
+    opt = torch.optim.Adam([tp], lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=wd, foreach=False)
+    gg = torch.Generator().manual_seed(1)
+    gs = torch.tensor(1.0, dtype=torch.float32) / torch.tensor(3.0, dtype=torch.float32)
+    for _ in range(5):
+        g = torch.randn(n, generator=gg) * 3.0
+        ops.adam_prepare_step(p, g.cuda(), m, v, None, st, hyper, zero_grad=True, grad_divisor=div, seed_base=seed)
+        tp.grad = g * gs
+        opt.step()
+    torch.cuda.synchronize()
+    s = opt.state[tp]
+
+    eps = torch.finfo(torch.float32).eps
+
+    def ulps(a, b):   # elementwise, in float32 ulps of the reference value
+        return ((a.double() - b.double()).abs() / eps / b.double().abs().clamp_min(1e-30))
+
+    def ulps_of_max(a, b):   # m and p: signed sums with cancellation -- ulps of the tensor's largest magnitude
+        return ((a.double() - b.double()).abs().max() / eps / b.double().abs().max()).item()
+    assert ulps(v.cpu(), s["exp_avg_sq"]).max().item() <= 4
+    assert ulps_of_max(m.cpu(), s["exp_avg"]) <= 4
+    assert ulps_of_max(p.cpu(), tp.detach()) <= 4
 
 
 @pytest.mark.parametrize("graph", [False, True])

@@ -111,8 +111,13 @@ def test_sas_loss_curve_at_the_bench_shape(dtype):
     implementation of the same math (the oracle in fp32, tools/diag/curve_noise.py) leaves the reference's fp32 run
     by up to 1.96e-3 (mean 2.4e-4, 1.5 % of the steps above 1e-3) -- two fp32 runs of this training drift apart by
     rounding alone, so a per-step 1e-3 bar cannot hold for every step here.  Bounds (measured in brackets):
-      fp32: max |loss - reference| <= 5e-3 [4.3e-3], mean <= 6e-4 [4.2e-4], >= 85 % of steps within 1e-3 [90.9 %],
-            50-step moving average <= 1.5e-3 [9.0e-4];
+      fp32: max |loss - reference| <= 5e-3 [2.5-3.0e-3], mean <= 6e-4 [2.9-3.5e-4], >= 85 % of steps within 1e-3
+            [94-96 %], 50-step moving average <= 1.5e-3 [6-7e-4]; against losses64 (exact math): max <= 3x the
+            reference's own fp32 drift (1.44e-3) [2.7-3.4e-3], mean <= 2x its mean drift (2.1e-4) [~3e-4].  Round 3
+            removed two systematic deviations from the reference's arithmetic (round 2 measured max 4.3e-3): the fp32
+            attention / softmax / BCE kernels used the fast exp / log intrinsics (argument rounding of exp2(x log2 e)),
+            and the fused Adam took fp32 betas (1 - 0.999f is 1.3e-5 relative off torch's float(1 - 0.999)).  The rest
+            varies run to run: the fp32 path's table gradients use float atomics, so each run is its own chaotic draw;
       bf16: the benchmarked path: max <= 5e-2 [2.5e-2], mean <= 3e-3 [1.4e-3], moving average <= 1e-2 [4.6e-3]."""
     z = load_golden("sas_curve_bench")
     losses, _ = _run("sas", z, int(z["steps"]), dtype=dtype)
@@ -128,5 +133,9 @@ def test_sas_loss_curve_at_the_bench_shape(dtype):
     if dtype == "fp32":
         assert err.max() <= 5e-3 and err.mean() <= 6e-4 and (err <= 1e-3).mean() >= 0.85 and dma.max() <= 1.5e-3, \
             (err.max(), err.mean(), (err <= 1e-3).mean(), dma.max())
+        # against the exact math: within 3x the reference's own fp32 envelope at its worst step and 2x on average
+        floor_mean = np.abs(ref - ref64).mean()
+        assert err64.max() <= 3 * floor and err64.mean() <= 2 * floor_mean, (err64.max(), floor, err64.mean(),
+                                                                             floor_mean)
     else:
         assert err.max() <= 5e-2 and err.mean() <= 3e-3 and dma.max() <= 1e-2, (err.mean(), err.max(), dma.max())
