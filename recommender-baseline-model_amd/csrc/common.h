@@ -149,9 +149,10 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
   return x;
 }
 __device__ __forceinline__ uint32_t seed32(uint64_t seed) { return (uint32_t)seed ^ (uint32_t)(seed >> 32) * 0x27d4eb2fU; }
-__device__ __forceinline__ uint32_t pair_hash(uint32_t s32, uint64_t idx) {
-  return hash32(((uint32_t)(idx >> 1) * 0x9E3779B1U) ^ s32 ^ ((uint32_t)(idx >> 33) * 0x85EBCA77U));
-}
+// one 32-bit hash per pair of adjacent elements (16 bits each).  Two multiplies (hash32's): the element-pair index
+// is XORed into the site seed directly (pair indices past 2^32 -- 8.6G elements of one site -- would repeat masks);
+// a golden-ratio pre-multiply and a high-word term cost two more 4-pass v_mul_lo_u32 per pair in every dropout site
+__device__ __forceinline__ uint32_t pair_hash(uint32_t s32, uint64_t idx) { return hash32((uint32_t)(idx >> 1) ^ s32); }
 __device__ __forceinline__ uint32_t drop_thr(float p) { return (uint32_t)fminf(p * 65536.0f, 65535.0f); }
 // keep with probability 1-p; returns the multiplier (0 or 1/(1-p))
 __device__ __forceinline__ float drop_mul(float p, uint64_t seed, uint64_t idx) {

@@ -213,7 +213,7 @@ def main():
     v1.abs_()
     pbf = torch.empty(n, dtype=torch.bfloat16, device=dev)
     st = torch.tensor([1.0, 0.001, 1.0, 1.0], dtype=torch.float64, device=dev)
-    hy = torch.tensor([1e-3, 0.9, 0.999, 1e-8, 0.0], device=dev)
+    hy = torch.tensor([1e-3, 0.9, 0.999, 1e-8, 0.0], dtype=torch.float64, device=dev)
     run(f"adam_step ({n} params)",lambda: ops.adam_step(p, gg, m1, v1, pbf, st, hy, zero_grad=True), n * 4 * 8 + n * 2)
     st144 = torch.zeros(144, dtype=torch.float64, device=dev)
     run(f"adam_prepare_step ({n} params)", lambda: ops.adam_prepare_step(p, gg, m1, v1, pbf, st144, hy, zero_grad=True),
