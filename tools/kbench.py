@@ -118,9 +118,11 @@ def main():
         4 * mb, aflops)
     dq, dkv = rn(M, d), rn(M, 2 * d)
     wat = torch.empty(B * H * T, device=dev)
+    # the step's variant (sas.py / bert.py): delta = rowsum(dO * O) handed in, O not read -- 7 activation tensors
+    ops.attn_row_delta(B, T, H, Dh, y, o, wat)
     run("attn_bwd causal drop",lambda: ops.attn_bwd(B, T, H, Dh, q, kv[:, :d], kv[:, d:], o, y, lse, dq,
                                                             dkv[:, :d], dkv[:, d:], 1 / math.sqrt(Dh), 0, ids, a.drop,
-                                                            9, sb, wat), 8 * mb, 2.5 * aflops)
+                                                            9, sb, wat, delta_in=True), 7 * mb, 2.0 * aflops)
     if a.config in ("cfg3", "cfg5"):
         # BERT block GEMMs with their fused epilogues (bert.py encode / encode_backward)
         hg, apre, gg = rn(M, d), rn(M, ff), rn(M, ff)
