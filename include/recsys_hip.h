@@ -340,9 +340,9 @@ int rs_wall_clock_khz(int* khz);
 /* *seed_base += 1 on the stream (advances every dropout mask; capturable). */
 int rs_seed_advance(uint64_t* seed_base, void* stream);
 
-/* ---- fused SAS sublayers (bf16, d in {64, 128}; rowfused.hip) ----------------------------
- * rowchain.hip: one workgroup per CU stages the block's weights in LDS once, each wave carries 16
- * tokens through the whole chain in registers (RS_ROWCHAIN=0: rowfused.hip's 64-row LDS tiles).
+/* ---- fused SAS sublayers (bf16, d in {64, 128}; rowchain.hip) ----------------------------
+ * One workgroup per CU stages the block's weights in LDS once, each wave carries 16 tokens
+ * through the whole chain in registers.
  * Same outputs, saved tensors and dropout masks as the unfused kernel sequence, so rs_* backward
  * kernels consume them unchanged.
  *

@@ -87,7 +87,7 @@ class Exact:
 
 
 class BF16Storage(Exact):
-    """The HIP bf16 path's storage roundings (rowfused.hip, attention_lds.hip, head.hip, embedding.hip)."""
+    """The HIP bf16 path's storage roundings (rowchain.hip, attention_lds.hip, head.hip, embedding.hip)."""
     def w(self, t):
         return _RoundFwd.apply(t)
 

@@ -656,10 +656,14 @@ hipError_t launch_cfg(GemmArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// tile choice: 128x128 when that still gives >= 512 workgroups (2 per CU), else 64x64
+// tile choice: 128x128 when that still gives >= 512 workgroups (2 per CU), else 64x64; the GELU /
+// GELU' + dropout epilogues (BERT FFN1 forward, FFN2 input gradient) always take 64x64: their VALU work
+// (tanh, the dropout hash) then overlaps the loads of the other resident workgroups (12800 x 1024 x 256:
+// 25.9 -> 24.3 us and 27.6 -> 25.6 us, tools/diag/gemm_epi.py)
 template <bool AK, bool BK, int EC>
 hipError_t launch_tiles(GemmArgs& a, hipStream_t s) {
-  if (cdiv(a.M, 128) * cdiv(a.N, 128) * a.split_k >= 512) return launch_cfg<AK, BK, 128, 128, EC>(a, s);
+  constexpr bool heavy_epi = EC >= 0 && (ec_act(EC) == 2 || ec_act(EC) == 4) && (EC & ED) != 0;
+  if (!heavy_epi && cdiv(a.M, 128) * cdiv(a.N, 128) * a.split_k >= 512) return launch_cfg<AK, BK, 128, 128, EC>(a, s);
   return launch_cfg<AK, BK, 64, 64, EC>(a, s);
 }
 

@@ -353,7 +353,7 @@ class SASEngine:
 
     @property
     def fused_head(self):
-        """True when forward/backward take the fused bf16 path (head.hip, rowfused.hip, itemgrad.hip)."""
+        """True when forward/backward take the fused bf16 path (head.hip, rowchain.hip, itemgrad.hip)."""
         return ops.sas_block_fused_ok(self.d, self.dt)
 
     # ---- backward ------------------------------------------------------------------
@@ -508,7 +508,7 @@ class SASEngine:
         return self._wT
 
     def _backward_blocks_fused(self, s, dx, grad, extra_segs=(), tail=None, pos=None):
-        """SAS blocks' backward with rs_sas_block_out_bwd / rs_sas_block_in_bwd (rowfused.hip) for the
+        """SAS blocks' backward with rs_sas_block_out_bwd / rs_sas_block_in_bwd (rowchain.hip) for the
         row-local chains; then ALL ten weight gradients and the four LayerNorm affine partial sets in
         one grouped GEMM launch + one grouped reduction (rs_wgrad_grouped, wgrad.hip).  Returns the
         gradient at the embedding output.  tail(dx): work on that gradient alone (the item table's

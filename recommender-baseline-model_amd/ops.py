@@ -458,7 +458,7 @@ def seed_advance(seed_base):
     call("rs_seed_advance", ptr(seed_base), stream())
 
 
-# ---- fused SAS sublayers (rowfused.hip) ----------------------------------------------------
+# ---- fused SAS sublayers (rowchain.hip) ----------------------------------------------------
 def sas_block_fused_ok(d, dtype):
     """rs_sas_block_in/out cover bf16 with d in {64, 128}; anything else runs the unfused kernels."""
     return dtype == torch.bfloat16 and d in (64, 128)
