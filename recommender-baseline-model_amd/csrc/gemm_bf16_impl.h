@@ -461,7 +461,22 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs a) {
   const int64_t Mb = (!AK && a.epi.rows_dev) ? min(a.M, (int64_t)*a.epi.rows_dev) : a.M;
   unsigned bid = blockIdx.x;
   unsigned tiles_m = gridDim.x / tiles_n;
-  {
+  int z = blockIdx.z;
+  if (gridDim.z > 1) {
+    // split-K: the tiles of one k slice share its B columns (the vocabulary GEMM dh = dlogits.E: a 16k-row
+    // slice of the 512 MB weight per split), so deal whole k slices to XCDs -- workgroups are dispatched
+    // x-fastest then z, round robin over the 8 XCDs -- instead of every XCD fetching every slice (cfg5:
+    // 1.32 -> 1.30 ms; the MALL serves most of the re-reads)
+    const unsigned tot = gridDim.x * gridDim.z, L = blockIdx.x + gridDim.x * blockIdx.z;
+    const unsigned q = tot >> 3, r = tot & 7, x = L & 7;
+    const unsigned lg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (L >> 3);
+    z = (int)(lg / gridDim.x);
+    bid = lg - (unsigned)z * gridDim.x;
+    if (!AK && a.epi.rows_dev) {
+      tiles_m = (unsigned)((Mb + BM - 1) / BM);
+      if (bid >= tiles_m * tiles_n) return;
+    }
+  } else {
     // a device row count (compacted rows) leaves only the first cdiv(Mb, BM) row tiles live: remap over
     // those, so the live tiles spread over all XCDs instead of the first few XCDs' contiguous ranges
     unsigned nwg = gridDim.x;
@@ -485,7 +500,6 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs a) {
     tn = bid - tm * tiles_n;
   }
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
-  const int z = blockIdx.z;
   const int64_t Kb = (AK && a.epi.rows_dev) ? min(a.K, (int64_t)*a.epi.rows_dev) : a.K;
   if (m0 >= Mb) return;
   const int64_t kbeg = (int64_t)z * a.k_per_split;

@@ -17,10 +17,12 @@
 //   * S^T = E_tile . h_tile^T is accumulated transposed (vocabulary on the accumulator's row axis), so
 //     a lane holds 4 consecutive vocabulary entries of one row: per-row softmax statistics reduce in
 //     registers + 2 shuffles, and dlogits leave as 8-byte LDS writes;
-//   * bwd: dlogits go to LDS [rows][vocab] (and, 16-B coalesced, to the global dlogits operand of dh);
-//     dE_tile [128][d] += dlogits^T . h accumulates in registers over all row tiles (both operands
-//     read k-major with ds_read_b64_tr_b16), db rides on extra MFMAs against a ones operand; dE / db
-//     are written once per vocabulary tile -- no dlogits re-read for the weight gradient.
+//   * bwd: dlogits go to LDS [rows][vocab] and, 16-B coalesced, to the global dlogits operand of
+//     dh = dlogits.E (split-K rs_gemm) and dE = dlogits^T.h, db = colsum (rs_linear_wgrad).  Forming dE here
+//     instead (a second pass over each row tile's h stages, dE^T accumulated in registers per vocabulary
+//     tile, db from the dlogits in LDS) was built and measured: the 128 x d fp32 dE tile is 64 more
+//     registers per lane on a kernel already near 256 with 8 waves, and it spilled 125 (d = 256) / 64
+//     (d = 128) -- not kept.
 // The fwd partials have exactly the layout of vocab_ce.hip's EC_CE_PART epilogue, so ce_tiles_kernel /
 // ce_sum_kernel finish the loss unchanged (the label logit is formed there as <h, E[label]> + b).
 //

@@ -334,7 +334,8 @@ def adam_prepare_step(p, g, m, v, p_bf16, state, hyper, zero_grad=False, grad_di
         td, host, wt = transposed
         nt = len(host)
         for rows, cols, off, lds, doff, ldd in host:
-            if lds % 4 or off % 4 or off + rows * lds > (p.numel() // 4) * 4 or doff + (cols - 1) * ldd + rows > wt.numel():
+            if lds % 4 or off % 4 or off + rows * lds > (p.numel() // 4) * 4 or doff + (cols - 1) * ldd + rows > wt.numel() \
+                    or rows * lds >= 2 ** 31:
                 raise ValueError("adam_prepare_step: transposed matrix outside the buffers or misaligned")
         if p_bf16 is None:
             raise ValueError("adam_prepare_step: transposed copies need the bf16 output")

@@ -21,7 +21,8 @@ from rbm_amd import ops  # noqa: E402
 
 SHAPES = {"cfg2": dict(B=128, T=200, d=128, V=3416, H=1, ff=128),
           "cfg3": dict(B=64, T=200, d=256, V=26744, H=2, ff=1024),
-          "cfg4": dict(B=128, T=50, d=128, V=54542, H=1, ff=128)}
+          "cfg4": dict(B=128, T=50, d=128, V=54542, H=1, ff=128),
+          "cfg5": dict(B=64, T=200, d=256, V=1000000, H=2, ff=1024)}
 
 
 def timeit(fn, reps):
@@ -162,6 +163,11 @@ def main():
         dh = rn(R, d)
         run("vocab dgrad",lambda: ops.linear_dgrad(dl, Wo, dh), R * V1 * es + V1 * d * es,
             2 * R * V1 * d)
+        sk = int(max(1, min(64, -(-V1 // 2048))))
+        slab_dh = torch.empty(sk * R * d, device=dev)
+        run(f"vocab dh split-K={sk}", lambda: ops.gemm(dl, Wo, slab_dh, R, d, V1, False, True, ops.epilogue(),
+                                                        split_k=sk, slab=slab_dh), R * V1 * es + V1 * d * es,
+            2 * R * V1 * d)
         dWo = torch.zeros(V1, d, device=dev)
         slab_o = torch.empty(ops.wgrad_slab_numel(R, V1, d), device=dev)
         run("vocab wgrad+bias",lambda: ops.linear_wgrad(dl, h, dWo, slab_o, db=bo),
@@ -220,6 +226,18 @@ def main():
     st144 = torch.zeros(144, dtype=torch.float64, device=dev)
     run(f"adam_prepare_step ({n} params)", lambda: ops.adam_prepare_step(p, gg, m1, v1, pbf, st144, hy, zero_grad=True),
         n * 4 * 8 + n * 2)
+    if a.config in ("cfg2", "cfg4"):
+        # the SAS step's form: + the transposed bf16 block weights (rs_transpose_bf16's descriptors, 2 blocks x
+        # in_proj / out_proj / conv1 / conv2 at the flat buffer's offsets)
+        dd, L = c["d"], 2
+        desc, off = [], n - L * 6 * dd * dd
+        for i in range(L):
+            for rows_, o in ((3 * dd, 0), (dd, 3 * dd * dd), (dd, 4 * dd * dd), (dd, 5 * dd * dd)):
+                desc.append([rows_, dd, off + i * 6 * dd * dd + o, dd, i * 6 * dd * dd + o, rows_])
+        td = torch.tensor(desc, dtype=torch.int64, device=dev)
+        wT = torch.empty(L * 6 * dd * dd, dtype=torch.bfloat16, device=dev)
+        run(f"adam_prepare_step +transposes ({n} params)", lambda: ops.adam_prepare_step(
+            p, gg, m1, v1, pbf, st144, hy, zero_grad=True, transposed=(td, desc, wT)), n * 4 * 8 + n * 2)
     print(f"{'op':45s} {'us':>9s} {'GB/s':>9s} {'TFLOP/s':>8s}")
     for name, us, gbs, tf in rows:
         print(f"{name:45s} {us:9.2f} {gbs:9.1f} {tf:8.2f}")
