@@ -54,7 +54,7 @@ __device__ __forceinline__ void adam4(int64_t i, float4 pp, float4 gg, float4 mm
                                       __bf16* __restrict__ pb, AdamElem h,
                                       float step_size, float bc2s, float gs, int zero_grad,
                                       const int64_t* __restrict__ tdesc, int ntd, int64_t tbase,
-                                      __bf16* __restrict__ wT) {
+                                      __bf16* __restrict__ wT, int64_t tlo, int64_t thi) {
   float* P = &pp.x; float* G = &gg.x; float* Mv = &mm.x; float* Vv = &vv.x;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -75,7 +75,10 @@ __device__ __forceinline__ void adam4(int64_t i, float4 pp, float4 gg, float4 mm
     reinterpret_cast<bf16x4*>(pb)[i] = o;
     // transposed bf16 copies of matrices inside the buffer (the SAS backward's [in][out] block weights,
     // rs_transpose_bf16's desc layout): the 4 elements share a row (host checks lds % 4 == 0)
-    for (int k = 0; k < ntd; ++k) {
+    // the descriptors' element span [tlo, thi) first: most of the buffer (the tables) is outside every matrix
+    const int64_t e0 = tbase + 4 * i;
+    const int nk = (e0 >= tlo && e0 < thi) ? ntd : 0;
+    for (int k = 0; k < nk; ++k) {
       const int64_t* dk = tdesc + 6 * k;
       const int64_t rel = tbase + 4 * i - dk[2];
       if (rel >= 0 && rel < dk[0] * dk[3]) {
@@ -118,6 +121,15 @@ __global__ __launch_bounds__(256) void adam_step_kernel(int64_t n, float* __rest
     bc2s = (float)state[2];
     gs = (float)state[3];
   }
+  int64_t tlo = 0, thi = 0;
+  if (BF16OUT && ntd > 0) {
+    tlo = INT64_MAX;
+    for (int k = 0; k < ntd; ++k) {
+      const int64_t* dk = tdesc + 6 * k;
+      tlo = min(tlo, dk[2]);
+      thi = max(thi, dk[2] + dk[0] * dk[3]);
+    }
+  }
   const int64_t n4 = n / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -134,7 +146,7 @@ __global__ __launch_bounds__(256) void adam_step_kernel(int64_t n, float* __rest
 #pragma unroll
     for (int u = 0; u < U; ++u)
       adam4<BF16OUT>(i + u * stride, pq[u], gq[u], mq[u], vq[u], p, g, m, v, pb, h, step_size, bc2s, gs,
-                     zero_grad, tdesc, ntd, tbase, wT);
+                     zero_grad, tdesc, ntd, tbase, wT, tlo, thi);
   }
   for (; i < n4; i += stride) {
     float4 pp = reinterpret_cast<float4*>(p)[i];
@@ -142,7 +154,7 @@ __global__ __launch_bounds__(256) void adam_step_kernel(int64_t n, float* __rest
     float4 mm = reinterpret_cast<float4*>(m)[i];
     float4 vv = reinterpret_cast<float4*>(v)[i];
     adam4<BF16OUT>(i, pp, gg, mm, vv, p, g, m, v, pb, h, step_size, bc2s, gs, zero_grad, tdesc, ntd,
-                   tbase, wT);
+                   tbase, wT, tlo, thi);
   }
   // tail
   if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
@@ -369,7 +381,10 @@ int rs_adam_prepare_step_loss(int64_t n, float* p, float* g, float* m, float* v,
   if (n <= 0 || !state || ((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16) return RS_ERR_ARG;
   if (!loss_out != !loss_sum || (loss_out && !grad_divisor)) return RS_ERR_ARG;
   if (ntd < 0 || (ntd > 0 && (!tdesc || !wT || !p_bf16))) return RS_ERR_ARG;
-  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(cdiv(n / 4, 256), 8192));
+  // at most 2048 workgroups: every workgroup pays an arrival atomic (the PREP step-count publication); 7k of
+  // them cost ~13 us at 7.4M parameters (kbench: 56 -> 40 us for the launch; flat at 0.66M and 20M; the
+  // cfg4 step within noise, 560k vs 567k seq/s)
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(cdiv(n / 4, 256), 2048));
   hipStream_t s = (hipStream_t)stream;
   if (p_bf16)
     ADAM_LAUNCH(true, true, dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
