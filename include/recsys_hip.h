@@ -494,6 +494,10 @@ int rs_item_index_build(int nsrc, const int64_t* keys0, const int64_t* keys1, co
 int rs_item_grad(const void* ws, int nsrc, int64_t rows, int64_t table_rows, int64_t d, const void* dx, float scale,
                  float drop_p, uint64_t salt, const uint64_t* seed_base, const void* f, const float* w1,
                  const float* w2, float* dtable, void* stream);
+/* The same for fp32 dx, f (the fp32 parity path, any d): one workgroup per table row, entries in sorted order. */
+int rs_item_grad_f32(const void* ws, int nsrc, int64_t rows, int64_t table_rows, int64_t d, const float* dx, float scale,
+                     float drop_p, uint64_t salt, const uint64_t* seed_base, const float* f, const float* w1,
+                     const float* w2, float* dtable, void* stream);
 
 /* ---- fused SASRec output head (head.hip), bf16, d in {64, 128, 256} ----------------------------
  * Forward (sas.py:87-100 + BCE of trainers/sas.py:40-49): f = LN_last(x) [f, mean, rstd saved];

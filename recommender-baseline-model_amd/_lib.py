@@ -119,6 +119,7 @@ SIGNATURES = {
     "rs_sas_head_finish": [i64, vp, vp, vp, vp],
     "rs_sas_head_bwd": [i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "rs_item_grad": [vp, i32, i64, i64, i64, vp, f32, f32, u64, vp, vp, vp, vp, vp, vp],
+    "rs_item_grad_f32": [vp, i32, i64, i64, i64, vp, f32, f32, u64, vp, vp, vp, vp, vp, vp],
     "rs_wgrad_grouped_pos": [i32, C.POINTER(WgradProblem), i64, i64, vp, i64, i32, C.POINTER(ReduceSegment),
                              vp, i64, vp, i64, f32, u64, vp, vp, vp],
     "rs_wgrad_grouped_pos_stats": [i32, C.POINTER(WgradProblem), i64, i64, vp, i64, i32, C.POINTER(ReduceSegment),

@@ -575,6 +575,36 @@ int rs_item_index_build(int nsrc, const int64_t* keys0, const int64_t* keys1, co
 
 }  // extern "C"
 
+namespace ig {
+// fp32 parity path: one workgroup per table row (key v >= 1), its entries summed in the index's sorted order --
+// deterministic like the bf16 chunk kernels (which the fp32 path's float-atomic scatter was not: each fp32 run of
+// a training curve was its own chaotic draw), with the atomic kernels' per-term arithmetic (embedding.hip)
+__global__ __launch_bounds__(256) void item_rows_f32_kernel(GradArgs a, const float* __restrict__ dx,
+                                                            const float* __restrict__ f, int64_t d) {
+  const int64_t v = (int64_t)blockIdx.x + 1;
+  const int b = a.start[v], e = a.start[v + 1];
+  if (b >= e) return;
+  const uint64_t seed = eff_seed(a.salt, a.seed_base);
+  for (int64_t c = threadIdx.x; c < d; c += blockDim.x) {
+    float acc = 0.f;
+    for (int k = b; k < e; ++k) {
+      const int64_t ent = a.sv[k];
+      const int src = (int)(ent / a.rows);
+      const int64_t m = ent - src * a.rows;
+      float t;
+      if (src == 0) {
+        t = dx[m * d + c] * a.scale;
+        if (a.drop_p > 0.f) t *= drop_mul(a.drop_p, seed, (uint64_t)(m * d + c));
+      } else {
+        t = (src == 1 ? a.w1[m] : a.w2[m]) * f[m * d + c];
+      }
+      acc += t;
+    }
+    a.dtable[v * d + c] += acc;
+  }
+}
+}  // namespace ig
+
 static int item_grad_args(const void* ws, int nsrc, int64_t rows, int64_t table_rows, int64_t d, const void* dx,
                           float scale, float drop_p, uint64_t salt, const uint64_t* seed_base, const void* f,
                           const float* w1, const float* w2, float* dtable, ig::GradArgs& a, ig::Layout& L) {
@@ -612,6 +642,20 @@ int rs_item_grad(const void* ws, int nsrc, int64_t rows, int64_t table_rows, int
   } else {
     return RS_ERR_UNSUPPORTED;
   }
+  return (int)hipGetLastError();
+}
+
+int rs_item_grad_f32(const void* ws, int nsrc, int64_t rows, int64_t table_rows, int64_t d, const float* dx, float scale,
+                     float drop_p, uint64_t salt, const uint64_t* seed_base, const float* f, const float* w1,
+                     const float* w2, float* dtable, void* stream) {
+  ig::GradArgs a;
+  ig::Layout L;
+  if (int e = item_grad_args(ws, nsrc, rows, table_rows, d, dx, scale, drop_p, salt, seed_base, f, w1, w2, dtable,
+                             a, L))
+    return e;
+  if (d <= 0 || table_rows < 2) return table_rows < 2 ? 0 : RS_ERR_ARG;
+  hipLaunchKernelGGL(ig::item_rows_f32_kernel, dim3((unsigned)(table_rows - 1)), dim3(d >= 256 ? 256 : (d >= 128 ? 128 : 64)),
+                     0, (hipStream_t)stream, a, dx, f, d);
   return (int)hipGetLastError();
 }
 

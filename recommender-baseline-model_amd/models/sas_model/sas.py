@@ -418,8 +418,12 @@ class SASEngine:
                 split("dense")          # every parameter gradient is final (data-parallel overlap)
             return len(stats) > 3
         df = e("df", (M, d))
+        # the item table's gradient (lookup + tied logits) by the inverted index after the blocks (rs_item_grad /
+        # rs_item_grad_f32): one writer per table row in a fixed order, so the unfused (fp32 parity) step is
+        # deterministic -- the float-atomic scatter made every fp32 curve its own chaotic draw
+        by_index = self.dt == torch.float32 or d in (64, 128, 256)   # else (bf16, other d): atomic scatter
         ops.sampled_logits_bwd(s["f"], self.W("item_emb.weight"), s["pos"], s["neg"], dpl, dnl, df,
-                               G("item_emb.weight"))
+                               None if by_index else G("item_emb.weight"))
         dx = e("dx", (M, d))
         ops.layernorm_bwd(s["xL"], df, self.Wf("last_layernorm.weight"), s["muf"], s["rf"], LN_EPS, dx,
                           G("last_layernorm.weight"), G("last_layernorm.bias"), wln, 0)
@@ -460,8 +464,14 @@ class SASEngine:
                               LN_EPS, dxi, G(f"attention_layernorms.{i}.weight"),
                               G(f"attention_layernorms.{i}.bias"), wln, 0, accumulate=True)
             dx = dxi
-        ops.embed_bwd(0, ids, T, dx, math.sqrt(d), p, self.salt["emb"], sb, G("item_emb.weight"),
+        ops.embed_bwd(0, ids, T, dx, math.sqrt(d), p, self.salt["emb"], sb, None if by_index else G("item_emb.weight"),
                       G("pos_emb.weight"))
+        if by_index:
+            V1 = self.flat.shapes["item_emb.weight"][0]
+            iws = self.ws.get("itemidx", (ops.item_index_ws_bytes(3, M, V1, d),), torch.uint8)
+            ops.item_index_build([ids, s["pos"], s["neg"]], V1, d, iws)
+            ops.item_grad(iws, 3, M, dx, math.sqrt(d), p, self.salt["emb"], sb, s["f"], dpl, dnl,
+                          G("item_emb.weight"))
 
     def _side_prologue(self, ids, pos, neg, after=None):
         """Work of the fused backward that depends only on the batch's keys and the weights, issued on a

@@ -636,7 +636,9 @@ def item_index_build(keys, table_rows, d, ws):
 
 def item_grad(ws, nsrc, rows, dx, scale, drop_p, salt, seed_base, f, w1, w2, dtable):
     table_rows, d = dtable.shape
-    call("rs_item_grad", ptr(ws), nsrc, rows, table_rows, d, ptr(dx), scale, drop_p, salt, ptr(seed_base),
+    # fp32 (the parity path): one workgroup per table row; bf16: the chunked kernels (d in {64, 128, 256})
+    call("rs_item_grad_f32" if dx.dtype == torch.float32 else "rs_item_grad", ptr(ws), nsrc, rows, table_rows, d,
+         ptr(dx), scale, drop_p, salt, ptr(seed_base),
          ptr(f) if f is not None else None, ptr(w1) if w1 is not None else None,
          ptr(w2) if w2 is not None else None, ptr(dtable), stream())
 
