@@ -27,3 +27,10 @@ for r in sel:
     prev = max(prev or 0, e)
     busy += e - s
 print(f"step span {(int(sel[-1]['End_Timestamp'])-t0)/1e3:.1f} us, kernel time {busy/1e3:.1f} us")
+# the true step period: optimizer end to optimizer end over consecutive clean steps (includes the gap before each
+# step's first kernel, which the span above does not)
+per = sorted((int(rows[ad[k]]["End_Timestamp"]) - int(rows[ad[k - 1]]["End_Timestamp"])) / 1e3
+             for k in clean if k - 1 in clean or k - 1 >= 1)
+if per:
+    print(f"optimizer-to-optimizer period over {len(per)} steps: median {per[len(per) // 2]:.1f} us, "
+          f"min {per[0]:.1f}, max {per[-1]:.1f}")
