@@ -79,7 +79,7 @@ def allreduce_grads(flat_grad, group=None, bucket_numel=None):
 
     bucket_numel: split into buckets of that many floats (None = one call); buckets are issued
     back to back on the current stream, RCCL pipelines them over the xGMI links."""
-    if world() == 1:
+    if world(group) == 1:
         return flat_grad
     if not bucket_numel or bucket_numel >= flat_grad.numel():
         dist.all_reduce(flat_grad, group=group)
