@@ -402,7 +402,9 @@ static hipError_t ln_bwd_t(const void* X, int64_t ldx, const void* dY, int64_t l
     }
     if (lpr) {
       const int64_t rpb = 4 * (64 / lpr);
-      const int nb = (int)std::min<int64_t>(LN_BWD_BLOCKS / 2, cdiv(M, rpb * 4));
+      // every row group's rows in ONE iteration of 4 (one dependent round trip per workgroup): up to 512
+      // workgroups (cfg3, 12,800 rows of 256: 400 -- 256 ran two iterations each)
+      const int nb = (int)std::min<int64_t>(LN_BWD_BLOCKS, cdiv(M, rpb * 4));
 #define LNBV1D(LPR, NCH, VAR, ACC, DR)                                                                      \
   hipLaunchKernelGGL((ln_bwd_v_kernel<T, LPR, NCH, VAR, ACC, DR>), dim3(nb), dim3(256), 0, s, x, ldx, dy, lddy, M, \
                      d, gamma, mean, rinv, eps, dx, lddx, ws, dr)
@@ -468,7 +470,7 @@ int64_t rs_layernorm_bwd_nparts(int dtype, int64_t M, int64_t d) {
   const int64_t lpr = (cpr == 4 || cpr == 8 || cpr == 16 || cpr == 32 || cpr == 64) ? cpr : cpr == 128 ? 64 : 0;
   if (!lpr) return 0;
   const int64_t rpb = 4 * (64 / lpr);
-  return std::min<int64_t>(LN_BWD_BLOCKS / 2, cdiv(M, rpb * 4));
+  return std::min<int64_t>(LN_BWD_BLOCKS, cdiv(M, rpb * 4));
 }
 
 int rs_layernorm_bwd_drop(int dtype, int variant, const void* X, int64_t ldx, const void* dY, int64_t lddy,

@@ -124,8 +124,11 @@ __global__ __launch_bounds__(NTH, 1) void vhead_kernel(Args a) {
   const int v0w = wm * (BV / 4);
   const int64_t Rl = a.rows_dev ? min(a.R, (int64_t)*a.rows_dev) : a.R;
   const int nmt = (int)((Rl + BR - 1) / BR);
-  if (nmt == 0) return;
-  const int NIT = nmt * C::NKS;
+  // row tiles of this workgroup: all of them, or (small vocabularies: fewer vocabulary tiles than CUs) the
+  // gridDim.y-th share blockIdx.y -- every (row, vocabulary tile) still formed by exactly one workgroup
+  const int mtb = (int)((int64_t)nmt * blockIdx.y / gridDim.y), mte = (int)((int64_t)nmt * (blockIdx.y + 1) / gridDim.y);
+  if (mte <= mtb) return;
+  const int NIT = (mte - mtb) * C::NKS;
 
   float sc = 0.f;
   if constexpr (BWD) sc = (a.dloss ? *a.dloss : 1.f) / *a.count;
@@ -136,7 +139,7 @@ __global__ __launch_bounds__(NTH, 1) void vhead_kernel(Args a) {
   bf16x8 hr[PF][C::HPT];
   auto h_load = [&](auto slot, int it) {
     constexpr int sl = decltype(slot)::value;
-    const int mt = it / C::NKS, ks = it - mt * C::NKS;
+    const int mo = it / C::NKS, ks = it - mo * C::NKS, mt = mtb + mo;
 #pragma unroll
     for (int c = 0; c < C::HPT; ++c) {
       const int ch = tid + NTH * c, r = ch / (BK / 8), k8 = (ch % (BK / 8)) * 8;
@@ -200,7 +203,7 @@ __global__ __launch_bounds__(NTH, 1) void vhead_kernel(Args a) {
     if (2 < NIT) h_load(std::integral_constant<int, 2 % PF>{}, 2);
     static_assert(PF == 3, "prologue loads PF - 1 stages ahead");
     h_store(std::integral_constant<int, 0>{}, 0);
-    meta_store(0);
+    meta_store(mtb);
     __syncthreads();
 
     f32x4 acc[FV][4];
@@ -208,7 +211,7 @@ __global__ __launch_bounds__(NTH, 1) void vhead_kernel(Args a) {
     // stage it & 1; stage it + 1 (slot (u + 1) % PF) -> the other LDS buffer; stage it + PF -> slot u
     auto body = [&](int it, auto U) {
       constexpr int u = decltype(U)::value;
-      const int mt = it / C::NKS, ks = it - mt * C::NKS;
+      const int mo = it / C::NKS, ks = it - mo * C::NKS, mt = mtb + mo;
       if (ks == 0) {
 #pragma unroll
         for (int i = 0; i < FV; ++i)
@@ -328,7 +331,7 @@ __global__ __launch_bounds__(NTH, 1) void vhead_kernel(Args a) {
         }
       }
       __syncthreads();                         // labs / red / Ds readers of this row tile are done
-      if (mt + 1 < nmt) meta_store(mt + 1);    // (visible after the next stage's barrier)
+      if (mt + 1 < mte) meta_store(mt + 1);    // (visible after the next stage's barrier)
       if constexpr (C::NKS == 1) __syncthreads();
     };
     for (int it0 = 0; it0 < NIT; it0 += PF) {
@@ -351,8 +354,12 @@ hipError_t launch(Args& a, hipStream_t s) {
   }
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const int64_t grid = std::min<int64_t>(cdiv(a.V1, BV), (int64_t)cus);
-  hipLaunchKernelGGL((vhead_kernel<DK, BV, BWD>), dim3((unsigned)grid), dim3(NTH), C::LDS, s, a);
+  const int64_t nvt = cdiv(a.V1, BV);
+  const int64_t grid = std::min<int64_t>(nvt, (int64_t)cus);
+  // fewer vocabulary tiles than CUs (cfg3: 105 / 209 of 256): split the row tiles over gridDim.y groups so that
+  // up to one workgroup per CU runs (the 1M-vocabulary shapes keep one group, persistent over vocabulary tiles)
+  const int64_t gy = std::max<int64_t>(1, std::min<int64_t>(cdiv(a.R, BR), (int64_t)cus / nvt));
+  hipLaunchKernelGGL((vhead_kernel<DK, BV, BWD>), dim3((unsigned)grid, (unsigned)gy), dim3(NTH), C::LDS, s, a);
   return hipGetLastError();
 }
 
