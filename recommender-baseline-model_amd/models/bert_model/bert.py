@@ -30,7 +30,7 @@ import torch.nn as nn
 
 from ... import ops
 from ...engine_util import Workspace, as_ids, compute_dtype, require_cuda, site_salt
-from ...flat import FlatParams
+from ...flat import ALIGN, FlatParams
 
 LN_EPS = 1e-6  # utils/layer_norm.py:8
 
@@ -374,6 +374,21 @@ class BERTEngine:
             wslab = self.ws.get(f"wslab{c}", (ops.wgrad_grouped_slab_numel(shapes, M, rows),), torch.float32)
             ops.wgrad_grouped(chunk, M, rows, wslab, extra=ln_segs if c == 0 else ())
 
+    def overwritten_grads(self):
+        """(lo, hi) flat range whose gradient the fused step writes whole every step (out.weight then out.bias,
+        train_loss_and_backward): the optimizer leaves it unzeroed (FusedAdam.step keep) when it is large enough
+        for the saved sweep (8 B per element) to pay for the extra launch -- the 1M-item vocabulary (256M
+        elements), not the 27k one."""
+        f = self.flat
+        ow, ob = f.offsets["out.weight"], f.offsets["out.bias"]
+        A = ALIGN   # FlatParams pads every parameter to a multiple of ALIGN floats
+        end = ob + -(-self.V1 // A) * A
+        if getattr(self, "vocab_shard", None) is not None or self.V1 * self.d < (1 << 24):
+            return None
+        if ob != ow + -(-self.V1 * self.d // A) * A or end > f.numel or ow % 4 or end % 4:
+            return None
+        return ow, min(end, f.numel)
+
     def _det_table(self):
         return self.dt == torch.bfloat16 and self.d in (64, 128, 256)
 
@@ -477,8 +492,10 @@ class BERTEngine:
                 dl = self.ws.get("dlogits", (cap, self.V1p), self.dt)[:, :self.V1]
             ops.ce_bwd(logits, lab, count, None, wce, dl, rows_dev=cnt)
         slab = self.ws.get("slab_out", (ops.wgrad_slab_numel(cap, self.V1, d),), torch.float32)
+        # out.weight / out.bias get their whole gradient here: written, not accumulated (no read of the old
+        # values; see overwritten_grads)
         ops.linear_wgrad(dl, hl, self.flat.view("out.weight", grad), slab, db=self.flat.view("out.bias", grad),
-                         rows_dev=cnt)
+                         rows_dev=cnt, accumulate=False)
         if split is not None:
             # join the side stream's token index here: a captured graph segment must not end with forked work
             if s.get("side") is not None and s["side"][0] is not None:

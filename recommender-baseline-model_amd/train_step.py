@@ -50,22 +50,29 @@ class FusedAdam:
         """StepLR hook (BS/trainers/base.py:40,87): lives on the device, so graph replays see it."""
         self.hyper[0] = lr
 
-    def step(self, grad_divisor=None, seed_base=None, ranges=None, transposed=None, loss=None):
+    def step(self, grad_divisor=None, seed_base=None, ranges=None, transposed=None, loss=None, keep=None):
         """One Adam update; also clears the gradient buffer (the next step accumulates from zero) and
         advances the dropout step seed when given.  ranges: [(lo, hi)] flat slices to update (default all; a
         vocabulary-sharded rank skips the output rows other ranks own).  loss = (sum, out): out = sum / grad_divisor
-        in the first launch."""
+        in the first launch.  keep = (lo, hi): a slice the backward OVERWRITES every step (BERT's out.weight /
+        out.bias with a large vocabulary): updated by its own launch that leaves its gradient in place -- no zero
+        written by this sweep, none read back by the next step's dE GEMM (2 GB per step at 1M items)."""
         f = self.flat
-        for k, (lo, hi) in enumerate(ranges or [(0, f.numel)]):
+        segs = [(lo, hi, True) for lo, hi in (ranges or [(0, f.numel)])]
+        if keep is not None and ranges is None:
+            klo, khi = keep
+            assert 0 < klo < khi <= f.numel and klo % 4 == 0 and khi % 4 == 0, keep
+            segs = [(0, klo, True), (klo, khi, False)] + ([(khi, f.numel, True)] if khi < f.numel else [])
+        for k, (lo, hi, zg) in enumerate(segs):
             bf = f.bf16[lo:hi] if f.bf16 is not None else None
             if k == 0:   # the first range's launch also prepares the step's scalars (rs_adam_prepare_step)
                 ops.adam_prepare_step(f.data[lo:hi], f.grad[lo:hi], self.m[lo:hi], self.v[lo:hi], bf, self.state,
-                                      self.hyper, zero_grad=True, grad_divisor=grad_divisor, seed_base=seed_base,
+                                      self.hyper, zero_grad=zg, grad_divisor=grad_divisor, seed_base=seed_base,
                                       transposed=transposed if lo == 0 else None,
                                       loss_sum=loss[0] if loss else None, loss_out=loss[1] if loss else None)
             else:
                 ops.adam_step(f.data[lo:hi], f.grad[lo:hi], self.m[lo:hi], self.v[lo:hi], bf, self.state,
-                              self.hyper, zero_grad=True)
+                              self.hyper, zero_grad=zg)
 
 
 class FusedTrainStep:
@@ -267,17 +274,18 @@ class FusedTrainStep:
             self.opt.step(seed_base=sb, ranges=self._adam_ranges())
         else:
             tr = self.engine.transposed_spec() if hasattr(self.engine, "transposed_spec") else None
+            kp = self.engine.overwritten_grads() if hasattr(self.engine, "overwritten_grads") else None
             if self.dp:
                 lsum, cnt = self.flat.aux[dpx.LOSS_SUM:dpx.LOSS_SUM + 1], self.flat.aux[dpx.COUNT:dpx.COUNT + 1]
                 if self.l2:
                     torch.div(lsum, cnt, out=self.loss_val)
                     self._l2(self.loss_val, scale=cnt)
-                    self.opt.step(grad_divisor=cnt, seed_base=sb, transposed=tr)
+                    self.opt.step(grad_divisor=cnt, seed_base=sb, transposed=tr, keep=kp)
                 else:   # the loss division rides in the optimizer's launch
-                    self.opt.step(grad_divisor=cnt, seed_base=sb, transposed=tr, loss=(lsum, self.loss_val))
+                    self.opt.step(grad_divisor=cnt, seed_base=sb, transposed=tr, loss=(lsum, self.loss_val), keep=kp)
             else:
                 self._l2(self.loss_out[2:3])
-                self.opt.step(seed_base=sb, transposed=tr)
+                self.opt.step(seed_base=sb, transposed=tr, keep=kp)
 
     # ---------------------------------------------------------------- one step
     def step(self, *batch):

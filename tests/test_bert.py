@@ -261,3 +261,35 @@ def test_bert_cfg5_token_table_gradient_touches_batch_rows_only():
     assert gt[0].abs().max().item() == 0.0
     go = tr.flat.view("out.weight", tr.flat.grad).cpu()
     assert (go.abs().sum(1) > 0).float().mean().item() > 0.99
+
+
+@pytest.mark.gpu
+def test_bert_large_vocab_overwritten_head_grads_match_zeroed():
+    """Large vocabulary (V * d >= 2^24): out.weight / out.bias get their whole gradient written every step (dE GEMM
+    without accumulate) and the optimizer updates that range in its own launch without zeroing it
+    (FusedAdam.step keep, BERTEngine.overwritten_grads).  Three steps must give the same bits as the same steps
+    with the range zeroed like the rest of the buffer."""
+    import rbm_amd.data as synth
+    from rbm_amd.train_step import FusedTrainStep
+    V, T, B = 70000, 40, 8
+    rng = np.random.default_rng(3)
+    batches = [tuple(torch.from_numpy(t).cuda() for t in synth.bert_batch(rng, B, T, V, mask_prob=0.2))
+               for _ in range(3)]
+    params = []
+    for keep in (True, False):
+        torch.manual_seed(0)     # the engine draws its dropout-site salts from torch's generator
+        m = _bert(V, T, 256, 1, 2, 0.1, "bf16", seed=11)
+        tr = FusedTrainStep(m, lr=1e-3, max_labelled=128)
+        assert (tr.engine.overwritten_grads() is not None) or not keep
+        if not keep:
+            tr.engine.overwritten_grads = lambda: None
+        tr.engine.seed_base.fill_(99)
+        for tok, lab in batches:
+            tr.step(tok, lab)
+        torch.cuda.synchronize()
+        params.append(tr.flat.data.clone())
+        if keep:   # the kept range holds the last step's gradient, the rest is zero
+            lo, hi = tr.engine.overwritten_grads()
+            assert float(tr.flat.grad[lo:hi].abs().sum()) > 0
+            assert float(tr.flat.grad[:lo].abs().sum()) == 0
+    assert torch.equal(params[0], params[1])
