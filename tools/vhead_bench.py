@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--d", type=int, default=256)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--only", default="fwd,bwd,wgrad,dgrad")
+    ap.add_argument("--sk", default="", help="','-separated split-K counts to time the dgrad at (default: the step's)")
     a = ap.parse_args()
     g = torch.Generator(device="cuda").manual_seed(0)
     R, V1, d = a.R, a.V + 1, a.d
@@ -63,11 +64,11 @@ def main():
         us = timeit(lambda: ops.linear_wgrad(dl, h, dE, slab, db=db), a.reps)
         print(f"wgrad dE=dl^T h  {us:9.1f} us  {fl / us / 1e6:7.1f} TFLOP/s")
     if "dgrad" in only:
-        sk = int(max(1, min(64, -(-V1 // 2048))))
-        slab_d = torch.empty(sk * R * d, device="cuda")
-        us = timeit(lambda: ops.gemm(dl, E, slab_d, R, d, V1, False, True, ops.epilogue(), split_k=sk, slab=slab_d),
-                    a.reps)
-        print(f"dgrad dh=dl E    {us:9.1f} us  {fl / us / 1e6:7.1f} TFLOP/s (split-K {sk} slabs, reduction not incl.)")
+        for sk in ([int(x) for x in a.sk.split(",")] if a.sk else [int(max(1, min(64, -(-V1 // 2048))))]):
+            slab_d = torch.empty(sk * R * d, device="cuda")
+            us = timeit(lambda: ops.gemm(dl, E, slab_d, R, d, V1, False, True, ops.epilogue(), split_k=sk,
+                                         slab=slab_d), a.reps)
+            print(f"dgrad dh=dl E    {us:9.1f} us  {fl / us / 1e6:7.1f} TFLOP/s (split-K {sk} slabs, reduction not incl.)")
 
 
 if __name__ == "__main__":
