@@ -83,50 +83,45 @@ __device__ __forceinline__ void group_tile(const Args& a, unsigned bid_raw, unsi
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
 
-  gbf::Stage<true, T> sa, sb;
-  sa.tid_ = tid;
-  sb.tid_ = tid;
-  const bool interior = ((kend - kbeg) % BKT) == 0;
-  auto kloop = [&](auto edge_tag) {
-    constexpr bool EDGE = decltype(edge_tag)::value;
-    auto issue = [&](int64_t k0) {
-      if (!EDGE) {
-        sa.load_next();
-        sb.load_next();
-        return;
+  // the MFMAs of one 64-deep LDS stage image (dY^T tile x X tile, + the bias column sums against ones)
+  auto mma_stage = [&](const bf16* cur) {
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      bf16x8 fa[FM], fb[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) fa[i] = gbf::frag<true, T>(cur, wm * (T / 2) + 16 * i, ss, lane);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) fb[j] = gbf::frag<true, T>(cur + I::ELEMS, wn * (T / 2) + 16 * j, ss, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      if (do_colsum) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], ones, accb[i], 0, 0, 0);
       }
+    }
+  };
+
+  const bool interior = ((kend - kbeg) % BKT) == 0;
+  // ragged row ranges (M not a multiple of 64): bounds-checked loads, one stage in flight
+  auto edge_loop = [&]() {
+    gbf::Stage<true, T> sa, sb;
+    sa.tid_ = tid;
+    sb.tid_ = tid;
+    auto issue = [&](int64_t k0) {
       sa.load_checked(P.dY, P.lddy, k0, n0, kend, P.N, tid);
       sb.load_checked(P.X, P.ldx, k0, c0, kend, P.K, tid);
     };
-    if (!EDGE) {
-      sa.init(P.dY, P.lddy, kbeg, n0, tid);
-      sb.init(P.X, P.ldx, kbeg, c0, tid);
-    }
     issue(kbeg);
     sa.store(smem, tid);
     sb.store(smem + I::ELEMS, tid);
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
-      const bf16* cur = smem + (kt & 1) * STAGE;
       const bool more = kt + 1 < nk;
       if (more) issue(kbeg + (int64_t)(kt + 1) * BKT);
-#pragma unroll
-      for (int ss = 0; ss < 2; ++ss) {
-        bf16x8 fa[FM], fb[FN];
-#pragma unroll
-        for (int i = 0; i < FM; ++i) fa[i] = gbf::frag<true, T>(cur, wm * (T / 2) + 16 * i, ss, lane);
-#pragma unroll
-        for (int j = 0; j < FN; ++j) fb[j] = gbf::frag<true, T>(cur + I::ELEMS, wn * (T / 2) + 16 * j, ss, lane);
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-        if (do_colsum) {
-#pragma unroll
-          for (int i = 0; i < FM; ++i) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], ones, accb[i], 0, 0, 0);
-        }
-      }
+      mma_stage(smem + (kt & 1) * STAGE);
       if (more) {
         bf16* nxt = smem + ((kt + 1) & 1) * STAGE;
         sa.store(nxt, tid);
@@ -135,9 +130,70 @@ __device__ __forceinline__ void group_tile(const Args& a, unsigned bid_raw, unsi
       __syncthreads();
     }
   };
+
+  // interior tiles: two stages in flight in registers (a ring of 2 register slots feeding the 2 LDS buffers), so
+  // each stage's L2 / HBM round trip hides under two stages of MFMAs instead of one.  Every iteration issues
+  // its loads unconditionally (past the last stage the pointers stop advancing and re-read it), so the wait
+  // before an LDS store covers exactly the older slot's loads.  cfg3 (16 BERT weights, 384 workgroups of 100
+  // stages): 170 -> 166 us for the launch + reduction, interleaved A/B; the step and cfg2 within noise -- the
+  // launch streams ~475 MB at ~3.6 TB/s, so one stage of prefetch was not what bounded it.
+  auto ring = [&]() {
+    static_assert(I::NCH % 256 == 0, "whole 16-B chunks per thread");
+    constexpr int PT = I::PER_T;
+    bf16x8 ra[2][PT], rb[2][PT];
+    const bf16* pa[PT];
+    const bf16* pb[PT];
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const int ch = tid + 256 * i, rr = ch / I::CPR, cc = (ch % I::CPR) * 8;
+      pa[i] = P.dY + (kbeg + rr) * P.lddy + n0 + cc;
+      pb[i] = P.X + (kbeg + rr) * P.ldx + c0 + cc;
+    }
+    const int64_t sta = (int64_t)BKT * P.lddy, stb = (int64_t)BKT * P.ldx;
+    int at = 0;   // stage the pointers address (stops at nk - 1)
+    auto load = [&](auto S) {
+      constexpr int sl = decltype(S)::value;
+#pragma unroll
+      for (int i = 0; i < PT; ++i) {
+        ra[sl][i] = *reinterpret_cast<const bf16x8*>(pa[i]);
+        rb[sl][i] = *reinterpret_cast<const bf16x8*>(pb[i]);
+      }
+      const bool adv = at + 1 < nk;
+      at += adv ? 1 : 0;
+#pragma unroll
+      for (int i = 0; i < PT; ++i) {
+        pa[i] += adv ? sta : 0;
+        pb[i] += adv ? stb : 0;
+      }
+    };
+    auto store = [&](auto S, bf16* img) {
+      constexpr int sl = decltype(S)::value;
+#pragma unroll
+      for (int i = 0; i < PT; ++i) {
+        const int ch = tid + 256 * i, rr = ch / I::CPR, cc = (ch % I::CPR) * 8;
+        *reinterpret_cast<bf16x8*>(img + rr * I::LD + cc) = ra[sl][i];
+        *reinterpret_cast<bf16x8*>(img + I::ELEMS + rr * I::LD + cc) = rb[sl][i];
+      }
+    };
+    load(std::integral_constant<int, 0>{});
+    load(std::integral_constant<int, 1>{});
+    store(std::integral_constant<int, 0>{}, smem);
+    __syncthreads();
+    auto body = [&](int kt, auto S) {
+      constexpr int sl = decltype(S)::value;      // == kt & 1
+      load(S);                                    // stage kt + 2 (or a re-read of the last one)
+      mma_stage(smem + sl * STAGE);
+      if (kt + 1 < nk) store(std::integral_constant<int, 1 - sl>{}, smem + (1 - sl) * STAGE);
+      __syncthreads();
+    };
+    for (int kt = 0; kt < nk; kt += 2) {
+      body(kt, std::integral_constant<int, 0>{});
+      if (kt + 1 < nk) body(kt + 1, std::integral_constant<int, 1>{});
+    }
+  };
   if (nk > 0) {
-    if (interior) kloop(std::integral_constant<bool, false>{});
-    else kloop(std::integral_constant<bool, true>{});
+    if (interior) ring();
+    else edge_loop();
   }
 
   // split partial -> slab (each 16-lane group stores 64 contiguous bytes per row)
