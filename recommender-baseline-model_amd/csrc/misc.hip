@@ -68,7 +68,10 @@ __device__ __forceinline__ void adam4(int64_t i, float4 pp, float4 gg, float4 mm
   reinterpret_cast<float4*>(p)[i] = pp;
   reinterpret_cast<float4*>(m)[i] = mm;
   reinterpret_cast<float4*>(v)[i] = vv;
-  if (zero_grad) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  // zero_grad: only where the gradient is not already zero -- the table rows no token of the step touched (most of
+  // a large item / token table) keep their zeros without a store (4 of the 34 bytes per element)
+  if (zero_grad && (__float_as_uint(gg.x) | __float_as_uint(gg.y) | __float_as_uint(gg.z) | __float_as_uint(gg.w)))
+    reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   if (BF16OUT) {
     bf16x4 o;
     o[0] = (__bf16)P[0]; o[1] = (__bf16)P[1]; o[2] = (__bf16)P[2]; o[3] = (__bf16)P[3];
