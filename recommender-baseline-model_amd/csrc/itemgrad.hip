@@ -12,9 +12,11 @@
 //                        blocks, a two-level scan over keys (group sums of 64 keys, one workgroup
 //                        scanning the groups, a wave scan per group), then each block places its
 //                        entries by a bitonic sort of (key, index) words in LDS for the in-block
-//                        rank -- all hand-written.  Only beyond the counting sort's reach (per-block
-//                        histogram table over 2^26 ints, or keys over 22 bits; no benchmarked shape)
-//                        is a library device radix sort (rocPRIM) used.  -> start[v] for v <= V
+//                        rank -- all hand-written -- for tables whose per-block histograms fit LDS
+//                        (<= 32k rows: cfg2, cfg3).  Larger tables (cfg4's 54.5k items, cfg5's 1M tokens)
+//                        take rocPRIM's stable device radix sort of the (key, entry) pairs instead: the
+//                        counting sort's nb x V global histogram was 33-100 MB of traffic beside the
+//                        forward.  -> start[v] for v <= V (a binary search per key)
 //   rs_item_grad:        chunks of 64 sorted entries: contribution rows summed per key run in
 //                        LDS; a key wholly inside one chunk is written by that chunk (+=); a
 //                        key spanning chunks leaves per-chunk partials that the chunk holding
@@ -59,7 +61,10 @@ static hipError_t layout(int nsrc, int64_t rows, int64_t table_rows, int64_t d, 
   L.nchunks = cdiv(L.n, CH);
   L.nb = cdiv(L.n, BE);
   L.V = table_rows;
-  L.cs = L.nb * table_rows <= HMAX && key_bits(table_rows) <= KBITS_MAX;
+  // counting sort only where the per-block histograms live in LDS; a larger table's nb x V global histogram
+  // (cfg4: 150 x 54.5k ints = 33 MB zeroed, scanned and re-read; cfg5: 100 MB) ran beside the forward and slowed
+  // it more than the sort costs: cfg4 0.2226 -> 0.2148 ms/step, cfg5 12.20 -> 12.09 with the radix sort
+  L.cs = table_rows <= VMAX_LDS && L.nb * table_rows <= HMAX && key_bits(table_rows) <= KBITS_MAX;
   size_t o = 0;
   L.sk = o; o = al256(o + L.n * 4);
   L.sv = o; o = al256(o + L.n * 4);
@@ -124,22 +129,6 @@ __global__ __launch_bounds__(256) void hist_kernel(Keys K, int* __restrict__ H) 
   __syncthreads();
   int* h = H + (int64_t)blockIdx.x * V;
   for (int v = tid; v < V; v += 256) h[v] = hist[v];
-}
-
-// larger tables: the same counts with integer atomics straight into the (zeroed) row of block b
-__global__ __launch_bounds__(256) void hist_global_kernel(Keys K, int* __restrict__ H) {
-  const int64_t e0 = (int64_t)blockIdx.x * BE;
-  int* h = H + (int64_t)blockIdx.x * K.V;
-  // the block zeroes its own histogram row first (no memset node in the step graph: at cfg4 the runtime's fill
-  // kernels of that node ran ~50 us late and held the whole index branch back into the backward)
-  for (int64_t v = threadIdx.x; v < K.V; v += 256) h[v] = 0;
-  __threadfence_block();
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < BE / 256; ++i) {
-    const int64_t e = e0 + threadIdx.x + i * 256;
-    if (e < K.n) atomicAdd(&h[K.get(e)], 1);
-  }
 }
 
 // H[b][v] <- sum_{b' < b} H[b'][v];  total[v] = sum_b H[b][v].  Workgroup = 64 keys (lanes) x 4
@@ -303,14 +292,19 @@ __global__ __launch_bounds__(256) void make_keys_kernel(Keys K, uint32_t* __rest
   vals[e] = (uint32_t)e;
 }
 
-// start[v] = first sorted position with key >= v, for v <= V
+// start[v] = first sorted position with key >= v, for v <= V: one thread per key, a binary search of the sorted
+// keys (a thread per ENTRY filling its gap of keys serialised the gap above the largest id, ~V entries, on one lane)
 __global__ __launch_bounds__(256) void lower_bounds_kernel(const uint32_t* __restrict__ sk, int64_t n, int64_t V,
                                                            int* __restrict__ start) {
-  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i > n) return;
-  const int64_t lo = i == 0 ? -1 : (int64_t)sk[i - 1];
-  const int64_t hi = i == n ? V : (int64_t)sk[i];
-  for (int64_t v = lo + 1; v <= hi; ++v) start[v] = (int)i;
+  const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (v > V) return;
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if ((int64_t)sk[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  start[v] = (int)lo;
 }
 
 // ---- gradient ---------------------------------------------------------------------------------
@@ -541,16 +535,12 @@ int rs_item_index_build(int nsrc, const int64_t* keys0, const int64_t* keys1, co
   if (L.cs) {
     int* H = (int*)(w + L.H);
     int* total = (int*)(w + L.total);
-    if (table_rows <= ig::VMAX_LDS) {
-      static const bool attr = [] {
-        return hipFuncSetAttribute((const void*)ig::hist_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   ig::VMAX_LDS * (int)sizeof(int)) == hipSuccess;
-      }();
-      if (!attr) return RS_ERR_UNSUPPORTED;
-      hipLaunchKernelGGL(ig::hist_kernel, dim3((unsigned)L.nb), dim3(256), (size_t)L.V * sizeof(int), s, K, H);
-    } else {
-      hipLaunchKernelGGL(ig::hist_global_kernel, dim3((unsigned)L.nb), dim3(256), 0, s, K, H);
-    }
+    static const bool attr = [] {
+      return hipFuncSetAttribute((const void*)ig::hist_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 ig::VMAX_LDS * (int)sizeof(int)) == hipSuccess;
+    }();
+    if (!attr) return RS_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL(ig::hist_kernel, dim3((unsigned)L.nb), dim3(256), (size_t)L.V * sizeof(int), s, K, H);
     int* gsum = (int*)(w + L.temp);
     const int64_t G = cdiv(table_rows, 64);
     hipLaunchKernelGGL(ig::prefix_blocks_kernel, dim3((unsigned)G), dim3(256), 0, s, H, L.nb, table_rows, total, gsum);
@@ -568,7 +558,7 @@ int rs_item_index_build(int nsrc, const int64_t* keys0, const int64_t* keys1, co
   size_t tb = L.temp_bytes;
   e = hipcub::DeviceRadixSort::SortPairs((void*)(w + L.temp), tb, kin, sk, vin, sv, (int)L.n, 0, bits, s);
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(ig::lower_bounds_kernel, dim3((unsigned)cdiv(L.n + 1, 256)), dim3(256), 0, s, sk, L.n,
+  hipLaunchKernelGGL(ig::lower_bounds_kernel, dim3((unsigned)cdiv(table_rows + 1, 256)), dim3(256), 0, s, sk, L.n,
                      table_rows, start);
   return (int)hipGetLastError();
 }

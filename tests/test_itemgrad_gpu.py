@@ -31,17 +31,18 @@ def _inputs(M, V1, d, seed):
 
 
 def _radix_path(M, V1):
-    """True when itemgrad.hip's layout() takes the library device radix sort instead of the counting sort:
-    (512-entry sort blocks) x (table rows) > 2^26 histogram ints, or keys wider than 22 bits."""
+    """True when itemgrad.hip's layout() takes the device radix sort instead of the counting sort: tables over
+    the LDS histogram's 32k rows, (512-entry sort blocks) x (table rows) > 2^26 histogram ints, or keys wider than
+    22 bits."""
     nb = -(-3 * M // 512)
-    return nb * V1 > (1 << 26) or (V1 - 1).bit_length() > 22
+    return V1 > 32768 or nb * V1 > (1 << 26) or (V1 - 1).bit_length() > 22
 
 
-# (30000, 800000, 64): 176 sort blocks x 800,000 rows = 1.4e8 > 2^26 -> the hipcub DeviceRadixSort path
+# tables over 32k rows (40,000; 800,000) -> the device radix sort path; the rest -> the counting sort
 @pytest.mark.parametrize("M,V1,d,p", [(25600, 3417, 128, 0.2), (5000, 300, 64, 0.0), (777, 50, 256, 0.1),
                                       (64, 5, 128, 0.0), (3000, 40000, 64, 0.0), (30000, 800000, 64, 0.0)])
 def test_item_grad_matches_atomic_scatter(M, V1, d, p):
-    assert _radix_path(M, V1) == (V1 == 800000)
+    assert _radix_path(M, V1) == (V1 > 32768)
     import rbm_amd  # noqa: F401
     from rbm_amd import ops
     ids, pos, neg, dx, f, dpl, dnl = _inputs(M, V1, d, seed=M + d)

@@ -7,7 +7,13 @@ import sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 nth = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-ad = [i for i, r in enumerate(rows) if "adam_step" in r["Kernel_Name"] or "adam_fused" in r["Kernel_Name"]]
+def is_opt(r):
+    return "adam_step" in r["Kernel_Name"] or "adam_fused" in r["Kernel_Name"]
+
+
+# a step ends with its optimizer group (one launch, or several when ranges are updated separately -- e.g. the
+# unzeroed out.weight range at a large vocabulary): the LAST launch of each consecutive group delimits steps
+ad = [i for i, r in enumerate(rows) if is_opt(r) and (i + 1 == len(rows) or not is_opt(rows[i + 1]))]
 # steps of the timed graph replays only: bench.py's event-timed leg runs eager steps with timing events and a
 # torch spin kernel around the dominant launch after the timed ones -- skip every step holding a non-HIP-graph kernel
 # of that kind (torch's spin / elementwise kernels)
