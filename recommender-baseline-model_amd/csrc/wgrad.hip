@@ -133,10 +133,12 @@ __device__ __forceinline__ void group_tile(const Args& a, unsigned bid_raw, unsi
 
   // interior tiles: two stages in flight in registers (a ring of 2 register slots feeding the 2 LDS buffers), so
   // each stage's L2 / HBM round trip hides under two stages of MFMAs instead of one.  Every iteration issues
-  // its loads unconditionally (past the last stage the pointers stop advancing and re-read it), so the wait
+  // its loads unconditionally (past the last stage every lane re-reads the tile's first word), so the wait
   // before an LDS store covers exactly the older slot's loads.  cfg3 (16 BERT weights, 384 workgroups of 100
   // stages): 170 -> 166 us for the launch + reduction, interleaved A/B; the step and cfg2 within noise -- the
-  // launch streams ~475 MB at ~3.6 TB/s, so one stage of prefetch was not what bounded it.
+  // launch streams ~475 MB at ~3.6 TB/s, so one stage of prefetch was not what bounded it.  The deeper ring raises
+  // the launch's HBM fetches 475 -> 536 MB (PMC; more stages in flight per XCD's L2 evict tiles' shared rows
+  // before their neighbours read them): kept for the time, the launch is latency- not bandwidth-bound.
   auto ring = [&]() {
     static_assert(I::NCH % 256 == 0, "whole 16-B chunks per thread");
     constexpr int PT = I::PER_T;
@@ -161,9 +163,9 @@ __device__ __forceinline__ void group_tile(const Args& a, unsigned bid_raw, unsi
       const bool adv = at + 1 < nk;
       at += adv ? 1 : 0;
 #pragma unroll
-      for (int i = 0; i < PT; ++i) {
-        pa[i] += adv ? sta : 0;
-        pb[i] += adv ? stb : 0;
+      for (int i = 0; i < PT; ++i) {   // past the last stage: every lane re-reads one 16-B word (one line per wave)
+        pa[i] = adv ? pa[i] + sta : P.dY + kbeg * P.lddy + n0;
+        pb[i] = adv ? pb[i] + stb : P.X + kbeg * P.ldx + c0;
       }
     };
     auto store = [&](auto S, bf16* img) {
@@ -181,7 +183,7 @@ __device__ __forceinline__ void group_tile(const Args& a, unsigned bid_raw, unsi
     __syncthreads();
     auto body = [&](int kt, auto S) {
       constexpr int sl = decltype(S)::value;      // == kt & 1
-      load(S);                                    // stage kt + 2 (or a re-read of the last one)
+      load(S);                                    // stage kt + 2 (or the one-word dummy past the last)
       mma_stage(smem + sl * STAGE);
       if (kt + 1 < nk) store(std::integral_constant<int, 1 - sl>{}, smem + (1 - sl) * STAGE);
       __syncthreads();
