@@ -226,7 +226,8 @@ struct Seg {
   int64_t stride;
   int splits, n;      // n floats (multiple of 4, 16-byte aligned src/out)
   float* out;
-  int cols;           // 1: column-per-thread form (few splits), 0: split groups + LDS tree
+  int cols;           // columns per thread of the column form (1, or 4 for large few-split segments), 0: split
+                      // groups + LDS tree
 };
 constexpr int COLS_MAX = 32;   // splits up to which a segment is summed column per thread
 struct RArgs {
@@ -322,8 +323,42 @@ __device__ __forceinline__ void reduce_cols_block(const RArgs& a, int b) {
   for (int q = 1; q < a.nseg; ++q)
     if (b >= a.blk0[q]) si = q;
   const Seg& S = a.s[si];
-  const int64_t i4 = (int64_t)(b - a.blk0[si]) * 256 + threadIdx.x;
   const int64_t n4 = S.n / 4;
+  if (S.cols == 4) {
+    // large segments of at most 4 splits (the BERT weight slabs): 4 columns per thread, every split's loads of
+    // all 4 issued before the first sum (16 float4 in flight instead of 2-4); each column still summed in split
+    // order, then the old value -- the same bits as the one-column form
+    const int64_t i0 = (int64_t)(b - a.blk0[si]) * 1024 + threadIdx.x;
+    const float4* src = reinterpret_cast<const float4*>(S.src);
+    const int64_t st4 = S.stride / 4;
+    float4 u[4][4];
+#pragma unroll
+    for (int z = 0; z < 4; ++z)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int64_t i4 = i0 + 256 * k;
+        u[z][k] = (z < S.splits && i4 < n4) ? src[(int64_t)z * st4 + i4] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    float4 old[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t i4 = i0 + 256 * k;
+      old[k] = (a.accumulate && i4 < n4) ? reinterpret_cast<const float4*>(S.out)[i4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t i4 = i0 + 256 * k;
+      if (i4 >= n4) continue;
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int z = 0; z < 4; ++z)
+        if (z < S.splits) { acc.x += u[z][k].x; acc.y += u[z][k].y; acc.z += u[z][k].z; acc.w += u[z][k].w; }
+      if (a.accumulate) { acc.x += old[k].x; acc.y += old[k].y; acc.z += old[k].z; acc.w += old[k].w; }
+      reinterpret_cast<float4*>(S.out)[i4] = acc;
+    }
+    return;
+  }
+  const int64_t i4 = (int64_t)(b - a.blk0[si]) * 256 + threadIdx.x;
   if (i4 >= n4) return;
   const float4* src = reinterpret_cast<const float4*>(S.src) + i4;
   const int64_t st4 = S.stride / 4;
@@ -371,11 +406,11 @@ static int reduce_args(int nseg, const rs_reduce_segment* segs, int accumulate, 
   for (int q = 0; q < nseg; ++q) {
     const rs_reduce_segment& g = segs[q];
     if (g.n <= 0 || g.n % 4 || g.stride % 4 || g.splits < 1 || !al16(g.src) || !al16(g.out)) return RS_ERR_ARG;
-    const int c = g.splits <= wg::COLS_MAX;
+    const int c = g.splits > wg::COLS_MAX ? 0 : (g.splits <= 4 && g.n / 4 >= 16384) ? 4 : 1;
     cols = cols && c;
     ra.s[q] = {g.src, g.stride, (int)g.splits, (int)g.n, g.out, c};
     ra.blk0[q] = blk;
-    blk += (int)cdiv(g.n / 4, c ? 256 : (g.splits > 64 ? 4 : wg::RED_C));
+    blk += (int)cdiv(g.n / 4, c ? 256 * c : (g.splits > 64 ? 4 : wg::RED_C));
   }
   ra.blk0[nseg] = blk;
   return 0;

@@ -20,6 +20,7 @@ compute and optimizer graphs around the eager RCCL call under DP) and
 ``replay`` runs it on new batches copied into the graphs' static inputs; the
 dropout step-seed lives in device memory and is advanced inside the graph.
 """
+import gc
 import os
 
 import torch
@@ -476,7 +477,20 @@ class FusedTrainStep:
     def _capture_graphs(self, compute, stamps=None, unrolled=False):
         """The compute graph (+ the optimizer in the same graph on one device).  DP: the compute graph is cut at
         every bucket the backward finishes (overlap: segments replayed with that bucket's all-reduce launched
-        between them) or ends after the backward, and the optimizer is a separate graph after the exchange."""
+        between them) or ends after the backward, and the optimizer is a separate graph after the exchange.
+        Python's cyclic garbage collector is held off for the whole capture: a collection that lands mid-capture
+        can destroy HIP objects of earlier steps or graphs (events, graph executables) while a stream is being
+        captured, which aborts the process (seen once in the BERT graph-collectives test)."""
+        gc_on = gc.isenabled()
+        gc.collect()
+        gc.disable()
+        try:
+            return self._capture_graphs_impl(compute, stamps, unrolled)
+        finally:
+            if gc_on:
+                gc.enable()
+
+    def _capture_graphs_impl(self, compute, stamps=None, unrolled=False):
         self._stamps = stamps
         if stamps is not None:
             ops.kernel_stamps(stamps[0], self.opt.state, stamps[1])
@@ -505,7 +519,7 @@ class FusedTrainStep:
                     import warnings
                     warnings.warn(f"all-reduce capture failed on some rank ({err or 'not this one'}); falling back "
                                   f"to segmented DP graphs on every rank")
-                    return self._capture_graphs(compute, stamps, unrolled)
+                    return self._capture_graphs_impl(compute, stamps, unrolled)
                 self.g_compute = g
                 self.g_segments = None
             elif self.overlap:
