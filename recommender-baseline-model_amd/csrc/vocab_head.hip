@@ -438,7 +438,25 @@ __global__ __launch_bounds__(256) void shard_lse_kernel(const float* __restrict_
     return;
   }
   float mx = -__builtin_inff(), sm = 0.f;
-  for (int64_t t = lane; t < ntn; t += 64) comb(mx, sm, part[(r * ntn + t) * 2], part[(r * ntn + t) * 2 + 1]);
+  const float2* pr = reinterpret_cast<const float2*>(part + r * ntn * 2);
+  int64_t t = lane;
+  constexpr int U = 8;   // eight tiles in flight per lane, folded against their common max (vocab_ce.hip's finish)
+  for (; t + 64 * (U - 1) < ntn; t += 64 * U) {
+    float2 q[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) q[u] = pr[t + 64 * u];
+    float mm = mx;
+#pragma unroll
+    for (int u = 0; u < U; ++u) mm = fmaxf(mm, q[u].x);
+    if (mm != -__builtin_inff()) {
+      float acc = sm * __expf(mx - mm);
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc += q[u].y * __expf(q[u].x - mm);
+      sm = acc;
+      mx = mm;
+    }
+  }
+  for (; t < ntn; t += 64) comb(mx, sm, pr[t].x, pr[t].y);
   for (int o = 32; o > 0; o >>= 1) comb(mx, sm, __shfl_xor(mx, o, 64), __shfl_xor(sm, o, 64));
   if (lane == 0) lse[r] = mx + __logf(sm);
 }
