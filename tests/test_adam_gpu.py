@@ -122,3 +122,32 @@ def test_optimizer_written_transposed_weights_match_a_fresh_transpose(graph):
     eng._refresh_transposed()
     torch.cuda.synchronize()
     assert torch.equal(got, eng._wT)
+
+
+def test_zero_grad_with_untouched_rows():
+    """zero_grad stores zeros only where the gradient is not already zero (the untouched rows of a large table keep
+    their zeros without a store): with rows of exact zeros (and -0.0) beside non-zero ones, every gradient element
+    is zero after the step and the update equals torch.optim.Adam's on the same sparse gradients."""
+    import rbm_amd  # noqa: F401
+    from rbm_amd import ops
+    n, d = 4096 * 64, 64
+    gen = torch.Generator().manual_seed(3)
+    p0 = torch.randn(n, generator=gen)
+    hyper = torch.tensor([1e-3, 0.9, 0.999, 1e-8, 0.0], dtype=torch.float64, device="cuda")
+    p, m, v = p0.cuda().clone(), torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
+    st, seed = _state(), torch.zeros(1, dtype=torch.int64, device="cuda")
+    tp = torch.nn.Parameter(p0.clone().double())
+    opt = torch.optim.Adam([tp], lr=1e-3, betas=(0.9, 0.999), eps=1e-8)
+    for step in range(3):
+        g = torch.randn(n, generator=gen)
+        touched = torch.rand(n // d, generator=gen) < 0.2            # 20 % of the rows carry a gradient
+        g = (g.view(-1, d) * touched[:, None]).view(-1)
+        g[g == 0] = -0.0 if step == 1 else 0.0                       # signed zeros are zeros too
+        gd = g.cuda()
+        ops.adam_prepare_step(p, gd, m, v, None, st, hyper, zero_grad=True, seed_base=seed)
+        torch.cuda.synchronize()
+        assert int(torch.count_nonzero(gd)) == 0
+        tp.grad = g.double()
+        opt.step()
+    err = (p.cpu().double() - tp.detach()).abs().max().item()
+    assert err < 2e-6, err
