@@ -21,10 +21,13 @@ int epi_class(const GemmArgs& a) {
   return ec | (e.act << 8);
 }
 
+#ifndef GBF_ANY_MIN
+#define GBF_ANY_MIN 512
+#endif
 template <bool AK, bool BK, int EC>
 hipError_t launch_any(GemmArgs& a, hipStream_t s) {
   auto blocks = [&](int bm, int bn) { return cdiv(a.M, bm) * cdiv(a.N, bn) * a.split_k; };
-  if (blocks(128, 128) >= 512) return launch_cfg<AK, BK, 128, 128, EC>(a, s);
+  if (blocks(128, 128) >= GBF_ANY_MIN) return launch_cfg<AK, BK, 128, 128, EC>(a, s);
   if (a.N >= 128 && blocks(64, 128) >= 512) return launch_cfg<AK, BK, 64, 128, EC>(a, s);
   if (blocks(128, 64) >= 512) return launch_cfg<AK, BK, 128, 64, EC>(a, s);
   return launch_cfg<AK, BK, 64, 64, EC>(a, s);

@@ -678,6 +678,10 @@ template <bool AK, bool BK, int EC>
 hipError_t launch_tiles(GemmArgs& a, hipStream_t s) {
   constexpr bool heavy_epi = EC >= 0 && (ec_act(EC) == 2 || ec_act(EC) == 4) && (EC & ED) != 0;
   if (!heavy_epi && cdiv(a.M, 128) * cdiv(a.N, 128) * a.split_k >= 512) return launch_cfg<AK, BK, 128, 128, EC>(a, s);
+#ifdef GBF_MID_MIN
+  if (!heavy_epi && a.N >= 128 && cdiv(a.M, 64) * cdiv(a.N, 128) * a.split_k >= GBF_MID_MIN)
+    return launch_cfg<AK, BK, 64, 128, EC>(a, s);
+#endif
   return launch_cfg<AK, BK, 64, 64, EC>(a, s);
 }
 

@@ -7,8 +7,14 @@ cd "$(dirname "$0")/.."
 PKG=recommender-baseline-model_amd
 OBJ=$PKG/csrc/build
 mkdir -p /tmp/rsvar
-/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -I include -I $PKG/csrc $FLAGS \
-  -c $PKG/csrc/$SRC -o /tmp/rsvar/$SRC.$NAME.o
-objs=$(ls $OBJ/*.o | grep -v "/$SRC.o$")
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 $objs /tmp/rsvar/$SRC.$NAME.o -o $PKG/librecsys_hip.$NAME.so
+# SRC may name several translation units (space-separated)
+vobjs=""
+objs=$(ls $OBJ/*.o)
+for f in $SRC; do
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -I include -I $PKG/csrc $FLAGS \
+    -c $PKG/csrc/$f -o /tmp/rsvar/$f.$NAME.o
+  vobjs="$vobjs /tmp/rsvar/$f.$NAME.o"
+  objs=$(echo "$objs" | grep -v "/$f.o$")
+done
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 $objs $vobjs -o $PKG/librecsys_hip.$NAME.so
 echo $PKG/librecsys_hip.$NAME.so
