@@ -143,14 +143,20 @@ def test_two_rank_step_equals_single_process(tmp_path, kind, dtype):
     # fp32: the DP sum runs in another order than the single batch's (rounding-level differences); bf16: the
     # per-rank partial sums round differently (LayerNorm bias gradients at 6 sequences per rank: ~0.1 of the update)
     loss_tol, upd_tol = (1e-5, 1e-2) if dtype == "fp32" else (2e-3, 0.2)
+    upd_med_tol = 1e-2 if dtype == "fp32" else 0.05     # the typical tensor, not the worst LayerNorm bias
     for mode in r0:
         a, b = r0[mode], r1[mode]
         assert a["counts"] == counts and b["counts"] == counts, (mode, a["counts"], b["counts"], counts)
         assert a["losses"] == b["losses"], mode
         assert np.allclose(a["losses"], ref_losses, rtol=loss_tol), (mode, a["losses"], ref_losses)
+        errs = {}
         for k in ref:
             assert torch.equal(a["sd"][k], b["sd"][k]), (mode, k)         # replicas bit-identical
             if _skip_key(kind, k):
                 continue
-            e = _update_err(kind, k, a["sd"][k], ref[k], init[k])
-            assert e < upd_tol, (mode, k, e)
+            errs[k] = _update_err(kind, k, a["sd"][k], ref[k], init[k])
+        worst = max(errs, key=errs.get)
+        med = float(np.median(list(errs.values())))
+        print(f"{kind} {dtype} {mode}: update error median {med:.3g}, max {errs[worst]:.3g} ({worst})")
+        assert errs[worst] < upd_tol, (mode, worst, errs[worst])
+        assert med < upd_med_tol, (mode, med)
