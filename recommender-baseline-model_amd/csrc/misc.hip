@@ -387,7 +387,10 @@ int rs_adam_prepare_step_loss(int64_t n, float* p, float* g, float* m, float* v,
   // at most 2048 workgroups: every workgroup pays an arrival atomic (the PREP step-count publication); 7k of
   // them cost ~13 us at 7.4M parameters (kbench: 56 -> 40 us for the launch; flat at 0.66M and 20M; the
   // cfg4 step within noise, 560k vs 567k seq/s)
-  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(cdiv(n / 4, 256), 2048));
+#ifndef ADAM_PREP_MAX_WG
+#define ADAM_PREP_MAX_WG 2048
+#endif
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(cdiv(n / 4, 256), ADAM_PREP_MAX_WG));
   hipStream_t s = (hipStream_t)stream;
   if (p_bf16)
     ADAM_LAUNCH(true, true, dim3((unsigned)blocks), dim3(256), 0, s, n, p, g, m, v,
