@@ -490,6 +490,10 @@ int rs_reduce_segments(int nseg, const rs_reduce_segment* segs, int accumulate, 
 int64_t rs_item_index_ws_bytes(int nsrc, int64_t rows, int64_t table_rows, int64_t d);
 int rs_item_index_build(int nsrc, const int64_t* keys0, const int64_t* keys1, const int64_t* keys2, int64_t rows,
                         int64_t table_rows, int64_t d, void* ws, int64_t ws_bytes, void* stream);
+/* Where the built index lives in ws (for tests and tools): out[0..3] = byte offsets of the sorted keys (u32 [n]),
+ * the sorted entries (u32 [n], entry = source * rows + row), start (int [table_rows + 1]), and the sort path
+ * (0 counting sort, 1 / 2 one-workgroup LDS radix sort with u32 / u64 words, 3 multi-workgroup radix sort). */
+int rs_item_index_layout(int nsrc, int64_t rows, int64_t table_rows, int64_t d, int64_t* out);
 /* dx, f: bf16 [rows][d] (d in {64, 128, 256}); w1, w2: fp32 [rows]; dtable fp32 [table_rows][d]. */
 int rs_item_grad(const void* ws, int nsrc, int64_t rows, int64_t table_rows, int64_t d, const void* dx, float scale,
                  float drop_p, uint64_t salt, const uint64_t* seed_base, const void* f, const float* w1,
@@ -537,6 +541,17 @@ int rs_sas_sample(const int64_t* user_offsets, const int64_t* user_items, int64_
 int rs_bert_mask(const int64_t* user_offsets, const int64_t* user_items, int64_t n_users, int64_t num_items,
                  int64_t batch, int64_t max_len, float mask_prob, const int64_t* perm, uint64_t* state, uint64_t salt,
                  int64_t* tokens, int64_t* labels, void* stream);
+/* The same two samplers, also recording the draws each row consumed (tests replay the reference's construction
+ * on them, oracle/sampling.py).  SAS: draws int64 [batch][1 + max_len*256] = {user, then per position the 256
+ * candidate negatives the rejection loop may try, in draw order (-1 where the position draws none)}.  BERT: draws int64 [batch][1 + 2*max_len]
+ * = {user, then per position (k, item): the masking uniform is k / 2^24, the replacement item is item; -1 on
+ * padding}. */
+int rs_sas_sample_draws(const int64_t* user_offsets, const int64_t* user_items, int64_t n_users, int64_t item_num,
+                        int64_t batch, int64_t max_len, uint64_t* seed_base, uint64_t salt, int64_t* seq, int64_t* pos,
+                        int64_t* neg, int64_t* draws, void* stream);
+int rs_bert_mask_draws(const int64_t* user_offsets, const int64_t* user_items, int64_t n_users, int64_t num_items,
+                       int64_t batch, int64_t max_len, float mask_prob, const int64_t* perm, uint64_t* state,
+                       uint64_t salt, int64_t* tokens, int64_t* labels, int64_t* draws, void* stream);
 
 /* rs_rank_metrics: recalls_ndcgs_and_mrr_for_ks (BS/trainers/utils.py:28-57) over scores/labels
  * fp32 [rows][cands] (labels 0/1 weights), ks: device int[nk] (nk <= 8).  out[3*q + {0,1,2}] =

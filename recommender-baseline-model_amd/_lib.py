@@ -115,6 +115,7 @@ SIGNATURES = {
     "rs_wgrad_grouped_slab_numel": [i32, C.POINTER(WgradProblem), i64, i64],
     "rs_item_index_ws_bytes": [i32, i64, i64, i64],
     "rs_item_index_build": [i32, vp, vp, vp, i64, i64, i64, vp, i64, vp],
+    "rs_item_index_layout": [i32, i64, i64, i64, C.POINTER(i64)],
     "rs_sas_head_fwd": [i64, i64, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "rs_sas_head_finish": [i64, vp, vp, vp, vp],
     "rs_sas_head_bwd": [i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
@@ -127,6 +128,8 @@ SIGNATURES = {
     "rs_transpose_bf16": [i64, vp, i64, vp, vp, vp],
     "rs_sas_sample": [vp, vp, i64, i64, i64, i64, vp, u64, vp, vp, vp, vp],
     "rs_bert_mask": [vp, vp, i64, i64, i64, i64, f32, vp, vp, u64, vp, vp, vp],
+    "rs_sas_sample_draws": [vp, vp, i64, i64, i64, i64, vp, u64, vp, vp, vp, vp, vp],
+    "rs_bert_mask_draws": [vp, vp, i64, i64, i64, i64, f32, vp, vp, u64, vp, vp, vp, vp],
     "rs_splitk_scatter_rows": [i32, vp, i32, i64, i64, vp, i64, vp, i64, vp],
     "rs_rank_metrics": [vp, vp, i64, i64, i32, vp, vp, vp, vp],
     "rs_kernel_stamps": [vp, vp, i32],

@@ -14,9 +14,14 @@
 //                        entries by a bitonic sort of (key, index) words in LDS for the in-block
 //                        rank -- all hand-written -- for tables whose per-block histograms fit LDS
 //                        (<= 32k rows: cfg2, cfg3).  Larger tables (cfg4's 54.5k items, cfg5's 1M tokens)
-//                        take rocPRIM's stable device radix sort of the (key, entry) pairs instead: the
-//                        counting sort's nb x V global histogram was 33-100 MB of traffic beside the
-//                        forward.  -> start[v] for v <= V (a binary search per key)
+//                        take a hand-written LSD radix sort instead (the counting sort's nb x V global
+//                        histogram was 33-100 MB of traffic beside the forward): while the entries fit
+//                        one CU's LDS (cfg4: 19,200, cfg5: 12,800) ONE 1024-thread workgroup first splits
+//                        off the padding keys (written straight to the front of the output), then sorts
+//                        the rest in LDS by 7-8-bit digits -- stable per-wave ranks from 8 ballots, wave x
+//                        digit counters, one workgroup scan per pass -- on a single CU beside the
+//                        forward; larger batches run the same ranking as a multi-workgroup
+//                        count / scan / scatter per digit.  -> start[v] for v <= V (a binary search per key)
 //   rs_item_grad:        chunks of 64 sorted entries: contribution rows summed per key run in
 //                        LDS; a key wholly inside one chunk is written by that chunk (+=); a
 //                        key spanning chunks leaves per-chunk partials that the chunk holding
@@ -24,8 +29,6 @@
 //
 // Every destination row has exactly one writer and a fixed summation order: bitwise
 // reproducible.  Rows with key 0 (padding_idx) are skipped.
-#include <hipcub/hipcub.hpp>
-
 #include "common.h"
 #include "../../include/recsys_hip.h"
 
@@ -41,11 +44,27 @@ constexpr int64_t HMAX = (int64_t)1 << 26;  // largest per-block histogram table
 constexpr int IBITS = 9;                    // BE = 2^IBITS: an entry's block index in the sort word's low bits
 constexpr int KBITS_MAX = 32 - IBITS - 1;   // key bits the counting-sort path's (key, index) sort word holds
 static_assert(BE == 1 << IBITS, "sort word layout");
+// LSD radix sort (tables past the counting sort's limits)
+constexpr int RT = 1024;                   // threads of a sort workgroup
+constexpr int RW = RT / 64;                // its waves
+constexpr int RB = 8;                      // widest digit (bits)
+constexpr int CPAD = (1 << RB) + 1;        // per-wave counter row pitch: rows start on different banks
+constexpr int RHDR = RW * CPAD * 4 + 128;  // LDS bytes ahead of the word buffer: counters + scan scratch
+constexpr int LDS_MAX = 160 * 1024;
+constexpr int IT32 = 36, IT64 = 18;        // words per thread of the one-workgroup sort (u32 / u64 words)
+constexpr int64_t N32 = (LDS_MAX - RHDR) / 4, N64 = (LDS_MAX - RHDR) / 8;   // 36,816 / 18,408 entries
+constexpr int ITB = 8;                     // words per thread of a multi-workgroup tile
+constexpr int TB = RT * ITB;               // entries per tile
+static_assert(N32 <= (int64_t)IT32 * RT && N64 <= (int64_t)IT64 * RT, "register words cover the LDS buffer");
+static_assert(RHDR % 16 == 0, "word buffer alignment");
+
+enum SortPath { SORT_COUNT = 0, SORT_LDS32 = 1, SORT_LDS64 = 2, SORT_TILES = 3 };
 
 struct Layout {
   int64_t n, nchunks, nb, V;
+  int path, kb, ib;          // SortPath; key bits; entry-index bits (one-workgroup u32 words)
   bool cs;
-  size_t sk, sv, start, part, H, total, keys_in, vals_in, temp, temp_bytes, total_bytes;
+  size_t sk, sv, start, part, H, total, ping, pong, hist, temp, temp_bytes, total_bytes;
 };
 
 static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -65,31 +84,27 @@ static hipError_t layout(int nsrc, int64_t rows, int64_t table_rows, int64_t d, 
   // (cfg4: 150 x 54.5k ints = 33 MB zeroed, scanned and re-read; cfg5: 100 MB) ran beside the forward and slowed
   // it more than the sort costs: cfg4 0.2226 -> 0.2148 ms/step, cfg5 12.20 -> 12.09 with the radix sort
   L.cs = table_rows <= VMAX_LDS && L.nb * table_rows <= HMAX && key_bits(table_rows) <= KBITS_MAX;
+  L.kb = key_bits(table_rows);
+  L.ib = key_bits(L.n);
+  L.path = L.cs ? SORT_COUNT
+                : (L.kb + L.ib <= 32 && L.n <= N32) ? SORT_LDS32 : (L.n <= N64 ? SORT_LDS64 : SORT_TILES);
   size_t o = 0;
   L.sk = o; o = al256(o + L.n * 4);
   L.sv = o; o = al256(o + L.n * 4);
   L.start = o; o = al256(o + (table_rows + 1) * 4);
   L.part = o; o = al256(o + L.nchunks * 2 * d * 4);
   L.temp_bytes = 0;
+  L.H = L.total = L.ping = L.pong = L.hist = L.temp = 0;
   if (L.cs) {
     L.H = o; o = al256(o + L.nb * table_rows * 4);
     L.total = o; o = al256(o + (table_rows + 1) * 4);   // [V] = 0: the scan's last entry is the total
-    L.keys_in = L.vals_in = 0;
     L.temp = o;                                          // group sums of the key scan: cdiv(V, 64) + 1 ints
     L.temp_bytes = (size_t)(cdiv(table_rows, 64) + 1) * 4;
     o = al256(o + L.temp_bytes);
-  } else {
-    L.H = L.total = 0;
-    L.keys_in = o; o = al256(o + L.n * 4);
-    L.vals_in = o; o = al256(o + L.n * 4);
-    L.temp = o;
-    size_t tb = 0;
-    const hipError_t e = hipcub::DeviceRadixSort::SortPairs(
-        nullptr, tb, (const uint32_t*)nullptr, (uint32_t*)nullptr, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-        (int)L.n, 0, key_bits(table_rows), (hipStream_t)0);
-    if (e != hipSuccess) return e;
-    L.temp_bytes = tb;
-    o = al256(o + tb);
+  } else if (L.path == SORT_TILES) {                     // word ping-pong + per-(digit, tile) counts
+    L.ping = o; o = al256(o + L.n * 8);
+    L.pong = o; o = al256(o + L.n * 8);
+    L.hist = o; o = al256(o + (size_t)(1 << RB) * cdiv(L.n, TB) * 4);
   }
   L.total_bytes = o;
   return hipSuccess;
@@ -283,13 +298,250 @@ __global__ __launch_bounds__(256) void place_kernel(Keys K, const int* __restric
   }
 }
 
-// ---- device radix sort path (large tables) --------------------------------------------------
-__global__ __launch_bounds__(256) void make_keys_kernel(Keys K, uint32_t* __restrict__ keys,
-                                                        uint32_t* __restrict__ vals) {
-  const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (e >= K.n) return;
-  keys[e] = K.get(e);
-  vals[e] = (uint32_t)e;
+// ---- hand-written LSD radix sort (tables past the counting sort's limits) ----------------------
+
+// Stable rank of this lane's element among the elements of its wave with the same digit: the lanes below it
+// holding that digit (peers from db ballots) plus the wave's running count row[dig] in LDS, which the highest
+// such lane advances.  A wave's LDS accesses complete in order, so the read-then-write needs no fence; the
+// calls must be made with every lane of the wave active.
+__device__ __forceinline__ int wave_rank(uint32_t dig, bool valid, int db, int* row, int lane) {
+  uint64_t m = __ballot(valid);
+#pragma unroll
+  for (int b = 0; b < RB; ++b) {
+    if (b < db) {
+      const bool bit = (dig >> b) & 1u;
+      const uint64_t x = __ballot(bit);
+      m &= bit ? x : ~x;
+    }
+  }
+  int r = 0;
+  if (valid) {
+    const int base = row[dig];
+    r = base + __popcll(m & ((1ull << lane) - 1ull));
+    if ((m >> lane) == 1ull) row[dig] = base + __popcll(m);
+  }
+  return r;
+}
+
+// cnt[w][d] (pitch CPAD) -> exclusive offsets in (digit, wave) order -- the stable order of a pass -- over
+// nbins digits; RT threads, 4 entries each (nbins * RW <= 4096).  Ends with a barrier.
+__device__ __forceinline__ void scan_counters(int* cnt, int* scr, int nbins) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int v[4], s = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int j = 4 * tid + q, d = j / RW, ww = j % RW;
+    v[q] = d < nbins ? cnt[ww * CPAD + d] : 0;
+    s += v[q];
+  }
+  int x = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) scr[w] = x;
+  __syncthreads();
+  int off = x - s;
+  for (int k = 0; k < w; ++k) off += scr[k];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int j = 4 * tid + q, d = j / RW, ww = j % RW;
+    if (d < nbins) cnt[ww * CPAD + d] = off;
+    off += v[q];
+  }
+  __syncthreads();
+}
+
+// digit width of an LSD sort over kb key bits: the fewest passes of <= RB bits, split evenly
+__host__ __device__ inline int sort_passes(int kb) { return (kb + RB - 1) / RB; }
+__host__ __device__ inline int sort_digit(int kb) { return (kb + sort_passes(kb) - 1) / sort_passes(kb); }
+
+// ONE workgroup sorts every entry in LDS.  Words: key << ib | entry (u32 when kb + ib <= 32, else u64).
+// Pass 0 sends the padding keys (0) straight to the front of the output in entry order and compacts the
+// others, stably, into the LDS buffer (cfg4's histories are ~80 % padding: the digit passes then rank ~3.5k
+// of the 19.2k entries); each digit pass ranks, scans and scatters them back (the last pass to sk/sv).
+// Element layout of a pass over c entries: wave w holds [w*S, (w+1)*S), S = 64 * ceil(c / RT), lane-fastest,
+// so (digit, wave, iteration, lane) order is the input order within each digit: stable.
+template <typename W, int IT>
+__global__ __launch_bounds__(RT) void lsort_kernel(Keys K, int ib, int kb, uint32_t* __restrict__ sk,
+                                                   uint32_t* __restrict__ sv) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  int* cnt = reinterpret_cast<int*>(smem);
+  int* scr = cnt + RW * CPAD;
+  W* buf = reinterpret_cast<W*>(smem + RHDR);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int n = (int)K.n;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const W emask = ((W)1 << ib) - (W)1;
+  W word[IT];
+  int rk[IT];
+  int iters = (n + RT - 1) / RT, S = iters * 64;
+  int zc = 0, nc = 0;
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    if (i < iters) {
+      const int e = w * S + i * 64 + lane;
+      const bool valid = e < n;
+      const uint32_t key = valid ? K.get(e) : 0u;
+      const bool nz = key != 0u;
+      const uint64_t bz = __ballot(valid && !nz), bn = __ballot(nz);
+      rk[i] = nz ? nc + (int)__popcll(bn & lt) : zc + (int)__popcll(bz & lt);
+      word[i] = (W)key << ib | (W)(uint32_t)e;
+      zc += (int)__popcll(bz);
+      nc += (int)__popcll(bn);
+    }
+  }
+  if (lane == 0) {
+    scr[w] = zc;
+    scr[RW + w] = nc;
+  }
+  __syncthreads();
+  int zoff = 0, noff = 0, Z = 0;
+  for (int k = 0; k < RW; ++k) {
+    const int a = scr[k], b = scr[RW + k];
+    zoff += k < w ? a : 0;
+    noff += k < w ? b : 0;
+    Z += a;
+  }
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    if (i < iters && w * S + i * 64 + lane < n) {
+      if ((word[i] >> ib) == (W)0) {
+        sk[zoff + rk[i]] = 0u;
+        sv[zoff + rk[i]] = (uint32_t)(word[i] & emask);
+      } else {
+        buf[noff + rk[i]] = word[i];
+      }
+    }
+  }
+  const int nnz = n - Z;
+  iters = (nnz + RT - 1) / RT;
+  S = iters * 64;
+  const int passes = sort_passes(kb), db0 = sort_digit(kb);
+  int* row = cnt + w * CPAD;
+  for (int p = 0; p < passes; ++p) {
+    const int shift = p * db0, db = min(db0, kb - shift);
+    const uint32_t dmask = (1u << db) - 1u;
+    __syncthreads();                                   // the previous scatter (buf, scr) is done
+    for (int j = tid; j < RW * CPAD; j += RT) cnt[j] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      if (i < iters) {
+        const int q = w * S + i * 64 + lane;
+        const bool valid = q < nnz;
+        word[i] = valid ? buf[q] : (W)0;
+        rk[i] = wave_rank((uint32_t)(word[i] >> (ib + shift)) & dmask, valid, db, row, lane);
+      }
+    }
+    __syncthreads();
+    scan_counters(cnt, scr, 1 << db);
+    const bool last = p + 1 == passes;
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      if (i < iters && w * S + i * 64 + lane < nnz) {
+        const int pos = row[(uint32_t)(word[i] >> (ib + shift)) & dmask] + rk[i];
+        if (last) {
+          sk[Z + pos] = (uint32_t)(word[i] >> ib);
+          sv[Z + pos] = (uint32_t)(word[i] & emask);
+        } else {
+          buf[pos] = word[i];
+        }
+      }
+    }
+  }
+}
+
+// Multi-workgroup form (more entries than one CU's LDS holds): words key << 32 | entry ping-pong in global
+// memory; per digit pass: count (per-tile digit totals, hist[digit][tile]) -> scan (one workgroup) -> scatter
+// (the same ranks again plus the tile's offsets).  in == null: the first pass reads the keys.
+__device__ __forceinline__ void tile_rank(const Keys& K, const uint64_t* in, int64_t tile, int shift, int db,
+                                          int* cnt, uint64_t (&word)[ITB], int (&rk)[ITB]) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int j = tid; j < RW * CPAD; j += RT) cnt[j] = 0;
+  __syncthreads();
+  int* row = cnt + w * CPAD;
+  const uint32_t dmask = (1u << db) - 1u;
+#pragma unroll
+  for (int i = 0; i < ITB; ++i) {
+    const int64_t e = tile * TB + w * (ITB * 64) + i * 64 + lane;
+    const bool valid = e < K.n;
+    if (in) word[i] = valid ? in[e] : 0ull;
+    else word[i] = valid ? ((uint64_t)K.get(e) << 32 | (uint64_t)e) : 0ull;
+    rk[i] = wave_rank((uint32_t)(word[i] >> (32 + shift)) & dmask, valid, db, row, lane);
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(RT) void rsort_count_kernel(Keys K, const uint64_t* __restrict__ in, int shift, int db,
+                                                         int* __restrict__ hist) {
+  __shared__ int cnt[RW * CPAD];
+  uint64_t word[ITB];
+  int rk[ITB];
+  tile_rank(K, in, blockIdx.x, shift, db, cnt, word, rk);
+  const int d = threadIdx.x;
+  if (d < (1 << db)) {
+    int s = 0;
+    for (int w = 0; w < RW; ++w) s += cnt[w * CPAD + d];
+    hist[(int64_t)d * gridDim.x + blockIdx.x] = s;
+  }
+}
+
+// exclusive scan of hist[0..m) in place, one workgroup, each thread a contiguous run
+__global__ __launch_bounds__(RT) void rsort_scan_kernel(int* __restrict__ hist, int64_t m) {
+  __shared__ int ts[RT];
+  const int tid = threadIdx.x;
+  const int64_t per = cdiv(m, RT), g0 = tid * per, g1 = min(m, g0 + per);
+  int s = 0;
+  for (int64_t g = g0; g < g1; ++g) s += hist[g];
+  ts[tid] = s;
+  __syncthreads();
+  for (int o = 1; o < RT; o <<= 1) {
+    const int x = tid >= o ? ts[tid - o] : 0;
+    __syncthreads();
+    ts[tid] += x;
+    __syncthreads();
+  }
+  int off = ts[tid] - s;
+  for (int64_t g = g0; g < g1; ++g) {
+    const int x = hist[g];
+    hist[g] = off;
+    off += x;
+  }
+}
+
+__global__ __launch_bounds__(RT) void rsort_scatter_kernel(Keys K, const uint64_t* __restrict__ in, int shift, int db,
+                                                           const int* __restrict__ hist, uint64_t* __restrict__ out,
+                                                           uint32_t* __restrict__ sk, uint32_t* __restrict__ sv) {
+  __shared__ int cnt[RW * CPAD];
+  uint64_t word[ITB];
+  int rk[ITB];
+  tile_rank(K, in, blockIdx.x, shift, db, cnt, word, rk);
+  const int d = threadIdx.x;
+  if (d < (1 << db)) {   // the tile's offset for digit d, then the waves' in order
+    int run = hist[(int64_t)d * gridDim.x + blockIdx.x];
+    for (int w = 0; w < RW; ++w) {
+      const int t = cnt[w * CPAD + d];
+      cnt[w * CPAD + d] = run;
+      run += t;
+    }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t dmask = (1u << db) - 1u;
+#pragma unroll
+  for (int i = 0; i < ITB; ++i) {
+    const int64_t e = (int64_t)blockIdx.x * TB + w * (ITB * 64) + i * 64 + lane;
+    if (e >= K.n) continue;
+    const int pos = cnt[w * CPAD + ((uint32_t)(word[i] >> (32 + shift)) & dmask)] + rk[i];
+    if (out) {
+      out[pos] = word[i];
+    } else {
+      sk[pos] = (uint32_t)(word[i] >> 32);
+      sv[pos] = (uint32_t)word[i];
+    }
+  }
 }
 
 // start[v] = first sorted position with key >= v, for v <= V: one thread per key, a binary search of the sorted
@@ -516,6 +768,17 @@ int64_t rs_item_index_ws_bytes(int nsrc, int64_t rows, int64_t table_rows, int64
   return (int64_t)L.total_bytes;
 }
 
+int rs_item_index_layout(int nsrc, int64_t rows, int64_t table_rows, int64_t d, int64_t* out) {
+  if (nsrc < 1 || nsrc > 3 || rows <= 0 || table_rows <= 0 || d <= 0 || !out) return RS_ERR_ARG;
+  ig::Layout L;
+  if (ig::layout(nsrc, rows, table_rows, d, L) != hipSuccess) return RS_ERR_ARG;
+  out[0] = (int64_t)L.sk;
+  out[1] = (int64_t)L.sv;
+  out[2] = (int64_t)L.start;
+  out[3] = L.path;
+  return 0;
+}
+
 int rs_item_index_build(int nsrc, const int64_t* keys0, const int64_t* keys1, const int64_t* keys2, int64_t rows,
                         int64_t table_rows, int64_t d, void* ws, int64_t ws_bytes, void* stream) {
   if (nsrc < 1 || nsrc > 3 || rows <= 0 || table_rows <= 0 || !ws || !keys0 || (nsrc > 1 && !keys1) ||
@@ -531,7 +794,6 @@ int rs_item_index_build(int nsrc, const int64_t* keys0, const int64_t* keys1, co
   uint32_t* sk = (uint32_t*)(w + L.sk);
   uint32_t* sv = (uint32_t*)(w + L.sv);
   int* start = (int*)(w + L.start);
-  const int bits = ig::key_bits(table_rows);
   if (L.cs) {
     int* H = (int*)(w + L.H);
     int* total = (int*)(w + L.total);
@@ -551,13 +813,38 @@ int rs_item_index_build(int nsrc, const int64_t* keys0, const int64_t* keys1, co
     hipLaunchKernelGGL(ig::place_kernel, dim3((unsigned)L.nb), dim3(256), 0, s, K, H, start, sk, sv);
     return (int)hipGetLastError();
   }
-  uint32_t* kin = (uint32_t*)(w + L.keys_in);
-  uint32_t* vin = (uint32_t*)(w + L.vals_in);
-  hipLaunchKernelGGL(ig::make_keys_kernel, dim3((unsigned)cdiv(L.n, 256)), dim3(256), 0, s, K, kin, vin);
+  if (L.path == ig::SORT_LDS32 || L.path == ig::SORT_LDS64) {
+    const bool u32 = L.path == ig::SORT_LDS32;
+    static const bool attr = [] {
+      return hipFuncSetAttribute((const void*)ig::lsort_kernel<uint32_t, ig::IT32>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, ig::LDS_MAX) == hipSuccess &&
+             hipFuncSetAttribute((const void*)ig::lsort_kernel<uint64_t, ig::IT64>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, ig::LDS_MAX) == hipSuccess;
+    }();
+    if (!attr) return RS_ERR_UNSUPPORTED;
+    const size_t lds = ig::RHDR + (size_t)L.n * (u32 ? 4 : 8);
+    if (u32)
+      hipLaunchKernelGGL((ig::lsort_kernel<uint32_t, ig::IT32>), dim3(1), dim3(ig::RT), lds, s, K, L.ib, L.kb, sk, sv);
+    else
+      hipLaunchKernelGGL((ig::lsort_kernel<uint64_t, ig::IT64>), dim3(1), dim3(ig::RT), lds, s, K, 32, L.kb, sk, sv);
+  } else {
+    uint64_t* ping = (uint64_t*)(w + L.ping);
+    uint64_t* pong = (uint64_t*)(w + L.pong);
+    int* hist = (int*)(w + L.hist);
+    const int64_t tiles = cdiv(L.n, ig::TB);
+    const int passes = ig::sort_passes(L.kb), db0 = ig::sort_digit(L.kb);
+    const uint64_t* in = nullptr;
+    for (int p = 0; p < passes; ++p) {
+      const int shift = p * db0, db = std::min(db0, L.kb - shift);
+      uint64_t* out = p + 1 == passes ? nullptr : (p % 2 == 0 ? ping : pong);
+      hipLaunchKernelGGL(ig::rsort_count_kernel, dim3((unsigned)tiles), dim3(ig::RT), 0, s, K, in, shift, db, hist);
+      hipLaunchKernelGGL(ig::rsort_scan_kernel, dim3(1), dim3(ig::RT), 0, s, hist, (int64_t)(1 << db) * tiles);
+      hipLaunchKernelGGL(ig::rsort_scatter_kernel, dim3((unsigned)tiles), dim3(ig::RT), 0, s, K, in, shift, db, hist,
+                         out, sk, sv);
+      in = out;
+    }
+  }
   if ((e = hipGetLastError()) != hipSuccess) return (int)e;
-  size_t tb = L.temp_bytes;
-  e = hipcub::DeviceRadixSort::SortPairs((void*)(w + L.temp), tb, kin, sk, vin, sv, (int)L.n, 0, bits, s);
-  if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(ig::lower_bounds_kernel, dim3((unsigned)cdiv(table_rows + 1, 256)), dim3(256), 0, s, sk, L.n,
                      table_rows, start);
   return (int)hipGetLastError();

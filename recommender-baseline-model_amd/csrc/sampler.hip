@@ -12,6 +12,10 @@
 //
 // rs_bert_mask replaces BertTrainDataset's per-token Python masking (BS/dataloaders/bert.py:77-110).
 //
+// The *_draws forms also record the random draws each row consumed (user index, candidate negatives / the
+// masking uniform and replacement item), so tests replay the reference's construction on them
+// (oracle/sampling.py) and compare the batch bit for bit.
+//
 // rs_rank_metrics restates recalls_ndcgs_and_mrr_for_ks (BS/trainers/utils.py:28-57) on the GPU:
 // per row the rank of every positive among the candidates (score descending, ties by index as a
 // stable sort), then Recall@k / NDCG@k / MRR@k summed over rows in a fixed order.
@@ -21,6 +25,7 @@
 namespace smp {
 
 constexpr int HS = 1024;   // LDS hash-set slots (>= 2 * window)
+constexpr int NA = 256;    // negative-draw attempts per position (the rejection loop's bound; a draws record keeps all)
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
@@ -46,7 +51,8 @@ __global__ __launch_bounds__(256) void sas_sample_kernel(const int64_t* __restri
                                                          const int64_t* __restrict__ items, int64_t n_users,
                                                          int64_t item_num, int T, const uint64_t* seed_base,
                                                          uint64_t salt, int64_t* __restrict__ seq,
-                                                         int64_t* __restrict__ pos, int64_t* __restrict__ neg) {
+                                                         int64_t* __restrict__ pos, int64_t* __restrict__ neg,
+                                                         int64_t* __restrict__ draws) {
   __shared__ int64_t tab[HS];
   const int tid = threadIdx.x;
   const int64_t b = blockIdx.x;
@@ -57,6 +63,9 @@ __global__ __launch_bounds__(256) void sas_sample_kernel(const int64_t* __restri
   const int64_t n = L < T ? L : T;          // window = the last n items (history[-max_len:])
   const int64_t w0 = s0 + L - n;
   const int64_t pad = T - n + 1;
+  // draws (tests): per row {u, then per position the first NA candidate negatives, -1 where no negative is drawn}
+  int64_t* dr = draws ? draws + b * (1 + (int64_t)T * NA) : nullptr;
+  if (dr && tid == 0) dr[0] = u;
   for (int i = tid; i < HS; i += 256) tab[i] = -1;
   __syncthreads();
   for (int64_t i = tid; i < n; i += 256) {
@@ -79,10 +88,13 @@ __global__ __launch_bounds__(256) void sas_sample_kernel(const int64_t* __restri
       pv = items[w0 + o + 1];
       const uint64_t base = seed + (((uint64_t)b * (uint64_t)T + (uint64_t)t) << 20);
       int64_t v = (int64_t)__umul64hi(splitmix64(base), V1);
-      for (int a = 1; a < 256 && contains(tab, v); ++a) v = (int64_t)__umul64hi(splitmix64(base + a), V1);
+      for (int a = 1; a < NA && contains(tab, v); ++a) v = (int64_t)__umul64hi(splitmix64(base + a), V1);
       for (int64_t k = 0; k < (int64_t)V1 && contains(tab, v); ++k) v = (v + 1) % (int64_t)V1;   // never reached in practice
       nv = v;
     }
+    if (dr)
+      for (int a = 0; a < NA; ++a)
+        dr[1 + (int64_t)t * NA + a] = o >= 0 ? (int64_t)__umul64hi(splitmix64(seed + (((uint64_t)b * (uint64_t)T + (uint64_t)t) << 20) + a), V1) : -1;
     seq[b * T + t] = sv;
     pos[b * T + t] = pv;
     neg[b * T + t] = nv;
@@ -103,7 +115,8 @@ __global__ __launch_bounds__(256) void bert_mask_kernel(const int64_t* __restric
                                                         int64_t num_items, int T, float p,
                                                         const int64_t* __restrict__ perm,
                                                         const uint64_t* __restrict__ state, uint64_t salt,
-                                                        int64_t* __restrict__ tokens, int64_t* __restrict__ labels) {
+                                                        int64_t* __restrict__ tokens, int64_t* __restrict__ labels,
+                                                        int64_t* __restrict__ draws) {
   const int64_t b = blockIdx.x;
   const uint64_t seed = salt ^ (state[0] * 0xD1B54A32D192ED03ull);
   const int64_t slot = (int64_t)(((state[1] - 1) * (uint64_t)gridDim.x + (uint64_t)b) % (uint64_t)n_users);
@@ -112,22 +125,35 @@ __global__ __launch_bounds__(256) void bert_mask_kernel(const int64_t* __restric
   const int64_t n = L < T ? L : T;
   const int64_t w0 = s0 + L - n, pad = T - n;
   const int64_t mask_token = num_items + 1;
+  // the reference's decision (prob = rng.rand(); prob < mask_prob; prob /= mask_prob; < 0.8; < 0.9) in double on
+  // the 24-bit uniform k / 2^24, exactly as Python evaluates it on that value
+  const double pd = (double)p;
+  // draws (tests): per row {u, then per position (k, the replacement item), -1 on padding}
+  int64_t* dr = draws ? draws + b * (1 + 2 * (int64_t)T) : nullptr;
+  if (dr && threadIdx.x == 0) dr[0] = u;
   for (int t = threadIdx.x; t < T; t += 256) {
-    int64_t tok = 0, lab = 0;
+    int64_t tok = 0, lab = 0, dk = -1, di = -1;
     if (t >= pad) {
       const int64_t it = items[w0 + t - pad];
       const uint64_t h = splitmix64(seed + (((uint64_t)b * (uint64_t)T + (uint64_t)t) << 8));
-      const float prob = (float)(h >> 40) * (1.0f / 16777216.0f);      // 24-bit uniform [0, 1)
+      const double prob = (double)(h >> 40) * (1.0 / 16777216.0);      // 24-bit uniform [0, 1), exact in double
+      const int64_t rnd = 1 + (int64_t)__umul64hi(splitmix64(h ^ 0x9E3779B97F4A7C15ull), (uint64_t)num_items);
       tok = it;
-      if (prob < p) {
-        const float q = prob / p;
-        if (q < 0.8f) tok = mask_token;
-        else if (q < 0.9f) tok = 1 + (int64_t)__umul64hi(splitmix64(h ^ 0x9E3779B97F4A7C15ull), (uint64_t)num_items);
+      if (prob < pd) {
+        const double q = prob / pd;
+        if (q < 0.8) tok = mask_token;
+        else if (q < 0.9) tok = rnd;
         lab = it;
       }
+      dk = (int64_t)(h >> 40);
+      di = rnd;
     }
     tokens[b * T + t] = tok;
     labels[b * T + t] = lab;
+    if (dr) {
+      dr[1 + 2 * t] = dk;
+      dr[2 + 2 * t] = di;
+    }
   }
 }
 
@@ -207,30 +233,44 @@ __global__ __launch_bounds__(256) void rank_mean_kernel(const float* __restrict_
 
 extern "C" {
 
-int rs_sas_sample(const int64_t* user_offsets, const int64_t* user_items, int64_t n_users, int64_t item_num,
-                  int64_t batch, int64_t max_len, uint64_t* seed_base, uint64_t salt, int64_t* seq, int64_t* pos,
-                  int64_t* neg, void* stream) {
+int rs_sas_sample_draws(const int64_t* user_offsets, const int64_t* user_items, int64_t n_users, int64_t item_num,
+                        int64_t batch, int64_t max_len, uint64_t* seed_base, uint64_t salt, int64_t* seq, int64_t* pos,
+                        int64_t* neg, int64_t* draws, void* stream) {
   if (n_users <= 0 || item_num <= 0 || batch <= 0 || max_len <= 0 || max_len > smp::HS / 2 || !user_offsets ||
       !user_items || !seq || !pos || !neg)
     return RS_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   if (seed_base) hipLaunchKernelGGL(smp::seed_step_kernel, dim3(1), dim3(64), 0, s, seed_base);
   hipLaunchKernelGGL(smp::sas_sample_kernel, dim3((unsigned)batch), dim3(256), 0, s, user_offsets, user_items, n_users,
-                     item_num, (int)max_len, seed_base, salt, seq, pos, neg);
+                     item_num, (int)max_len, seed_base, salt, seq, pos, neg, draws);
   return (int)hipGetLastError();
 }
 
-int rs_bert_mask(const int64_t* user_offsets, const int64_t* user_items, int64_t n_users, int64_t num_items,
-                 int64_t batch, int64_t max_len, float mask_prob, const int64_t* perm, uint64_t* state, uint64_t salt,
-                 int64_t* tokens, int64_t* labels, void* stream) {
+int rs_sas_sample(const int64_t* user_offsets, const int64_t* user_items, int64_t n_users, int64_t item_num,
+                  int64_t batch, int64_t max_len, uint64_t* seed_base, uint64_t salt, int64_t* seq, int64_t* pos,
+                  int64_t* neg, void* stream) {
+  return rs_sas_sample_draws(user_offsets, user_items, n_users, item_num, batch, max_len, seed_base, salt, seq, pos,
+                             neg, nullptr, stream);
+}
+
+int rs_bert_mask_draws(const int64_t* user_offsets, const int64_t* user_items, int64_t n_users, int64_t num_items,
+                       int64_t batch, int64_t max_len, float mask_prob, const int64_t* perm, uint64_t* state,
+                       uint64_t salt, int64_t* tokens, int64_t* labels, int64_t* draws, void* stream) {
   if (n_users <= 0 || num_items <= 0 || batch <= 0 || max_len <= 0 || !(mask_prob >= 0.f && mask_prob <= 1.f) ||
       !user_offsets || !user_items || !state || !tokens || !labels)
     return RS_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(smp::mask_step_kernel, dim3(1), dim3(64), 0, s, state);
   hipLaunchKernelGGL(smp::bert_mask_kernel, dim3((unsigned)batch), dim3(256), 0, s, user_offsets, user_items, n_users,
-                     num_items, (int)max_len, mask_prob, perm, state, salt, tokens, labels);
+                     num_items, (int)max_len, mask_prob, perm, state, salt, tokens, labels, draws);
   return (int)hipGetLastError();
+}
+
+int rs_bert_mask(const int64_t* user_offsets, const int64_t* user_items, int64_t n_users, int64_t num_items,
+                 int64_t batch, int64_t max_len, float mask_prob, const int64_t* perm, uint64_t* state, uint64_t salt,
+                 int64_t* tokens, int64_t* labels, void* stream) {
+  return rs_bert_mask_draws(user_offsets, user_items, n_users, num_items, batch, max_len, mask_prob, perm, state, salt,
+                            tokens, labels, nullptr, stream);
 }
 
 int rs_rank_metrics(const float* scores, const float* labels, int64_t rows, int64_t cands, int nk, const int* ks,

@@ -51,9 +51,11 @@ class DeviceWarpSampler:
         self.seed_base = torch.zeros(1, dtype=torch.int64, device=self.device)
         self.cnt = 0
 
-    def sample_into(self, seq, pos, neg):
-        """Write the next batch into existing (batch_size, max_len) int64 device tensors."""
-        ops.sas_sample(self.offsets, self.items, self.n_users, self.item_num, self.seed_base, self.salt, seq, pos, neg)
+    def sample_into(self, seq, pos, neg, draws=None):
+        """Write the next batch into existing (batch_size, max_len) int64 device tensors (draws: see
+        ops.sas_sample)."""
+        ops.sas_sample(self.offsets, self.items, self.n_users, self.item_num, self.seed_base, self.salt, seq, pos, neg,
+                       draws)
 
     def sample(self):
         shape = (self.batch_size, self.max_len)
@@ -107,9 +109,9 @@ class DeviceBertMasker:
         torch.randperm(self.n_users, generator=self.gen, device=self.device, out=self.perm)
         self.state[1:2].zero_()
 
-    def sample_into(self, tokens, labels):
+    def sample_into(self, tokens, labels, draws=None):
         ops.bert_mask(self.offsets, self.items, self.n_users, self.num_items, self.mask_prob, self.perm, self.state,
-                      self.salt, tokens, labels)
+                      self.salt, tokens, labels, draws)
 
     def sample(self):
         shape = (self.batch_size, self.max_len)

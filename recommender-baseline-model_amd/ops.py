@@ -634,6 +634,17 @@ def item_index_build(keys, table_rows, d, ws):
     call("rs_item_index_build", len(keys), kp[0], kp[1], kp[2], rows, table_rows, d, ptr(ws), ws.numel(), stream())
 
 
+def item_index_view(nsrc, rows, table_rows, d, ws):
+    """(sorted keys, sorted entries, start, sort path) of a built index: views into ws (tests and tools)."""
+    out = (_lib.i64 * 4)()
+    call("rs_item_index_layout", nsrc, rows, table_rows, d, out)
+    n = nsrc * rows
+    sk = ws[out[0]:out[0] + 4 * n].view(torch.int32)
+    sv = ws[out[1]:out[1] + 4 * n].view(torch.int32)
+    start = ws[out[2]:out[2] + 4 * (table_rows + 1)].view(torch.int32)
+    return sk, sv, start, int(out[3])
+
+
 def item_grad(ws, nsrc, rows, dx, scale, drop_p, salt, seed_base, f, w1, w2, dtable):
     table_rows, d = dtable.shape
     # fp32 (the parity path): one workgroup per table row; bf16: the chunked kernels (d in {64, 128, 256})
@@ -663,15 +674,25 @@ def sas_head_finish(part, divisor, out):
 
 
 # ---- on-device sampler and ranking metrics (sampler.hip) -----------------------------------
-def sas_sample(user_offsets, user_items, n_users, item_num, seed_base, salt, seq, pos, neg):
+def sas_sample(user_offsets, user_items, n_users, item_num, seed_base, salt, seq, pos, neg, draws=None):
+    """draws (optional, tests): int64 (batch, 1 + 256 * max_len) record of the draws (rs_sas_sample_draws)."""
     B, T = seq.shape
+    if draws is not None:
+        call("rs_sas_sample_draws", ptr(user_offsets), ptr(user_items), n_users, item_num, B, T, ptr(seed_base), salt,
+             ptr(seq), ptr(pos), ptr(neg), ptr(draws), stream())
+        return
     call("rs_sas_sample", ptr(user_offsets), ptr(user_items), n_users, item_num, B, T, ptr(seed_base), salt,
          ptr(seq), ptr(pos), ptr(neg), stream())
 
 
-def bert_mask(offsets, items, n_users, num_items, mask_prob, perm, state, salt, tokens, labels):
-    """rs_bert_mask: the next (tokens, labels) batch into (batch, max_len) int64 device tensors."""
+def bert_mask(offsets, items, n_users, num_items, mask_prob, perm, state, salt, tokens, labels, draws=None):
+    """rs_bert_mask: the next (tokens, labels) batch into (batch, max_len) int64 device tensors; draws (optional,
+    tests): int64 (batch, 1 + 2 * max_len) record of the draws (rs_bert_mask_draws)."""
     B, T = tokens.shape
+    if draws is not None:
+        call("rs_bert_mask_draws", ptr(offsets), ptr(items), n_users, num_items, B, T, mask_prob, ptr(perm),
+             ptr(state), salt, ptr(tokens), ptr(labels), ptr(draws), stream())
+        return
     call("rs_bert_mask", ptr(offsets), ptr(items), n_users, num_items, B, T, mask_prob, ptr(perm), ptr(state), salt,
          ptr(tokens), ptr(labels), stream())
 

@@ -31,16 +31,18 @@ def _inputs(M, V1, d, seed):
 
 
 def _radix_path(M, V1):
-    """True when itemgrad.hip's layout() takes the device radix sort instead of the counting sort: tables over
-    the LDS histogram's 32k rows, (512-entry sort blocks) x (table rows) > 2^26 histogram ints, or keys wider than
-    22 bits."""
+    """True when itemgrad.hip's layout() takes the hand-written radix sort instead of the counting sort: tables
+    over the LDS histogram's 32k rows, (512-entry sort blocks) x (table rows) > 2^26 histogram ints, or keys wider
+    than 22 bits."""
     nb = -(-3 * M // 512)
     return V1 > 32768 or nb * V1 > (1 << 26) or (V1 - 1).bit_length() > 22
 
 
-# tables over 32k rows (40,000; 800,000) -> the device radix sort path; the rest -> the counting sort
+# tables over 32k rows (40,000; 54,543; 800,000) -> the radix sort (one workgroup in LDS for 9,000 / 19,200 entries,
+# multi-workgroup for 90,000); the rest -> the counting sort
 @pytest.mark.parametrize("M,V1,d,p", [(25600, 3417, 128, 0.2), (5000, 300, 64, 0.0), (777, 50, 256, 0.1),
-                                      (64, 5, 128, 0.0), (3000, 40000, 64, 0.0), (30000, 800000, 64, 0.0)])
+                                      (64, 5, 128, 0.0), (3000, 40000, 64, 0.0), (6400, 54543, 128, 0.2),
+                                      (30000, 800000, 64, 0.0)])
 def test_item_grad_matches_atomic_scatter(M, V1, d, p):
     assert _radix_path(M, V1) == (V1 > 32768)
     import rbm_amd  # noqa: F401
@@ -74,3 +76,48 @@ def test_item_grad_matches_atomic_scatter(M, V1, d, p):
     ops.item_index_build([ids, pos, neg], V1, d, ws)
     ops.item_grad(ws, 3, M, dx, scale, p, salt, seed_base, f, dpl, dnl, again)
     assert torch.equal(again, ours)
+
+
+def _index_keys(nsrc, M, V1, pad, seed):
+    rng = np.random.default_rng(seed)
+    w = 1.0 / np.arange(1, V1) ** 1.05
+    w /= w.sum()
+    ks = []
+    for _ in range(nsrc):
+        k = rng.choice(np.arange(1, V1), size=M, p=w)
+        k[rng.random(M) < pad] = 0
+        ks.append(k)
+    return ks
+
+
+# (nsrc, rows, table rows, padding share, expected sort path): 0 counting sort, 1 / 2 one-workgroup LDS radix sort
+# with u32 / u64 words, 3 multi-workgroup radix sort.  cfg4 = 3 x 6,400 entries over 54,543 rows (~80 % padding);
+# cfg5 = 12,800 token ids over 1,000,002 rows.
+@pytest.mark.parametrize("nsrc,M,V1,pad,path", [
+    (3, 25600, 3417, 0.2, 0), (3, 6400, 54543, 0.8, 1), (3, 3000, 40000, 0.15, 1), (1, 12800, 1000002, 0.28, 2),
+    (3, 30000, 800000, 0.15, 3), (1, 40000, 1000002, 0.3, 3), (3, 12272, 54543, 0.0, 1), (1, 1, 40000, 0.0, 1),
+    (3, 6400, 54543, 1.0, 1), (1, 18408, 1000002, 0.0, 2), (1, 18409, 1000002, 0.0, 3)])
+def test_item_index_is_the_stable_sort(nsrc, M, V1, pad, path):
+    """The built index equals numpy's stable argsort of the concatenated keys bit for bit (sorted keys, entries,
+    and start[v] = first position of key >= v), on every sort path incl. all-padding and single-entry batches."""
+    import rbm_amd  # noqa: F401
+    from rbm_amd import ops
+    d = 128
+    ks = _index_keys(nsrc, M, V1, pad, seed=M + V1)
+    dev = [torch.from_numpy(k).cuda() for k in ks]
+    ws = torch.empty(ops.item_index_ws_bytes(nsrc, M, V1, d), dtype=torch.uint8, device="cuda")
+    ops.item_index_build(dev, V1, d, ws)
+    sk, sv, start, got_path = ops.item_index_view(nsrc, M, V1, d, ws)
+    torch.cuda.synchronize()
+    assert got_path == path
+    allk = np.concatenate(ks)
+    order = np.argsort(allk, kind="stable")
+    srt = allk[order]
+    assert np.array_equal(sk.cpu().numpy().astype(np.int64), srt)
+    assert np.array_equal(sv.cpu().numpy().astype(np.int64), order)
+    assert np.array_equal(start.cpu().numpy().astype(np.int64), np.searchsorted(srt, np.arange(V1 + 1), "left"))
+    # a second build over the same workspace: the same bits (no state carried between builds)
+    ws2 = ws.clone()
+    ops.item_index_build(dev, V1, d, ws2)
+    sk2, sv2, _, _ = ops.item_index_view(nsrc, M, V1, d, ws2)
+    assert torch.equal(sk2, sk) and torch.equal(sv2, sv)
