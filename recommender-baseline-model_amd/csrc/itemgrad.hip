@@ -15,13 +15,15 @@
 //                        rank -- all hand-written -- for tables whose per-block histograms fit LDS
 //                        (<= 32k rows: cfg2, cfg3).  Larger tables (cfg4's 54.5k items, cfg5's 1M tokens)
 //                        take a hand-written LSD radix sort instead (the counting sort's nb x V global
-//                        histogram was 33-100 MB of traffic beside the forward): while the entries fit
-//                        one CU's LDS (cfg4: 19,200, cfg5: 12,800) ONE 1024-thread workgroup first splits
-//                        off the padding keys (written straight to the front of the output), then sorts
-//                        the rest in LDS by 7-8-bit digits -- stable per-wave ranks from 8 ballots, wave x
-//                        digit counters, one workgroup scan per pass -- on a single CU beside the
-//                        forward; larger batches run the same ranking as a multi-workgroup
-//                        count / scan / scatter per digit.  -> start[v] for v <= V (a binary search per key)
+//                        histogram was 33-100 MB of traffic beside the forward): per pass of <= 8 key
+//                        bits, a count launch (per-tile digit histograms) and a scatter launch (stable
+//                        per-wave ranks from 8 ballots, wave x digit counters, each tile's digit offsets
+//                        scanned by the tile itself).  The workgroups are thin on purpose: a one-CU
+//                        LDS-resident sort (tried) held a CU for 42-51 us, and every forward kernel runs
+//                        one workgroup per CU, so its last workgroup waited behind it (+9 us per step
+//                        at cfg4); these co-reside with the forward's workgroups instead.  No per-key start table (a 1M-row table's
+//                        4 MB of it was a launch of its own): the gradient kernels find a key run's
+//                        extent from the neighbouring sorted keys
 //   rs_item_grad:        chunks of 64 sorted entries: contribution rows summed per key run in
 //                        LDS; a key wholly inside one chunk is written by that chunk (+=); a
 //                        key spanning chunks leaves per-chunk partials that the chunk holding
@@ -44,25 +46,22 @@ constexpr int64_t HMAX = (int64_t)1 << 26;  // largest per-block histogram table
 constexpr int IBITS = 9;                    // BE = 2^IBITS: an entry's block index in the sort word's low bits
 constexpr int KBITS_MAX = 32 - IBITS - 1;   // key bits the counting-sort path's (key, index) sort word holds
 static_assert(BE == 1 << IBITS, "sort word layout");
-// LSD radix sort (tables past the counting sort's limits)
-constexpr int RT = 1024;                   // threads of a sort workgroup
+// LSD radix sort (tables past the counting sort's limits): thin workgroups that co-reside with the forward's
+// one-workgroup-per-CU kernels (~20 VGPRs of words, 5 KB LDS), so the side-queue sort takes no CU from them
+constexpr int RT = 256;                    // threads of a sort workgroup
 constexpr int RW = RT / 64;                // its waves
-constexpr int RB = 8;                      // widest digit (bits)
-constexpr int CPAD = (1 << RB) + 1;        // per-wave counter row pitch: rows start on different banks
-constexpr int RHDR = RW * CPAD * 4 + 128;  // LDS bytes ahead of the word buffer: counters + scan scratch
-constexpr int LDS_MAX = 160 * 1024;
-constexpr int IT32 = 36, IT64 = 18;        // words per thread of the one-workgroup sort (u32 / u64 words)
-constexpr int64_t N32 = (LDS_MAX - RHDR) / 4, N64 = (LDS_MAX - RHDR) / 8;   // 36,816 / 18,408 entries
-constexpr int ITB = 8;                     // words per thread of a multi-workgroup tile
-constexpr int TB = RT * ITB;               // entries per tile
-static_assert(N32 <= (int64_t)IT32 * RT && N64 <= (int64_t)IT64 * RT, "register words cover the LDS buffer");
-static_assert(RHDR % 16 == 0, "word buffer alignment");
-
-enum SortPath { SORT_COUNT = 0, SORT_LDS32 = 1, SORT_LDS64 = 2, SORT_TILES = 3 };
+constexpr int RB = 8;                      // widest digit (bits): one digit per thread in the scans
+constexpr int NBIN = 1 << RB;
+constexpr int CPAD = NBIN + 1;             // per-wave counter row pitch: rows start on different banks
+constexpr int ITB = 8;                     // words per thread of a tile
+constexpr int TB = RT * ITB;               // entries per tile (2,048: cfg4's 19,200 entries are 10 tiles)
+constexpr int64_t FUSED_SCAN_TILES = 64;   // up to this many tiles each scatter workgroup scans the counts itself
+static_assert(NBIN == RT, "one thread per digit");
+enum SortPath { SORT_COUNT = 0, SORT_TILES = 3 };
 
 struct Layout {
   int64_t n, nchunks, nb, V;
-  int path, kb, ib;          // SortPath; key bits; entry-index bits (one-workgroup u32 words)
+  int path, kb;              // SortPath; key bits
   bool cs;
   size_t sk, sv, start, part, H, total, ping, pong, hist, temp, temp_bytes, total_bytes;
 };
@@ -85,13 +84,12 @@ static hipError_t layout(int nsrc, int64_t rows, int64_t table_rows, int64_t d, 
   // it more than the sort costs: cfg4 0.2226 -> 0.2148 ms/step, cfg5 12.20 -> 12.09 with the radix sort
   L.cs = table_rows <= VMAX_LDS && L.nb * table_rows <= HMAX && key_bits(table_rows) <= KBITS_MAX;
   L.kb = key_bits(table_rows);
-  L.ib = key_bits(L.n);
-  L.path = L.cs ? SORT_COUNT
-                : (L.kb + L.ib <= 32 && L.n <= N32) ? SORT_LDS32 : (L.n <= N64 ? SORT_LDS64 : SORT_TILES);
+  L.path = L.cs ? SORT_COUNT : SORT_TILES;
   size_t o = 0;
   L.sk = o; o = al256(o + L.n * 4);
   L.sv = o; o = al256(o + L.n * 4);
-  L.start = o; o = al256(o + (table_rows + 1) * 4);
+  L.start = 0;
+  if (L.cs) { L.start = o; o = al256(o + (table_rows + 1) * 4); }   // the counting sort's placement offsets
   L.part = o; o = al256(o + L.nchunks * 2 * d * 4);
   L.temp_bytes = 0;
   L.H = L.total = L.ping = L.pong = L.hist = L.temp = 0;
@@ -104,7 +102,7 @@ static hipError_t layout(int nsrc, int64_t rows, int64_t table_rows, int64_t d, 
   } else if (L.path == SORT_TILES) {                     // word ping-pong + per-(digit, tile) counts
     L.ping = o; o = al256(o + L.n * 8);
     L.pong = o; o = al256(o + L.n * 8);
-    L.hist = o; o = al256(o + (size_t)(1 << RB) * cdiv(L.n, TB) * 4);
+    L.hist = o; o = al256(o + (size_t)NBIN * cdiv(L.n, TB) * 4);
   }
   L.total_bytes = o;
   return hipSuccess;
@@ -113,12 +111,12 @@ static hipError_t layout(int nsrc, int64_t rows, int64_t table_rows, int64_t d, 
 struct Keys {
   const int64_t* k[3];
   int64_t rows, n, V;
-  __device__ __forceinline__ uint32_t get(int64_t e) const {
-    const int src = (int)(e / rows);
-    const int64_t r = e - src * rows;
-    int64_t v = k[src][r];
-    return (v < 0 || v >= V) ? 0u : (uint32_t)v;
+  __device__ __forceinline__ const int64_t* addr(int64_t e) const {   // source by comparison: no 64-bit division
+    const int src = (e >= rows) + (e >= 2 * rows);
+    return k[src] + (e - src * rows);
   }
+  __device__ __forceinline__ uint32_t key_of(int64_t v) const { return (v < 0 || v >= V) ? 0u : (uint32_t)v; }
+  __device__ __forceinline__ uint32_t get(int64_t e) const { return key_of(*addr(e)); }
 };
 
 // ---- counting sort ------------------------------------------------------------------------
@@ -323,172 +321,49 @@ __device__ __forceinline__ int wave_rank(uint32_t dig, bool valid, int db, int* 
   return r;
 }
 
-// cnt[w][d] (pitch CPAD) -> exclusive offsets in (digit, wave) order -- the stable order of a pass -- over
-// nbins digits; RT threads, 4 entries each (nbins * RW <= 4096).  Ends with a barrier.
-__device__ __forceinline__ void scan_counters(int* cnt, int* scr, int nbins) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  int v[4], s = 0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int j = 4 * tid + q, d = j / RW, ww = j % RW;
-    v[q] = d < nbins ? cnt[ww * CPAD + d] : 0;
-    s += v[q];
-  }
-  int x = s;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) scr[w] = x;
-  __syncthreads();
-  int off = x - s;
-  for (int k = 0; k < w; ++k) off += scr[k];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int j = 4 * tid + q, d = j / RW, ww = j % RW;
-    if (d < nbins) cnt[ww * CPAD + d] = off;
-    off += v[q];
-  }
-  __syncthreads();
-}
-
 // digit width of an LSD sort over kb key bits: the fewest passes of <= RB bits, split evenly
 __host__ __device__ inline int sort_passes(int kb) { return (kb + RB - 1) / RB; }
 __host__ __device__ inline int sort_digit(int kb) { return (kb + sort_passes(kb) - 1) / sort_passes(kb); }
 
-// ONE workgroup sorts every entry in LDS.  Words: key << ib | entry (u32 when kb + ib <= 32, else u64).
-// Pass 0 sends the padding keys (0) straight to the front of the output in entry order and compacts the
-// others, stably, into the LDS buffer (cfg4's histories are ~80 % padding: the digit passes then rank ~3.5k
-// of the 19.2k entries); each digit pass ranks, scans and scatters them back (the last pass to sk/sv).
-// Element layout of a pass over c entries: wave w holds [w*S, (w+1)*S), S = 64 * ceil(c / RT), lane-fastest,
-// so (digit, wave, iteration, lane) order is the input order within each digit: stable.
-template <typename W, int IT>
-__global__ __launch_bounds__(RT) void lsort_kernel(Keys K, int ib, int kb, uint32_t* __restrict__ sk,
-                                                   uint32_t* __restrict__ sv) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  int* cnt = reinterpret_cast<int*>(smem);
-  int* scr = cnt + RW * CPAD;
-  W* buf = reinterpret_cast<W*>(smem + RHDR);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int n = (int)K.n;
-  const uint64_t lt = (1ull << lane) - 1ull;
-  const W emask = ((W)1 << ib) - (W)1;
-  W word[IT];
-  int rk[IT];
-  int iters = (n + RT - 1) / RT, S = iters * 64;
-  int zc = 0, nc = 0;
+// Words key << 32 | entry; a pass reads its input in tiles of TB entries, wave w of a tile holding entries
+// [w*ITB*64, (w+1)*ITB*64) lane-fastest, so (digit, tile, wave, iteration, lane) order is the input order within
+// each digit: stable.  in == null: the first pass reads the keys.
+__device__ __forceinline__ bool tile_load(const Keys& K, const uint64_t* in, int64_t tile, uint64_t (&word)[ITB]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t e0 = tile * TB + w * (ITB * 64) + lane;
+  if (in) {
 #pragma unroll
-  for (int i = 0; i < IT; ++i) {
-    if (i < iters) {
-      const int e = w * S + i * 64 + lane;
-      const bool valid = e < n;
-      const uint32_t key = valid ? K.get(e) : 0u;
-      const bool nz = key != 0u;
-      const uint64_t bz = __ballot(valid && !nz), bn = __ballot(nz);
-      rk[i] = nz ? nc + (int)__popcll(bn & lt) : zc + (int)__popcll(bz & lt);
-      word[i] = (W)key << ib | (W)(uint32_t)e;
-      zc += (int)__popcll(bz);
-      nc += (int)__popcll(bn);
-    }
-  }
-  if (lane == 0) {
-    scr[w] = zc;
-    scr[RW + w] = nc;
-  }
-  __syncthreads();
-  int zoff = 0, noff = 0, Z = 0;
-  for (int k = 0; k < RW; ++k) {
-    const int a = scr[k], b = scr[RW + k];
-    zoff += k < w ? a : 0;
-    noff += k < w ? b : 0;
-    Z += a;
-  }
+    for (int i = 0; i < ITB; ++i) word[i] = e0 + i * 64 < K.n ? in[e0 + i * 64] : 0ull;
+  } else {
+    int64_t raw[ITB];
 #pragma unroll
-  for (int i = 0; i < IT; ++i) {
-    if (i < iters && w * S + i * 64 + lane < n) {
-      if ((word[i] >> ib) == (W)0) {
-        sk[zoff + rk[i]] = 0u;
-        sv[zoff + rk[i]] = (uint32_t)(word[i] & emask);
-      } else {
-        buf[noff + rk[i]] = word[i];
-      }
-    }
-  }
-  const int nnz = n - Z;
-  iters = (nnz + RT - 1) / RT;
-  S = iters * 64;
-  const int passes = sort_passes(kb), db0 = sort_digit(kb);
-  int* row = cnt + w * CPAD;
-  for (int p = 0; p < passes; ++p) {
-    const int shift = p * db0, db = min(db0, kb - shift);
-    const uint32_t dmask = (1u << db) - 1u;
-    __syncthreads();                                   // the previous scatter (buf, scr) is done
-    for (int j = tid; j < RW * CPAD; j += RT) cnt[j] = 0;
-    __syncthreads();
+    for (int i = 0; i < ITB; ++i) raw[i] = e0 + i * 64 < K.n ? *K.addr(e0 + i * 64) : 0;
 #pragma unroll
-    for (int i = 0; i < IT; ++i) {
-      if (i < iters) {
-        const int q = w * S + i * 64 + lane;
-        const bool valid = q < nnz;
-        word[i] = valid ? buf[q] : (W)0;
-        rk[i] = wave_rank((uint32_t)(word[i] >> (ib + shift)) & dmask, valid, db, row, lane);
-      }
-    }
-    __syncthreads();
-    scan_counters(cnt, scr, 1 << db);
-    const bool last = p + 1 == passes;
-#pragma unroll
-    for (int i = 0; i < IT; ++i) {
-      if (i < iters && w * S + i * 64 + lane < nnz) {
-        const int pos = row[(uint32_t)(word[i] >> (ib + shift)) & dmask] + rk[i];
-        if (last) {
-          sk[Z + pos] = (uint32_t)(word[i] >> ib);
-          sv[Z + pos] = (uint32_t)(word[i] & emask);
-        } else {
-          buf[pos] = word[i];
-        }
-      }
-    }
+    for (int i = 0; i < ITB; ++i) word[i] = (uint64_t)K.key_of(raw[i]) << 32 | (uint64_t)(e0 + i * 64);
   }
+  return true;
 }
 
-// Multi-workgroup form (more entries than one CU's LDS holds): words key << 32 | entry ping-pong in global
-// memory; per digit pass: count (per-tile digit totals, hist[digit][tile]) -> scan (one workgroup) -> scatter
-// (the same ranks again plus the tile's offsets).  in == null: the first pass reads the keys.
-__device__ __forceinline__ void tile_rank(const Keys& K, const uint64_t* in, int64_t tile, int shift, int db,
-                                          int* cnt, uint64_t (&word)[ITB], int (&rk)[ITB]) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  for (int j = tid; j < RW * CPAD; j += RT) cnt[j] = 0;
-  __syncthreads();
-  int* row = cnt + w * CPAD;
-  const uint32_t dmask = (1u << db) - 1u;
-#pragma unroll
-  for (int i = 0; i < ITB; ++i) {
-    const int64_t e = tile * TB + w * (ITB * 64) + i * 64 + lane;
-    const bool valid = e < K.n;
-    if (in) word[i] = valid ? in[e] : 0ull;
-    else word[i] = valid ? ((uint64_t)K.get(e) << 32 | (uint64_t)e) : 0ull;
-    rk[i] = wave_rank((uint32_t)(word[i] >> (32 + shift)) & dmask, valid, db, row, lane);
-  }
-  __syncthreads();
-}
-
+// per-(digit, tile) counts of pass (shift, db): hist[d * tiles + tile]
 __global__ __launch_bounds__(RT) void rsort_count_kernel(Keys K, const uint64_t* __restrict__ in, int shift, int db,
                                                          int* __restrict__ hist) {
-  __shared__ int cnt[RW * CPAD];
+  __shared__ int h[NBIN];
+  const int tid = threadIdx.x;
+  h[tid] = 0;
   uint64_t word[ITB];
-  int rk[ITB];
-  tile_rank(K, in, blockIdx.x, shift, db, cnt, word, rk);
-  const int d = threadIdx.x;
-  if (d < (1 << db)) {
-    int s = 0;
-    for (int w = 0; w < RW; ++w) s += cnt[w * CPAD + d];
-    hist[(int64_t)d * gridDim.x + blockIdx.x] = s;
-  }
+  tile_load(K, in, blockIdx.x, word);
+  __syncthreads();
+  const int lane = tid & 63, w = tid >> 6;
+  const uint32_t dmask = (1u << db) - 1u;
+#pragma unroll
+  for (int i = 0; i < ITB; ++i)
+    if ((int64_t)blockIdx.x * TB + w * (ITB * 64) + i * 64 + lane < K.n)
+      atomicAdd(&h[(uint32_t)(word[i] >> (32 + shift)) & dmask], 1);   // integer counts: order-free
+  __syncthreads();
+  if (tid < (1 << db)) hist[(int64_t)tid * gridDim.x + blockIdx.x] = h[tid];
 }
 
-// exclusive scan of hist[0..m) in place, one workgroup, each thread a contiguous run
+// exclusive scan of hist[0..m) in place (tile counts past FUSED_SCAN_TILES), one workgroup
 __global__ __launch_bounds__(RT) void rsort_scan_kernel(int* __restrict__ hist, int64_t m) {
   __shared__ int ts[RT];
   const int tid = threadIdx.x;
@@ -511,30 +386,74 @@ __global__ __launch_bounds__(RT) void rsort_scan_kernel(int* __restrict__ hist, 
   }
 }
 
+// one pass: rank the tile stably, place every word at (offset of its digit before this tile) + (waves before
+// it) + rank.  scanned == 0: the workgroup forms its digits' offsets from the raw counts itself (thread d sums
+// digit d over the tiles, then an exclusive scan over digits); else hist already holds them.  out == null:
+// the last pass, writing the sorted keys / entries.
 __global__ __launch_bounds__(RT) void rsort_scatter_kernel(Keys K, const uint64_t* __restrict__ in, int shift, int db,
-                                                           const int* __restrict__ hist, uint64_t* __restrict__ out,
-                                                           uint32_t* __restrict__ sk, uint32_t* __restrict__ sv) {
+                                                           const int* __restrict__ hist, int scanned,
+                                                           uint64_t* __restrict__ out, uint32_t* __restrict__ sk,
+                                                           uint32_t* __restrict__ sv) {
   __shared__ int cnt[RW * CPAD];
+  __shared__ int wsum[RW];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nb = 1 << db;
+  const int64_t tiles = gridDim.x, tile = blockIdx.x;
+  // this tile's global digit offsets (thread = digit), issued ahead of the ranking
+  int tot = 0, before = 0;
+  if (tid < nb) {
+    if (scanned) {
+      before = hist[(int64_t)tid * tiles + tile];
+    } else {
+      for (int64_t t = 0; t < tiles; ++t) {
+        const int x = hist[(int64_t)tid * tiles + t];
+        tot += x;
+        before += t < tile ? x : 0;
+      }
+    }
+  }
   uint64_t word[ITB];
+  tile_load(K, in, tile, word);
+  for (int j = tid; j < RW * CPAD; j += RT) cnt[j] = 0;
+  __syncthreads();
+  int* row = cnt + w * CPAD;
+  const uint32_t dmask = (1u << db) - 1u;
   int rk[ITB];
-  tile_rank(K, in, blockIdx.x, shift, db, cnt, word, rk);
-  const int d = threadIdx.x;
-  if (d < (1 << db)) {   // the tile's offset for digit d, then the waves' in order
-    int run = hist[(int64_t)d * gridDim.x + blockIdx.x];
-    for (int w = 0; w < RW; ++w) {
-      const int t = cnt[w * CPAD + d];
-      cnt[w * CPAD + d] = run;
+#pragma unroll
+  for (int i = 0; i < ITB; ++i) {
+    const bool valid = tile * TB + w * (ITB * 64) + i * 64 + lane < K.n;
+    rk[i] = wave_rank((uint32_t)(word[i] >> (32 + shift)) & dmask, valid, db, row, lane);
+  }
+  if (!scanned) {   // exclusive scan of the digit totals over digits (wave scan + wave sums)
+    int x = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    int off = x - tot;
+    for (int k = 0; k < w; ++k) off += wsum[k];
+    before += off;
+  } else {
+    __syncthreads();
+  }
+  if (tid < nb) {   // + the waves before, per digit
+    int run = before;
+#pragma unroll
+    for (int ww = 0; ww < RW; ++ww) {
+      const int t = cnt[ww * CPAD + tid];
+      cnt[ww * CPAD + tid] = run;
       run += t;
     }
   }
   __syncthreads();
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const uint32_t dmask = (1u << db) - 1u;
 #pragma unroll
   for (int i = 0; i < ITB; ++i) {
-    const int64_t e = (int64_t)blockIdx.x * TB + w * (ITB * 64) + i * 64 + lane;
+    const int64_t e = tile * TB + w * (ITB * 64) + i * 64 + lane;
     if (e >= K.n) continue;
-    const int pos = cnt[w * CPAD + ((uint32_t)(word[i] >> (32 + shift)) & dmask)] + rk[i];
+    const int pos = row[(uint32_t)(word[i] >> (32 + shift)) & dmask] + rk[i];
     if (out) {
       out[pos] = word[i];
     } else {
@@ -544,26 +463,10 @@ __global__ __launch_bounds__(RT) void rsort_scatter_kernel(Keys K, const uint64_
   }
 }
 
-// start[v] = first sorted position with key >= v, for v <= V: one thread per key, a binary search of the sorted
-// keys (a thread per ENTRY filling its gap of keys serialised the gap above the largest id, ~V entries, on one lane)
-__global__ __launch_bounds__(256) void lower_bounds_kernel(const uint32_t* __restrict__ sk, int64_t n, int64_t V,
-                                                           int* __restrict__ start) {
-  const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (v > V) return;
-  int64_t lo = 0, hi = n;
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    if ((int64_t)sk[mid] < v) lo = mid + 1;
-    else hi = mid;
-  }
-  start[v] = (int)lo;
-}
-
 // ---- gradient ---------------------------------------------------------------------------------
 struct GradArgs {
   const uint32_t* sk;
   const uint32_t* sv;
-  const int* start;      // [V + 1]
   float* part;
   int64_t n, rows;
   const __bf16* dx;      // source 0 rows: scale * drop(m*d + c) * dx[m]
@@ -582,7 +485,7 @@ template <int D>
 struct ChunkLds {
   float rowsum[CH][D + 4];   // +4: rows start on different banks
   uint32_t skey[CH + 1], sent[CH];
-  int kst[CH], ken[CH];
+  uint32_t prevk, nextk;     // the sorted keys just before and just after the chunk (or a sentinel)
 };
 
 // chunk `chunk` of the sorted entries (one 256-thread workgroup), LDS at `L`
@@ -592,8 +495,6 @@ __device__ __forceinline__ void item_chunk(const GradArgs& a, int64_t chunk, Chu
   auto& rowsum = L.rowsum;
   auto& skey = L.skey;
   auto& sent = L.sent;
-  auto& kst = L.kst;
-  auto& ken = L.ken;
   const int tid = threadIdx.x;
   const int64_t base = chunk * CH;
   const int cnt = (int)min((int64_t)CH, a.n - base);
@@ -604,12 +505,9 @@ __device__ __forceinline__ void item_chunk(const GradArgs& a, int64_t chunk, Chu
     sent[tid] = tid < cnt ? a.sv[base + tid] : 0u;
   }
   if (tid == 0) skey[0] = 0xfffffffeu;   // sentinel: entry 0 always starts a run
+  if (tid == CH) L.prevk = base > 0 ? a.sk[base - 1] : 0xfffffffeu;
+  if (tid == CH + 1) L.nextk = base + cnt < a.n ? a.sk[base + cnt] : 0xfffffffeu;
   __syncthreads();
-  if (tid < cnt) {                        // key bounds, consumed only by the emit pass
-    const uint32_t k = skey[tid + 1];
-    kst[tid] = a.start[k];
-    ken[tid] = a.start[k + 1];
-  }
   // contribution rows + the current table rows of run heads (prefetched for the emit pass)
   float4 tab[NPASS][2];
 #pragma unroll
@@ -681,7 +579,9 @@ __device__ __forceinline__ void item_chunk(const GradArgs& a, int64_t chunk, Chu
     if (j >= cnt || skey[j] == k || k == 0) continue;
     const float4 r0 = *reinterpret_cast<const float4*>(&rowsum[j][c0]);
     const float4 r1 = *reinterpret_cast<const float4*>(&rowsum[j][c0 + 4]);
-    if (kst[j] >= base && ken[j] <= base + cnt) {
+    // the key's run lies wholly in this chunk: it starts here (not continued from the entry before the chunk)
+    // and ends here (the chunk's last key differs, or the entry after the chunk does)
+    if ((j > 0 || L.prevk != k) && (skey[cnt] != k || L.nextk != k)) {
       float4* t = reinterpret_cast<float4*>(a.dtable + (int64_t)k * D + c0);
       float4 t0 = tab[ps][0], t1 = tab[ps][1];
       t0.x += r0.x; t0.y += r0.y; t0.z += r0.z; t0.w += r0.w;
@@ -714,36 +614,39 @@ __device__ __forceinline__ void item_span(const GradArgs& a, int64_t nchunks, in
   const int64_t last = min(a.n, base + CH) - 1;
   const uint32_t k = a.sk[last];
   if (k == 0) return;
-  const int64_t ks = a.start[k], ke = a.start[k + 1];
-  if (ke <= last + 1 || ks < base) return;               // key ends here, or owned by an earlier chunk
-  const int64_t cl = (ke - 1) / CH;                      // chunk of the key's last entry
-  const int own_slot = ks == base ? 0 : 1;
+  // the key continues past this chunk, and its run starts here (not in an earlier chunk)
+  if (last + 1 >= a.n || a.sk[last + 1] != k) return;
+  const bool head_here = a.sk[base] != k;
+  if (!head_here && base > 0 && a.sk[base - 1] == k) return;
+  const int own_slot = head_here ? 1 : 0;
   float acc[CPL];
 #pragma unroll
   for (int q = 0; q < CPL; ++q) {
     const int c = lane + 64 * q;
     acc[q] = c < D ? a.part[(ch * 2 + own_slot) * D + c] : 0.f;
   }
-  int64_t cc = ch + 1;
-  for (; cc + 7 <= cl; cc += 8) {
+  // later chunks whose first entry still has key k, in chunk order; eight chunks' heads and partials in flight
+  const int64_t nch = cdiv(a.n, CH);
+  bool more = true;
+  for (int64_t cc = ch + 1; more && cc < nch; cc += 8) {
+    uint32_t f[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) f[t] = cc + t < nch ? a.sk[(cc + t) * CH] : 0xfffffffeu;
 #pragma unroll
     for (int q = 0; q < CPL; ++q) {
       const int c = lane + 64 * q;
-      if (c < D) {
-        float u[8];
+      float u[8];
 #pragma unroll
-        for (int t = 0; t < 8; ++t) u[t] = a.part[((cc + t) * 2) * D + c];
+      for (int t = 0; t < 8; ++t) u[t] = (c < D && cc + t < nch) ? a.part[((cc + t) * 2) * D + c] : 0.f;
+      bool run = true;
 #pragma unroll
-        for (int t = 0; t < 8; ++t) acc[q] += u[t];
+      for (int t = 0; t < 8; ++t) {
+        run = run && f[t] == k;
+        if (run) acc[q] += u[t];
       }
     }
-  }
-  for (; cc <= cl; ++cc) {
 #pragma unroll
-    for (int q = 0; q < CPL; ++q) {
-      const int c = lane + 64 * q;
-      if (c < D) acc[q] += a.part[(cc * 2) * D + c];
-    }
+    for (int t = 0; t < 8; ++t) more = more && f[t] == k;
   }
 #pragma unroll
   for (int q = 0; q < CPL; ++q) {
@@ -774,7 +677,7 @@ int rs_item_index_layout(int nsrc, int64_t rows, int64_t table_rows, int64_t d, 
   if (ig::layout(nsrc, rows, table_rows, d, L) != hipSuccess) return RS_ERR_ARG;
   out[0] = (int64_t)L.sk;
   out[1] = (int64_t)L.sv;
-  out[2] = (int64_t)L.start;
+  out[2] = L.cs ? (int64_t)L.start : -1;
   out[3] = L.path;
   return 0;
 }
@@ -813,40 +716,26 @@ int rs_item_index_build(int nsrc, const int64_t* keys0, const int64_t* keys1, co
     hipLaunchKernelGGL(ig::place_kernel, dim3((unsigned)L.nb), dim3(256), 0, s, K, H, start, sk, sv);
     return (int)hipGetLastError();
   }
-  if (L.path == ig::SORT_LDS32 || L.path == ig::SORT_LDS64) {
-    const bool u32 = L.path == ig::SORT_LDS32;
-    static const bool attr = [] {
-      return hipFuncSetAttribute((const void*)ig::lsort_kernel<uint32_t, ig::IT32>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, ig::LDS_MAX) == hipSuccess &&
-             hipFuncSetAttribute((const void*)ig::lsort_kernel<uint64_t, ig::IT64>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, ig::LDS_MAX) == hipSuccess;
-    }();
-    if (!attr) return RS_ERR_UNSUPPORTED;
-    const size_t lds = ig::RHDR + (size_t)L.n * (u32 ? 4 : 8);
-    if (u32)
-      hipLaunchKernelGGL((ig::lsort_kernel<uint32_t, ig::IT32>), dim3(1), dim3(ig::RT), lds, s, K, L.ib, L.kb, sk, sv);
-    else
-      hipLaunchKernelGGL((ig::lsort_kernel<uint64_t, ig::IT64>), dim3(1), dim3(ig::RT), lds, s, K, 32, L.kb, sk, sv);
-  } else {
+  {
     uint64_t* ping = (uint64_t*)(w + L.ping);
     uint64_t* pong = (uint64_t*)(w + L.pong);
     int* hist = (int*)(w + L.hist);
     const int64_t tiles = cdiv(L.n, ig::TB);
+    const int scanned = tiles > ig::FUSED_SCAN_TILES;
     const int passes = ig::sort_passes(L.kb), db0 = ig::sort_digit(L.kb);
     const uint64_t* in = nullptr;
     for (int p = 0; p < passes; ++p) {
       const int shift = p * db0, db = std::min(db0, L.kb - shift);
       uint64_t* out = p + 1 == passes ? nullptr : (p % 2 == 0 ? ping : pong);
       hipLaunchKernelGGL(ig::rsort_count_kernel, dim3((unsigned)tiles), dim3(ig::RT), 0, s, K, in, shift, db, hist);
-      hipLaunchKernelGGL(ig::rsort_scan_kernel, dim3(1), dim3(ig::RT), 0, s, hist, (int64_t)(1 << db) * tiles);
+      if (scanned)
+        hipLaunchKernelGGL(ig::rsort_scan_kernel, dim3(1), dim3(ig::RT), 0, s, hist, (int64_t)(1 << db) * tiles);
       hipLaunchKernelGGL(ig::rsort_scatter_kernel, dim3((unsigned)tiles), dim3(ig::RT), 0, s, K, in, shift, db, hist,
-                         out, sk, sv);
+                         scanned, out, sk, sv);
       in = out;
     }
   }
   if ((e = hipGetLastError()) != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(ig::lower_bounds_kernel, dim3((unsigned)cdiv(table_rows + 1, 256)), dim3(256), 0, s, sk, L.n,
-                     table_rows, start);
   return (int)hipGetLastError();
 }
 
@@ -859,7 +748,17 @@ namespace ig {
 __global__ __launch_bounds__(256) void item_rows_f32_kernel(GradArgs a, const float* __restrict__ dx,
                                                             const float* __restrict__ f, int64_t d) {
   const int64_t v = (int64_t)blockIdx.x + 1;
-  const int b = a.start[v], e = a.start[v + 1];
+  int64_t b = 0, e = a.n;                  // [first entry with key >= v, first with key > v)
+  for (int64_t hi = a.n; b < hi;) {
+    const int64_t mid = (b + hi) >> 1;
+    if ((int64_t)a.sk[mid] < v) b = mid + 1;
+    else hi = mid;
+  }
+  for (int64_t lo = b; lo < e;) {
+    const int64_t mid = (lo + e) >> 1;
+    if ((int64_t)a.sk[mid] <= v) lo = mid + 1;
+    else e = mid;
+  }
   if (b >= e) return;
   const uint64_t seed = eff_seed(a.salt, a.seed_base);
   for (int64_t c = threadIdx.x; c < d; c += blockDim.x) {
@@ -890,7 +789,7 @@ static int item_grad_args(const void* ws, int nsrc, int64_t rows, int64_t table_
   hipError_t e = ig::layout(nsrc, rows, table_rows, d, L);
   if (e != hipSuccess) return (int)e;
   const char* w = (const char*)ws;
-  a = {(const uint32_t*)(w + L.sk), (const uint32_t*)(w + L.sv), (const int*)(w + L.start), (float*)(w + L.part),
+  a = {(const uint32_t*)(w + L.sk), (const uint32_t*)(w + L.sv), (float*)(w + L.part),
        L.n, rows, (const __bf16*)dx, scale, drop_p, salt, seed_base, (const __bf16*)f, w1, w2, dtable};
   return 0;
 }

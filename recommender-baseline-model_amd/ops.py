@@ -635,13 +635,14 @@ def item_index_build(keys, table_rows, d, ws):
 
 
 def item_index_view(nsrc, rows, table_rows, d, ws):
-    """(sorted keys, sorted entries, start, sort path) of a built index: views into ws (tests and tools)."""
+    """(sorted keys, sorted entries, start, sort path) of a built index: views into ws (tests and tools); start
+    (first sorted position of each key) exists on the counting-sort path only, else None."""
     out = (_lib.i64 * 4)()
     call("rs_item_index_layout", nsrc, rows, table_rows, d, out)
     n = nsrc * rows
     sk = ws[out[0]:out[0] + 4 * n].view(torch.int32)
     sv = ws[out[1]:out[1] + 4 * n].view(torch.int32)
-    start = ws[out[2]:out[2] + 4 * (table_rows + 1)].view(torch.int32)
+    start = ws[out[2]:out[2] + 4 * (table_rows + 1)].view(torch.int32) if out[2] >= 0 else None
     return sk, sv, start, int(out[3])
 
 

@@ -90,16 +90,18 @@ def _index_keys(nsrc, M, V1, pad, seed):
     return ks
 
 
-# (nsrc, rows, table rows, padding share, expected sort path): 0 counting sort, 1 / 2 one-workgroup LDS radix sort
-# with u32 / u64 words, 3 multi-workgroup radix sort.  cfg4 = 3 x 6,400 entries over 54,543 rows (~80 % padding);
-# cfg5 = 12,800 token ids over 1,000,002 rows.
+# (nsrc, rows, table rows, padding share, expected sort path): 0 counting sort, 3 radix sort (2,048-entry tiles; up
+# to 64 tiles the scatter workgroups scan the tile counts themselves, past that a scan launch: 131,072 = 64 tiles,
+# 133,121 = 66).  cfg4 = 3 x 6,400 entries over 54,543 rows (~80 % padding); cfg5 = 12,800 token ids over 1,000,002
+# rows (20-bit keys: three 7-bit passes).
 @pytest.mark.parametrize("nsrc,M,V1,pad,path", [
-    (3, 25600, 3417, 0.2, 0), (3, 6400, 54543, 0.8, 1), (3, 3000, 40000, 0.15, 1), (1, 12800, 1000002, 0.28, 2),
-    (3, 30000, 800000, 0.15, 3), (1, 40000, 1000002, 0.3, 3), (3, 12272, 54543, 0.0, 1), (1, 1, 40000, 0.0, 1),
-    (3, 6400, 54543, 1.0, 1), (1, 18408, 1000002, 0.0, 2), (1, 18409, 1000002, 0.0, 3)])
+    (3, 25600, 3417, 0.2, 0), (3, 6400, 54543, 0.8, 3), (3, 3000, 40000, 0.15, 3), (1, 12800, 1000002, 0.28, 3),
+    (3, 30000, 800000, 0.15, 3), (1, 300000, 1000002, 0.3, 3), (3, 12272, 54543, 0.0, 3), (1, 1, 40000, 0.0, 3),
+    (3, 6400, 54543, 1.0, 3), (1, 131072, 1000002, 0.0, 3), (1, 133121, 1000002, 0.0, 3)])
 def test_item_index_is_the_stable_sort(nsrc, M, V1, pad, path):
     """The built index equals numpy's stable argsort of the concatenated keys bit for bit (sorted keys, entries,
-    and start[v] = first position of key >= v), on every sort path incl. all-padding and single-entry batches."""
+    and on the counting-sort path start[v] = first position of key >= v), on every sort path incl. all-padding
+    and single-entry batches."""
     import rbm_amd  # noqa: F401
     from rbm_amd import ops
     d = 128
@@ -115,7 +117,9 @@ def test_item_index_is_the_stable_sort(nsrc, M, V1, pad, path):
     srt = allk[order]
     assert np.array_equal(sk.cpu().numpy().astype(np.int64), srt)
     assert np.array_equal(sv.cpu().numpy().astype(np.int64), order)
-    assert np.array_equal(start.cpu().numpy().astype(np.int64), np.searchsorted(srt, np.arange(V1 + 1), "left"))
+    assert (start is not None) == (path == 0)
+    if start is not None:
+        assert np.array_equal(start.cpu().numpy().astype(np.int64), np.searchsorted(srt, np.arange(V1 + 1), "left"))
     # a second build over the same workspace: the same bits (no state carried between builds)
     ws2 = ws.clone()
     ops.item_index_build(dev, V1, d, ws2)
