@@ -393,7 +393,7 @@ def main():
                                      shape=cfg["shape"])
         sampler = DeviceBertMasker(users, cfg["V"], B, cfg["T"], cfg["mask"], seed=5 + rank)
         sampler.new_epoch()
-        trainer.capture_sampled(sampler, stamps=stamps, steps_per_graph=S)
+        capture(lambda s: trainer.capture_sampled(sampler, stamps=stamps, steps_per_graph=s))
         batches = [()]
         run = trainer.replay_sampled
         eager = lambda i: (sampler.sample_into(*trainer.static), trainer.step(*trainer.static))  # noqa: E731

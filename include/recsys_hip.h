@@ -209,6 +209,13 @@ int rs_scatter_rows(int dtype, const void* src, int64_t lds, int64_t d, const in
 int rs_splitk_scatter_rows(int dtype, const float* slab, int splits, int64_t cap, int64_t d, const int32_t* rank,
                            int64_t n, void* dst, int64_t ldd, void* stream);
 
+/* Eval scores at candidate ids (replaces SAS.predict's item_emb(candidates).matmul(final_feat), BS/models/sas_model/
+ * sas.py:107-118, and BERTTrainer.calculate_metrics' logits[:, -1, :].gather(1, candidates), BS/trainers/bert.py:
+ * 43-49): out[b][c] = <h[b*ldh .. + d], E[cand[b][c]]> (+ bias[cand[b][c]] when bias != NULL), fp32.  h, E in dtype
+ * (RS_DTYPE_*); cand int64 [B][C] in [0, V) (others score NaN). */
+int rs_candidate_scores(int dtype, const void* h, int64_t ldh, int64_t B, int64_t d, const void* E, const float* bias,
+                        const int64_t* cand, int64_t C, int64_t V, float* out, void* stream);
+
 /* torch.optim.Adam step (BS/trainers/base.py:225-228; amsgrad=False) over a
  * flat fp32 buffer.  hyper (device double[5]) = {lr, beta1, beta2, eps, weight_decay} (doubles, as torch's Python
  * floats: the scalars are formed in double and cast to float where they meet the tensors, like torch's).

@@ -73,6 +73,7 @@ SIGNATURES = {
     "rs_compact_rows": [vp, i64, i64, vp, vp, vp, vp],
     "rs_gather_rows": [i32, vp, i64, i64, vp, vp, i64, vp, i64, vp, vp, vp],
     "rs_scatter_rows": [i32, vp, i64, i64, vp, i64, vp, i64, vp],
+    "rs_candidate_scores": [i32, vp, i64, i64, i64, vp, vp, vp, i64, i64, vp, vp],
     "rs_adam_prepare": [vp, vp, vp, vp, vp],
     "rs_adam_step": [i64, vp, vp, vp, vp, vp, vp, vp, i32, vp],
     "rs_adam_prepare_step": [i64, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, i32, i64, vp, vp],

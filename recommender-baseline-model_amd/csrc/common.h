@@ -149,10 +149,23 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
   return x;
 }
 __device__ __forceinline__ uint32_t seed32(uint64_t seed) { return (uint32_t)seed ^ (uint32_t)(seed >> 32) * 0x27d4eb2fU; }
-// one 32-bit hash per pair of adjacent elements (16 bits each).  Two multiplies (hash32's): the element-pair index
-// is XORed into the site seed directly (pair indices past 2^32 -- 8.6G elements of one site -- would repeat masks);
-// a golden-ratio pre-multiply and a high-word term cost two more 4-pass v_mul_lo_u32 per pair in every dropout site
-__device__ __forceinline__ uint32_t pair_hash(uint32_t s32, uint64_t idx) { return hash32((uint32_t)(idx >> 1) ^ s32); }
+// one 32-bit hash per pair of adjacent elements (16 bits each).  Two multiplies per pair, as lowbias32: the
+// element-pair index is XORed into the site seed, and the seed ALSO picks the first multiplier (an odd constant
+// derived from it, loop-invariant: formed once per thread / in scalar registers, not per pair).  With the seed
+// in the XOR alone, two sites' (or steps') masks were the same sequence shifted by s1 ^ s2 pairs -- copies of each
+// other whenever the seeds differed by less than the pair count; a seed-dependent multiplier makes them distinct
+// functions of the pair index.  (Pair indices past 2^32 -- 8.6G elements of one site -- would repeat masks; a
+// golden-ratio pre-multiply and a high-word term would cost two more 4-pass v_mul_lo_u32 per pair in every site.)
+__device__ __forceinline__ uint32_t seed_mult(uint32_t s32) { return ((s32 * 0x9E3779B9u) ^ 0x7feb352dU) | 1u; }
+__device__ __forceinline__ uint32_t pair_hash(uint32_t s32, uint64_t idx) {
+  uint32_t x = (uint32_t)(idx >> 1) ^ s32;
+  x ^= x >> 16;
+  x *= seed_mult(s32);
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
 __device__ __forceinline__ uint32_t drop_thr(float p) { return (uint32_t)fminf(p * 65536.0f, 65535.0f); }
 // keep with probability 1-p; returns the multiplier (0 or 1/(1-p))
 __device__ __forceinline__ float drop_mul(float p, uint64_t seed, uint64_t idx) {

@@ -141,6 +141,33 @@ __global__ __launch_bounds__(256) void splitk_scatter_kernel(const float* __rest
   for (int j = 0; j < 4; ++j) dst[r * ldd + c + j] = from_f<T>(v[j]);
 }
 
+// Eval scores at candidate ids: out[b][c] = <h[b], E[cand[b][c]]> (+ bias[cand[b][c]]).  SAS.predict
+// (BS/models/sas_model/sas.py:107-118: last-position features . item_emb[candidates]) and BERT's validation
+// scores (BS/trainers/bert.py:43-49: the last position's logits gathered at the candidates) without forming the
+// (B, V+1) logits -- cfg5's full-vocabulary eval would be 51 GB fp32.  One wave per (row, candidate): lanes
+// stride over the d features, fp32 products summed lane-wise in feature order then by a fixed butterfly.
+// A candidate outside [0, V) scores NaN (the reference indexes out of range and raises; the Python wrapper checks).
+template <typename T>
+__global__ __launch_bounds__(256) void cand_scores_kernel(const T* __restrict__ h, int64_t ldh, int64_t B, int64_t d,
+                                                          const T* __restrict__ E, const float* __restrict__ bias,
+                                                          const int64_t* __restrict__ cand, int64_t C, int64_t V,
+                                                          float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= B * C) return;
+  const int64_t b = q / C, v = cand[q];
+  if (v < 0 || v >= V) {
+    if (lane == 0) out[q] = __builtin_nanf("");
+    return;
+  }
+  const T* hr = h + b * ldh;
+  const T* er = E + v * d;
+  float acc = 0.f;
+  for (int64_t k = lane; k < d; k += 64) acc = fmaf(to_f(hr[k]), to_f(er[k]), acc);
+  acc = wave_sum(acc);
+  if (lane == 0) out[q] = bias ? acc + bias[v] : acc;
+}
+
 extern "C" {
 
 int rs_splitk_scatter_rows(int dtype, const float* slab, int splits, int64_t cap, int64_t d, const int32_t* rank,
@@ -194,6 +221,22 @@ int rs_scatter_rows(int dtype, const void* src, int64_t lds, int64_t d, const in
   else
     hipLaunchKernelGGL((scatter_rows_kernel<float>), dim3((unsigned)cdiv(m, 256)), dim3(256), 0, s,
                        (const float*)src, lds, d, rank, n, (float*)dst, ldd);
+  return (int)hipGetLastError();
+}
+
+int rs_candidate_scores(int dtype, const void* h, int64_t ldh, int64_t B, int64_t d, const void* E, const float* bias,
+                        const int64_t* cand, int64_t C, int64_t V, float* out, void* stream) {
+  if (B <= 0 || C <= 0 || d <= 0 || V <= 0 || ldh < d || !h || !E || !cand || !out) return RS_ERR_ARG;
+  const dim3 g((unsigned)cdiv(B * C, 4)), blk(256);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == RS_DTYPE_BF16)
+    hipLaunchKernelGGL(cand_scores_kernel<__bf16>, g, blk, 0, s, (const __bf16*)h, ldh, B, d, (const __bf16*)E, bias,
+                       cand, C, V, out);
+  else if (dtype == RS_DTYPE_F32)
+    hipLaunchKernelGGL(cand_scores_kernel<float>, g, blk, 0, s, (const float*)h, ldh, B, d, (const float*)E, bias, cand,
+                       C, V, out);
+  else
+    return RS_ERR_ARG;
   return (int)hipGetLastError();
 }
 

@@ -4,6 +4,7 @@ descending sort (ties by candidate index)."""
 import torch
 
 from . import ops
+from .engine_util import as_ids
 
 
 def recalls_ndcgs_and_mrr_for_ks(scores, labels, ks):
@@ -25,3 +26,15 @@ def recalls_ndcgs_and_mrr_for_ks(scores, labels, ks):
         res["NDCG@%d" % k] = v[3 * q + 1]
         res["MRR@%d" % k] = v[3 * q + 2]
     return res
+
+
+def calculate_metrics(model, batch, metric_ks):
+    """The trainers' ``calculate_metrics`` (BS/trainers/sas.py:56-62, BS/trainers/bert.py:43-52) on the GPU: the
+    model's scores at the candidates -- ``SASModel.predict`` / ``BERTModel.predict`` (the last position only, no
+    (B, T, V+1) logits) -- ranked by rs_rank_metrics.  batch = (seqs, candidates, labels) as the eval loaders
+    yield it."""
+    seqs, candidates, labels = batch
+    dev = model.engine().flat.device if hasattr(model, "engine") else next(model.parameters()).device
+    with torch.no_grad():
+        scores = model.predict(as_ids(seqs, dev), as_ids(candidates, dev))
+    return recalls_ndcgs_and_mrr_for_ks(scores, torch.as_tensor(labels).to(dev), metric_ks)

@@ -2,7 +2,10 @@
 
 ``forward(x)`` returns the full-vocabulary logits (B, T, V+1) like the
 reference; training through :class:`rbm_amd.train_step.FusedTrainStep` uses the
-labelled-rows-only loss head instead (same loss and gradients).
+labelled-rows-only loss head instead (same loss and gradients).  ``predict(x,
+candidates)`` gives the validation scores ``forward(x)[:, -1, :].gather(1,
+candidates)`` (``BS/trainers/bert.py:43-49``) without forming the (B, T, V+1)
+logits (51 GB fp32 at a 1M-item catalogue and B = 64).
 """
 import torch
 import torch.nn as nn
@@ -45,6 +48,14 @@ class BERTModel(BaseModel):
         if self._engine is None:
             self._engine = BERTEngine(self, self._flat)
         return self._engine
+
+    @torch.no_grad()
+    def predict(self, x, candidates):
+        """(B, C) fp32 scores of the last position at ``candidates`` (long ids): the same values as
+        ``self(x)[:, -1, :].gather(1, candidates)`` (the reference's calculate_metrics), eval-mode encoder."""
+        eng = self.engine()
+        dev = self._flat.device
+        return eng.predict(as_ids(x, dev), as_ids(candidates, dev))
 
     def forward(self, x):
         eng = self.engine()

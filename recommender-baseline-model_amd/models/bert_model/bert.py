@@ -419,6 +419,16 @@ class BERTEngine:
         splits = max(1, round(384 / tiles))
         return max(64, -(-(-(-M // splits)) // 64) * 64)
 
+    # ---- eval scores at candidates (BS/trainers/bert.py:43-49 without the (B, T, V+1) logits) --------
+    def predict(self, ids, cand):
+        """logits[:, -1, :].gather(1, cand) of the reference's validation: the encoder in eval mode (no dropout),
+        then only the last position's scores at the candidates (out.weight rows . h_last + out.bias)."""
+        self.sync_compute_weights()
+        B, T = ids.shape
+        xL, _ = self.encode(ids, False)
+        h = xL.view(B, T, self.d)[:, -1, :]
+        return ops.candidate_scores(h, self.W("out.weight"), cand, bias=self.Wf("out.bias"))
+
     # ---- full-vocabulary logits (the reference forward API) ---------------------------
     def logits(self, xL):
         M = xL.shape[0]

@@ -608,12 +608,6 @@ class SASEngine:
         return s["f"].view(B, T, self.d)
 
     def predict(self, ids, cand):
-        f = self.features(ids)[:, -1, :].contiguous()       # sas.py:110
-        B, C = cand.shape
-        # candidate scores <f_b, E[c]> (sas.py:112-114) via the sampled-logit kernel on repeated rows
-        frep = f.unsqueeze(1).expand(B, C, self.d).reshape(B * C, self.d).contiguous()
-        out = torch.empty(B * C, dtype=torch.float32, device=self.dev)
-        junk = torch.empty(B * C, dtype=torch.float32, device=self.dev)
-        cflat = cand.reshape(-1).contiguous()
-        ops.sampled_logits_fwd(frep, self.W("item_emb.weight"), cflat, cflat, out, junk)
-        return out.view(B, C)
+        f = self.features(ids)[:, -1, :]                    # sas.py:110 (a strided view: row stride T*d)
+        # candidate scores <f_b, item_emb[c]> (sas.py:112-114): one wave per (row, candidate), rs_candidate_scores
+        return ops.candidate_scores(f, self.W("item_emb.weight"), cand)

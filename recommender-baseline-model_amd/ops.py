@@ -655,6 +655,21 @@ def item_grad(ws, nsrc, rows, dx, scale, drop_p, salt, seed_base, f, w1, w2, dta
          ptr(w2) if w2 is not None else None, ptr(dtable), stream())
 
 
+def candidate_scores(h, E, cand, bias=None):
+    """(B, C) fp32 scores <h[b], E[cand[b, c]]> (+ bias[cand[b, c]]): rs_candidate_scores.  h: (B, d) rows (row stride
+    may exceed d), E: (V, d) in h's dtype, cand: (B, C) int64 on the device; raises on an id outside [0, V) like
+    the reference's embedding / gather."""
+    B, d = h.shape
+    V = E.shape[0]
+    cand = cand.contiguous()
+    if bool(((cand < 0) | (cand >= V)).any()):
+        raise IndexError("candidate id out of range")
+    out = torch.empty(cand.shape, dtype=torch.float32, device=h.device)
+    call("rs_candidate_scores", dtype_code(h), ptr(h), h.stride(0), B, d, ptr(E), ptr(bias), ptr(cand), cand.shape[1], V,
+         ptr(out), stream())
+    return out
+
+
 # ---- fused SAS output head (head.hip) --------------------------------------------------------
 def sas_head_fwd(x, ln_w, ln_b, eps, f, mean, rstd, E, pos, neg, pl, nl, part):
     M, d = x.shape

@@ -76,6 +76,34 @@ class FusedAdam:
                               self.hyper, zero_grad=zg)
 
 
+class FusedStepLR:
+    """``torch.optim.lr_scheduler.StepLR(optimizer, step_size, gamma)`` for a FusedAdam (BS/trainers/base.py:40, stepped
+    once per epoch at :87): every ``step_size``-th ``step()`` multiplies the learning rate by ``gamma`` -- chained in
+    Python floats exactly as torch's StepLR forms it -- and writes it into the optimizer's device hyperparameters, so
+    captured step graphs replayed afterwards use it without re-capture."""
+
+    def __init__(self, optimizer, step_size, gamma=0.1):
+        self.optimizer = optimizer.opt if isinstance(optimizer, FusedTrainStep) else optimizer
+        self.step_size = int(step_size)
+        self.gamma = float(gamma)
+        self.base_lr = float(self.optimizer.hyper[0].item())
+        self.lr = self.base_lr
+        self.last_epoch = 0
+
+    def step(self):
+        self.last_epoch += 1
+        if self.last_epoch % self.step_size == 0:
+            self.lr = self.lr * self.gamma
+            self.optimizer.set_lr(self.lr)
+
+    def get_last_lr(self):
+        return [self.lr]
+
+    def state_dict(self):
+        return {"step_size": self.step_size, "gamma": self.gamma, "base_lrs": [self.base_lr],
+                "last_epoch": self.last_epoch, "_last_lr": [self.lr]}
+
+
 class FusedTrainStep:
     def __init__(self, model, lr=1e-3, weight_decay=0.0, process_group=None, dp=None, max_labelled=None,
                  bucket_numel=None, overlap=None, vocab_shard=False, sparse_rows="auto"):

@@ -39,13 +39,20 @@ def golden():
 #  * PASS CRITERION -- vs the bf16-storage emulation of the same math (oracle.sas.BF16Storage: fp64 arithmetic, bf16
 #    rounding exactly where the kernels store bf16): the KERNELS' own error (accumulation order, fp32 vs fp64),
 #    held to EMU_TOL = 2e-2 (measured <= 1.3 %);
-#  * a fixed cap vs the exact math: the bf16 FORMAT's error on top of that.  tools/diag/bf16_budget.py shows it is
-#    forward-rounding sensitivity of a few ill-conditioned gradients (the FFN conv1 weight of a randomly initialised
-#    model moves 3-9 % when ANY single forward tensor -- even just the weights -- is rounded to bf16; 9.3 % measured
-#    for the emulation itself at cfg1's d = 50), so the cap is a stated constant, BF16_EXACT_CAP = 0.15, independent
-#    of the measurement it bounds.
+#  * a per-tensor bound vs the exact math: the bf16 FORMAT's error on top of that, min(BF16_EXACT_CAP,
+#    max(BF16_EXACT_FLOOR, 2 x fmt)) where fmt = the emulation's own distance to the exact math for THAT tensor.
+#    Well-conditioned tensors (fmt ~ 1e-3) are held to 3 %; the few ill-conditioned gradients whose bf16 rounding
+#    sensitivity is large (tools/diag/bf16_budget.py: the FFN conv1 weight of a randomly initialised model moves
+#    3-9 % when ANY single forward tensor -- even just the weights -- is rounded to bf16; 9.3 % measured for the
+#    emulation itself at cfg1's d = 50) get twice their own format error, never more than 15 %.
+#    RS_PARITY_LOG=<file> appends every checked tensor's (err vs emulation, err vs exact, fmt) as JSON lines.
 EMU_TOL = 2e-2
 BF16_EXACT_CAP = 0.15
+BF16_EXACT_FLOOR = 3e-2
+
+
+def exact_bound(fmt):
+    return min(BF16_EXACT_CAP, max(BF16_EXACT_FLOOR, 2.0 * fmt))
 
 
 def check_bf16_grads(get, g_emu, g_exact, d, kbias=lambda n: False, strip="", emu_tol=EMU_TOL):
@@ -69,7 +76,15 @@ def check_bf16_grads(get, g_emu, g_exact, d, kbias=lambda n: False, strip="", em
             g, e, x = (np.concatenate([t[:d], t[2 * d:]]) for t in (g, e, x))
         r_emu, r_ex, fmt = rel(g, e), rel(g, x), rel(e, x)
         out[name] = (r_emu, r_ex, fmt)
-        if r_emu >= emu_tol or r_ex >= BF16_EXACT_CAP:
+        if r_emu >= emu_tol or r_ex >= exact_bound(fmt):
             bad[name] = out[name]
+    log = os.environ.get("RS_PARITY_LOG")
+    if log:
+        import json
+        with open(log, "a") as fh:
+            test = os.environ.get("PYTEST_CURRENT_TEST", "?").split(" ")[0]
+            for name, (a, b, c) in out.items():
+                fh.write(json.dumps({"test": test, "tensor": name, "emu": a, "exact": b, "fmt": c,
+                                     "bound": exact_bound(c), "emu_tol": emu_tol}) + "\n")
     assert not bad, bad
     return out

@@ -151,3 +151,73 @@ def test_zero_grad_with_untouched_rows():
         opt.step()
     err = (p.cpu().double() - tp.detach()).abs().max().item()
     assert err < 2e-6, err
+
+
+def test_step_lr_matches_torch_steplr_and_reaches_captured_graphs():
+    """StepLR (BS/trainers/base.py:40, stepped per epoch at :87) through FusedStepLR: (1) the learning rates equal torch's
+    StepLR's, and the fused Adam driven by them tracks torch.optim.Adam + StepLR to a few float32 ulps over 4 epochs;
+    (2) a FusedTrainStep captured ONCE and replayed across epochs applies each epoch's rate: bit for bit the eager
+    steps of a twin trainer under the same schedule, and a zero rate leaves the parameters unchanged."""
+    import argparse
+    import numpy as np
+    import rbm_amd  # noqa: F401
+    import rbm_amd.data as synth
+    from rbm_amd import ops
+    from rbm_amd.models import model_factory
+    from rbm_amd.train_step import FusedAdam, FusedStepLR, FusedTrainStep
+    n = 50_000
+    p0 = torch.randn(n, generator=torch.Generator().manual_seed(2))
+    tp = torch.nn.Parameter(p0.clone())
+    opt = torch.optim.Adam([tp], lr=1e-3, foreach=False)
+    sched = torch.optim.lr_scheduler.StepLR(opt, step_size=2, gamma=0.5)
+
+    class _Flat:
+        device = torch.device("cuda")
+        numel = n
+    fa = FusedAdam(_Flat(), lr=1e-3)
+    fs = FusedStepLR(fa, step_size=2, gamma=0.5)
+    p, st, seed = p0.cuda().clone(), fa.state, torch.zeros(1, dtype=torch.int64, device="cuda")
+    gg = torch.Generator().manual_seed(3)
+    for epoch in range(4):
+        for _ in range(3):
+            g = torch.randn(n, generator=gg)
+            ops.adam_prepare_step(p, g.cuda(), fa.m, fa.v, None, st, fa.hyper, zero_grad=True, seed_base=seed)
+            tp.grad = g
+            opt.step()
+        sched.step()
+        fs.step()
+        assert fs.get_last_lr() == sched.get_last_lr(), (epoch, fs.get_last_lr(), sched.get_last_lr())
+        assert float(fa.hyper[0].item()) == sched.get_last_lr()[0]
+    torch.cuda.synchronize()
+    eps = torch.finfo(torch.float32).eps
+    assert ((p.cpu().double() - tp.detach().double()).abs().max() / eps / tp.detach().double().abs().max()) <= 4
+
+    V, T, B = 300, 32, 8
+    a = argparse.Namespace(model_code="sas", num_items=V, max_len=T, device="cuda", sas_hidden_units=64,
+                           sas_num_blocks=2, sas_heads=1, sas_dropout=0.2, l2_emb=0.0, rs_dtype="bf16")
+    rng = np.random.default_rng(4)
+    batches = [tuple(torch.from_numpy(x).cuda() for x in synth.sas_batch(rng, B, T, V)) for _ in range(9)]
+    runs = []
+    for graph in (True, False):
+        torch.manual_seed(0)
+        m = model_factory(a)
+        tr = FusedTrainStep(m, lr=1e-3)
+        sch = FusedStepLR(tr, step_size=1, gamma=0.1)
+        if graph:
+            tr.capture(*batches[0], warmup=1)
+        else:
+            tr.step(*batches[0])
+        snaps = []
+        for epoch in range(3):
+            for i in range(3):
+                b = batches[3 * epoch + i]
+                (tr.replay if graph else tr.step)(*b)
+            snaps.append(tr.flat.data.clone())
+            sch.step()
+        sch.optimizer.set_lr(0.0)
+        before = tr.flat.data.clone()
+        (tr.replay if graph else tr.step)(*batches[0])
+        assert torch.equal(tr.flat.data, before), "lr 0 still moved the parameters"
+        runs.append(snaps)
+    for x, y in zip(*runs):
+        assert torch.equal(x, y)

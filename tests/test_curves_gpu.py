@@ -24,6 +24,8 @@ import torch
 from conftest import load_golden
 
 pytestmark = pytest.mark.gpu
+# per-step envelope of the small-shape SAS curve past step 300 (test_sas_loss_curve_matches_reference_1000_steps)
+ENV_K, ENV_W, ENV_C = 2.0, 25, 1e-3
 
 
 def _run(kind, z, steps, dtype="fp32"):
@@ -63,7 +65,14 @@ def test_sas_loss_curve_matches_reference_1000_steps():
     err = np.abs(losses - ref)
     floor = np.abs(load_golden("sas_curve_oracle64")["losses"] - ref)
     assert err[:300].max() <= 1e-3, (err[:300].max(), int(err[:300].argmax()))
-    assert err.max() <= 1.5 * floor.max(), (err.max(), floor.max())
+    # steps 300-1000, per step: within ENV_K x the reference's own fp32 drift from the exact math around that step
+    # (the largest |ref - fp64| within +-ENV_W steps: where the two trajectories happen to cross, the drift at the
+    # step itself is ~0 while both runs still carry their accumulated rounding) plus ENV_C
+    env = ENV_K * np.array([floor[max(0, t - ENV_W):t + ENV_W + 1].max() for t in range(len(floor))]) + ENV_C
+    ratio = err / env
+    print("sas_curve fp32: max err", err.max(), "at", int(err.argmax()), "; max err / envelope", ratio.max(), "at",
+          int(ratio.argmax()), "; global floor", floor.max())
+    assert (err <= env).all(), (ratio.max(), int(ratio.argmax()), err[ratio.argmax()], env[ratio.argmax()])
 
     def ma(x):
         return np.convolve(x, np.ones(50) / 50, mode="valid")

@@ -143,8 +143,9 @@ def test_two_rank_step_equals_single_process(tmp_path, kind, dtype):
     # fp32: the DP sum runs in another order than the single batch's (rounding-level differences); bf16: the
     # per-rank partial sums round differently (LayerNorm bias gradients at 6 sequences per rank: ~0.1 of the update)
     # measured (round 3): fp32 max 3.7e-5 / median 7e-7; bf16 SAS max 0.105 (a LayerNorm bias) / median 0.020, BERT
-    # max 0.090 / median 0.0065 -- the bars hold the worst tensor and the typical one separately
-    loss_tol, upd_tol = (1e-5, 1e-3) if dtype == "fp32" else (2e-3, 0.15)
+    # max 0.090 / median 0.0065 -- the bars hold the worst tensor and the typical one separately (bf16 worst: 0.12,
+    # 1.15x the measured 0.105)
+    loss_tol, upd_tol = (1e-5, 1e-3) if dtype == "fp32" else (2e-3, 0.12)
     upd_med_tol = 1e-5 if dtype == "fp32" else 0.04
     for mode in r0:
         a, b = r0[mode], r1[mode]

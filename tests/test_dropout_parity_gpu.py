@@ -246,3 +246,24 @@ def test_dropout_seed_advances_per_step_and_differs_per_rank():
     tr.replay(*b)
     tr.replay(*b)
     assert int(tr.engine.seed_base.item()) == s1 + 2
+
+
+@pytest.mark.parametrize("dist", [1, 2, 3, 37, 1000])
+def test_dropout_masks_of_nearby_seeds_are_not_shifted_copies(dist):
+    """Two sites (or steps) whose 32-bit seeds differ by a small XOR distance d: with the seed entering the pair hash
+    only by XOR, mask_B(pair j) was exactly mask_A(pair j ^ d) -- a permuted copy.  The seed-dependent first
+    multiplier (common.h pair_hash) makes them unrelated: the d-aligned masks correlate at the independent rate."""
+    from rbm_amd import ops
+    M, N, p = 512, 512, 0.2
+    x = torch.ones(M, N, device="cuda")
+    salt = 0x5A5A_1234_0000_0000
+    ma, mb = torch.empty_like(x), torch.empty_like(x)
+    ops.dropout_rowmask(x, p, salt, None, None, ma)
+    ops.dropout_rowmask(x, p, salt ^ dist, None, None, mb)
+    a, b = (t.ne(0).flatten() for t in (ma, mb))
+    idx = torch.arange(a.numel(), device="cuda")
+    a_aligned = a[((idx >> 1) ^ dist) << 1 | (idx & 1)]
+    lim = 4 / math.sqrt(a.numel())
+    assert abs(_corr(b, a_aligned)) < lim, _corr(b, a_aligned)
+    assert abs(_corr(a, b)) < lim
+    assert abs(a.double().mean().item() - (1 - p)) < 4 * math.sqrt(p * (1 - p) / a.numel())

@@ -90,3 +90,49 @@ def test_bert_hr_at_10_matches_oracle(dtype):
     else:
         assert rel(ours, ref) < 3e-2
         assert abs(mo["Recall@10"] - mr["Recall@10"]) <= 2.0 / B, (mo, mr)
+    # the eval route without full-vocabulary logits (BERTModel.predict -> rs_candidate_scores) gives the same scores
+    # as the gathered logits (same encoder; only the head's summation order differs) and the same metrics
+    from rbm_amd.metrics import calculate_metrics
+    pred = m.predict(torch.from_numpy(seq), torch.from_numpy(cand)).cpu().numpy()
+    assert rel(pred, ours) < (1e-6 if dtype == "fp32" else 1e-2)
+    mp = calculate_metrics(m, (torch.from_numpy(seq), torch.from_numpy(cand), torch.from_numpy(labels)), KS)
+    mg = {k: v for k, v in om.recalls_ndcgs_and_mrr_for_ks(ours, labels, KS).items()}
+    for k in mg:
+        if dtype == "fp32":
+            assert abs(mp[k] - mg[k]) < 1e-6, (k, mp[k], mg[k])
+        elif k.startswith("Recall"):
+            assert abs(mp[k] - mg[k]) <= 1.0 / B + 1e-6, (k, mp[k], mg[k])
+
+
+def test_bert_predict_at_1m_items_without_full_logits():
+    """cfg5's eval shape (V = 1,000,000, T = 200, d = 256, 4 blocks, B = 64, 101 candidates): BERTModel.predict
+    allocates no (B, T, V+1) logits (51 GB fp32) and equals the last position's hidden state times the gathered
+    out.weight rows plus out.bias (torch fp64 on the same hidden state)."""
+    import rbm_amd  # noqa: F401
+    from rbm_amd.models import model_factory
+    V, T, d, L, h, B, C = 1_000_000, 200, 256, 4, 2, 64, 101
+    a = argparse.Namespace(model_code="bert", num_items=V, max_len=T, device="cuda", bert_hidden_units=d,
+                           bert_num_blocks=L, bert_num_heads=h, bert_dropout=0.1, bert_hidden_dropout=0.1,
+                           bert_mask_prob=0.2, model_init_seed=0, rs_dtype="bf16")
+    m = model_factory(a)
+    m.eval()
+    rng = np.random.default_rng(3)
+    seq = rng.integers(1, V + 1, size=(B, T))
+    seq[:, :50] = 0
+    seq[:, -1] = V + 1
+    cand = rng.integers(1, V + 1, size=(B, C))
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated()
+    torch.cuda.reset_peak_memory_stats()
+    scores = m.predict(torch.from_numpy(seq), torch.from_numpy(cand))
+    torch.cuda.synchronize()
+    assert torch.cuda.max_memory_allocated() - base < 2 * 1024 ** 3
+    eng = m.engine()
+    xL, _ = eng.encode(torch.from_numpy(seq).cuda(), False)
+    hl = xL.view(B, T, d)[:, -1, :].double()
+    W = eng.W("out.weight").double()[torch.from_numpy(cand).cuda()]
+    ref = torch.einsum("bd,bcd->bc", hl, W) + eng.Wf("out.bias").double()[torch.from_numpy(cand).cuda()]
+    assert rel(scores.cpu().numpy(), ref.cpu().numpy()) < 1e-5
+    assert torch.isfinite(scores).all()
+    with pytest.raises(IndexError):
+        m.predict(torch.from_numpy(seq), torch.from_numpy(cand + V))
