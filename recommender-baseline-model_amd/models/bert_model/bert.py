@@ -378,7 +378,11 @@ class BERTEngine:
         """(lo, hi) flat range whose gradient the fused step writes whole every step (out.weight then out.bias,
         train_loss_and_backward): the optimizer leaves it unzeroed (FusedAdam.step keep) when it is large enough
         for the saved sweep (8 B per element) to pay for the extra launch -- the 1M-item vocabulary (256M
-        elements), not the 27k one."""
+        elements), not the 27k one.  Contract: every head path WRITES this whole range (dE = dlogits^T h and the
+        bias column sums with accumulate off; rows without labelled logits get exact zeros) and nothing else
+        accumulates into it -- a head variant that accumulated would double-count the previous step's gradient
+        (tests/test_bert.py ...overwritten_head_grads_match_zeroed, tests/test_dp_gpu.py
+        ...unzeroed_head_grads_equal_zeroed under the in-place all-reduce)."""
         f = self.flat
         ow, ob = f.offsets["out.weight"], f.offsets["out.bias"]
         A = ALIGN   # FlatParams pads every parameter to a multiple of ALIGN floats

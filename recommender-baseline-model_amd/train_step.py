@@ -22,6 +22,7 @@ dropout step-seed lives in device memory and is advanced inside the graph.
 """
 import gc
 import os
+import warnings
 
 import torch
 
@@ -502,15 +503,28 @@ class FusedTrainStep:
         else:
             self._exchange()
 
+    def _release_graphs(self):
+        """Drop every graph (and the exchange's pending work handles) of an earlier capture and let their HIP objects
+        go NOW, with no stream capturing: graph executables, their memory pools and the events of earlier eager steps
+        are destroyed here, before a new capture begins, instead of whenever Python's collector happens to run --
+        a collection that landed mid-capture and destroyed such an object aborted the process once (round 3)."""
+        torch.cuda.synchronize()
+        self.g_compute = self.g_segments = self.g_update = None
+        self.graphs = None
+        self._empty_graphs = []
+        if self.exchange is not None:
+            self.exchange.works, self.exchange.sent = [], []
+        gc.collect()
+        torch.cuda.synchronize()
+
     def _capture_graphs(self, compute, stamps=None, unrolled=False):
         """The compute graph (+ the optimizer in the same graph on one device).  DP: the compute graph is cut at
         every bucket the backward finishes (overlap: segments replayed with that bucket's all-reduce launched
         between them) or ends after the backward, and the optimizer is a separate graph after the exchange.
-        Python's cyclic garbage collector is held off for the whole capture: a collection that lands mid-capture
-        can destroy HIP objects of earlier steps or graphs (events, graph executables) while a stream is being
-        captured, which aborts the process (seen once in the BERT graph-collectives test)."""
+        The previous capture's objects are released explicitly first (_release_graphs); the cyclic collector is
+        also held off for the capture itself, so no collection can run while a stream is capturing."""
+        self._release_graphs()
         gc_on = gc.isenabled()
-        gc.collect()
         gc.disable()
         try:
             return self._capture_graphs_impl(compute, stamps, unrolled)
@@ -539,7 +553,12 @@ class FusedTrainStep:
                 if self.exchange is not None:
                     self.exchange.works, self.exchange.sent = [], []
                 # the ranks agree on the outcome (eager MIN of a flag) before anything else is issued: a rank that
-                # fell back alone would run eager / segmented collectives against the others' captured ones
+                # fell back alone would run eager / segmented collectives against the others' captured ones.
+                # Unverified beyond that flag: after a MIXED outcome the ranks that captured hold collectives that
+                # never run (their graphs are dropped), the failed rank fewer; RCCL orders a communicator's
+                # collectives by issue, and a captured-but-never-launched one is not expected to take a slot, but
+                # no test covers it (every test succeeds or fails on all ranks together).  If that ever misbehaves,
+                # re-capture on a fresh process subgroup instead of self.pg.
                 if not dpx.agree(err is None, self.pg):
                     self.graph_collectives = False
                     if self.steps_per_graph > 1:   # every rank raises alike; the caller re-captures with S = 1
@@ -573,7 +592,7 @@ class FusedTrainStep:
             self.g_update = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g_update, capture_error_mode=CAPTURE_MODE):
                 self._update()
-        segs = [seg[0] for seg in self.g_segments] if self.g_segments else [self.g_compute]
+        segs = [seg[0] for seg in self.g_segments if seg[0] is not None] if self.g_segments else [self.g_compute]
         self.graphs = tuple(segs) + ((self.g_update,) if self.dp else ())
 
     def _capture_segments(self, compute):
@@ -585,19 +604,36 @@ class FusedTrainStep:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         segs, cur = [], [torch.cuda.CUDAGraph()]
+        self._empty_graphs = []
+
+        def end():
+            # a segment that captured no work (a split point right at the start, e.g. the sparse token-table
+            # exchange's id all-gather before the first kernel) is not replayed: its action still runs.  The empty
+            # graph object itself is kept alive with the others (destroying it here releases the shared memory
+            # pool's use count out of order: torch's caching allocator asserts)
+            with warnings.catch_warnings(record=True) as w:
+                warnings.simplefilter("always")
+                cur[0].capture_end()
+            empty = any("Graph is empty" in str(x.message) for x in w)
+            for x in w:
+                if "Graph is empty" not in str(x.message):
+                    warnings.warn_explicit(x.message, x.category, x.filename, x.lineno)
+            if empty:
+                self._empty_graphs.append(cur[0])
+                return None
+            return cur[0]
         with torch.cuda.stream(s):
             cur[0].capture_begin(pool=pool, capture_error_mode=CAPTURE_MODE)
 
             def split(tag, action=None):
-                cur[0].capture_end()
-                segs.append((cur[0], tag, action))
+                segs.append((end(), tag, action))
                 cur[0] = torch.cuda.CUDAGraph()
                 cur[0].capture_begin(pool=pool, capture_error_mode=CAPTURE_MODE)
             try:
                 compute(split)
             finally:
-                cur[0].capture_end()
-            segs.append((cur[0], "final", None))
+                last = end()
+            segs.append((last, "final", None))
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         return segs
@@ -614,7 +650,8 @@ class FusedTrainStep:
             return self.loss_steps if self.steps_per_graph > 1 else self.loss_val
         if self.overlap:
             for g, tag, action in self.g_segments:
-                g.replay()
+                if g is not None:
+                    g.replay()
                 if action is not None:
                     action()                  # a collective of the computation itself (vocabulary shards)
                 elif tag in self.exchange.buckets:

@@ -3,6 +3,7 @@ one MI355X per test box), eager and HIP-graph-captured: unnormalised backward + 
 (loss sum, count) + all-reduce + Adam-side division gives the same update as the
 single-device step (which divides inside the loss kernel like the reference)."""
 import argparse
+import warnings
 import socket
 
 import numpy as np
@@ -165,7 +166,13 @@ def test_dp_graph_collectives_equal_segmented_bert(nccl_group, monkeypatch, vari
         tr = FusedTrainStep(model_factory(a), lr=1e-3, dp=True, vocab_shard=variant == "vocab_shard",
                             sparse_rows="on" if variant == "sparse" else "off")
         assert tr.graph_collectives == (mode == "1")
-        tr.capture(*batches[0], steps_per_graph=S)
+        with warnings.catch_warnings(record=True) as caught:
+            warnings.simplefilter("always")
+            tr.capture(*batches[0], steps_per_graph=S)
+        # no segment graph captures nothing (the sparse form's leading id all-gather used to leave an empty one)
+        assert not [str(w.message) for w in caught if "Graph is empty" in str(w.message)]
+        if mode == "0":
+            assert all(g is not None for g in tr.graphs)
         if variant == "sparse":
             assert tr.sparse is not None
         if mode == "1":
@@ -182,3 +189,34 @@ def test_dp_graph_collectives_equal_segmented_bert(nccl_group, monkeypatch, vari
     for losses, params in res[1:]:
         assert losses == res[0][0], (losses, res[0][0])
         assert torch.equal(params, res[0][1])
+
+
+def test_dp_large_vocab_unzeroed_head_grads_equal_zeroed(nccl_group):
+    """DP (in-graph all-reduce) with a vocabulary large enough (V * d >= 2^24) that the optimizer leaves the output
+    layer's gradient range unzeroed (BERTEngine.overwritten_grads -> FusedAdam.step keep): the bucket holding that
+    range is all-reduced IN PLACE every step, so the head must overwrite it whole before the exchange.  Three
+    graph-replayed steps equal, bit for bit, the same steps with the range zeroed by the optimizer."""
+    import rbm_amd  # noqa: F401
+    from rbm_amd.models import model_factory
+    from rbm_amd.train_step import FusedTrainStep
+    V, T, d, B = 262_144, 32, 64, 4
+    rng = np.random.default_rng(9)
+    import rbm_amd.data as synth
+    batches = [tuple(torch.from_numpy(x).cuda() for x in synth.bert_batch(rng, B, T, V, mask_prob=0.3))
+               for _ in range(3)]
+    res = []
+    for keep in (True, False):
+        torch.manual_seed(6)
+        a = argparse.Namespace(model_code="bert", num_items=V, max_len=T, device="cuda", bert_hidden_units=d,
+                               bert_num_blocks=1, bert_num_heads=2, bert_dropout=0.1, bert_hidden_dropout=0.1,
+                               bert_mask_prob=0.3, model_init_seed=6, rs_dtype="bf16")
+        tr = FusedTrainStep(model_factory(a), lr=1e-3, dp=True)
+        assert tr.engine.overwritten_grads() is not None
+        if not keep:
+            tr.engine.overwritten_grads = lambda: None
+        tr.capture(*batches[0], warmup=1)
+        losses = [float(tr.replay(*b).item()) for b in batches]
+        torch.cuda.synchronize()
+        res.append((losses, tr.flat.data.detach().cpu().clone()))
+    assert res[0][0] == res[1][0]
+    assert torch.equal(res[0][1], res[1][1])
