@@ -271,14 +271,20 @@ def cpu_baseline(cfg, B, seconds):
     from oracle import bert as obert
     from oracle import sas as osas
     from oracle.optim import AdamOracle
-    cores = max(1, min(16, os.cpu_count() or 1))
+    cores = max(1, min(16, os.cpu_count() or 1))     # the GPU box's CPU share is 16 threads (os.cpu_count: the host's)
+    try:
+        import psutil
+        physical = psutil.cpu_count(logical=False)
+    except Exception:   # noqa: BLE001 -- informational only
+        physical = None
     torch.set_num_threads(cores)
     torch.manual_seed(0)
     m = make_model(cfg, "fp32", device="cpu")
     P = {k: v.detach().clone() for k, v in m.state_dict().items()}
     opt = AdamOracle(list(P.values()))
-    # bounded sample: the oracle materialises all-position logits like the reference (B*T*(V+1) fp32)
-    Bc = B if cfg["model"] == "sas" else max(1, min(B, 16 if cfg["V"] < 100000 else 2))
+    # bounded sample: the workload's batch, except at a 1M-item vocabulary, where the oracle (like the reference)
+    # materialises all-position logits B*T*(V+1) fp32 -- 51 GB at B = 64 -- so it runs batch 2 there
+    Bc = B if (cfg["model"] == "sas" or cfg["V"] < 100000) else max(1, min(B, 2))
     batch = [torch.from_numpy(a) for a in make_batches(cfg, Bc, 1, 99)[0]]
 
     def one():
@@ -299,7 +305,8 @@ def cpu_baseline(cfg, B, seconds):
     dt = time.perf_counter() - t0
     return {"value": round(steps * Bc / dt, 2), "unit": "sequences/s", "cores": cores, "kind": "port",
             "sample": f"{steps} full train steps (fwd+loss+bwd+Adam, fp32, dropout {cfg['p']}) at batch {Bc} of the "
-                      f"workload with the CPU oracle (oracle/{cfg['model']}.py), {dt:.1f} s on {cores} threads"}
+                      f"workload with the CPU oracle (oracle/{cfg['model']}.py), {dt:.1f} s on {cores} threads"
+                      f" (host: {os.cpu_count()} logical / {physical} physical cores)"}
 
 
 # ------------------------------------------------------------------------------------ main

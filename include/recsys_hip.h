@@ -209,6 +209,17 @@ int rs_scatter_rows(int dtype, const void* src, int64_t lds, int64_t d, const in
 int rs_splitk_scatter_rows(int dtype, const float* slab, int splits, int64_t cap, int64_t d, const int32_t* rank,
                            int64_t n, void* dst, int64_t ldd, void* stream);
 
+/* Large-tile bf16 GEMM with a 256-wide output (gemm_n256.hip; the vocabulary head's weight-sized products at
+ * d = 256, BS/models/bert.py:10,16 + BS/trainers/bert.py:36-40): C[m][0..256) = sum_k A(m, k) B(k, n), fp32 out.
+ * A(m, k) = A[k*lda + m] (a_kmajor: dE = dlogits^T h) or A[m*lda + k] (dh = dlogits E); B(k, n) = B[k*ldb + n].
+ * colsum (a_kmajor only, nullable): colsum[m] = sum_k A(m, k) (the bias gradient).  rows_dev (nullable, device int):
+ * bounds K (a_kmajor) or M (else) -- the labelled-row count of a compacted batch.  split != 0 splits K into
+ * rs_gemm_n256_splits(M, K) slices written to C + z * c_split_stride (fp32 partial slabs).  16-B aligned operands,
+ * lda / ldb multiples of 8. */
+int rs_gemm_n256_splits(int64_t M, int64_t K);
+int rs_gemm_n256(int a_kmajor, int64_t M, int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb, float* C,
+                 int64_t ldc, int split, int64_t c_split_stride, float* colsum, const int* rows_dev, void* stream);
+
 /* Eval scores at candidate ids (replaces SAS.predict's item_emb(candidates).matmul(final_feat), BS/models/sas_model/
  * sas.py:107-118, and BERTTrainer.calculate_metrics' logits[:, -1, :].gather(1, candidates), BS/trainers/bert.py:
  * 43-49): out[b][c] = <h[b*ldh .. + d], E[cand[b][c]]> (+ bias[cand[b][c]] when bias != NULL), fp32.  h, E in dtype

@@ -74,6 +74,8 @@ SIGNATURES = {
     "rs_gather_rows": [i32, vp, i64, i64, vp, vp, i64, vp, i64, vp, vp, vp],
     "rs_scatter_rows": [i32, vp, i64, i64, vp, i64, vp, i64, vp],
     "rs_candidate_scores": [i32, vp, i64, i64, i64, vp, vp, vp, i64, i64, vp, vp],
+    "rs_gemm_n256_splits": [i64, i64],
+    "rs_gemm_n256": [i32, i64, i64, vp, i64, vp, i64, vp, i64, i32, i64, vp, vp, vp],
     "rs_adam_prepare": [vp, vp, vp, vp, vp],
     "rs_adam_step": [i64, vp, vp, vp, vp, vp, vp, vp, i32, vp],
     "rs_adam_prepare_step": [i64, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, i32, i64, vp, vp],

@@ -41,7 +41,10 @@ namespace ig {
 #endif
 constexpr int CH = IG_CH;       // sorted entries per gradient chunk
 constexpr int BE = 512;         // entries per counting-sort block (512: 150 blocks at cfg2, 1024 took 75)
-constexpr int VMAX_LDS = 32768;            // largest table for the LDS histogram
+#ifndef IG_COUNT_VMAX
+#define IG_COUNT_VMAX 32768
+#endif
+constexpr int VMAX_LDS = IG_COUNT_VMAX;     // largest table for the counting sort's LDS histogram
 constexpr int64_t HMAX = (int64_t)1 << 26;  // largest per-block histogram table (ints) for the counting sort
 constexpr int IBITS = 9;                    // BE = 2^IBITS: an entry's block index in the sort word's low bits
 constexpr int KBITS_MAX = 32 - IBITS - 1;   // key bits the counting-sort path's (key, index) sort word holds

@@ -22,6 +22,7 @@ rs_gather_rows), runs the vocabulary GEMM + CE on those rows only, and scatters
 the hidden-state gradient back (rs_scatter_rows).
 """
 import math
+import os
 import random
 
 import numpy as np
@@ -131,6 +132,9 @@ def _storage_order(names):
             out.append(n)
             seen.add(n)
     return out
+
+
+N256_MIN_V1 = 1 << 16   # see BERTEngine._n256_head
 
 
 class BERTEngine:
@@ -433,6 +437,15 @@ class BERTEngine:
         h = xL.view(B, T, self.d)[:, -1, :]
         return ops.candidate_scores(h, self.W("out.weight"), cand, bias=self.Wf("out.bias"))
 
+    def _n256_head(self):
+        """The vocabulary head's dE / dh products on the 256-wide-tile GEMM (gemm_n256.hip): bf16, d = 256, and a
+        vocabulary of at least N256_MIN_V1 classes (enough 256-row tiles to fill the chip; the 27k-class cfg3 head
+        keeps the 128x128 kernels).  RS_N256_HEAD=0/1 overrides (A/B timing)."""
+        env = os.environ.get("RS_N256_HEAD")
+        if env is not None:
+            return env == "1" and self.dt == torch.bfloat16 and self.d == 256
+        return self.dt == torch.bfloat16 and self.d == 256 and self.V1 >= N256_MIN_V1
+
     # ---- full-vocabulary logits (the reference forward API) ---------------------------
     def logits(self, xL):
         M = xL.shape[0]
@@ -505,11 +518,16 @@ class BERTEngine:
             else:
                 dl = self.ws.get("dlogits", (cap, self.V1p), self.dt)[:, :self.V1]
             ops.ce_bwd(logits, lab, count, None, wce, dl, rows_dev=cnt)
-        slab = self.ws.get("slab_out", (ops.wgrad_slab_numel(cap, self.V1, d),), torch.float32)
+        big = self._n256_head()
         # out.weight / out.bias get their whole gradient here: written, not accumulated (no read of the old
         # values; see overwritten_grads)
-        ops.linear_wgrad(dl, hl, self.flat.view("out.weight", grad), slab, db=self.flat.view("out.bias", grad),
-                         rows_dev=cnt, accumulate=False)
+        if big:     # 256-wide tiles: dlogits streams once (gemm_n256.hip)
+            ops.gemm_n256(dl, hl, self.flat.view("out.weight", grad), True, self.V1, cap,
+                          colsum=self.flat.view("out.bias", grad), rows_dev=cnt)
+        else:
+            slab = self.ws.get("slab_out", (ops.wgrad_slab_numel(cap, self.V1, d),), torch.float32)
+            ops.linear_wgrad(dl, hl, self.flat.view("out.weight", grad), slab, db=self.flat.view("out.bias", grad),
+                             rows_dev=cnt, accumulate=False)
         if split is not None:
             # join the side stream's token index here: a captured graph segment must not end with forked work
             if s.get("side") is not None and s["side"][0] is not None:
@@ -518,10 +536,16 @@ class BERTEngine:
             split("out")                # the vocabulary head's gradient is final (data-parallel overlap)
         # contraction over the whole vocabulary with few rows: split-K into slabs, then ONE pass that sums
         # the live rows' partials in a fixed order, casts and scatters them back to the token rows
-        sk = int(max(1, min(64, -(-self.V1 // 2048))))
-        slab_d = self.ws.get("slab_dh", (sk * cap * d,), torch.float32)
-        ops.gemm(dl, self.W("out.weight"), slab_d, cap, d, self.V1, False, True, ops.epilogue(rows_dev=cnt),
-                 split_k=sk, slab=slab_d)
+        if big:
+            sk = ops.gemm_n256_splits(cap, self.V1)
+            slab_d = self.ws.get("slab_dh", (sk * cap * d,), torch.float32)
+            ops.gemm_n256(dl, self.W("out.weight"), slab_d.view(sk, cap, d), False, cap, self.V1, split=True,
+                          rows_dev=cnt)
+        else:
+            sk = int(max(1, min(64, -(-self.V1 // 2048))))
+            slab_d = self.ws.get("slab_dh", (sk * cap * d,), torch.float32)
+            ops.gemm(dl, self.W("out.weight"), slab_d, cap, d, self.V1, False, True, ops.epilogue(rows_dev=cnt),
+                     split_k=sk, slab=slab_d)
         dxL = self._buf((M, d))
         ops.splitk_scatter_rows(slab_d, sk, cap, rank, dxL)
         self.encode_backward(s, dxL, grad)

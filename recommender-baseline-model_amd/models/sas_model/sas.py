@@ -6,17 +6,23 @@ torch modules below are only parameter containers and initialisers: they never
 run), same ``forward``/``predict`` results (``sas.py:59-118``).  The math runs
 as HIP kernels through the C ABI, orchestrated by :class:`SASEngine`:
 
-forward (per step)                      kernels (include/recsys_hip.h)
-  x = emb*sqrt(d)+pos, drop, mask         rs_embed_fwd
-  per block: Q = LN1(x)                   rs_layernorm_fwd (variant 0, eps 1e-8)
-             q = Q Wq^T+bq; kv = x Wkv^T  rs_gemm x2 (MFMA)
-             o = attn(q, k, v) causal     rs_attn_fwd (mask_kind 0, dropout on P)
-             x1 = Q + o Wo^T + bo         rs_gemm (+bias+residual epilogue)
-             z = LN2(x1)                  rs_layernorm_fwd
-             h = relu(drop(z W1^T + b1))  rs_gemm (+bias+relu+dropout epilogue)
-             x = (drop(h W2^T+b2) + z)*m  rs_gemm (+bias+dropout+residual+rowmask)
-  f = LN(x); pl/nl = <f, E[pos/neg]>      rs_layernorm_fwd, rs_sampled_logits_fwd
-backward: the mirror image (rs_*_bwd, dgrad/wgrad GEMMs, split-K slabs).
+bf16 fused step (FusedTrainStep, d in {64, 128}: the benchmarked path) -- per block two row-chain kernels per
+direction (rowchain.hip: one workgroup per CU, the block's three d x d weights in LDS, each wave carrying 16-token
+tiles through the sublayer chain in registers) around the LDS-resident attention (attention_lds.hip):
+  x = emb*sqrt(d)+pos, drop, mask;  Q = LN1(x);      rs_sas_block_in_embed (first block) / rs_sas_block_in
+  q = Q Wq^T+bq;  kv = x Wkv^T+bkv                   (same launch; sas.py:59-67, 73-76)
+  o = attn(q, k, v) causal, dropout on P             rs_attn_fwd (mask_kind 0; sas.py:75)
+  x1 = Q + o Wo^T + bo;  z = LN2(x1);                rs_sas_block_out (sas.py:75-84, PointWiseFeedForward)
+  x = (drop(relu(drop(z W1^T+b1)) W2^T+b2) + z)*m    (same launch)
+  f = LN(x); pl/nl = <f, E[pos/neg]>; BCE + grads   rs_sas_block_out_head (the last block's output kernel)
+backward: rs_sas_block_out_bwd_delta -> rs_attn_bwd (dQ and dK/dV workgroups in one launch) ->
+rs_sas_block_in_bwd per block, then ONE grouped launch of every weight / bias / LayerNorm-affine gradient
+(rs_wgrad_grouped_pos_stats, with the positional table's gradient and the loss statistics) beside the item-table
+gradient by inverted index (rs_item_index_build on a side stream during the forward, rs_item_grad), then the fused
+Adam (rs_adam_prepare_step_loss).
+fp32 parity mode and other widths run the generic unfused kernels: rs_embed_fwd, rs_layernorm_fwd/bwd (variant 0,
+eps 1e-8), rs_gemm (MFMA, fused bias / ReLU / dropout / residual / row-mask epilogues), rs_attn_fwd/bwd,
+rs_sampled_logits_fwd/bwd, rs_bce_*, split-K weight gradients.
 """
 import math
 

@@ -655,6 +655,20 @@ def item_grad(ws, nsrc, rows, dx, scale, drop_p, salt, seed_base, f, w1, w2, dta
          ptr(w2) if w2 is not None else None, ptr(dtable), stream())
 
 
+def gemm_n256_splits(M, K):
+    return int(_lib.lib().rs_gemm_n256_splits(M, K))
+
+
+def gemm_n256(A, B, C, a_kmajor, M, K, split=False, colsum=None, rows_dev=None):
+    """C[m, :256] = sum_k A(m, k) B(k, :) fp32 (rs_gemm_n256).  A: bf16 2-D view, A(m, k) = A[k, m] (a_kmajor) or
+    A[m, k]; B: bf16 (K, 256) rows (row stride ld(B)); C: fp32 rows of 256 (ld(C)); split: C is a [splits, M, 256]
+    slab (one k slice each, gemm_n256_splits(M, K) of them)."""
+    cz = C[0].numel() if split else 0
+    Cm = C[0] if split else C
+    call("rs_gemm_n256", int(a_kmajor), M, K, ptr(A), ld(A), ptr(B), ld(B), ptr(C), ld(Cm), int(split), cz,
+         ptr(colsum), ptr(rows_dev), stream())
+
+
 def candidate_scores(h, E, cand, bias=None):
     """(B, C) fp32 scores <h[b], E[cand[b, c]]> (+ bias[cand[b, c]]): rs_candidate_scores.  h: (B, d) rows (row stride
     may exceed d), E: (V, d) in h's dtype, cand: (B, C) int64 on the device; raises on an id outside [0, V) like
