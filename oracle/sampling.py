@@ -48,29 +48,24 @@ def sas_sample(user_train, user, item_num, max_len, candidates):
 
 
 def bert_getitem(u2seq, user, max_len, mask_prob, mask_token, draws):
-    """``BertTrainDataset.__getitem__`` (bert.py:77-110).  draws[t] = (k, item) for output position t: the
-    reference's ``rng.rand()`` is k / 2^24 and ``rng.randint(1, num_items + 1)`` is item.  The device draws only
-    for the items the final ``[-max_len:]`` keeps; the items that truncation drops take no draw (their masking
-    cannot reach the output) and are treated as unmasked."""
+    """``BertTrainDataset.__getitem__`` (bert.py:77-110).  draws[i] = (prob, item) for item i of the user's FULL
+    history: the reference's ``rng.rand()`` for that item and, where the 10 % branch calls it,
+    ``rng.randint(1, num_items + 1)`` (None elsewhere).  (The device sampler draws only for the items the final
+    ``[-max_len:]`` keeps -- the masking of a dropped item cannot reach the output -- and its recorded uniform is
+    k / 2^24; tests pass prob = 1.0, i.e. unmasked, for the dropped items.)"""
     seq = list(u2seq[user])
-    first_kept = len(seq) - min(len(seq), max_len)
-    pad = max_len - (len(seq) - first_kept)
 
     tokens = []
     labels = []
     for i, s in enumerate(seq):
-        if i < first_kept:
-            prob, rnd = 1.0, None
-        else:
-            k, rnd = draws[pad + i - first_kept]
-            prob = k / 16777216.0
+        prob, rnd = draws[i]
         if prob < mask_prob:
             prob /= mask_prob
 
             if prob < 0.8:
                 tokens.append(mask_token)
             elif prob < 0.9:
-                tokens.append(rnd)
+                tokens.append(int(rnd))
             else:
                 tokens.append(s)
 
@@ -87,6 +82,18 @@ def bert_getitem(u2seq, user, max_len, mask_prob, mask_token, draws):
     tokens = [0] * mask_len + tokens
     labels = [0] * mask_len + labels
     return tokens, labels
+
+
+def device_bert_draws(history_len, max_len, rec):
+    """Full-history draws for bert_getitem from a device record row rec[t] = (k, item) per output position t (-1 on
+    padding): prob = k / 2^24 for the kept tail, 1.0 (unmasked) for the items truncation drops."""
+    kept = min(history_len, max_len)
+    pad = max_len - kept
+    out = [(1.0, None)] * (history_len - kept)
+    for t in range(pad, max_len):
+        k, item = rec[t]
+        out.append((float(k) / 16777216.0, int(item)))
+    return out
 
 
 def bert_epoch_user(perm, batch_size, batch_index, row):

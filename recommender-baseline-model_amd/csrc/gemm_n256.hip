@@ -167,9 +167,12 @@ __global__ __launch_bounds__(NTH) void gemm_n256_kernel(Args a) {
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-      if (do_colsum) {   // the quadrant's m fragments 2wn, 2wn+1 (every row's sum formed once per row half)
-        accb[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2 * wn], ones, accb[0], 0, 0, 0);
-        accb[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2 * wn + 1], ones, accb[1], 0, 0, 0);
+      if (do_colsum) {   // the quadrant's m fragments 2wn, 2wn+1 (every row's sum formed once per row half);
+                         // compile-time fragment indices behind a wave-uniform test (a runtime index into fa[]
+                         // would send the fragments through scratch)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          if ((i >> 1) == wn) accb[i & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], ones, accb[i & 1], 0, 0, 0);
       }
     }
   };

@@ -80,6 +80,6 @@ def test_bert_masker_equals_reference_construction(n_users, V, T, B, p, lo, hi):
             d = dr[b, 1:].reshape(T, 2)
             live = d[:, 0] >= 0
             assert ((d[live, 1] >= 1) & (d[live, 1] <= V)).all(), "replacement item outside 1..num_items"
-            rt, rl = osmp.bert_getitem(users, u, T, pf, V + 1, [tuple(x) for x in d])
+            rt, rl = osmp.bert_getitem(users, u, T, pf, V + 1, osmp.device_bert_draws(len(users[u]), T, d))
             assert tok[b].tolist() == rt, (c, b, "tokens")
             assert lab[b].tolist() == rl, (c, b, "labels")
