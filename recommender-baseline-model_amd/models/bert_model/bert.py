@@ -438,13 +438,16 @@ class BERTEngine:
         return ops.candidate_scores(h, self.W("out.weight"), cand, bias=self.Wf("out.bias"))
 
     def _n256_head(self):
-        """The vocabulary head's dE / dh products on the 256-wide-tile GEMM (gemm_n256.hip): bf16, d = 256, and a
-        vocabulary of at least N256_MIN_V1 classes (enough 256-row tiles to fill the chip; the 27k-class cfg3 head
-        keeps the 128x128 kernels).  RS_N256_HEAD=0/1 overrides (A/B timing)."""
+        """(dE, dh) on the 256-wide-tile GEMM (gemm_n256.hip)?  bf16 and d = 256 only.  dh = dlogits E (split over
+        the vocabulary) at every vocabulary size; dE = dlogits^T h from N256_MIN_V1 classes on (3.9k row tiles at
+        1M classes; the 27k-class cfg3 head has 105, under the 256 CUs, where the 128x128 kernel's 418 tiles are
+        faster).  Measured (tools/diag/vocab_gemm_probe.py, R = 1,792): 1M classes dE 1,745 -> 1,278 us, dh 1,262 ->
+        1,059 us; 26,745 classes dh 60.5 -> 41.1 us, dE 94.8 -> 112.7 us.  RS_N256_HEAD=0/1 forces both off / on."""
+        ok = self.dt == torch.bfloat16 and self.d == 256
         env = os.environ.get("RS_N256_HEAD")
         if env is not None:
-            return env == "1" and self.dt == torch.bfloat16 and self.d == 256
-        return self.dt == torch.bfloat16 and self.d == 256 and self.V1 >= N256_MIN_V1
+            return (ok and env == "1",) * 2
+        return ok and self.V1 >= N256_MIN_V1, ok
 
     # ---- full-vocabulary logits (the reference forward API) ---------------------------
     def logits(self, xL):
@@ -518,10 +521,10 @@ class BERTEngine:
             else:
                 dl = self.ws.get("dlogits", (cap, self.V1p), self.dt)[:, :self.V1]
             ops.ce_bwd(logits, lab, count, None, wce, dl, rows_dev=cnt)
-        big = self._n256_head()
+        big_dE, big_dh = self._n256_head()
         # out.weight / out.bias get their whole gradient here: written, not accumulated (no read of the old
         # values; see overwritten_grads)
-        if big:     # 256-wide tiles: dlogits streams once (gemm_n256.hip)
+        if big_dE:  # 256-wide tiles: dlogits streams once (gemm_n256.hip)
             ops.gemm_n256(dl, hl, self.flat.view("out.weight", grad), True, self.V1, cap,
                           colsum=self.flat.view("out.bias", grad), rows_dev=cnt)
         else:
@@ -536,7 +539,7 @@ class BERTEngine:
             split("out")                # the vocabulary head's gradient is final (data-parallel overlap)
         # contraction over the whole vocabulary with few rows: split-K into slabs, then ONE pass that sums
         # the live rows' partials in a fixed order, casts and scatters them back to the token rows
-        if big:
+        if big_dh:
             sk = ops.gemm_n256_splits(cap, self.V1)
             slab_d = self.ws.get("slab_dh", (sk * cap * d,), torch.float32)
             ops.gemm_n256(dl, self.W("out.weight"), slab_d.view(sk, cap, d), False, cap, self.V1, split=True,
