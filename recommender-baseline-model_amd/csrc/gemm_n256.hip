@@ -271,6 +271,224 @@ __global__ __launch_bounds__(NTH) void gemm_n256_kernel(Args a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// LDS-DMA form (the default): 32-deep stages loaded by global_load_lds_dwordx4 straight into FOUR LDS stage buffers,
+// three stages in flight -- no staging registers, and the HBM latency (~1-2 us under load) hidden behind three
+// stages of MFMAs (~0.4 us each) instead of one.  A DMA writes 1 KB lane-linear, so the images are unpadded and the
+// bank-conflict-free layouts are applied to the SOURCE address:
+//  * k-major images ([32 k][256] as two halves of [32][128] bf16, 256-B rows): chunk ch of row r is stored at
+//    16 * (ch ^ ((r & 3) << 2 | (r >> 2) & 3)) -- conflict-free for the transposing fragment reads;
+//  * k-contiguous image ([256 m][32 k], 64-B rows): chunk ch of row r at 16 * (ch ^ (r >> 2) & 3).
+// Every DMA source is clamped into the operand; the last (partial) stage zeroes its k rows / columns past the end in
+// LDS before use.  One raw s_barrier per stage (after this wave's counted vmcnt and lgkmcnt(0)) publishes the
+// stage and frees the buffer the next DMA overwrites.
+constexpr int DBK = 32, NBUF = 4, DIST = 3;
+constexpr int KM_HALF = DBK * 128 * 2;          // bytes of one [32][128] half image
+constexpr int IMG_BYTES = DBK * 256 * 2;        // 16 KB: one operand's stage image
+constexpr int DSTAGE = 2 * IMG_BYTES;           // A + B
+constexpr int PIECES = IMG_BYTES / 1024;        // 16 DMA pieces per image, 2 per wave
+
+__device__ __forceinline__ uint32_t km_swz(int r) { return (uint32_t)(((r & 3) << 2) | ((r >> 2) & 3)); }
+// byte offset of element (k-row r, column c) of a k-major stage image
+__device__ __forceinline__ uint32_t km_off(int r, int c) {
+  return (uint32_t)((c >> 7) * KM_HALF + 256 * r + 16 * (((c & 127) >> 3) ^ km_swz(r)) + 2 * (c & 7));
+}
+// byte offset of element (row m, k) of the k-contiguous stage image
+__device__ __forceinline__ uint32_t kc_off(int m, int k) {
+  return (uint32_t)(64 * m + 16 * ((k >> 3) ^ ((m >> 2) & 3)) + 2 * (k & 7));
+}
+
+typedef __attribute__((address_space(3))) void* lds_vptr;
+__device__ __forceinline__ uint32_t lds_u32(const void* p) { return (uint32_t)(uintptr_t)(lds_vptr)p; }
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(dst)
+               : "memory");
+}
+template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory"); }
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// piece j (0..15) of a k-major image: rows 4 (j & 7) .. +3 of half j >> 3; lane l stores chunk l & 15 of row
+// 4 (j & 7) + (l >> 4), which holds logical chunk (l & 15) ^ swz(row): source (k0 + row, c0 + half*128 + 8 ch)
+__device__ __forceinline__ void km_piece(const __bf16* base, int64_t ld, int64_t k0, int64_t c0, int64_t klim,
+                                         int64_t clim, int j, int lane, uint32_t img) {
+  const int r = 4 * (j & 7) + (lane >> 4), half = j >> 3;
+  const int ch = (lane & 15) ^ (int)km_swz(r);
+  const int64_t k = min(k0 + r, klim - 1), c = min(c0 + half * 128 + 8 * ch, clim - 8);
+  dma16(base + k * ld + c, __builtin_amdgcn_readfirstlane(img + (uint32_t)j * 1024));
+}
+// piece j of the k-contiguous image: rows 16 j .. +15; lane l stores chunk l & 3 of row 16 j + (l >> 2)
+__device__ __forceinline__ void kc_piece(const __bf16* base, int64_t ld, int64_t m0, int64_t k0, int64_t mlim,
+                                         int64_t kcap, int j, int lane, uint32_t img) {
+  const int r = 16 * j + (lane >> 2);
+  const int ch = (lane & 3) ^ ((r >> 2) & 3);
+  const int64_t m = min(m0 + r, mlim - 1), k = min(k0 + 8 * ch, kcap - 8);
+  dma16(base + m * ld + k, __builtin_amdgcn_readfirstlane(img + (uint32_t)j * 1024));
+}
+
+// fragment (16 rows from row0, the stage's 32 k) of a k-major image: two transposing reads
+__device__ __forceinline__ bf16x8 km_frag(const char* img, int row0, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int c = row0 + 4 * p, r = 8 * g + q;
+  const bf4 x = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf4*)(img + km_off(r, c)));
+  const bf4 y =
+      __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf4*)(img + km_off(r + 4, c)));
+  return __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+__device__ __forceinline__ bf16x8 kc_frag(const char* img, int row0, int lane) {
+  const int g = lane >> 4, li = lane & 15;
+  return *reinterpret_cast<const bf16x8*>(img + kc_off(row0 + li, 8 * g));
+}
+
+template <bool AK>
+__global__ __launch_bounds__(NTH) void gemm_n256_dma_kernel(Args a) {
+  constexpr int LDC = BN + 4;
+  constexpr int LDS_BYTES = NBUF * DSTAGE > (BM / 2) * LDC * 4 ? NBUF * DSTAGE : (BM / 2) * LDC * 4;
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  constexpr int FM = 8, FN = 4;
+
+  const int64_t Mb = (!AK && a.rows_dev) ? min(a.M, (int64_t)*a.rows_dev) : a.M;
+  const int64_t Kb = (AK && a.rows_dev) ? min(a.K, (int64_t)*a.rows_dev) : a.K;
+  const unsigned tiles_m = (unsigned)((a.M + BM - 1) / BM);
+  unsigned tm, z;
+  {
+    const unsigned tot = gridDim.x, L = blockIdx.x, q = tot >> 3, r = tot & 7, x = L & 7;
+    const unsigned lg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (L >> 3);
+    z = lg / tiles_m;
+    tm = lg - z * tiles_m;
+  }
+  const int64_t m0 = (int64_t)tm * BM;
+  if (m0 >= Mb) return;
+  const int64_t kbeg = (int64_t)z * a.k_per_split;
+  const int64_t kend = min(Kb, kbeg + a.k_per_split);
+  const int nk = kend > kbeg ? (int)((kend - kbeg + DBK - 1) / DBK) : 0;
+  const uint32_t lds0 = lds_u32(smem);
+
+  f32x4 acc[FM][FN], accb[2];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  accb[0] = accb[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
+  const bool do_colsum = AK && a.colsum != nullptr;
+  // A's column bound for clamping: the allocated row length (k-major A: the m extent; the k-contiguous A: k)
+  const int64_t a_cols = a.lda;
+
+  // this wave's 4 DMA pieces of stage t (A pieces 2w, 2w+1; B pieces 2w, 2w+1)
+  auto issue = [&](int t) {
+    const uint32_t buf = lds0 + (uint32_t)((t % NBUF) * DSTAGE);
+    const int64_t k0 = kbeg + (int64_t)t * DBK;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int pc = 2 * wave + j;
+      if (AK) km_piece(a.A, a.lda, k0, m0, kend, a_cols, pc, lane, buf);
+      else kc_piece(a.A, a.lda, m0, k0, a.M, a_cols, pc, lane, buf);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) km_piece(a.B, a.ldb, k0, 0, kend, a.ldb, 2 * wave + j, lane, buf + IMG_BYTES);
+  };
+  // zero the k positions past kend of stage t's images (the last stage only)
+  auto zero_tail = [&](int t) {
+    char* buf = smem + (t % NBUF) * DSTAGE;
+    const int kv = (int)(kend - (kbeg + (int64_t)t * DBK));      // valid k in this stage, 1..31
+    // k-major images: rows >= kv, 256 columns each (B always; A when AK)
+    for (int e = tid; e < (DBK - kv) * 256; e += NTH) {
+      const int r = kv + e / 256, c = e % 256;
+      *reinterpret_cast<__bf16*>(buf + IMG_BYTES + km_off(r, c)) = (__bf16)0.0f;
+      if (AK) *reinterpret_cast<__bf16*>(buf + km_off(r, c)) = (__bf16)0.0f;
+    }
+    if (!AK)
+      for (int e = tid; e < BM * (DBK - kv); e += NTH) {
+        const int m = e / (DBK - kv), k = kv + e % (DBK - kv);
+        *reinterpret_cast<__bf16*>(buf + kc_off(m, k)) = (__bf16)0.0f;
+      }
+  };
+  auto compute = [&](int t) {
+    const char* buf = smem + (t % NBUF) * DSTAGE;
+    bf16x8 fa[FM], fb[FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) fa[i] = AK ? km_frag(buf, wm * 128 + 16 * i, lane) : kc_frag(buf, wm * 128 + 16 * i, lane);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) fb[j] = km_frag(buf + IMG_BYTES, wn * 64 + 16 * j, lane);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    if (do_colsum) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        if ((i >> 1) == wn) accb[i & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], ones, accb[i & 1], 0, 0, 0);
+    }
+  };
+
+  const bool tail = ((kend - kbeg) % DBK) != 0;
+  for (int t = 0; t < min(nk, DIST); ++t) issue(t);
+  for (int t = 0; t < nk; ++t) {
+    const int after = min(nk - 1, t + DIST - 1) - t;   // stages issued after t, allowed to stay in flight
+    if (after >= 2) vm_wait<8>();
+    else if (after == 1) vm_wait<4>();
+    else vm_wait<0>();
+    raw_barrier();                                      // stage t landed everywhere; buffer (t - 1) % NBUF free
+    if (t + DIST < nk) issue(t + DIST);
+    if (tail && t == nk - 1) {
+      zero_tail(t);
+      raw_barrier();
+    }
+    compute(t);
+  }
+  vm_wait<0>();
+
+  // ---- epilogue: as the register-staged kernel's
+  float* Cs = reinterpret_cast<float*>(smem);
+  float* Cz = a.C + (int64_t)z * a.cz;
+  const int g = lane >> 4, cl = lane & 15;
+  if (do_colsum && cl == 0) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t m = m0 + wm * 128 + 16 * (2 * wn + t) + 4 * g + r;
+        if (m < a.M) a.colsum[m] = accb[t][r];
+      }
+  }
+  constexpr int TPR = BN / 8, RPP = NTH / TPR;
+  const int c8 = (tid % TPR) * 8;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    __syncthreads();
+    if (wm == half) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Cs[(16 * i + 4 * g + r) * LDC + wn * 64 + 16 * j + cl] = acc[i][j][r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int row = tid / TPR; row < BM / 2; row += RPP) {
+      const int64_t m = m0 + half * 128 + row;
+      if (m >= a.M) break;
+      const float4 v0 = *reinterpret_cast<const float4*>(Cs + row * LDC + c8);
+      const float4 v1 = *reinterpret_cast<const float4*>(Cs + row * LDC + c8 + 4);
+      float* dst = Cz + m * a.ldc + c8;
+      *reinterpret_cast<float4*>(dst) = v0;
+      *reinterpret_cast<float4*>(dst + 4) = v1;
+    }
+  }
+}
+
 // the k split of a k-contiguous product (dh): as many splits as fill the 256 CUs with whole row tiles, each a
 // multiple of the 64-deep stage
 static void splits_for(int64_t M, int64_t K, int& splits, int64_t& kps) {
@@ -307,8 +525,13 @@ int rs_gemm_n256(int a_kmajor, int64_t M, int64_t K, const void* A, int64_t lda,
   }
   const dim3 grid((unsigned)(((M + g256::BM - 1) / g256::BM) * splits)), blk(g256::NTH);
   hipStream_t s = (hipStream_t)stream;
+#ifndef G256_REGSTAGE
+  if (a_kmajor) hipLaunchKernelGGL(g256::gemm_n256_dma_kernel<true>, grid, blk, 0, s, a);
+  else hipLaunchKernelGGL(g256::gemm_n256_dma_kernel<false>, grid, blk, 0, s, a);
+#else
   if (a_kmajor) hipLaunchKernelGGL(g256::gemm_n256_kernel<true>, grid, blk, 0, s, a);
   else hipLaunchKernelGGL(g256::gemm_n256_kernel<false>, grid, blk, 0, s, a);
+#endif
   return (int)hipGetLastError();
 }
 
