@@ -363,10 +363,273 @@ hipError_t launch(Args& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// fwd: 256-entry vocabulary tiles (E tile 132 KB at d = 256); bwd: 128 (room for the dlogits staging tile)
+// ---- forward, ping-pong form -------------------------------------------------------------------------------
+// The form above runs its eight waves in lock step (a barrier per 64-deep h stage), so the two waves of a SIMD
+// are in their softmax epilogue (VALU + transcendental) at the same time and the matrix core idles through it.
+// Here:
+//   * each wave keeps its 64 vocabulary entries x d of E in REGISTERS for the whole vocabulary tile (the A
+//     operand; 128 VGPRs at d = 256), so LDS carries only h, and a whole 32-row tile of h (16 KB at d = 256)
+//     arrives by LDS-DMA in one piece: one barrier per row tile instead of one per k stage;
+//   * waves 0-3 (group 0) and 4-7 (group 1) -- one of each per SIMD, same vocabulary quarter -- take alternate
+//     row tiles ("items") and run half an interval apart: in interval n group 0 runs the MFMAs of item 2n and
+//     then its epilogue, group 1 the epilogue of item 2n - 1 and then the MFMAs of item 2n + 1, so on every
+//     SIMD one wave's MFMAs overlap the other's epilogue;
+//   * the per-(row, 128-column) partials of a row tile combine two quarters' (max, sum) pairs through LDS one
+//     interval later (the next barrier orders them), into the same `part` layout as above.
+// Four h buffers: the two items of interval n + 1 stream in during interval n.
+namespace pp {
+constexpr int BV = 256, BRT = 32, NBUF = 4, NJ = BRT / 16;
+template <int DK> struct C {
+  static constexpr int KS = DK / 32;                  // 32-deep k steps
+  static constexpr int CPR = DK / 8;                  // 16-B chunks per h row
+  static constexpr int TILE = BRT * DK;               // h tile elements
+  static constexpr int PIECES = TILE * 2 / 1024;      // 1-KB LDS-DMA pieces per h tile
+  static constexpr int RPP = 1024 / (DK * 2);         // h rows per piece
+  static constexpr int LDS = NBUF * TILE * 2 + 2 * 2 * 4 * BRT * 8 + 8 * 64 * 4;
+};
+
+typedef __attribute__((address_space(3))) void* lds_vptr;
+__device__ __forceinline__ uint32_t lds_u32(const void* p) { return (uint32_t)(uintptr_t)(lds_vptr)p; }
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(dst)
+               : "memory");
+}
+
+template <int DK, bool BWD>
+__global__ __launch_bounds__(NTH, 1) void pp_kernel(Args a) {
+  KStampBegin stamp_b_(a.ks);
+  KStampEnd stamp_e_(a.ks);
+  using P = C<DK>;
+  constexpr int KS = P::KS, CPR = P::CPR;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* Hb = reinterpret_cast<bf16*>(smem);                               // NBUF h tiles [BRT][DK], swizzled
+  float2* red = reinterpret_cast<float2*>(smem + NBUF * P::TILE * 2);     // [group][parity][quarter][BRT]
+  float* bsl = reinterpret_cast<float*>(red + 2 * 2 * 4 * BRT);           // [wave][64]: this wave's bias quarter
+
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, cl = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), q = wave & 3, G = wave >> 2;
+  const int64_t Rl = a.rows_dev ? min(a.R, (int64_t)*a.rows_dev) : a.R;
+  const int nmt = (int)((Rl + BRT - 1) / BRT);
+  const int mtb = (int)((int64_t)nmt * blockIdx.y / gridDim.y), mte = (int)((int64_t)nmt * (blockIdx.y + 1) / gridDim.y);
+  const int nloc = mte - mtb;
+  const int64_t nvt = (a.V1 + BV - 1) / BV;
+  if (nloc <= 0 || (int64_t)blockIdx.x >= nvt) return;
+  const int nvl = (int)((nvt - 1 - blockIdx.x) / gridDim.x + 1);         // this workgroup's vocabulary tiles
+  const int F = nvl * nloc;                                               // items: (vocabulary tile, row tile)
+  const uint32_t hb0 = lds_u32(Hb);
+
+  // items fa, fa + 1 -> h buffers (fa & 3), (fa + 1) & 3: 2 * PIECES DMA pieces dealt over the 8 waves.  A
+  // wave's pieces j all have j = wave (mod 8), so its lanes' (row in piece, swizzled chunk) are fixed: lane row
+  // lr, source chunk hc; only the piece's first row (scalar) varies
+  const int lr = lane / CPR;
+  const int hc = 8 * ((lane % CPR) ^ swz<CPR>((wave % P::PIECES) * P::RPP + lr));
+  auto issue = [&](int fa) {
+#pragma unroll
+    for (int p0 = 0; p0 < 2 * P::PIECES; p0 += 8) {
+      const int p = p0 + wave, f = fa + p / P::PIECES, j = p % P::PIECES;
+      if (f < F) {
+        const int64_t rb = (int64_t)(mtb + f % nloc) * BRT + j * P::RPP;
+        const int64_t gr = min(rb + lr, Rl - 1);
+        dma16(a.h + gr * a.ldh + hc, __builtin_amdgcn_readfirstlane(hb0 + (uint32_t)((f & 3) * P::TILE * 2 + j * 1024)));
+      }
+    }
+  };
+
+  bf16x8 ef[4][KS];          // this wave's E quarter of the current vocabulary tile (A operand fragments)
+  f32x4 acc[4][NJ];          // S^T[vocab 64 q + 16 i + 4 g + r][row 16 j + cl] of the wave's last item
+  int cur_vtl = -1;
+
+  auto mfma_item = [&](int f) {
+    const int vtl = f / nloc;
+    if (vtl != cur_vtl) {
+      cur_vtl = vtl;
+      const int64_t vt = (int64_t)blockIdx.x + (int64_t)vtl * gridDim.x;
+      // the quarter's bias -> this wave's LDS slot; entries past the vocabulary get -inf there, which masks them
+      // in the epilogue (E rows past it are clamped, so their products are finite)
+      {
+        const int64_t v = vt * BV + 64 * q + lane;
+        bsl[wave * 64 + lane] = v < a.V1 ? (a.bias ? a.bias[v] : 0.f) : -__builtin_inff();
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t v = min(vt * BV + 64 * q + 16 * i + cl, a.V1 - 1);
+#pragma unroll
+        for (int s = 0; s < KS; ++s) ef[i][s] = *reinterpret_cast<const bf16x8*>(a.E + v * a.lde + 32 * s + 8 * g);
+      }
+    }
+    const bf16* H = Hb + (f & 3) * P::TILE;
+    // the accumulators start from the bias of their vocabulary rows (-inf past the vocabulary)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const f32x4 b4 = *reinterpret_cast<const f32x4*>(bsl + wave * 64 + 16 * i + 4 * g);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = b4;
+    }
+    // one k step's h fragments at a time (the other wave of the SIMD covers the LDS latency); the scheduling
+    // fence keeps the compiler from hoisting every step's reads at once (128 registers at d = 256)
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      bf16x8 fb[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) fb[j] = row_frag<CPR>(H, 16 * j, 4 * s, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma(ef[i][s], fb[j], acc[i][j]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  float sc = 0.f;
+  if constexpr (BWD) sc = (a.dloss ? *a.dloss : 1.f) / *a.count;
+
+  // bwd: dlogits of item f over this wave's quarter, straight from the accumulators: a lane holds 4
+  // consecutive vocabulary entries of a row (one 8-B store; the wave's 4 stores per row fill 128 contiguous
+  // bytes).  Dead rows (label 0) take lse = +inf and scale 0, so their dlogits are exactly 0 with no select;
+  // rows >= the live count are not written
+  auto epi_bwd = [&](int f) {
+    const int vtl = f / nloc, u = f - vtl * nloc;
+    const int64_t n0 = ((int64_t)blockIdx.x + (int64_t)vtl * gridDim.x) * BV, vb = n0 + 64 * q + 4 * g;
+    const bool full = n0 + BV <= a.V1;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int64_t row = (int64_t)(mtb + u) * BRT + 16 * j + cl;
+      const bool inr = row < Rl;
+      const int64_t lb = inr ? a.labels[row] : 0;
+      const bool live = inr && lb != 0;
+      const float Ll = live ? a.lse[row] * 1.4426950408889634f : __builtin_inff();
+      const float scr = live ? sc : 0.f;
+      const int64_t offl = lb - a.voff - vb;               // the label's entry among this lane's rows
+      const int off = offl < 0 || offl >= 64 ? -1 : (int)offl;
+      bf16* dst = a.dl + row * a.lddl + vb;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        bf4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[i][j][r], 1.4426950408889634f, -Ll));
+          o[r] = (bf16)((e - (off == 16 * i + r ? 1.f : 0.f)) * scr);
+        }
+        if (inr) {
+          if (full || vb + 16 * i + 4 <= a.V1) {
+            *reinterpret_cast<bf4*>(dst + 16 * i) = o;
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (vb + 16 * i + r < a.V1) dst[16 * i + r] = o[r];
+          }
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // softmax statistics of item f over this wave's quarter -> red[G][parity][q]
+  auto epi_item = [&](int f) {
+    float2* rd = red + ((G * 2 + ((f >> 1) & 1)) * 4 + q) * BRT;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      float mx = -__builtin_inff();
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          mx = fmaxf(mx, acc[i][j][r]);
+        }
+      float sm = 0.f;
+      const float mxl = mx * 1.4426950408889634f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sm += __builtin_amdgcn_exp2f(__builtin_fmaf(acc[i][j][r], 1.4426950408889634f, -mxl));
+      if (mx == -__builtin_inff()) sm = 0.f;
+#pragma unroll
+      for (int o = 16; o < 64; o <<= 1) comb(mx, sm, __shfl_xor(mx, o, 64), __shfl_xor(sm, o, 64));
+      if (g == 0) rd[16 * j + cl] = make_float2(mx, sm);
+      __builtin_amdgcn_sched_barrier(0);     // one row fragment's statistics at a time (register pressure)
+    }
+  };
+
+  // quarters {0, 1} / {2, 3} of item f -> its two 128-column partial tiles (one barrier after epi_item(f))
+  auto combine_item = [&](int f) {
+    const int tg = tid & 255;
+    if (tg < 2 * BRT) {
+      const int rl = tg & (BRT - 1), half = tg / BRT;
+      const int vtl = f / nloc, u = f - vtl * nloc;
+      const int64_t n0 = ((int64_t)blockIdx.x + (int64_t)vtl * gridDim.x) * BV;
+      const int64_t row = (int64_t)(mtb + u) * BRT + rl, pt = (n0 >> 7) + half;
+      const float2* rd = red + (G * 2 + ((f >> 1) & 1)) * 4 * BRT;
+      float2 e0 = rd[(2 * half) * BRT + rl];
+      const float2 e1 = rd[(2 * half + 1) * BRT + rl];
+      comb(e0.x, e0.y, e1.x, e1.y);
+      if (row < Rl && pt < a.ntn) *reinterpret_cast<float2*>(a.part + (row * a.ntn + pt) * 2) = e0;
+    }
+  };
+
+  const int NI = (F + 1) / 2;
+  issue(0);
+#pragma unroll 1
+  for (int n = 0; n <= NI + 1; ++n) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's pieces of items 2n, 2n + 1 landed
+    __syncthreads();                                    // ... everyone's; interval n - 1's readers are done
+    if (2 * n + 2 < F) issue(2 * n + 2);
+    // group 0: MFMAs of item 2n, then its epilogue; group 1: epilogue of item 2n - 1, then the MFMAs of 2n + 1
+    // (one copy of each phase in the code: phase ph runs the MFMAs where ph == G)
+    const int fm = 2 * n + G, fe = 2 * n - G, fc = fe - 2;
+#pragma unroll 1
+    for (int ph = 0; ph < 2; ++ph) {
+      if (ph == G) {
+        if (fm < F) mfma_item(fm);
+      } else {
+        if constexpr (BWD) {
+          if (fe >= 0 && fe < F) epi_bwd(fe);
+        } else {
+          if (fc >= 0 && fc < F) combine_item(fc);
+          if (fe >= 0 && fe < F) epi_item(fe);
+        }
+      }
+    }
+  }
+}
+
+template <int DK, bool BWD>
+hipError_t launch_pp(Args& a, hipStream_t s) {
+  using P = C<DK>;
+  static_assert(P::LDS <= 163840, "LDS budget");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)pp_kernel<DK, BWD>, hipFuncAttributeMaxDynamicSharedMemorySize, P::LDS);
+    attr = true;
+  }
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int64_t nvt = cdiv(a.V1, BV);
+  const int64_t grid = std::min<int64_t>(nvt, (int64_t)cus);
+  const int64_t gy = std::max<int64_t>(1, std::min<int64_t>(cdiv(a.R, BRT), (int64_t)cus / nvt));
+  hipLaunchKernelGGL((pp_kernel<DK, BWD>), dim3((unsigned)grid, (unsigned)gy), dim3(NTH), P::LDS, s, a);
+  return hipGetLastError();
+}
+}  // namespace pp
+
+// RS_VHEAD_PP=1 selects the ping-pong forms (read per launch, for A/B); default: the lock-step forms
+inline bool use_pp() {
+  const char* e = getenv("RS_VHEAD_PP");
+  return e ? atoi(e) != 0 : false;
+}
+
+// lock-step forms: fwd 256-entry vocabulary tiles (E tile 132 KB at d = 256); bwd 128 (room for the dlogits
+// staging tile)
 template <bool BWD>
 hipError_t dispatch(Args& a, int64_t d, hipStream_t s) {
   constexpr int BV = BWD ? 128 : 256;
+  if (use_pp()) {
+    if (d == 256) return pp::launch_pp<256, BWD>(a, s);
+    if (d == 128) return pp::launch_pp<128, BWD>(a, s);
+    return pp::launch_pp<64, BWD>(a, s);
+  }
   if (d == 256) return launch<256, BV, BWD>(a, s);
   if (d == 128) return launch<128, BV, BWD>(a, s);
   return launch<64, BV, BWD>(a, s);

@@ -54,11 +54,17 @@ def main():
     ops.vocab_head_fwd(h, E, bias, lab, ws, out)
     torch.cuda.synchronize()
     if "fwd" in only:
-        us = timeit(lambda: ops.vocab_head_fwd(h, E, bias, lab, ws, out), a.reps)
-        print(f"vocab_head_fwd   {us:9.1f} us  {fl / us / 1e6:7.1f} TFLOP/s")
+        for pp in ("1", "0"):     # RS_VHEAD_PP: the ping-pong form, then the lock-step form
+            os.environ["RS_VHEAD_PP"] = pp
+            us = timeit(lambda: ops.vocab_head_fwd(h, E, bias, lab, ws, out), a.reps)
+            print(f"vocab_head_fwd   {us:9.1f} us  {fl / us / 1e6:7.1f} TFLOP/s  (RS_VHEAD_PP={pp}) loss {float(out[0]):.6e}")
+        os.environ.pop("RS_VHEAD_PP")
     if "bwd" in only:
-        us = timeit(lambda: ops.vocab_head_bwd(h, E, bias, lab, ws, cnt, dl), a.reps)
-        print(f"vocab_head_bwd   {us:9.1f} us  {fl / us / 1e6:7.1f} TFLOP/s")
+        for pp in ("1", "0"):
+            os.environ["RS_VHEAD_PP"] = pp
+            us = timeit(lambda: ops.vocab_head_bwd(h, E, bias, lab, ws, cnt, dl), a.reps)
+            print(f"vocab_head_bwd   {us:9.1f} us  {fl / us / 1e6:7.1f} TFLOP/s  (RS_VHEAD_PP={pp})")
+        os.environ.pop("RS_VHEAD_PP")
     if "wgrad" in only:
         slab = torch.empty(1, device="cuda")
         us = timeit(lambda: ops.linear_wgrad(dl, h, dE, slab, db=db), a.reps)
