@@ -276,9 +276,9 @@ __global__ __launch_bounds__(NTH) void gemm_n256_kernel(Args a) {
 // three stages in flight -- no staging registers, and the HBM latency (~1-2 us under load) hidden behind three
 // stages of MFMAs (~0.4 us each) instead of one.  A DMA writes 1 KB lane-linear, so the images are unpadded and the
 // bank-conflict-free layouts are applied to the SOURCE address:
-//  * k-major images ([32 k][256] as two halves of [32][128] bf16, 256-B rows): chunk ch of row r is stored at
-//    16 * (ch ^ ((r & 3) << 2 | (r >> 2) & 3)) -- conflict-free for the transposing fragment reads;
-//  * k-contiguous image ([256 m][32 k], 64-B rows): chunk ch of row r at 16 * (ch ^ (r >> 2) & 3).
+//  * k-major images ([32 k][256] as two halves of [32][128] bf16) in 8-row x 32-column subtiles (km_off) --
+//    conflict-free for the transposing fragment reads;
+//  * k-contiguous image ([256 m][32 k], 64-B rows): chunk ch of row r at 16 * (ch ^ h(r >> 2 & 3)) (kc_off).
 // Every DMA source is clamped into the operand; the last (partial) stage zeroes its k rows / columns past the end in
 // LDS before use.  One raw s_barrier per stage (after this wave's counted vmcnt and lgkmcnt(0)) publishes the
 // stage and frees the buffer the next DMA overwrites.
@@ -288,14 +288,23 @@ constexpr int IMG_BYTES = DBK * 256 * 2;        // 16 KB: one operand's stage im
 constexpr int DSTAGE = 2 * IMG_BYTES;           // A + B
 constexpr int PIECES = IMG_BYTES / 1024;        // 16 DMA pieces per image, 2 per wave
 
-__device__ __forceinline__ uint32_t km_swz(int r) { return (uint32_t)(((r & 3) << 2) | ((r >> 2) & 3)); }
-// byte offset of element (k-row r, column c) of a k-major stage image
+// byte offset of element (k-row r, column c) of a k-major stage image: two halves of [32][128]; within a half the
+// guide's 8-row x 32-column subtile layout (cdna_hip_programming.md T10, image (a)): subtile (r >> 3, ch >> 2) of
+// 512 B, row r & 7 at 64 B, 16-B chunk (ch & 3) ^ ((r >> 2) & 3).  Conflict-free for the transposing fragment
+// reads, and a wave's fragments differ by compile-time offsets except for the (ch & 3) bit pattern (two address
+// bases), so the fragment addresses cost almost no VALU (the 256-B-row XOR layout cost ~110 VALU per stage)
 __device__ __forceinline__ uint32_t km_off(int r, int c) {
-  return (uint32_t)((c >> 7) * KM_HALF + 256 * r + 16 * (((c & 127) >> 3) ^ km_swz(r)) + 2 * (c & 7));
+  const int cc = c & 127, ch = cc >> 3;
+  return (uint32_t)((c >> 7) * KM_HALF + 2048 * (r >> 3) + 512 * (ch >> 2) + 64 * (r & 7) +
+                    16 * ((ch & 3) ^ ((r >> 2) & 3)) + 2 * (cc & 7));
 }
-// byte offset of element (row m, k) of the k-contiguous stage image
+// byte offset of element (row m, k) of the k-contiguous stage image: chunk g of row m is stored at position
+// g ^ h((m >> 2) & 3), h = {0, 2, 3, 1} -- with ds_read_b128's lane groups ({0-3, 12-15, 20-27}, {4-11, 16-19,
+// 28-31}, ...) every group's 16 reads of a 16-row fragment then land on 16 distinct 16-B slots of a 256-B bank
+// row (h = identity left 40 % of the LDS cycles as conflicts: SQ_LDS_BANK_CONFLICT 56M of 141M)
+__device__ __forceinline__ uint32_t kc_swz(int m) { return (uint32_t)((0x1320u >> (4 * ((m >> 2) & 3))) & 3u); }
 __device__ __forceinline__ uint32_t kc_off(int m, int k) {
-  return (uint32_t)(64 * m + 16 * ((k >> 3) ^ ((m >> 2) & 3)) + 2 * (k & 7));
+  return (uint32_t)(64 * m + 16 * ((uint32_t)(k >> 3) ^ kc_swz(m)) + 2 * (k & 7));
 }
 
 typedef __attribute__((address_space(3))) void* lds_vptr;
@@ -314,12 +323,13 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// piece j (0..15) of a k-major image: rows 4 (j & 7) .. +3 of half j >> 3; lane l stores chunk l & 15 of row
-// 4 (j & 7) + (l >> 4), which holds logical chunk (l & 15) ^ swz(row): source (k0 + row, c0 + half*128 + 8 ch)
+// piece j (0..15) of a k-major image: bytes [1024 (j & 7), +1024) of half j >> 3; lane l's 16 B at byte
+// b = 1024 (j & 7) + 16 l hold (row r, logical chunk ch) of the subtile layout: source (k0 + r, c0 + 128 half + 8 ch)
 __device__ __forceinline__ void km_piece(const __bf16* base, int64_t ld, int64_t k0, int64_t c0, int64_t klim,
                                          int64_t clim, int j, int lane, uint32_t img) {
-  const int r = 4 * (j & 7) + (lane >> 4), half = j >> 3;
-  const int ch = (lane & 15) ^ (int)km_swz(r);
+  const int b = 1024 * (j & 7) + 16 * lane, half = j >> 3;
+  const int r = 8 * (b >> 11) + ((b >> 6) & 7);
+  const int ch = 4 * ((b >> 9) & 3) + (((b >> 4) & 3) ^ ((r >> 2) & 3));
   const int64_t k = min(k0 + r, klim - 1), c = min(c0 + half * 128 + 8 * ch, clim - 8);
   dma16(base + k * ld + c, __builtin_amdgcn_readfirstlane(img + (uint32_t)j * 1024));
 }
@@ -327,7 +337,7 @@ __device__ __forceinline__ void km_piece(const __bf16* base, int64_t ld, int64_t
 __device__ __forceinline__ void kc_piece(const __bf16* base, int64_t ld, int64_t m0, int64_t k0, int64_t mlim,
                                          int64_t kcap, int j, int lane, uint32_t img) {
   const int r = 16 * j + (lane >> 2);
-  const int ch = (lane & 3) ^ ((r >> 2) & 3);
+  const int ch = (lane & 3) ^ (int)kc_swz(r);
   const int64_t m = min(m0 + r, mlim - 1), k = min(k0 + 8 * ch, kcap - 8);
   dma16(base + m * ld + k, __builtin_amdgcn_readfirstlane(img + (uint32_t)j * 1024));
 }
