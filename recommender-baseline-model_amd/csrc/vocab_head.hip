@@ -363,29 +363,44 @@ hipError_t launch(Args& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// ---- forward, ping-pong form -------------------------------------------------------------------------------
-// The form above runs its eight waves in lock step (a barrier per 64-deep h stage), so the two waves of a SIMD
-// are in their softmax epilogue (VALU + transcendental) at the same time and the matrix core idles through it.
-// Here:
+// ---- ping-pong forms (forward and backward) -----------------------------------------------------------------
+// The forms above run their eight waves in lock step (a barrier per h stage), so the two waves of a SIMD are in
+// their softmax epilogue (VALU + transcendental) at the same time and the matrix core idles through it.  Here:
 //   * each wave keeps its 64 vocabulary entries x d of E in REGISTERS for the whole vocabulary tile (the A
 //     operand; 128 VGPRs at d = 256), so LDS carries only h, and a whole 32-row tile of h (16 KB at d = 256)
-//     arrives by LDS-DMA in one piece: one barrier per row tile instead of one per k stage;
+//     arrives by LDS-DMA in one piece: one barrier per row tile ("item") instead of one per k stage;
 //   * waves 0-3 (group 0) and 4-7 (group 1) -- one of each per SIMD, same vocabulary quarter -- take alternate
-//     row tiles ("items") and run half an interval apart: in interval n group 0 runs the MFMAs of item 2n and
-//     then its epilogue, group 1 the epilogue of item 2n - 1 and then the MFMAs of item 2n + 1, so on every
-//     SIMD one wave's MFMAs overlap the other's epilogue;
-//   * the per-(row, 128-column) partials of a row tile combine two quarters' (max, sum) pairs through LDS one
-//     interval later (the next barrier orders them), into the same `part` layout as above.
-// Four h buffers: the two items of interval n + 1 stream in during interval n.
+//     items and run half an interval apart: in interval n group 0 runs the MFMAs of item 2n and then its
+//     epilogue, group 1 the epilogue of item 2n - 1 and then the MFMAs of item 2n + 1, so on every SIMD one
+//     wave's MFMAs overlap the other's epilogue;
+//   * h tiles are prefetched two intervals ahead (six buffers).  DMA completion is only visible through vmcnt,
+//     which retires in order and counts stores too, so every interval issues its global traffic in a fixed order
+//     -- the previous interval's stores, then (at a vocabulary-tile change, waited at once) the E reload, then
+//     the DMAs two intervals ahead -- and no vector-memory load follows the DMAs: the wait at the next interval
+//     is then exactly "all but this wave's DMAs of the last interval" (stores and the previous DMAs had a whole
+//     interval to land).  Per-row backward metadata (label entry, lse) sits in LDS for the launch;
+//   * fwd: each quarter's per-row (max, sum) pairs combine with the neighbouring quarter's into the 128-column
+//     `part` layout above one interval later; bwd: dlogits are staged per wave in LDS and leave as 16-B stores at
+//     the next interval's start;
+//   * a workgroup walks its (vocabulary tile, row tile) items from a rotated start, so the E reloads of the 256
+//     CUs (32 MB when they coincide) are spread over the launch.
 namespace pp {
-constexpr int BV = 256, BRT = 32, NBUF = 4, NJ = BRT / 16;
-template <int DK> struct C {
+#ifndef VPP_EXPT
+#define VPP_EXPT 0   // timing-only builds (tools/build_variant.sh): 1 no exp, 2 no fwd epilogue, 3 no dlogits
+#endif               // stores, 4 no MFMAs
+constexpr int BV = 256, BRT = 32, NJ = BRT / 16, PD = 2, NBUF = 2 * (PD + 1), SLD = 64 + 8;
+constexpr int LDS_MAX = 163840;
+template <int DK, bool BWD> struct C {
   static constexpr int KS = DK / 32;                  // 32-deep k steps
   static constexpr int CPR = DK / 8;                  // 16-B chunks per h row
   static constexpr int TILE = BRT * DK;               // h tile elements
   static constexpr int PIECES = TILE * 2 / 1024;      // 1-KB LDS-DMA pieces per h tile
   static constexpr int RPP = 1024 / (DK * 2);         // h rows per piece
-  static constexpr int LDS = NBUF * TILE * 2 + 2 * 2 * 4 * BRT * 8 + 8 * 64 * 4;
+  static constexpr int H_BYTES = NBUF * TILE * 2;
+  static constexpr int BSL_BYTES = 8 * 64 * 4;        // per wave: its bias quarter
+  static constexpr int RED_BYTES = BWD ? 0 : 2 * 2 * 4 * 4 * BRT * 8;   // fwd: [group][parity][quarter][g][BRT]
+  static constexpr int STG_BYTES = BWD ? 8 * BRT * SLD * 2 : 0;     // bwd: per wave [BRT][SLD] bf16 dlogits
+  static constexpr int FIXED = H_BYTES + BSL_BYTES + RED_BYTES + STG_BYTES;   // + bwd: 8 B per row of the range
 };
 
 typedef __attribute__((address_space(3))) void* lds_vptr;
@@ -397,17 +412,37 @@ __device__ __forceinline__ void dma16(const void* gsrc, uint32_t dst) {
                : "v"(gsrc), "s"(dst)
                : "memory");
 }
+// s_waitcnt vmcnt(N) (expcnt / lgkmcnt not waited)
+template <int N> __device__ __forceinline__ void wait_vm() {
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);
+}
+__device__ __forceinline__ void wait_vm_n(int n) {
+  switch (n) {
+    case 0: wait_vm<0>(); break;
+    case 1: wait_vm<1>(); break;
+    case 2: wait_vm<2>(); break;
+    case 3: wait_vm<3>(); break;
+    default: wait_vm<4>(); break;
+  }
+}
+__device__ __forceinline__ void raw_barrier() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);     // lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
 
 template <int DK, bool BWD>
 __global__ __launch_bounds__(NTH, 1) void pp_kernel(Args a) {
   KStampBegin stamp_b_(a.ks);
   KStampEnd stamp_e_(a.ks);
-  using P = C<DK>;
+  using P = C<DK, BWD>;
   constexpr int KS = P::KS, CPR = P::CPR;
+  static_assert(2 * P::PIECES / 8 <= 4, "wait_vm_n covers up to 4 pieces per wave and interval");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16* Hb = reinterpret_cast<bf16*>(smem);                               // NBUF h tiles [BRT][DK], swizzled
-  float2* red = reinterpret_cast<float2*>(smem + NBUF * P::TILE * 2);     // [group][parity][quarter][BRT]
-  float* bsl = reinterpret_cast<float*>(red + 2 * 2 * 4 * BRT);           // [wave][64]: this wave's bias quarter
+  bf16* Hb = reinterpret_cast<bf16*>(smem);                                    // NBUF h tiles [BRT][DK], swizzled
+  float* bsl = reinterpret_cast<float*>(smem + P::H_BYTES);                    // [wave][64]
+  float2* red = reinterpret_cast<float2*>(smem + P::H_BYTES + P::BSL_BYTES);  // fwd
+  bf16* stg = reinterpret_cast<bf16*>(smem + P::H_BYTES + P::BSL_BYTES + P::RED_BYTES);   // bwd
 
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, cl = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), q = wave & 3, G = wave >> 2;
@@ -419,9 +454,36 @@ __global__ __launch_bounds__(NTH, 1) void pp_kernel(Args a) {
   if (nloc <= 0 || (int64_t)blockIdx.x >= nvt) return;
   const int nvl = (int)((nvt - 1 - blockIdx.x) / gridDim.x + 1);         // this workgroup's vocabulary tiles
   const int F = nvl * nloc;                                               // items: (vocabulary tile, row tile)
+  const int rot = (int)((blockIdx.x * 37u + blockIdx.y * 11u) % (unsigned)F);   // rotated start (see above)
+  const int64_t rbase = (int64_t)mtb * BRT;
   const uint32_t hb0 = lds_u32(Hb);
+  int* mlab = reinterpret_cast<int*>(smem + P::FIXED);          // bwd: [rows] label entry (-1: none here, -2: dead)
+  float* mlse = reinterpret_cast<float*>(mlab + nloc * BRT);    // bwd: [rows] lse * log2(e) (+inf: dead)
 
-  // items fa, fa + 1 -> h buffers (fa & 3), (fa + 1) & 3: 2 * PIECES DMA pieces dealt over the 8 waves.  A
+  float sc = 0.f;
+  if constexpr (BWD) {
+    sc = (a.dloss ? *a.dloss : 1.f) / *a.count;
+    for (int r = tid; r < nloc * BRT; r += NTH) {
+      const int64_t row = rbase + r;
+      int le = -2;
+      float L = __builtin_inff();
+      if (row < Rl) {
+        const int64_t lb = a.labels[row];
+        if (lb != 0) {
+          const int64_t o = lb - a.voff;
+          le = (o >= 0 && o < a.V1) ? (int)o : -1;
+          L = a.lse[row] * 1.4426950408889634f;
+        }
+      }
+      mlab[r] = le;
+      mlse[r] = L;
+    }
+  }
+  // flat item f (in processing order) -> (local vocabulary tile, row tile)
+  auto item_vt = [&](int f) { const int ff = f + rot < F ? f + rot : f + rot - F; return ff / nloc; };
+  auto item_u = [&](int f) { const int ff = f + rot < F ? f + rot : f + rot - F; return ff - (ff / nloc) * nloc; };
+
+  // items fa, fa + 1 -> h buffers fa % NBUF, (fa + 1) % NBUF: 2 * PIECES DMA pieces dealt over the 8 waves.  A
   // wave's pieces j all have j = wave (mod 8), so its lanes' (row in piece, swizzled chunk) are fixed: lane row
   // lr, source chunk hc; only the piece's first row (scalar) varies
   const int lr = lane / CPR;
@@ -431,36 +493,45 @@ __global__ __launch_bounds__(NTH, 1) void pp_kernel(Args a) {
     for (int p0 = 0; p0 < 2 * P::PIECES; p0 += 8) {
       const int p = p0 + wave, f = fa + p / P::PIECES, j = p % P::PIECES;
       if (f < F) {
-        const int64_t rb = (int64_t)(mtb + f % nloc) * BRT + j * P::RPP;
+        const int64_t rb = (int64_t)(mtb + item_u(f)) * BRT + j * P::RPP;
         const int64_t gr = min(rb + lr, Rl - 1);
-        dma16(a.h + gr * a.ldh + hc, __builtin_amdgcn_readfirstlane(hb0 + (uint32_t)((f & 3) * P::TILE * 2 + j * 1024)));
+        dma16(a.h + gr * a.ldh + hc,
+              __builtin_amdgcn_readfirstlane(hb0 + (uint32_t)((f % NBUF) * P::TILE * 2 + j * 1024)));
       }
     }
+  };
+  // DMA pieces this wave issued for items fa, fa + 1
+  auto issued = [&](int fa) {
+    int c = 0;
+#pragma unroll
+    for (int p0 = 0; p0 < 2 * P::PIECES; p0 += 8) c += (fa + (p0 + wave) / P::PIECES < F) ? 1 : 0;
+    return c;
   };
 
   bf16x8 ef[4][KS];          // this wave's E quarter of the current vocabulary tile (A operand fragments)
   f32x4 acc[4][NJ];          // S^T[vocab 64 q + 16 i + 4 g + r][row 16 j + cl] of the wave's last item
   int cur_vtl = -1;
 
-  auto mfma_item = [&](int f) {
-    const int vtl = f / nloc;
-    if (vtl != cur_vtl) {
-      cur_vtl = vtl;
-      const int64_t vt = (int64_t)blockIdx.x + (int64_t)vtl * gridDim.x;
-      // the quarter's bias -> this wave's LDS slot; entries past the vocabulary get -inf there, which masks them
-      // in the epilogue (E rows past it are clamped, so their products are finite)
-      {
-        const int64_t v = vt * BV + 64 * q + lane;
-        bsl[wave * 64 + lane] = v < a.V1 ? (a.bias ? a.bias[v] : 0.f) : -__builtin_inff();
-      }
+  // E quarter + bias of local vocabulary tile vtl (waited here: no vector load may follow the interval's DMAs).
+  // The bias goes to this wave's LDS slot, -inf past the vocabulary, which masks those entries (E rows past it
+  // are clamped, so their products are finite)
+  auto load_e = [&](int vtl) {
+    cur_vtl = vtl;
+    const int64_t vt = (int64_t)blockIdx.x + (int64_t)vtl * gridDim.x;
+    const int64_t vb = vt * BV + 64 * q + lane;
+    const float bv = vb < a.V1 ? (a.bias ? a.bias[vb] : 0.f) : -__builtin_inff();
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int64_t v = min(vt * BV + 64 * q + 16 * i + cl, a.V1 - 1);
+    for (int i = 0; i < 4; ++i) {
+      const int64_t v = min(vt * BV + 64 * q + 16 * i + cl, a.V1 - 1);
 #pragma unroll
-        for (int s = 0; s < KS; ++s) ef[i][s] = *reinterpret_cast<const bf16x8*>(a.E + v * a.lde + 32 * s + 8 * g);
-      }
+      for (int s = 0; s < KS; ++s) ef[i][s] = *reinterpret_cast<const bf16x8*>(a.E + v * a.lde + 32 * s + 8 * g);
     }
-    const bf16* H = Hb + (f & 3) * P::TILE;
+    bsl[wave * 64 + lane] = bv;
+    wait_vm<0>();
+  };
+
+  auto mfma_item = [&](int f) {
+    const bf16* H = Hb + (f % NBUF) * P::TILE;
     // the accumulators start from the bias of their vocabulary rows (-inf past the vocabulary)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -468,156 +539,184 @@ __global__ __launch_bounds__(NTH, 1) void pp_kernel(Args a) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) acc[i][j] = b4;
     }
-    // one k step's h fragments at a time (the other wave of the SIMD covers the LDS latency); the scheduling
-    // fence keeps the compiler from hoisting every step's reads at once (128 registers at d = 256)
+    // h fragments one k step ahead (the MFMA phase of a wave often has the SIMD to itself, so the LDS latency
+    // must hide under its own MFMAs); the scheduling fence keeps the compiler from hoisting more steps' reads
+    bf16x8 fb[2][NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) fb[0][j] = row_frag<CPR>(H, 16 * j, 0, lane);
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      bf16x8 fb[NJ];
+      if (s + 1 < KS) {
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) fb[j] = row_frag<CPR>(H, 16 * j, 4 * s, lane);
+        for (int j = 0; j < NJ; ++j) fb[(s + 1) & 1][j] = row_frag<CPR>(H, 16 * j, 4 * (s + 1), lane);
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma(ef[i][s], fb[j], acc[i][j]);
+        for (int j = 0; j < NJ; ++j) {
+          if (VPP_EXPT == 4) acc[i][j][0] += (float)fb[s & 1][j][0] * (float)ef[i][s][0];
+          else acc[i][j] = mfma(ef[i][s], fb[s & 1][j], acc[i][j]);
+        }
       __builtin_amdgcn_sched_barrier(0);
     }
   };
 
-  float sc = 0.f;
-  if constexpr (BWD) sc = (a.dloss ? *a.dloss : 1.f) / *a.count;
-
-  // bwd: dlogits of item f over this wave's quarter, straight from the accumulators: a lane holds 4
-  // consecutive vocabulary entries of a row (one 8-B store; the wave's 4 stores per row fill 128 contiguous
-  // bytes).  Dead rows (label 0) take lse = +inf and scale 0, so their dlogits are exactly 0 with no select;
-  // rows >= the live count are not written
-  auto epi_bwd = [&](int f) {
-    const int vtl = f / nloc, u = f - vtl * nloc;
-    const int64_t n0 = ((int64_t)blockIdx.x + (int64_t)vtl * gridDim.x) * BV, vb = n0 + 64 * q + 4 * g;
-    const bool full = n0 + BV <= a.V1;
+  // fwd: softmax statistics of item f: per lane (max, sum) over its 16 entries of each of its rows (four
+  // independent sum chains, no cross-lane step) -> red[G][parity][q][g][row]; the combine folds the 4 lane groups
+  // x 2 quarters of a 128-column tile
+  auto epi_fwd = [&](int f) {
+    float2* rd = red + (((G * 2 + ((f >> 1) & 1)) * 4 + q) * 4 + g) * BRT;
+    if (VPP_EXPT == 2) {
+      rd[cl] = make_float2(acc[0][0][0], acc[3][NJ - 1][3]);
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int64_t row = (int64_t)(mtb + u) * BRT + 16 * j + cl;
-      const bool inr = row < Rl;
-      const int64_t lb = inr ? a.labels[row] : 0;
-      const bool live = inr && lb != 0;
-      const float Ll = live ? a.lse[row] * 1.4426950408889634f : __builtin_inff();
-      const float scr = live ? sc : 0.f;
-      const int64_t offl = lb - a.voff - vb;               // the label's entry among this lane's rows
-      const int off = offl < 0 || offl >= 64 ? -1 : (int)offl;
-      bf16* dst = a.dl + row * a.lddl + vb;
+      float m0 = fmaxf(fmaxf(acc[0][j][0], acc[0][j][1]), fmaxf(acc[0][j][2], acc[0][j][3]));
+      float m1 = fmaxf(fmaxf(acc[1][j][0], acc[1][j][1]), fmaxf(acc[1][j][2], acc[1][j][3]));
+      float m2 = fmaxf(fmaxf(acc[2][j][0], acc[2][j][1]), fmaxf(acc[2][j][2], acc[2][j][3]));
+      float m3 = fmaxf(fmaxf(acc[3][j][0], acc[3][j][1]), fmaxf(acc[3][j][2], acc[3][j][3]));
+      const float mx = fmaxf(fmaxf(m0, m1), fmaxf(m2, m3));
+      const float mxl = mx * 1.4426950408889634f;
+      float sp[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        sp[i] = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float ea = __builtin_fmaf(acc[i][j][r], 1.4426950408889634f, -mxl);
+          sp[i] += VPP_EXPT == 1 ? ea : __builtin_amdgcn_exp2f(ea);
+        }
+      }
+      const float sm = mx == -__builtin_inff() ? 0.f : (sp[0] + sp[1]) + (sp[2] + sp[3]);
+      rd[16 * j + cl] = make_float2(mx, sm);
+    }
+  };
+
+  // fwd: lane groups x quarters {0, 1} / {2, 3} of item f -> its two 128-column partial tiles (one barrier after
+  // epi_fwd(f)); the fold order is fixed
+  auto combine = [&](int f) {
+    const int tg = tid & 255;
+    if (tg < 2 * BRT) {
+      const int rl = tg & (BRT - 1), half = tg / BRT;
+      const int64_t n0 = ((int64_t)blockIdx.x + (int64_t)item_vt(f) * gridDim.x) * BV;
+      const int64_t row = (int64_t)(mtb + item_u(f)) * BRT + rl, pt = (n0 >> 7) + half;
+      const float2* rd = red + (G * 2 + ((f >> 1) & 1)) * 16 * BRT + 2 * half * 4 * BRT + rl;
+      float2 e[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) e[k] = rd[k * BRT];
+      float mx = e[0].x;
+#pragma unroll
+      for (int k = 1; k < 8; ++k) mx = fmaxf(mx, e[k].x);
+      float sm = 0.f;
+      if (mx != -__builtin_inff()) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) sm += e[k].y * __expf(e[k].x - mx);
+      }
+      if (row < Rl && pt < a.ntn) *reinterpret_cast<float2*>(a.part + (row * a.ntn + pt) * 2) = make_float2(mx, sm);
+    }
+  };
+
+  // bwd: dlogits of item f over this wave's quarter -> the wave's LDS stage [row][64 entries] (a lane holds 4
+  // consecutive entries of a row: one 8-B write).  Dead rows take lse = +inf and scale 0: exactly 0, no select
+  bf16* st = stg + wave * BRT * SLD;
+  auto epi_bwd = [&](int f) {
+    const int u = item_u(f);
+    const int64_t vb = ((int64_t)blockIdx.x + (int64_t)item_vt(f) * gridDim.x) * BV + 64 * q + 4 * g;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int rr = u * BRT + 16 * j + cl;
+      const int le = mlab[rr];
+      const float Ll = mlse[rr];
+      const float scr = le == -2 ? 0.f : sc;
+      const int64_t offl = (int64_t)le - vb;             // the label's entry among this lane's rows
+      const int off = le < 0 || offl < 0 || offl >= 64 ? -1 : (int)offl;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         bf4 o;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[i][j][r], 1.4426950408889634f, -Ll));
+          const float ea = __builtin_fmaf(acc[i][j][r], 1.4426950408889634f, -Ll);
+          const float e = VPP_EXPT == 1 ? ea : __builtin_amdgcn_exp2f(ea);
           o[r] = (bf16)((e - (off == 16 * i + r ? 1.f : 0.f)) * scr);
         }
-        if (inr) {
-          if (full || vb + 16 * i + 4 <= a.V1) {
-            *reinterpret_cast<bf4*>(dst + 16 * i) = o;
-          } else {
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              if (vb + 16 * i + r < a.V1) dst[16 * i + r] = o[r];
-          }
-        }
+        *reinterpret_cast<bf4*>(st + (16 * j + cl) * SLD + 16 * i + 4 * g) = o;
       }
       __builtin_amdgcn_sched_barrier(0);
     }
   };
-
-  // softmax statistics of item f over this wave's quarter -> red[G][parity][q]
-  auto epi_item = [&](int f) {
-    float2* rd = red + ((G * 2 + ((f >> 1) & 1)) * 4 + q) * BRT;
+  // bwd: the stage of item f -> dlogits, 16-B stores (8 rows x 128 B per instruction); rows >= the live count are
+  // not written; a chunk starting below V1 may run into the row's padding up to lddl (zeros there)
+  auto flush = [&](int f) {
+    const int u = item_u(f);
+    const int64_t c0 = ((int64_t)blockIdx.x + (int64_t)item_vt(f) * gridDim.x) * BV + 64 * q;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      float mx = -__builtin_inff();
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          mx = fmaxf(mx, acc[i][j][r]);
-        }
-      float sm = 0.f;
-      const float mxl = mx * 1.4426950408889634f;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) sm += __builtin_amdgcn_exp2f(__builtin_fmaf(acc[i][j][r], 1.4426950408889634f, -mxl));
-      if (mx == -__builtin_inff()) sm = 0.f;
-#pragma unroll
-      for (int o = 16; o < 64; o <<= 1) comb(mx, sm, __shfl_xor(mx, o, 64), __shfl_xor(sm, o, 64));
-      if (g == 0) rd[16 * j + cl] = make_float2(mx, sm);
-      __builtin_amdgcn_sched_barrier(0);     // one row fragment's statistics at a time (register pressure)
-    }
-  };
-
-  // quarters {0, 1} / {2, 3} of item f -> its two 128-column partial tiles (one barrier after epi_item(f))
-  auto combine_item = [&](int f) {
-    const int tg = tid & 255;
-    if (tg < 2 * BRT) {
-      const int rl = tg & (BRT - 1), half = tg / BRT;
-      const int vtl = f / nloc, u = f - vtl * nloc;
-      const int64_t n0 = ((int64_t)blockIdx.x + (int64_t)vtl * gridDim.x) * BV;
-      const int64_t row = (int64_t)(mtb + u) * BRT + rl, pt = (n0 >> 7) + half;
-      const float2* rd = red + (G * 2 + ((f >> 1) & 1)) * 4 * BRT;
-      float2 e0 = rd[(2 * half) * BRT + rl];
-      const float2 e1 = rd[(2 * half + 1) * BRT + rl];
-      comb(e0.x, e0.y, e1.x, e1.y);
-      if (row < Rl && pt < a.ntn) *reinterpret_cast<float2*>(a.part + (row * a.ntn + pt) * 2) = e0;
+    for (int k = 0; k < BRT / 8; ++k) {
+      const int r = 8 * k + (lane >> 3), ch = lane & 7;
+      const int64_t row = (int64_t)(mtb + u) * BRT + r, v = c0 + 8 * ch;
+      const bf16x8 x = *reinterpret_cast<const bf16x8*>(st + r * SLD + 8 * ch);
+      if (row < Rl && v < a.V1 && (VPP_EXPT != 3 || a.V1 < 0)) *reinterpret_cast<bf16x8*>(a.dl + row * a.lddl + v) = x;
     }
   };
 
   const int NI = (F + 1) / 2;
   issue(0);
+  issue(2);
 #pragma unroll 1
   for (int n = 0; n <= NI + 1; ++n) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's pieces of items 2n, 2n + 1 landed
-    __syncthreads();                                    // ... everyone's; interval n - 1's readers are done
-    if (2 * n + 2 < F) issue(2 * n + 2);
+    wait_vm_n(issued(2 * n + 2));      // items 2n, 2n + 1 landed (this wave's); interval n + 1's may be in flight
+    raw_barrier();                     // ... everyone's; interval n - 1's readers are done
+    const int fm = 2 * n + G, fe = 2 * n - G, fc = fe - 2;
+    if constexpr (BWD) {
+      if (fc >= 0 && fc < F) flush(fc);
+    } else {
+      if (fc >= 0 && fc < F) combine(fc);
+    }
+    if (fm < F && item_vt(fm) != cur_vtl) load_e(item_vt(fm));
+    if (2 * n + 4 < F) issue(2 * n + 4);
     // group 0: MFMAs of item 2n, then its epilogue; group 1: epilogue of item 2n - 1, then the MFMAs of 2n + 1
     // (one copy of each phase in the code: phase ph runs the MFMAs where ph == G)
-    const int fm = 2 * n + G, fe = 2 * n - G, fc = fe - 2;
 #pragma unroll 1
     for (int ph = 0; ph < 2; ++ph) {
       if (ph == G) {
         if (fm < F) mfma_item(fm);
-      } else {
-        if constexpr (BWD) {
-          if (fe >= 0 && fe < F) epi_bwd(fe);
-        } else {
-          if (fc >= 0 && fc < F) combine_item(fc);
-          if (fe >= 0 && fe < F) epi_item(fe);
-        }
+      } else if (fe >= 0 && fe < F) {
+        if constexpr (BWD) epi_bwd(fe);
+        else epi_fwd(fe);
       }
     }
   }
 }
 
+// returns hipErrorNotSupported when the backward's per-row metadata would not fit LDS (the caller falls back)
 template <int DK, bool BWD>
 hipError_t launch_pp(Args& a, hipStream_t s) {
-  using P = C<DK>;
-  static_assert(P::LDS <= 163840, "LDS budget");
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)pp_kernel<DK, BWD>, hipFuncAttributeMaxDynamicSharedMemorySize, P::LDS);
-    attr = true;
-  }
+  using P = C<DK, BWD>;
+  static_assert(P::FIXED <= LDS_MAX, "LDS budget");
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int64_t nvt = cdiv(a.V1, BV);
   const int64_t grid = std::min<int64_t>(nvt, (int64_t)cus);
-  const int64_t gy = std::max<int64_t>(1, std::min<int64_t>(cdiv(a.R, BRT), (int64_t)cus / nvt));
-  hipLaunchKernelGGL((pp_kernel<DK, BWD>), dim3((unsigned)grid, (unsigned)gy), dim3(NTH), P::LDS, s, a);
+  const int64_t nmt = cdiv(a.R, BRT);
+  const int64_t gy = std::max<int64_t>(1, std::min<int64_t>(nmt, (int64_t)cus / nvt));
+  const int64_t lds = P::FIXED + (BWD ? 8 * BRT * cdiv(nmt, gy) : 0);
+  if (lds > LDS_MAX) return hipErrorNotSupported;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)pp_kernel<DK, BWD>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    attr = true;
+  }
+  hipLaunchKernelGGL((pp_kernel<DK, BWD>), dim3((unsigned)grid, (unsigned)gy), dim3(NTH), (unsigned)lds, s, a);
   return hipGetLastError();
 }
 }  // namespace pp
 
-// RS_VHEAD_PP=1 selects the ping-pong forms (read per launch, for A/B); default: the lock-step forms
+// RS_VHEAD_PP=0 selects the lock-step forms (read per launch, for A/B); default: the ping-pong forms
+// (R = 1,750, 1M + 1 classes, d = 256: fwd 1,876 -> 1,427 us, bwd 3,064 -> 1,715 us; cfg3's 26,745 classes:
+// 74.1 -> 62.6 / 86.8 -> 61.1 us; tools/vhead_bench.py, same session)
 inline bool use_pp() {
   const char* e = getenv("RS_VHEAD_PP");
-  return e ? atoi(e) != 0 : false;
+  return e ? atoi(e) != 0 : true;
 }
 
 // lock-step forms: fwd 256-entry vocabulary tiles (E tile 132 KB at d = 256); bwd 128 (room for the dlogits
@@ -626,9 +725,9 @@ template <bool BWD>
 hipError_t dispatch(Args& a, int64_t d, hipStream_t s) {
   constexpr int BV = BWD ? 128 : 256;
   if (use_pp()) {
-    if (d == 256) return pp::launch_pp<256, BWD>(a, s);
-    if (d == 128) return pp::launch_pp<128, BWD>(a, s);
-    return pp::launch_pp<64, BWD>(a, s);
+    const hipError_t e = d == 256 ? pp::launch_pp<256, BWD>(a, s)
+                         : d == 128 ? pp::launch_pp<128, BWD>(a, s) : pp::launch_pp<64, BWD>(a, s);
+    if (e != hipErrorNotSupported) return e;
   }
   if (d == 256) return launch<256, BV, BWD>(a, s);
   if (d == 128) return launch<128, BV, BWD>(a, s);
