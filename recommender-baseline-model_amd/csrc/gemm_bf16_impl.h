@@ -674,8 +674,14 @@ hipError_t launch_cfg(GemmArgs& a, hipStream_t s) {
 // GELU' + dropout epilogues (BERT FFN1 forward, FFN2 input gradient) always take 64x64: their VALU work
 // (tanh, the dropout hash) then overlaps the loads of the other resident workgroups (12800 x 1024 x 256:
 // 25.9 -> 24.3 us and 27.6 -> 25.6 us, tools/diag/gemm_epi.py)
+#include "gemm_dma.h"
+
 template <bool AK, bool BK, int EC>
 hipError_t launch_tiles(GemmArgs& a, hipStream_t s) {
+  if constexpr (!AK && EC >= 0) {
+    const hipError_t e = dma::launch<BK, EC>(a, s);
+    if (e != hipErrorNotSupported) return e;
+  }
   constexpr bool heavy_epi = EC >= 0 && (ec_act(EC) == 2 || ec_act(EC) == 4) && (EC & ED) != 0;
   if (!heavy_epi && cdiv(a.M, 128) * cdiv(a.N, 128) * a.split_k >= 512) return launch_cfg<AK, BK, 128, 128, EC>(a, s);
 #ifdef GBF_MID_MIN

@@ -1,0 +1,223 @@
+// LDS-DMA pipelined form of the bf16 block GEMM (gfx950), included by gemm_bf16_impl.h before its tile dispatch.
+//
+// The BERT block products (M = B*T = 12,800 token rows, N / K = 256 / 768 / 1,024: QKV, output projection, FFN
+// in both orientations) are short in K (8-32 stages of 32) and wide in M, so the register-staged kernel above
+// spends its time waiting: one stage in flight, and HBM / L2 latency under load (~1-2 us) paid once per stage.
+// Here, as in gemm_n256.hip's vocabulary GEMM:
+//
+//  * 32-deep k stages loaded by global_load_lds_dwordx4 straight into FOUR LDS stage buffers, three stages in
+//    flight per wave (counted vmcnt, never drained in the main loop), one raw s_barrier per stage;
+//  * no staging registers: the images are lane-linear 1-KB DMA pieces, so the bank-conflict-free layouts move to
+//    the SOURCE address -- k-contiguous images [rows][32 k] (64-B rows) with chunk g of row m at g ^ h((m >> 2) & 3),
+//    h = {0, 2, 3, 1}; the k-major weight image of the input-gradient products [32 k][128 n] in 8-row x 32-column
+//    subtiles (read by ds_read_b64_tr_b16);
+//  * tiles BM x 128 (BM = 64 or 128) over 4 waves (2 x 2), 2 workgroups per CU; every k stage is one
+//    mfma_f32_16x16x32_bf16 step, in k order -- so each output element sees exactly the register-staged kernel's
+//    accumulation sequence (bit-identical results, tests/test_gemm_dma_gpu.py);
+//  * the epilogue is the register-staged kernel's epi_rows (all compile-time epilogue classes), staged through LDS
+//    64 rows at a time.
+//
+// Taken for A k-contiguous (forward X.W^T and input gradient dY.W), N % 128 == 0, K % 32 == 0, no split-K, a
+// compile-time epilogue class.  RS_GEMM_DMA=0 selects the register-staged kernel (read per launch, for A/B);
+// RS_GEMM_DMA_BM=64/128 forces the row tile.
+// (included inside namespace gbf: epi_rows, GemmArgs and the epilogue classes are those above)
+#pragma once
+
+namespace dma {
+
+constexpr int DBK = 32, NBUF = 4, DIST = 3, BN = 128, NTH = 256;
+constexpr int IMG_B = BN * DBK * 2;   // the B operand's stage image (8 KB, either orientation)
+
+__device__ __forceinline__ uint32_t kc_swz(int m) { return (uint32_t)((0x1320u >> (4 * ((m >> 2) & 3))) & 3u); }
+// byte offset of element (row m, k) of a k-contiguous stage image [rows][32]
+__device__ __forceinline__ uint32_t kc_off(int m, int k) {
+  return (uint32_t)(64 * m + 16 * ((uint32_t)(k >> 3) ^ kc_swz(m)) + 2 * (k & 7));
+}
+// byte offset of element (k row r, column c < 128) of the k-major stage image [32][128]: 8-row x 32-column subtiles
+// of 512 B, chunk (ch & 3) ^ ((r >> 2) & 3) inside its 64-B subtile row (cdna_hip_programming.md T10, image (a))
+__device__ __forceinline__ uint32_t km_off(int r, int c) {
+  const int ch = c >> 3;
+  return (uint32_t)(2048 * (r >> 3) + 512 * (ch >> 2) + 64 * (r & 7) + 16 * ((ch & 3) ^ ((r >> 2) & 3)) + 2 * (c & 7));
+}
+
+typedef __attribute__((address_space(3))) void* lds_vptr;
+__device__ __forceinline__ uint32_t lds_u32(const void* p) { return (uint32_t)(uintptr_t)(lds_vptr)p; }
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(dst)
+               : "memory");
+}
+template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory"); }
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// piece j of a k-contiguous image: rows 16j .. 16j+15 (64 B each); lane l stores chunk position l & 3 of row
+// 16j + (l >> 2), which holds logical chunk (l & 3) ^ h(row).  Rows past rlim read row rlim - 1 (finite; their
+// outputs are never stored).
+__device__ __forceinline__ void kc_piece(const __bf16* base, int64_t ld, int64_t r0, int64_t k0, int64_t rlim, int j,
+                                         int lane, uint32_t img) {
+  const int r = 16 * j + (lane >> 2);
+  const int ch = (lane & 3) ^ (int)kc_swz(r);
+  const int64_t row = min(r0 + r, rlim - 1);
+  dma16(base + row * ld + k0 + 8 * ch, __builtin_amdgcn_readfirstlane(img + (uint32_t)j * 1024));
+}
+// piece j (0..7) of the k-major image: byte b = 1024 j + 16 l holds (k row r, logical chunk ch) of the subtile layout
+__device__ __forceinline__ void km_piece(const __bf16* base, int64_t ld, int64_t k0, int64_t c0, int j, int lane,
+                                         uint32_t img) {
+  const int b = 1024 * j + 16 * lane;
+  const int r = 8 * (b >> 11) + ((b >> 6) & 7);
+  const int ch = 4 * ((b >> 9) & 3) + (((b >> 4) & 3) ^ ((r >> 2) & 3));
+  dma16(base + (k0 + r) * ld + c0 + 8 * ch, __builtin_amdgcn_readfirstlane(img + (uint32_t)j * 1024));
+}
+__device__ __forceinline__ bf16x8 kc_frag(const char* img, int row0, int lane) {
+  const int g = lane >> 4, li = lane & 15;
+  return *reinterpret_cast<const bf16x8*>(img + kc_off(row0 + li, 8 * g));
+}
+__device__ __forceinline__ bf16x8 km_frag(const char* img, int col0, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int c = col0 + 4 * p, r = 8 * g + q;
+  const bf4 x = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf4*)(img + km_off(r, c)));
+  const bf4 y =
+      __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf4*)(img + km_off(r + 4, c)));
+  return __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+template <bool BK, int BM, int EC>
+__global__ __launch_bounds__(NTH, 2) void gemm_dma_kernel(GemmArgs a) {
+  KStampBegin stamp_b_(a.ks);
+  KStampEnd stamp_e_(a.ks);
+  constexpr int IMG_A = BM * DBK * 2, DSTAGE = IMG_A + IMG_B;
+  constexpr int LDC = BN + 4, HR = 64;            // epilogue: 64 rows of the fp32 tile per LDS pass
+  constexpr int LDS_BYTES = NBUF * DSTAGE > HR * LDC * 4 ? NBUF * DSTAGE : HR * LDC * 4;
+  constexpr int PA = BM / 64, PB = 2, PPS = PA + PB;   // DMA pieces per wave per stage (A, B)
+  constexpr int FM = BM / 32, FN = 4;
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // block -> tile as the register-staged kernel (XCD-contiguous ranges, shorter tile axis fastest)
+  const unsigned tiles_n = (unsigned)(a.N / BN);
+  const int64_t Mb = a.epi.rows_dev ? min(a.M, (int64_t)*a.epi.rows_dev) : a.M;
+  unsigned tiles_m = gridDim.x / tiles_n, bid = blockIdx.x, nwg = gridDim.x;
+  if (a.epi.rows_dev) {
+    tiles_m = (unsigned)((Mb + BM - 1) / BM);
+    nwg = tiles_m * tiles_n;
+    if (bid >= nwg) return;
+  }
+  {
+    const unsigned q = nwg >> 3, r = nwg & 7, x = bid & 7;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+  }
+  unsigned tm, tn;
+  if (tiles_m < tiles_n) {
+    tn = bid / tiles_m;
+    tm = bid - tn * tiles_m;
+  } else {
+    tm = bid / tiles_n;
+    tn = bid - tm * tiles_n;
+  }
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  if (m0 >= Mb) return;
+  const int nk = (int)(a.K / DBK);
+  const __bf16* A = reinterpret_cast<const __bf16*>(a.A);
+  const __bf16* B = reinterpret_cast<const __bf16*>(a.B);
+  const uint32_t lds0 = lds_u32(smem);
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  auto issue = [&](int t) {
+    const uint32_t buf = lds0 + (uint32_t)((t % NBUF) * DSTAGE);
+    const int64_t k0 = (int64_t)t * DBK;
+#pragma unroll
+    for (int j = 0; j < PA; ++j) kc_piece(A, a.lda, m0, k0, a.M, wave * PA + j, lane, buf);
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+      if (BK) km_piece(B, a.ldb, k0, n0, wave * PB + j, lane, buf + IMG_A);
+      else kc_piece(B, a.ldb, n0, k0, a.N, wave * PB + j, lane, buf + IMG_A);
+    }
+  };
+  auto compute = [&](int t) {
+    const char* buf = smem + (t % NBUF) * DSTAGE;
+    bf16x8 fa[FM], fb[FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) fa[i] = kc_frag(buf, wm * (BM / 2) + 16 * i, lane);
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+      fb[j] = BK ? km_frag(buf + IMG_A, wn * 64 + 16 * j, lane) : kc_frag(buf + IMG_A, wn * 64 + 16 * j, lane);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+  };
+
+  for (int t = 0; t < min(nk, DIST); ++t) issue(t);
+  for (int t = 0; t < nk; ++t) {
+    const int after = min(nk - 1, t + DIST - 1) - t;   // stages issued after t, allowed to stay in flight
+    if (after >= 2) vm_wait<2 * PPS>();
+    else if (after == 1) vm_wait<PPS>();
+    else vm_wait<0>();
+    raw_barrier();                                      // stage t landed everywhere; buffer (t - 1) % NBUF free
+    if (t + DIST < nk) issue(t + DIST);
+    compute(t);
+  }
+
+  // ---- epilogue through LDS, 64 rows per pass
+  float* Cs = reinterpret_cast<float*>(smem);
+  const int g = lane >> 4, cl = lane & 15;
+  constexpr int TPR = BN / 8, RPP = NTH / TPR;          // 16 threads per row, 16 rows per pass
+  const int c8 = (tid % TPR) * 8;
+  const int64_t n = n0 + c8;
+  uint32_t s1 = 0, s2 = 0;
+  if constexpr ((EC & ED) != 0) s1 = seed32(eff_seed(a.epi.drop_seed, a.epi.seed_base));
+  if constexpr ((EC & EP) != 0) s2 = seed32(eff_seed(a.epi.post_drop_seed, a.epi.seed_base));
+#pragma unroll
+  for (int half = 0; half < BM / HR; ++half) {
+    __syncthreads();
+    if (BM == HR || wm == half) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            Cs[((BM == HR ? wm * (BM / 2) : 0) + 16 * i + 4 * g + r) * LDC + wn * 64 + 16 * j + cl] = acc[i][j][r];
+    }
+    __syncthreads();
+    epi_rows<EC, HR / RPP, RPP, LDC>(a, Cs, tid / TPR, c8, m0 + half * HR, Mb, n, s1, s2);
+  }
+}
+
+inline bool enabled() {
+  const char* e = getenv("RS_GEMM_DMA");
+  return e ? atoi(e) != 0 : false;   // default off until measured on the GPU
+}
+
+// launch the DMA form when the call fits it (returns hipErrorNotSupported otherwise)
+template <bool BK, int EC>
+hipError_t launch(GemmArgs& a, hipStream_t s) {
+  if (!enabled() || a.split_k != 1 || a.N % BN || a.K % DBK || a.K < DBK || a.lda % 8 || a.ldb % 8 ||
+      ((uintptr_t)a.A & 15) || ((uintptr_t)a.B & 15))
+    return hipErrorNotSupported;
+  const char* f = getenv("RS_GEMM_DMA_BM");
+  const int force = f ? atoi(f) : 0;
+  const int64_t big = cdiv(a.M, 128) * (a.N / BN);
+  const bool bm128 = force == 128 || (force != 64 && big >= 512);
+  if (bm128) {
+    hipLaunchKernelGGL((gemm_dma_kernel<BK, 128, EC>), dim3((unsigned)big), dim3(NTH), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((gemm_dma_kernel<BK, 64, EC>), dim3((unsigned)(cdiv(a.M, 64) * (a.N / BN))), dim3(NTH), 0, s,
+                       a);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace dma

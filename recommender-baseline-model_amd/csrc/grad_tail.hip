@@ -86,9 +86,7 @@ int rs_wgrad_grouped_pos_stats(int nprob, const rs_wgrad_problem* probs, int64_t
   a.ks = kstamp_next(RS_STAMP_WGRAD_GROUPED);
   r.ks = a.ks;
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid((unsigned)(a.ntiles * a.splits));
-  if (T == 128) hipLaunchKernelGGL(wg::wgrad_group_kernel<128>, grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(wg::wgrad_group_kernel<64>, grid, dim3(256), 0, s, a);
+  wg::launch_group(a, T, s);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   const gt::HeadStats hs{(int)head_blocks, head_part, head_divisor, loss_out, aux_out};

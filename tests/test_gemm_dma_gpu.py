@@ -1,0 +1,137 @@
+"""LDS-DMA pipelined bf16 GEMM (csrc/gemm_dma.h) for the BERT block products: the same call with RS_GEMM_DMA=1
+(the DMA form, both row tiles) and RS_GEMM_DMA=0 (the register-staged kernel) gives the SAME bits -- every output
+element takes the same sequence of 32-deep MFMA steps in k order and the same epilogue -- at the cfg3 shapes
+(BS/models/bert_modules/attention/multi_head.py:24-40 QKV / output projection, utils/feed_forward.py:15-16 FFN), in
+both orientations, with every epilogue class the BERT layer uses, ragged M and a device row count; and the plain
+product matches torch float64 on the same bf16 operands."""
+import os
+
+import pytest
+import torch
+
+from conftest import rel
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(shape, scale=1.0, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    return (torch.randn(*shape, device="cuda", generator=g) * scale).bfloat16()
+
+
+def _run(fn, env):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return fn()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def _three_ways(fn):
+    """(register-staged, DMA 128-row tiles, DMA 64-row tiles) results of fn()."""
+    ref = _run(fn, {"RS_GEMM_DMA": "0"})
+    d128 = _run(fn, {"RS_GEMM_DMA": "1", "RS_GEMM_DMA_BM": "128"})
+    d64 = _run(fn, {"RS_GEMM_DMA": "1", "RS_GEMM_DMA_BM": "64"})
+    return ref, d128, d64
+
+
+def _same(outs):
+    ref = outs[0]
+    for o in outs[1:]:
+        if isinstance(ref, tuple):
+            for x, y in zip(ref, o):
+                assert torch.equal(x, y)
+        else:
+            assert torch.equal(ref, o)
+
+
+CASES = [  # M, N (output width), K
+    (12800, 768, 256),    # QKV forward
+    (12800, 256, 256),    # output projection forward / its input gradient
+    (12800, 1024, 256),   # FFN1 forward / FFN2 input gradient
+    (12800, 256, 1024),   # FFN2 forward / FFN1 input gradient
+    (12800, 256, 768),    # QKV input gradient
+    (1000, 384, 96),      # ragged rows, 3 k stages
+    (70, 128, 32),        # one partial row tile, one stage
+]
+
+
+@pytest.mark.parametrize("M,N,K", CASES)
+def test_forward_plain_bitwise_and_float64(M, N, K):
+    import rbm_amd  # noqa: F401
+    from rbm_amd import ops
+    x, W = _bf((M, K), 1.0, 1), _bf((N, K), 0.05, 2)
+
+    def f():
+        y = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+        ops.linear_fwd(x, W, y)
+        torch.cuda.synchronize()
+        return y
+    outs = _three_ways(f)
+    _same(outs)
+    ref = x.double() @ W.double().t()
+    assert rel(outs[1].double().cpu().numpy(), ref.cpu().numpy()) < 5e-3   # bf16 output rounding
+
+
+@pytest.mark.parametrize("M,N,K", CASES)
+def test_dgrad_plain_bitwise_and_float64(M, N, K):
+    import rbm_amd  # noqa: F401
+    from rbm_amd import ops
+    dy, W = _bf((M, K), 1.0, 3), _bf((K, N), 0.05, 4)    # dX[M,N] = dY[M,K] . W[K,N]
+
+    def f():
+        dx = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+        ops.linear_dgrad(dy, W, dx)
+        torch.cuda.synchronize()
+        return dx
+    outs = _three_ways(f)
+    _same(outs)
+    ref = dy.double() @ W.double()
+    assert rel(outs[1].double().cpu().numpy(), ref.cpu().numpy()) < 5e-3
+
+
+def test_bert_layer_epilogues_bitwise():
+    """The fused epilogues of the BERT layer (tools/diag/gemm_epi.py's set): bias + GELU + dropout + saved
+    pre-activation (FFN1), bias + dropout + residual + post-dropout (FFN2), GELU' + dropout (FFN2 input gradient),
+    bias + dropout + residual (output projection), bias (QKV), accumulate, fp32 output; a device row count."""
+    import rbm_amd  # noqa: F401
+    from rbm_amd import ops
+    B, T, d, ff = 16, 200, 256, 1024
+    M = B * T
+    sb = torch.tensor([5], dtype=torch.int64, device="cuda")
+    x, W1, W2, Wq, Wo = _bf((M, d), 1, 5), _bf((ff, d), .05, 6), _bf((d, ff), .05, 7), _bf((3 * d, d), .05, 8), \
+        _bf((d, d), .05, 9)
+    b1, b2, bq = (torch.randn(n, device="cuda") for n in (ff, d, 3 * d))
+    z, dy2 = _bf((M, d), 1, 10), _bf((M, d), 1, 11)
+    dk = dict(drop_p=0.1, drop_seed=7, seed_base=sb)
+    rows = torch.tensor([M - 77], dtype=torch.int32, device="cuda")
+
+    def f():
+        h = torch.zeros(M, ff, device="cuda", dtype=torch.bfloat16)
+        pre = torch.zeros_like(h)
+        ops.linear_fwd(x, W1, h, bias=b1, act=ops.ACT_GELU, aux_out=pre, drop_ld=ff, **dk)
+        y = torch.zeros(M, d, device="cuda", dtype=torch.bfloat16)
+        ops.linear_fwd(h, W2, y, bias=b2, drop_ld=d, resid=z, post_drop_p=0.1, post_drop_seed=8, **dk)
+        dh = torch.zeros(M, ff, device="cuda", dtype=torch.bfloat16)
+        ops.linear_dgrad(dy2, W2, dh, act=ops.ACT_GELU_BWD, aux=pre, drop_ld=ff, **dk)
+        o = torch.zeros(M, d, device="cuda", dtype=torch.bfloat16)
+        ops.linear_fwd(x, Wo, o, bias=b2, drop_ld=d, resid=z, **dk)
+        q = torch.zeros(M, 3 * d, device="cuda", dtype=torch.bfloat16)
+        ops.linear_fwd(x, Wq, q, bias=bq)
+        acc = z.clone()
+        ops.linear_fwd(x, Wo, acc, accumulate=True)
+        f32 = torch.zeros(M, d, device="cuda", dtype=torch.float32)
+        ops.linear_fwd(x, Wo, f32, bias=b2)
+        rd = torch.full((M, d), 3.0, device="cuda", dtype=torch.bfloat16)
+        ops.linear_fwd(x, Wo, rd, rows_dev=rows)
+        torch.cuda.synchronize()
+        return h, pre, y, dh, o, q, acc, f32, rd
+    outs = _three_ways(f)
+    _same(outs)
+    rd = outs[1][-1]
+    assert torch.all(rd[M - 77:] == 3.0)          # rows past the device count untouched

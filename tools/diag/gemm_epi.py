@@ -80,6 +80,12 @@ def main():
     run("torch.mm qkv", lambda: torch.mm(x, Wq.t(), out=qkv), mb * 4, 6.0 * M * d * d)
     Wo = rn(d, d)
     run("out plain", lambda: ops.linear_fwd(x, Wo, y), mb * 2, 2.0 * M * d * d)
+    run("qkv dgrad plain", lambda: ops.linear_dgrad(qkv, Wq, y), mb * 4, 6.0 * M * d * d)
+    run("out dgrad plain", lambda: ops.linear_dgrad(z, Wo, y), mb * 2, 2.0 * M * d * d)
+    run("out +bias+drop+resid", lambda: ops.linear_fwd(x, Wo, y, bias=b2, drop_ld=d, resid=z, **dk), mb * 3,
+        2.0 * M * d * d)
+    run("qkv +bias", lambda: ops.linear_fwd(x, Wq, qkv, bias=torch.zeros(3 * d, device=dev)), mb * 4,
+        6.0 * M * d * d)
     run("torch.mm out", lambda: torch.mm(x, Wo.t(), out=y), mb * 2, 2.0 * M * d * d)
     torch.cuda.synchronize()
     print(f"{'op':60s} {'us':>8s} {'GB/s':>8s} {'TFLOP/s':>8s}")
