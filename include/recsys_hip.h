@@ -249,6 +249,10 @@ int rs_adam_prepare(double* state, const double* hyper, const float* grad_diviso
                     void* stream);
 int rs_adam_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16,
                  const double* state, const double* hyper, int zero_grad, void* stream);
+/* rs_adam_step on at most max_wg workgroups (grid-stride; same results bit for bit): a range updated on a side
+ * stream beside other kernels (BERT's out.weight during the encoder backward) takes a bounded share of the CUs. */
+int rs_adam_step_wg(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, const double* state,
+                    const double* hyper, int zero_grad, int max_wg, void* stream);
 int rs_adam_prepare_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, double* state,
                          const double* hyper, int zero_grad, const float* grad_divisor, uint64_t* seed_base,
                          const int64_t* tdesc, int ntd, int64_t tbase, void* wT, void* stream);

@@ -355,8 +355,13 @@ int rs_adam_prepare(double* state, const double* hyper, const float* grad_diviso
 
 int rs_adam_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, const double* state,
                  const double* hyper, int zero_grad, void* stream) {
-  if (n <= 0 || ((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16) return RS_ERR_ARG;
-  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(cdiv(n / 4, 256), 8192));
+  return rs_adam_step_wg(n, p, g, m, v, p_bf16, state, hyper, zero_grad, 8192, stream);
+}
+
+int rs_adam_step_wg(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, const double* state,
+                    const double* hyper, int zero_grad, int max_wg, void* stream) {
+  if (n <= 0 || max_wg <= 0 || ((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16) return RS_ERR_ARG;
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(cdiv(n / 4, 256), max_wg));
   hipStream_t s = (hipStream_t)stream;
   double* st = const_cast<double*>(state);   // read only without PREP
   if (p_bf16)

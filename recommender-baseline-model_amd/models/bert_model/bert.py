@@ -549,6 +549,9 @@ class BERTEngine:
             slab_d = self.ws.get("slab_dh", (sk * cap * d,), torch.float32)
             ops.gemm(dl, self.W("out.weight"), slab_d, cap, d, self.V1, False, True, ops.epilogue(rows_dev=cnt),
                      split_k=sk, slab=slab_d)
+        hook = getattr(self, "after_head_grads", None)
+        if hook is not None:
+            hook()                      # out.weight / out.bias are final and no longer read this step
         dxL = self._buf((M, d))
         ops.splitk_scatter_rows(slab_d, sk, cap, rank, dxL)
         self.encode_backward(s, dxL, grad)

@@ -317,7 +317,11 @@ def adam_prepare(state, hyper, grad_divisor=None, seed_base=None):
     call("rs_adam_prepare", ptr(state), ptr(hyper), ptr(grad_divisor), ptr(seed_base), stream())
 
 
-def adam_step(p, g, m, v, p_bf16, state, hyper, zero_grad=False):
+def adam_step(p, g, m, v, p_bf16, state, hyper, zero_grad=False, max_wg=None):
+    if max_wg:
+        call("rs_adam_step_wg", p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), ptr(p_bf16), ptr(state), ptr(hyper),
+             int(zero_grad), int(max_wg), stream())
+        return
     call("rs_adam_step", p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), ptr(p_bf16), ptr(state), ptr(hyper),
          int(zero_grad), stream())
 

@@ -77,6 +77,31 @@ class FusedAdam:
                               self.hyper, zero_grad=zg)
 
 
+    def step_keep_early(self, keep, max_wg=None):
+        """The first part of a step whose `keep` range is final before the rest of the backward (BERT's out.weight /
+        out.bias, after the head's dE / dh): rs_adam_prepare (t += 1 and the step's scalars; no seed advance -- the
+        backward still draws this step's dropout masks) and that range's update, gradient left in place.
+        step_rest() finishes the step: the same per-element math as step(keep=...), bit for bit."""
+        lo, hi = keep
+        f = self.flat
+        ops.adam_prepare(self.state, self.hyper)
+        bf = f.bf16[lo:hi] if f.bf16 is not None else None
+        ops.adam_step(f.data[lo:hi], f.grad[lo:hi], self.m[lo:hi], self.v[lo:hi], bf, self.state, self.hyper,
+                      zero_grad=False, max_wg=max_wg)
+
+    def step_rest(self, keep, seed_base=None):
+        """The rest of a step_keep_early step: every range outside `keep` (gradient cleared), then the seed."""
+        lo, hi = keep
+        f = self.flat
+        for a, b in ((0, lo), (hi, f.numel)):
+            if b > a:
+                bf = f.bf16[a:b] if f.bf16 is not None else None
+                ops.adam_step(f.data[a:b], f.grad[a:b], self.m[a:b], self.v[a:b], bf, self.state, self.hyper,
+                              zero_grad=True)
+        if seed_base is not None:
+            ops.seed_advance(seed_base)
+
+
 class FusedStepLR:
     """``torch.optim.lr_scheduler.StepLR(optimizer, step_size, gamma)`` for a FusedAdam (BS/trainers/base.py:40, stepped
     once per epoch at :87): every ``step_size``-th ``step()`` multiplies the learning rate by ``gamma`` -- chained in
@@ -180,6 +205,16 @@ class FusedTrainStep:
         self.sparse_mode = sparse_rows
         self.sparse = None
         self._sparse_checked = False
+        # BERT on one device with a vocabulary whose head gradient the backward overwrites whole (overwritten_grads:
+        # the 1M-item head): out.weight / out.bias are final once the head's dE / dh are formed, so their Adam update
+        # (256M elements: ~1 ms of HBM streaming at cfg5) runs on a side stream BESIDE the encoder's backward, on a
+        # bounded grid, and joins before the rest of the optimizer (RS_EARLY_HEAD_ADAM=0: at the end, as before).
+        self._early_kp = None
+        self._early_ev = None
+        self._early_ok = (self.kind == "bert" and not self.dp and self.vshard is None and not self.l2
+                          and os.environ.get("RS_EARLY_HEAD_ADAM", "0") != "0"
+                          and hasattr(self.engine, "overwritten_grads"))
+        self._opt_stream = torch.cuda.Stream(device=self.flat.device) if self._early_ok else None
 
     # ---------------------------------------------------------------- pieces
     def _divisor(self, local_count):
@@ -227,6 +262,17 @@ class FusedTrainStep:
                                              partial=True)
 
     def _compute(self, *batch, split=None):
+        # the early out.weight update hook is live only inside this trainer's own steps (the engine may also be
+        # driven directly, with no optimizer step to join it)
+        if not self._early_ok:
+            return self._compute_impl(*batch, split=split)
+        self.engine.after_head_grads = self._early_head_update
+        try:
+            return self._compute_impl(*batch, split=split)
+        finally:
+            self.engine.after_head_grads = None
+
+    def _compute_impl(self, *batch, split=None):
         """Forward + loss + backward into the flat gradient.  split(tag): called by the engine when the bucket
         `tag` is final (DP only: the aux tail -- loss sum, count -- is written before it).
 
@@ -313,9 +359,33 @@ class FusedTrainStep:
                     self.opt.step(grad_divisor=cnt, seed_base=sb, transposed=tr, keep=kp)
                 else:   # the loss division rides in the optimizer's launch
                     self.opt.step(grad_divisor=cnt, seed_base=sb, transposed=tr, loss=(lsum, self.loss_val), keep=kp)
+            elif self._early_ev is not None:
+                assert tr is None and kp == self._early_kp, (kp, self._early_kp)
+                torch.cuda.current_stream().wait_event(self._early_ev)
+                self._early_ev = None
+                self.opt.step_rest(kp, seed_base=sb)
             else:
                 self._l2(self.loss_out[2:3])
                 self.opt.step(seed_base=sb, transposed=tr, keep=kp)
+
+    # max workgroups of the early out.weight update: a bounded share of the CUs beside the encoder's backward
+    EARLY_HEAD_ADAM_WG = int(os.environ.get("RS_EARLY_HEAD_ADAM_WG", "1024"))
+
+    def _early_head_update(self):
+        """Engine hook (BERTEngine: right after the head's dE / dh): fork the out.weight / out.bias update onto the
+        optimizer's side stream; _update joins it."""
+        kp = self.engine.overwritten_grads()
+        if kp is None:
+            return
+        self._early_kp = kp
+        cur = torch.cuda.current_stream()
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        self._opt_stream.wait_event(ev)
+        with torch.cuda.stream(self._opt_stream):
+            self.opt.step_keep_early(self._early_kp, max_wg=self.EARLY_HEAD_ADAM_WG)
+            self._early_ev = torch.cuda.Event()
+            self._early_ev.record(self._opt_stream)
 
     # ---------------------------------------------------------------- one step
     def step(self, *batch):

@@ -293,3 +293,37 @@ def test_bert_large_vocab_overwritten_head_grads_match_zeroed():
             assert float(tr.flat.grad[lo:hi].abs().sum()) > 0
             assert float(tr.flat.grad[:lo].abs().sum()) == 0
     assert torch.equal(params[0], params[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graph", [False, True])
+def test_bert_early_head_adam_equals_end_of_step(graph, monkeypatch):
+    """The out.weight / out.bias update forked onto a side stream right after the head's dE / dh (beside the encoder's
+    backward; FusedTrainStep._early_head_update, RS_EARLY_HEAD_ADAM) gives the same bits as the update at the end of
+    the step: three steps, eager and graph-replayed (two steps unrolled per replay)."""
+    import rbm_amd.data as synth
+    from rbm_amd.train_step import FusedTrainStep
+    V, T, B = 70000, 40, 8
+    rng = np.random.default_rng(5)
+    batches = [tuple(torch.from_numpy(t).cuda() for t in synth.bert_batch(rng, B, T, V, mask_prob=0.2))
+               for _ in range(4)]
+    res = []
+    for early in ("1", "0"):
+        monkeypatch.setenv("RS_EARLY_HEAD_ADAM", early)
+        torch.manual_seed(0)
+        m = _bert(V, T, 256, 1, 2, 0.1, "bf16", seed=12)
+        tr = FusedTrainStep(m, lr=1e-3, max_labelled=128)
+        assert tr._early_ok == (early == "1")
+        tr.engine.seed_base.fill_(77)
+        if graph:
+            tr.capture(*batches[0], warmup=1, steps_per_graph=2)
+            pk = lambda bs: torch.stack([torch.stack(b) for b in bs])   # noqa: E731  [S, 2, B, T]
+            losses = [tr.replay_packed(pk(batches[0:2])).cpu().tolist(),
+                      tr.replay_packed(pk(batches[2:4])).cpu().tolist()]
+        else:
+            losses = [float(tr.step(tok, lab).item()) for tok, lab in batches[:3]]
+        torch.cuda.synchronize()
+        res.append((losses, tr.flat.data.clone(), tr.opt.m.clone(), tr.opt.v.clone(), tr.opt.state.clone()))
+    assert res[0][0] == res[1][0]
+    for a, b in zip(res[0][1:], res[1][1:]):
+        assert torch.equal(a, b)

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-dma}
 mkdir -p $OUT
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gemm_dma_gpu.py tests/test_wgrad_gpu.py > $OUT/test.log 2>&1; rc=$?; tail -3 $OUT/test.log
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gemm_dma_gpu.py tests/test_wgrad_gpu.py tests/test_bert.py -k 'dma or wgrad or early_head' > $OUT/test.log 2>&1; rc=$?; tail -3 $OUT/test.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python tools/diag/gemm_epi.py --reps 50 --envs 'RS_GEMM_DMA=0;RS_GEMM_DMA=1,RS_GEMM_DMA_BM=128;RS_GEMM_DMA=1,RS_GEMM_DMA_BM=64' > $OUT/gemm_epi.log 2>&1 || exit $?
 for c in cfg2 cfg3; do for f in 0 1; do
@@ -15,9 +15,12 @@ for c in cfg2 cfg3; do for f in 0 1; do
 done; done
 for c in cfg3 cfg2; do
   RS_GEMM_DMA=0 RS_WGRAD_DMA=0 timeout -k 10 300 python bench.py --config $c --cpu-baseline-seconds 0 > $OUT/bench_${c}_old.log 2>&1 || exit $?
-  timeout -k 10 300 python bench.py --config $c --cpu-baseline-seconds 0 > $OUT/bench_${c}_new.log 2>&1 || exit $?
+  RS_GEMM_DMA=1 RS_WGRAD_DMA=1 timeout -k 10 300 python bench.py --config $c --cpu-baseline-seconds 0 > $OUT/bench_${c}_new.log 2>&1 || exit $?
   RS_GEMM_DMA=0 RS_WGRAD_DMA=0 timeout -k 10 300 python bench.py --config $c --cpu-baseline-seconds 0 > $OUT/bench_${c}_old2.log 2>&1 || exit $?
-  timeout -k 10 300 python bench.py --config $c --cpu-baseline-seconds 0 > $OUT/bench_${c}_new2.log 2>&1 || exit $?
+  RS_GEMM_DMA=1 RS_WGRAD_DMA=1 timeout -k 10 300 python bench.py --config $c --cpu-baseline-seconds 0 > $OUT/bench_${c}_new2.log 2>&1 || exit $?
+done
+for f in 0 1; do
+  RS_EARLY_HEAD_ADAM=$f RS_GEMM_DMA=1 RS_WGRAD_DMA=1 timeout -k 10 400 python bench.py --config cfg5 --steps 30 --warmup 5 --cpu-baseline-seconds 0 > $OUT/bench_cfg5_early$f.log 2>&1 || exit $?
 done
 grep -h "" $OUT/gemm_epi.log | tail -60
 for f in $OUT/kb_*.log; do echo "== $f"; tail -4 $f; done
