@@ -53,6 +53,10 @@ hipError_t gemm_bf16_launch(int ak, int bk, GemmArgs& a, hipStream_t s) {
   }
   if (!ak && !bk) return launch_fwd(a, s);
   if (!ak && bk) return launch_dgrad(a, s);
-  if (ak && bk) return launch_any<true, true, EC_GENERIC>(a, s);
+  if (ak && bk) {
+    const hipError_t e = dma::launch_wgrad(a, s);
+    if (e != hipErrorNotSupported) return e;
+    return launch_any<true, true, EC_GENERIC>(a, s);
+  }
   return launch_any<true, false, EC_GENERIC>(a, s);
 }

@@ -196,6 +196,123 @@ __global__ __launch_bounds__(NTH, 2) void gemm_dma_kernel(GemmArgs a) {
   }
 }
 
+// Weight-gradient orientation, one split (the BERT vocabulary head's dE = dlogits^T h below the 64k classes where
+// gemm_n256 takes over; rs_linear_wgrad's direct path): C[m][n] (+)= sum_k A[k][m] B[k][n], both operands k-major
+// ([32 k][128] stage images, transposing reads), 128 x 128 tiles, the k bound from the device row count, the last
+// partial stage zeroed in LDS; the bias column sums colsum_out[m] ride on MFMAs against ones in the tiles of column
+// tile 0 (as the register-staged kernel); fp32 C stored from the accumulators.
+template <int UNUSED = 0>   // a template: the header is compiled into several translation units
+__global__ __launch_bounds__(NTH, 2) void gemm_dma_wgrad_kernel(GemmArgs a) {
+  KStampBegin stamp_b_(a.ks);
+  KStampEnd stamp_e_(a.ks);
+  constexpr int IMG = 32 * 128 * 2, DSTAGE = 2 * IMG, PPS = 4, FM = 4, FN = 4;
+  __shared__ __attribute__((aligned(1024))) char smem[NBUF * DSTAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const unsigned tiles_n = (unsigned)(a.N / BN), tiles_m = gridDim.x / tiles_n;
+  unsigned bid = blockIdx.x;
+  {
+    const unsigned nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, x = bid & 7;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+  }
+  unsigned tm, tn;
+  if (tiles_m < tiles_n) {
+    tn = bid / tiles_m;
+    tm = bid - tn * tiles_m;
+  } else {
+    tm = bid / tiles_n;
+    tn = bid - tm * tiles_n;
+  }
+  const int64_t m0 = (int64_t)tm * 128, n0 = (int64_t)tn * BN;
+  const int64_t Kb = a.epi.rows_dev ? min(a.K, (int64_t)*a.epi.rows_dev) : a.K;
+  const int nk = Kb > 0 ? (int)((Kb + DBK - 1) / DBK) : 0;
+  const __bf16* A = reinterpret_cast<const __bf16*>(a.A);
+  const __bf16* B = reinterpret_cast<const __bf16*>(a.B);
+  const bool do_colsum = a.colsum_out != nullptr && tn == 0 && wn == 0;
+  const uint32_t lds0 = lds_u32(smem);
+  f32x4 acc[FM][FN], accb[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    accb[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
+  auto issue = [&](int t) {
+    const uint32_t buf = lds0 + (uint32_t)((t % NBUF) * DSTAGE);
+    const int64_t k0 = (int64_t)t * DBK;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int pc = 2 * wave + j, b = 1024 * pc + 16 * lane;
+      const int r = 8 * (b >> 11) + ((b >> 6) & 7);
+      const int ch = 4 * ((b >> 9) & 3) + (((b >> 4) & 3) ^ ((r >> 2) & 3));
+      const int64_t k = min(k0 + r, Kb - 1);
+      const int64_t ca = min(m0 + 8 * ch, a.lda - 8);        // columns past M: inside the row, never stored
+      dma16(A + k * a.lda + ca, __builtin_amdgcn_readfirstlane(buf + (uint32_t)pc * 1024));
+      dma16(B + k * a.ldb + n0 + 8 * ch, __builtin_amdgcn_readfirstlane(buf + IMG + (uint32_t)pc * 1024));
+    }
+  };
+  auto zero_tail = [&](int t) {
+    char* buf = smem + (t % NBUF) * DSTAGE;
+    const int kv = (int)(Kb - (int64_t)t * DBK);
+    for (int e = tid; e < (DBK - kv) * 128; e += NTH) {
+      const int r = kv + e / 128, c = e % 128;
+      *reinterpret_cast<__bf16*>(buf + km_off(r, c)) = (__bf16)0.0f;
+      *reinterpret_cast<__bf16*>(buf + IMG + km_off(r, c)) = (__bf16)0.0f;
+    }
+  };
+  auto compute = [&](int t) {
+    const char* buf = smem + (t % NBUF) * DSTAGE;
+    bf16x8 fa[FM], fb[FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) fa[i] = km_frag(buf, wm * 64 + 16 * i, lane);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) fb[j] = km_frag(buf + IMG, wn * 64 + 16 * j, lane);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    if (do_colsum) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], ones, accb[i], 0, 0, 0);
+    }
+  };
+  const bool tail = (Kb % DBK) != 0;
+  for (int t = 0; t < min(nk, DIST); ++t) issue(t);
+  for (int t = 0; t < nk; ++t) {
+    const int after = min(nk - 1, t + DIST - 1) - t;
+    if (after >= 2) vm_wait<2 * PPS>();
+    else if (after == 1) vm_wait<PPS>();
+    else vm_wait<0>();
+    raw_barrier();
+    if (t + DIST < nk) issue(t + DIST);
+    if (tail && t == nk - 1) {
+      zero_tail(t);
+      raw_barrier();
+    }
+    compute(t);
+  }
+  vm_wait<0>();
+  float* C = reinterpret_cast<float*>(a.C);
+  const int g = lane >> 4, cl = lane & 15;
+  const bool accum = a.epi.accumulate != 0;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t m = m0 + wm * 64 + 16 * i + 4 * g + r;
+      if (m >= a.M) continue;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        float* c = C + m * a.ldc + n0 + wn * 64 + 16 * j + cl;
+        *c = accum ? *c + acc[i][j][r] : acc[i][j][r];
+      }
+      if (do_colsum && cl == 0) a.colsum_out[m] = (accum ? a.colsum_out[m] : 0.f) + accb[i][r];
+    }
+}
+
 inline bool enabled() {
   const char* e = getenv("RS_GEMM_DMA");
   return e ? atoi(e) != 0 : false;   // default off until measured on the GPU
@@ -217,6 +334,18 @@ hipError_t launch(GemmArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((gemm_dma_kernel<BK, 64, EC>), dim3((unsigned)(cdiv(a.M, 64) * (a.N / BN))), dim3(NTH), 0, s,
                        a);
   }
+  return hipGetLastError();
+}
+
+// the weight-gradient form when the call fits it (hipErrorNotSupported otherwise): one split, fp32 C, alpha 1, no
+// other epilogue, N % 128 == 0
+inline hipError_t launch_wgrad(GemmArgs& a, hipStream_t s) {
+  const rs_epilogue& e = a.epi;
+  if (!enabled() || a.split_k != 1 || a.slab || !a.c_f32 || e.alpha != 1.0f || e.bias || e.act || e.aux ||
+      e.aux_out || e.drop_p > 0.f || e.resid || e.rowmask_ids || e.post_drop_p > 0.f || a.N % BN || a.M < 8 ||
+      a.lda % 8 || a.ldb % 8 || a.lda < a.M || ((uintptr_t)a.A & 15) || ((uintptr_t)a.B & 15))
+    return hipErrorNotSupported;
+  hipLaunchKernelGGL(gemm_dma_wgrad_kernel<0>, dim3((unsigned)(cdiv(a.M, 128) * (a.N / BN))), dim3(NTH), 0, s, a);
   return hipGetLastError();
 }
 

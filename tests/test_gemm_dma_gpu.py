@@ -135,3 +135,30 @@ def test_bert_layer_epilogues_bitwise():
     _same(outs)
     rd = outs[1][-1]
     assert torch.all(rd[M - 77:] == 3.0)          # rows past the device count untouched
+
+
+@pytest.mark.parametrize("R,V,count,accumulate", [(2600, 26745, 2531, False), (512, 1000, None, True),
+                                                  (77, 300, 40, False)])
+def test_wgrad_direct_bitwise(R, V, count, accumulate):
+    """rs_linear_wgrad's one-split path (the BERT vocabulary head's dE = dlogits^T h + the bias column sums below the
+    64k classes, BS/models/bert.py:10,16) on the DMA weight-gradient kernel equals the register-staged kernel bit for
+    bit: ragged vocabulary tiles, a device row count with a partial last stage, accumulate on and off."""
+    import rbm_amd  # noqa: F401
+    from rbm_amd import ops
+    Vp = V + (-V) % 64
+    dl = _bf((R, Vp), 1e-2, 21)[:, :V]
+    h = _bf((R, 256), 1.0, 22)
+    rows = None if count is None else torch.tensor([count], dtype=torch.int32, device="cuda")
+    slab = torch.empty(1, device="cuda")
+
+    def f():
+        dE = torch.full((V, 256), 0.5, device="cuda")
+        db = torch.full((V,), 0.25, device="cuda")
+        ops.linear_wgrad(dl, h, dE, slab, db=db, split_k=1, accumulate=accumulate, rows_dev=rows)
+        torch.cuda.synchronize()
+        return dE, db
+    outs = _three_ways(f)
+    _same(outs)
+    k = R if count is None else count
+    ref = dl[:k].double().t() @ h[:k].double() + (0.5 if accumulate else 0.0)
+    assert rel(outs[1][0].double().cpu().numpy(), ref.cpu().numpy()) < 2e-6
