@@ -19,7 +19,12 @@
 //
 // Taken for A k-contiguous (forward X.W^T and input gradient dY.W), N % 128 == 0, K % 32 == 0, no split-K, a
 // compile-time epilogue class.  RS_GEMM_DMA=0 selects the register-staged kernel (read per launch, for A/B);
-// RS_GEMM_DMA_BM=64/128 forces the row tile.
+// RS_GEMM_DMA_BM=128 takes 128-row tiles.  Measured at the cfg3 shapes (tools/diag/gemm_epi.py, M = 12,800, same
+// session; register-staged -> DMA 128-row -> DMA 64-row tiles, us): QKV + bias 24.7 -> 16.2 -> 15.2, QKV input
+// gradient 16.5 -> 14.4 -> 12.9, FFN1 + bias + GELU + dropout + pre-activation 24.9 -> 25.9 -> 22.5, FFN2 + bias +
+// dropout + residual + post-dropout 20.2 -> 17.7 -> 17.7, FFN2 input gradient + GELU' + dropout 26.0 -> 27.4 -> 22.9,
+// FFN1 input gradient 19.0 -> 16.7 -> 15.0, output projection 9.1 / 9.0 / 9.0 (both orientations); whole cfg3 step
+// 41.1k -> 43.3k seq/s.  64-row tiles (3 workgroups per CU) are the default.
 // (included inside namespace gbf: epi_rows, GemmArgs and the epilogue classes are those above)
 #pragma once
 
@@ -315,7 +320,7 @@ __global__ __launch_bounds__(NTH, 2) void gemm_dma_wgrad_kernel(GemmArgs a) {
 
 inline bool enabled() {
   const char* e = getenv("RS_GEMM_DMA");
-  return e ? atoi(e) != 0 : false;   // default off until measured on the GPU
+  return e ? atoi(e) != 0 : true;
 }
 
 // launch the DMA form when the call fits it (returns hipErrorNotSupported otherwise)
@@ -327,7 +332,7 @@ hipError_t launch(GemmArgs& a, hipStream_t s) {
   const char* f = getenv("RS_GEMM_DMA_BM");
   const int force = f ? atoi(f) : 0;
   const int64_t big = cdiv(a.M, 128) * (a.N / BN);
-  const bool bm128 = force == 128 || (force != 64 && big >= 512);
+  const bool bm128 = force == 128;   // 64-row tiles by default: at every cfg3 shape as fast or faster (header)
   if (bm128) {
     hipLaunchKernelGGL((gemm_dma_kernel<BK, 128, EC>), dim3((unsigned)big), dim3(NTH), 0, s, a);
   } else {

@@ -336,7 +336,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_group_dma_kernel(Args a) {
 
 inline bool dma_enabled() {
   const char* e = getenv("RS_WGRAD_DMA");
-  return e ? atoi(e) != 0 : false;   // default off until measured on the GPU
+  return e ? atoi(e) != 0 : false;   // default off: measured no faster (cfg2 31.9 -> 36.8 us, cfg3 175 -> 176 us)
 }
 
 // the grouped launch (T = output tile edge)

@@ -212,7 +212,7 @@ class FusedTrainStep:
         self._early_kp = None
         self._early_ev = None
         self._early_ok = (self.kind == "bert" and not self.dp and self.vshard is None and not self.l2
-                          and os.environ.get("RS_EARLY_HEAD_ADAM", "0") != "0"
+                          and os.environ.get("RS_EARLY_HEAD_ADAM", "1") != "0"
                           and hasattr(self.engine, "overwritten_grads"))
         self._opt_stream = torch.cuda.Stream(device=self.flat.device) if self._early_ok else None
 
