@@ -368,8 +368,10 @@ class FusedTrainStep:
                 self._l2(self.loss_out[2:3])
                 self.opt.step(seed_base=sb, transposed=tr, keep=kp)
 
-    # max workgroups of the early out.weight update: a bounded share of the CUs beside the encoder's backward
-    EARLY_HEAD_ADAM_WG = int(os.environ.get("RS_EARLY_HEAD_ADAM_WG", "1024"))
+    # max workgroups of the early out.weight update: a bounded share of the CUs beside the encoder's backward.  cfg5
+    # (two interleaved rounds, seq/s): end of step 6,776 / 6,607; early on 128 workgroups 6,573 / 6,444, 256: 7,184 /
+    # 7,130, 512: 6,889 / 6,858, 1,024: 6,801 / 6,695 (1,024 took the CUs from the encoder's first backward GEMM)
+    EARLY_HEAD_ADAM_WG = int(os.environ.get("RS_EARLY_HEAD_ADAM_WG", "256"))
 
     def _early_head_update(self):
         """Engine hook (BERTEngine: right after the head's dE / dh): fork the out.weight / out.bias update onto the
