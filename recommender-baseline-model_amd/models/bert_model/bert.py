@@ -364,6 +364,9 @@ class BERTEngine:
         else:
             ops.embed_bwd(1, ids, T, dx, 1.0, hp, self.salt["emb"], sb, G("bert.embedding.token.weight"),
                           G("bert.embedding.position.pe.weight"))
+        hook = getattr(self, "after_token_grads", None)
+        if hook is not None:
+            hook("bert.embedding.token.weight")   # the token table's gradient is final
         ex, sp = getattr(self, "sparse_tok", None), getattr(self, "_split", None)
         if ex is not None and sp is not None:
             # data parallel, union-of-touched-rows exchange of the token table's gradient (dp.SparseRowExchange):

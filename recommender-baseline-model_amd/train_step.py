@@ -89,15 +89,24 @@ class FusedAdam:
         ops.adam_step(f.data[lo:hi], f.grad[lo:hi], self.m[lo:hi], self.v[lo:hi], bf, self.state, self.hyper,
                       zero_grad=False, max_wg=max_wg)
 
-    def step_rest(self, keep, seed_base=None):
-        """The rest of a step_keep_early step: every range outside `keep` (gradient cleared), then the seed."""
-        lo, hi = keep
+    def step_range(self, lo, hi, zero_grad=True, max_wg=None):
+        """rs_adam_step over [lo, hi) with the step's scalars already prepared (a step_keep_early step)."""
         f = self.flat
-        for a, b in ((0, lo), (hi, f.numel)):
-            if b > a:
-                bf = f.bf16[a:b] if f.bf16 is not None else None
-                ops.adam_step(f.data[a:b], f.grad[a:b], self.m[a:b], self.v[a:b], bf, self.state, self.hyper,
-                              zero_grad=True)
+        bf = f.bf16[lo:hi] if f.bf16 is not None else None
+        ops.adam_step(f.data[lo:hi], f.grad[lo:hi], self.m[lo:hi], self.v[lo:hi], bf, self.state, self.hyper,
+                      zero_grad=zero_grad, max_wg=max_wg)
+
+    def step_rest(self, keep, seed_base=None, done=()):
+        """The rest of a step_keep_early step: every range outside `keep` and the ranges in `done` (already updated
+        by step_range) with the gradient cleared, then the seed."""
+        f = self.flat
+        cuts = sorted([tuple(keep)] + [tuple(r) for r in done])
+        a = 0
+        for lo, hi in cuts + [(f.numel, f.numel)]:
+            assert lo >= a, (cuts, a)
+            if lo > a:
+                self.step_range(a, lo)
+            a = hi
         if seed_base is not None:
             ops.seed_advance(seed_base)
 
@@ -215,6 +224,9 @@ class FusedTrainStep:
                           and os.environ.get("RS_EARLY_HEAD_ADAM", "1") != "0"
                           and hasattr(self.engine, "overwritten_grads"))
         self._opt_stream = torch.cuda.Stream(device=self.flat.device) if self._early_ok else None
+        self._early_done = []
+        # ... and the token table's update (256M elements at cfg5) beside the grouped weight gradients
+        self._early_token = self._early_ok and os.environ.get("RS_EARLY_TOKEN_ADAM", "0") != "0"
 
     # ---------------------------------------------------------------- pieces
     def _divisor(self, local_count):
@@ -267,10 +279,12 @@ class FusedTrainStep:
         if not self._early_ok:
             return self._compute_impl(*batch, split=split)
         self.engine.after_head_grads = self._early_head_update
+        self.engine.after_token_grads = self._early_token_update if self._early_token else None
         try:
             return self._compute_impl(*batch, split=split)
         finally:
             self.engine.after_head_grads = None
+            self.engine.after_token_grads = None
 
     def _compute_impl(self, *batch, split=None):
         """Forward + loss + backward into the flat gradient.  split(tag): called by the engine when the bucket
@@ -363,7 +377,8 @@ class FusedTrainStep:
                 assert tr is None and kp == self._early_kp, (kp, self._early_kp)
                 torch.cuda.current_stream().wait_event(self._early_ev)
                 self._early_ev = None
-                self.opt.step_rest(kp, seed_base=sb)
+                done, self._early_done = self._early_done, []
+                self.opt.step_rest(kp, seed_base=sb, done=done)
             else:
                 self._l2(self.loss_out[2:3])
                 self.opt.step(seed_base=sb, transposed=tr, keep=kp)
@@ -373,6 +388,27 @@ class FusedTrainStep:
     # 7,130, 512: 6,889 / 6,858, 1,024: 6,801 / 6,695 (1,024 took the CUs from the encoder's first backward GEMM)
     EARLY_HEAD_ADAM_WG = int(os.environ.get("RS_EARLY_HEAD_ADAM_WG", "256"))
 
+    def _early_token_update(self, name):
+        """Engine hook (BERTEngine: right after the token table's gradient, before the grouped weight gradients): that
+        range's update follows the early head update on the side stream (same prepared scalars, gradient cleared),
+        beside the grouped weight-gradient launch; step_rest skips it."""
+        if self._early_ev is None:
+            return
+        f = self.flat
+        lo = f.offsets[name]
+        hi = min(lo + -(-f.view(name).numel() // 4) * 4, f.numel)
+        kp = self._early_kp
+        if not (hi <= kp[0] or lo >= kp[1]) or lo % 4:
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream())
+        self._opt_stream.wait_event(ev)
+        with torch.cuda.stream(self._opt_stream):
+            self.opt.step_range(lo, hi, zero_grad=True, max_wg=self.EARLY_HEAD_ADAM_WG)
+            self._early_ev = torch.cuda.Event()
+            self._early_ev.record(self._opt_stream)
+        self._early_done.append((lo, hi))
+
     def _early_head_update(self):
         """Engine hook (BERTEngine: right after the head's dE / dh): fork the out.weight / out.bias update onto the
         optimizer's side stream; _update joins it."""
@@ -380,6 +416,7 @@ class FusedTrainStep:
         if kp is None:
             return
         self._early_kp = kp
+        self._early_done = []
         cur = torch.cuda.current_stream()
         ev = torch.cuda.Event()
         ev.record(cur)

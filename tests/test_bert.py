@@ -300,7 +300,8 @@ def test_bert_large_vocab_overwritten_head_grads_match_zeroed():
 def test_bert_early_head_adam_equals_end_of_step(graph, monkeypatch):
     """The out.weight / out.bias update forked onto a side stream right after the head's dE / dh (beside the encoder's
     backward; FusedTrainStep._early_head_update, RS_EARLY_HEAD_ADAM) gives the same bits as the update at the end of
-    the step: three steps, eager and graph-replayed (two steps unrolled per replay)."""
+    the step -- and the token table's update forked after its gradient, beside the grouped weight gradients
+    (RS_EARLY_TOKEN_ADAM): three steps, eager and graph-replayed (two steps unrolled per replay)."""
     import rbm_amd.data as synth
     from rbm_amd.train_step import FusedTrainStep
     V, T, B = 70000, 40, 8
@@ -310,6 +311,7 @@ def test_bert_early_head_adam_equals_end_of_step(graph, monkeypatch):
     res = []
     for early in ("1", "0"):
         monkeypatch.setenv("RS_EARLY_HEAD_ADAM", early)
+        monkeypatch.setenv("RS_EARLY_TOKEN_ADAM", early)
         torch.manual_seed(0)
         m = _bert(V, T, 256, 1, 2, 0.1, "bf16", seed=12)
         tr = FusedTrainStep(m, lr=1e-3, max_labelled=128)
