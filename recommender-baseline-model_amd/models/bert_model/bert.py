@@ -390,11 +390,18 @@ class BERTEngine:
         accumulates into it -- a head variant that accumulated would double-count the previous step's gradient
         (tests/test_bert.py ...overwritten_head_grads_match_zeroed, tests/test_dp_gpu.py
         ...unzeroed_head_grads_equal_zeroed under the in-place all-reduce)."""
+        if self.V1 * self.d < (1 << 24):
+            return None
+        return self.head_grad_range()
+
+    def head_grad_range(self):
+        """(lo, hi) flat range of out.weight then out.bias (their gradient is final once the head's dE / dh are
+        formed), or None when the layout does not make it one 16-B aligned range (or the head is sharded)."""
         f = self.flat
         ow, ob = f.offsets["out.weight"], f.offsets["out.bias"]
         A = ALIGN   # FlatParams pads every parameter to a multiple of ALIGN floats
         end = ob + -(-self.V1 // A) * A
-        if getattr(self, "vocab_shard", None) is not None or self.V1 * self.d < (1 << 24):
+        if getattr(self, "vocab_shard", None) is not None:
             return None
         if ob != ow + -(-self.V1 * self.d // A) * A or end > f.numel or ow % 4 or end % 4:
             return None

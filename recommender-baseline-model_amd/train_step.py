@@ -77,7 +77,7 @@ class FusedAdam:
                               self.hyper, zero_grad=zg)
 
 
-    def step_keep_early(self, keep, max_wg=None):
+    def step_keep_early(self, keep, max_wg=None, zero_grad=False):
         """The first part of a step whose `keep` range is final before the rest of the backward (BERT's out.weight /
         out.bias, after the head's dE / dh): rs_adam_prepare (t += 1 and the step's scalars; no seed advance -- the
         backward still draws this step's dropout masks) and that range's update, gradient left in place.
@@ -87,7 +87,7 @@ class FusedAdam:
         ops.adam_prepare(self.state, self.hyper)
         bf = f.bf16[lo:hi] if f.bf16 is not None else None
         ops.adam_step(f.data[lo:hi], f.grad[lo:hi], self.m[lo:hi], self.v[lo:hi], bf, self.state, self.hyper,
-                      zero_grad=False, max_wg=max_wg)
+                      zero_grad=zero_grad, max_wg=max_wg)
 
     def step_range(self, lo, hi, zero_grad=True, max_wg=None):
         """rs_adam_step over [lo, hi) with the step's scalars already prepared (a step_keep_early step)."""
@@ -225,8 +225,12 @@ class FusedTrainStep:
                           and hasattr(self.engine, "overwritten_grads"))
         self._opt_stream = torch.cuda.Stream(device=self.flat.device) if self._early_ok else None
         self._early_done = []
-        # ... and the token table's update (256M elements at cfg5) beside the grouped weight gradients
-        self._early_token = self._early_ok and os.environ.get("RS_EARLY_TOKEN_ADAM", "0") != "0"
+        # ... also below the unzeroed-head vocabulary size (cfg3's 27k classes: 6.8M elements) -- measured slower there
+        # (with the token table's early update: 44.2-44.4k -> 43.6-43.7k seq/s, three interleaved rounds), so off
+        self._early_small = os.environ.get("RS_EARLY_HEAD_ADAM_SMALL", "0") != "0"
+        # ... and the token table's update (256M elements at cfg5) beside the grouped weight gradients: cfg5
+        # 7,140 / 7,043 / 7,051 -> 7,144 / 7,167 / 7,195 seq/s (three interleaved rounds)
+        self._early_token = self._early_ok and os.environ.get("RS_EARLY_TOKEN_ADAM", "1") != "0"
 
     # ---------------------------------------------------------------- pieces
     def _divisor(self, local_count):
@@ -374,11 +378,11 @@ class FusedTrainStep:
                 else:   # the loss division rides in the optimizer's launch
                     self.opt.step(grad_divisor=cnt, seed_base=sb, transposed=tr, loss=(lsum, self.loss_val), keep=kp)
             elif self._early_ev is not None:
-                assert tr is None and kp == self._early_kp, (kp, self._early_kp)
+                assert tr is None and kp in (None, self._early_kp), (kp, self._early_kp)
                 torch.cuda.current_stream().wait_event(self._early_ev)
                 self._early_ev = None
                 done, self._early_done = self._early_done, []
-                self.opt.step_rest(kp, seed_base=sb, done=done)
+                self.opt.step_rest(self._early_kp, seed_base=sb, done=done)
             else:
                 self._l2(self.loss_out[2:3])
                 self.opt.step(seed_base=sb, transposed=tr, keep=kp)
@@ -412,17 +416,22 @@ class FusedTrainStep:
     def _early_head_update(self):
         """Engine hook (BERTEngine: right after the head's dE / dh): fork the out.weight / out.bias update onto the
         optimizer's side stream; _update joins it."""
-        kp = self.engine.overwritten_grads()
-        if kp is None:
+        rng = self.engine.head_grad_range()
+        if rng is None:
             return
-        self._early_kp = kp
+        # the unzeroed-gradient contract (overwritten_grads) only at large vocabularies: elsewhere the early update
+        # clears the range's gradient like the rest of the buffer
+        keep = self.engine.overwritten_grads() is not None
+        if not keep and not self._early_small:
+            return
+        self._early_kp = rng
         self._early_done = []
         cur = torch.cuda.current_stream()
         ev = torch.cuda.Event()
         ev.record(cur)
         self._opt_stream.wait_event(ev)
         with torch.cuda.stream(self._opt_stream):
-            self.opt.step_keep_early(self._early_kp, max_wg=self.EARLY_HEAD_ADAM_WG)
+            self.opt.step_keep_early(rng, max_wg=self.EARLY_HEAD_ADAM_WG, zero_grad=not keep)
             self._early_ev = torch.cuda.Event()
             self._early_ev.record(self._opt_stream)
 
