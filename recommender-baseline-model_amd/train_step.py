@@ -77,7 +77,7 @@ class FusedAdam:
                               self.hyper, zero_grad=zg)
 
 
-    def step_keep_early(self, keep, max_wg=None, zero_grad=False):
+    def step_keep_early(self, keep, max_wg=None, zero_grad=False, prep_event=None):
         """The first part of a step whose `keep` range is final before the rest of the backward (BERT's out.weight /
         out.bias, after the head's dE / dh): rs_adam_prepare (t += 1 and the step's scalars; no seed advance -- the
         backward still draws this step's dropout masks) and that range's update, gradient left in place.
@@ -85,6 +85,8 @@ class FusedAdam:
         lo, hi = keep
         f = self.flat
         ops.adam_prepare(self.state, self.hyper)
+        if prep_event is not None:
+            prep_event.record(torch.cuda.current_stream())
         bf = f.bf16[lo:hi] if f.bf16 is not None else None
         ops.adam_step(f.data[lo:hi], f.grad[lo:hi], self.m[lo:hi], self.v[lo:hi], bf, self.state, self.hyper,
                       zero_grad=zero_grad, max_wg=max_wg)
@@ -392,6 +394,9 @@ class FusedTrainStep:
     # 7,130, 512: 6,889 / 6,858, 1,024: 6,801 / 6,695 (1,024 took the CUs from the encoder's first backward GEMM)
     EARLY_HEAD_ADAM_WG = int(os.environ.get("RS_EARLY_HEAD_ADAM_WG", "256"))
 
+    EARLY_TOKEN_ADAM_WG = int(os.environ.get("RS_EARLY_TOKEN_ADAM_WG", "256"))
+    EARLY_TOKEN_ON_MAIN = os.environ.get("RS_EARLY_TOKEN_MAIN", "0") != "0"
+
     def _early_token_update(self, name):
         """Engine hook (BERTEngine: right after the token table's gradient, before the grouped weight gradients): that
         range's update follows the early head update on the side stream (same prepared scalars, gradient cleared),
@@ -404,13 +409,19 @@ class FusedTrainStep:
         kp = self._early_kp
         if not (hi <= kp[0] or lo >= kp[1]) or lo % 4:
             return
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream())
-        self._opt_stream.wait_event(ev)
-        with torch.cuda.stream(self._opt_stream):
-            self.opt.step_range(lo, hi, zero_grad=True, max_wg=self.EARLY_HEAD_ADAM_WG)
-            self._early_ev = torch.cuda.Event()
-            self._early_ev.record(self._opt_stream)
+        if self.EARLY_TOKEN_ON_MAIN:
+            # on the step's own stream, full grid: beside the head update still streaming on the side stream (the
+            # scalars it reads were prepared there first: join that prepare)
+            torch.cuda.current_stream().wait_event(self._early_prep_ev)
+            self.opt.step_range(lo, hi, zero_grad=True, max_wg=self.EARLY_TOKEN_ADAM_WG)
+        else:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream())
+            self._opt_stream.wait_event(ev)
+            with torch.cuda.stream(self._opt_stream):
+                self.opt.step_range(lo, hi, zero_grad=True, max_wg=self.EARLY_TOKEN_ADAM_WG)
+                self._early_ev = torch.cuda.Event()
+                self._early_ev.record(self._opt_stream)
         self._early_done.append((lo, hi))
 
     def _early_head_update(self):
@@ -426,12 +437,14 @@ class FusedTrainStep:
             return
         self._early_kp = rng
         self._early_done = []
+        self._early_prep_ev = torch.cuda.Event()
         cur = torch.cuda.current_stream()
         ev = torch.cuda.Event()
         ev.record(cur)
         self._opt_stream.wait_event(ev)
         with torch.cuda.stream(self._opt_stream):
-            self.opt.step_keep_early(rng, max_wg=self.EARLY_HEAD_ADAM_WG, zero_grad=not keep)
+            self.opt.step_keep_early(rng, max_wg=self.EARLY_HEAD_ADAM_WG, zero_grad=not keep,
+                                     prep_event=self._early_prep_ev)
             self._early_ev = torch.cuda.Event()
             self._early_ev.record(self._opt_stream)
 

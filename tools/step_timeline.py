@@ -12,8 +12,13 @@ def is_opt(r):
 
 
 # a step ends with its optimizer group (one launch, or several when ranges are updated separately -- e.g. the
-# unzeroed out.weight range at a large vocabulary): the LAST launch of each consecutive group delimits steps
-ad = [i for i, r in enumerate(rows) if is_opt(r) and (i + 1 == len(rows) or not is_opt(rows[i + 1]))]
+# unzeroed out.weight range at a large vocabulary): the LAST launch of each consecutive group delimits steps.  A step
+# whose optimizer updates some ranges early on a side stream (BERT at 1M items: out.weight beside the encoder
+# backward) ends with rs_seed_advance instead: when that kernel is in the trace it delimits the steps.
+if any("seed_advance" in r["Kernel_Name"] for r in rows):
+    ad = [i for i, r in enumerate(rows) if "seed_advance" in r["Kernel_Name"]]
+else:
+    ad = [i for i, r in enumerate(rows) if is_opt(r) and (i + 1 == len(rows) or not is_opt(rows[i + 1]))]
 # steps of the timed graph replays only: bench.py's event-timed leg runs eager steps with timing events and a
 # torch spin kernel around the dominant launch after the timed ones -- skip every step holding a non-HIP-graph kernel
 # of that kind (torch's spin / elementwise kernels)
