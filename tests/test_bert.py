@@ -332,3 +332,29 @@ def test_bert_early_head_adam_equals_end_of_step(graph, V, monkeypatch):
     assert res[0][0] == res[1][0]
     for a, b in zip(res[0][1:], res[1][1:]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+def test_bert_split_wgrad_equals_one_launch(monkeypatch):
+    """The upper blocks' grouped weight gradients on a side stream beside the lower blocks' backward
+    (RS_BERT_WGRAD_SPLIT) use the same row splits as the single grouped launch: the same bits, over two
+    graph-replayed steps of a 4-block model."""
+    import rbm_amd.data as synth
+    from rbm_amd.train_step import FusedTrainStep
+    V, T, B = 3000, 40, 8
+    rng = np.random.default_rng(6)
+    batches = [tuple(torch.from_numpy(t).cuda() for t in synth.bert_batch(rng, B, T, V, mask_prob=0.2))
+               for _ in range(3)]
+    res = []
+    for split in ("1", "0"):
+        monkeypatch.setenv("RS_BERT_WGRAD_SPLIT", split)
+        torch.manual_seed(0)
+        m = _bert(V, T, 256, 4, 4, 0.1, "bf16", seed=13)
+        tr = FusedTrainStep(m, lr=1e-3, max_labelled=128)
+        tr.engine.seed_base.fill_(55)
+        tr.capture(*batches[0], warmup=1)
+        losses = [float(tr.replay(*b).item()) for b in batches[1:]]
+        torch.cuda.synchronize()
+        res.append((losses, tr.flat.data.clone()))
+    assert res[0][0] == res[1][0]
+    assert torch.equal(res[0][1], res[1][1])
