@@ -250,7 +250,8 @@ int rs_adam_prepare(double* state, const double* hyper, const float* grad_diviso
 int rs_adam_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16,
                  const double* state, const double* hyper, int zero_grad, void* stream);
 /* rs_adam_step on at most max_wg workgroups (grid-stride; same results bit for bit): a range updated on a side
- * stream beside other kernels (BERT's out.weight during the encoder backward) takes a bounded share of the CUs. */
+ * stream beside other kernels (BERT's out.weight during the encoder backward) takes a bounded share of the CUs.
+ * Replaces the same torch.optim.Adam step (BS/trainers/base.py:225-228) over that range. */
 int rs_adam_step_wg(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, const double* state,
                     const double* hyper, int zero_grad, int max_wg, void* stream);
 int rs_adam_prepare_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, double* state,
