@@ -279,10 +279,10 @@ class FusedTrainStep:
         self.exchange = dpx.BucketedExchange(self.flat.grad, dpx.carve(self._buckets(), lo, lo + rows * d), self.pg,
                                              partial=True)
 
-    def _compute(self, *batch, split=None):
-        # the early out.weight update hook is live only inside this trainer's own steps (the engine may also be
-        # driven directly, with no optimizer step to join it)
-        if not self._early_ok:
+    def _compute(self, *batch, split=None, update=False):
+        # the early optimizer hooks are live only inside this trainer's own steps, whose _update joins them
+        # (update=True); a bare forward + backward (tests reading the gradient, the engine driven directly) runs none
+        if not (self._early_ok and update):
             return self._compute_impl(*batch, split=split)
         self.engine.after_head_grads = self._early_head_update
         self.engine.after_token_grads = self._early_token_update if self._early_token else None
@@ -453,11 +453,11 @@ class FusedTrainStep:
         """batch: SAS (seq, pos, neg) / BERT (tokens, labels) int64 device tensors.  Returns the
         device loss (the global batch's mean loss, as the reference's calculate_loss)."""
         if self.overlap:
-            self._compute(*batch, split=self._eager_split)
+            self._compute(*batch, split=self._eager_split, update=True)
             self.exchange.launch("final")
             self.exchange.finish()
         else:
-            self._compute(*batch)
+            self._compute(*batch, update=True)
             self._exchange()
         self._update()
         return self.loss_val if self.dp else self.loss_out[2:3]
@@ -579,7 +579,7 @@ class FusedTrainStep:
         if S > 1:
             self._capture_graphs(self._unrolled(lambda k: self.static_steps[k]), stamps, unrolled=True)
         else:
-            self._capture_graphs(lambda split=None: self._compute(*self.static, split=split), stamps)
+            self._capture_graphs(lambda split=None: self._compute(*self.static, split=split, update=True), stamps)
         return self
 
     def _unroll_check(self, steps_per_graph):
@@ -609,7 +609,7 @@ class FusedTrainStep:
                     self.loss_val = self.loss_rows[k, 2:3]    # DP: the global mean loss lands in the step's row
                     if sample is not None:
                         sample()
-                    self._compute(*inputs(k), split=self._inline_split())
+                    self._compute(*inputs(k), split=self._inline_split(), update=True)
                     self._graph_exchange()
                     self._update()
             finally:
@@ -827,7 +827,7 @@ class FusedTrainStep:
 
         def compute(split=None):
             sampler.sample_into(*self.static)
-            self._compute(*self.static, split=split)
+            self._compute(*self.static, split=split, update=True)
         self._capture_graphs(compute, stamps)
         return self
 
