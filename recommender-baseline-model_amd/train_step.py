@@ -381,10 +381,19 @@ class FusedTrainStep:
                     self.opt.step(grad_divisor=cnt, seed_base=sb, transposed=tr, loss=(lsum, self.loss_val), keep=kp)
             elif self._early_ev is not None:
                 assert tr is None and kp in (None, self._early_kp), (kp, self._early_kp)
-                torch.cuda.current_stream().wait_event(self._early_ev)
-                self._early_ev = None
+                cur = torch.cuda.current_stream()
                 done, self._early_done = self._early_done, []
-                self.opt.step_rest(self._early_kp, seed_base=sb, done=done)
+                if self.REST_BEFORE_JOIN:
+                    # the remaining ranges (the token table: 256M elements at cfg5) on this stream with the full
+                    # grid, beside the tail of the out.weight update, which is joined only before the seed advance
+                    cur.wait_event(self._early_prep_ev)
+                    self.opt.step_rest(self._early_kp, seed_base=None, done=done)
+                    cur.wait_event(self._early_ev)
+                    ops.seed_advance(sb)
+                else:
+                    cur.wait_event(self._early_ev)
+                    self.opt.step_rest(self._early_kp, seed_base=sb, done=done)
+                self._early_ev = None
             else:
                 self._l2(self.loss_out[2:3])
                 self.opt.step(seed_base=sb, transposed=tr, keep=kp)
@@ -395,6 +404,7 @@ class FusedTrainStep:
     EARLY_HEAD_ADAM_WG = int(os.environ.get("RS_EARLY_HEAD_ADAM_WG", "256"))
 
     EARLY_TOKEN_ADAM_WG = int(os.environ.get("RS_EARLY_TOKEN_ADAM_WG", "256"))
+    REST_BEFORE_JOIN = os.environ.get("RS_ADAM_REST_BEFORE_JOIN", "0") != "0"
     EARLY_TOKEN_ON_MAIN = os.environ.get("RS_EARLY_TOKEN_MAIN", "0") != "0"
 
     def _early_token_update(self, name):
