@@ -537,6 +537,9 @@ class BERTEngine:
         if getattr(self, "vocab_shard", None) is not None:
             return self._sharded_head_and_backward(s, xL, hl, lab, idx, rank, cnt, labels, cap, loss_out, grad, split)
         ops.gather_rows(xL, idx, cnt, cap, hl, labels, lab)
+        hook = getattr(self, "before_head", None)
+        if hook is not None:
+            hook()                      # out.weight / out.bias are read from here on
         if self.dt == torch.bfloat16 and ops.vocab_head_supported(d):
             # vocabulary-tile-stationary kernels (vocab_head.hip): logits never materialised
             wce = self.ws.get("vce", (ops.vocab_ce_ws_numel(cap, self.V1),), torch.float32)

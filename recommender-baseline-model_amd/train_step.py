@@ -227,6 +227,7 @@ class FusedTrainStep:
                           and hasattr(self.engine, "overwritten_grads"))
         self._opt_stream = torch.cuda.Stream(device=self.flat.device) if self._early_ok else None
         self._early_done = []
+        self._pending_head_ev = None
         # ... also below the unzeroed-head vocabulary size (cfg3's 27k classes: 6.8M elements) -- measured slower there
         # (with the token table's early update: 44.2-44.4k -> 43.6-43.7k seq/s, three interleaved rounds), so off
         self._early_small = os.environ.get("RS_EARLY_HEAD_ADAM_SMALL", "0") != "0"
@@ -286,11 +287,20 @@ class FusedTrainStep:
             return self._compute_impl(*batch, split=split)
         self.engine.after_head_grads = self._early_head_update
         self.engine.after_token_grads = self._early_token_update if self._early_token else None
+        self.engine.before_head = self._before_head
         try:
             return self._compute_impl(*batch, split=split)
         finally:
             self.engine.after_head_grads = None
             self.engine.after_token_grads = None
+            self.engine.before_head = None
+
+    def _before_head(self):
+        """Engine hook (BERTEngine: right before the head reads out.weight): join the previous unrolled step's
+        out.weight update when its join was deferred (_update(defer=True))."""
+        if self._pending_head_ev is not None:
+            torch.cuda.current_stream().wait_event(self._pending_head_ev)
+            self._pending_head_ev = None
 
     def _compute_impl(self, *batch, split=None):
         """Forward + loss + backward into the flat gradient.  split(tag): called by the engine when the bucket
@@ -362,7 +372,10 @@ class FusedTrainStep:
         if self.l2:
             ops.l2_penalty(self.flat.data, self.flat.grad, self.l2_desc, self.l2, self.l2_ws, loss=loss, scale=scale)
 
-    def _update(self):
+    def _update(self, defer=False):
+        """defer (an unrolled step that is not the graph's last, RS_DEFER_HEAD_JOIN): the early out.weight update is
+        joined by the NEXT step right before its head (_before_head), so its tail runs beside that step's encoder
+        forward instead of ending this step."""
         sb = self.engine.seed_base
         if self.vshard is not None:
             # the sharded head normalised by the global count already; the loss is the global batch's
@@ -383,12 +396,16 @@ class FusedTrainStep:
                 assert tr is None and kp in (None, self._early_kp), (kp, self._early_kp)
                 cur = torch.cuda.current_stream()
                 done, self._early_done = self._early_done, []
-                if self.REST_BEFORE_JOIN:
+                if self.REST_BEFORE_JOIN or defer:
                     # the remaining ranges (the token table: 256M elements at cfg5) on this stream with the full
                     # grid, beside the tail of the out.weight update, which is joined only before the seed advance
+                    # (or, deferred, before the next step's head)
                     cur.wait_event(self._early_prep_ev)
                     self.opt.step_rest(self._early_kp, seed_base=None, done=done)
-                    cur.wait_event(self._early_ev)
+                    if defer:
+                        self._pending_head_ev = self._early_ev
+                    else:
+                        cur.wait_event(self._early_ev)
                     ops.seed_advance(sb)
                 else:
                     cur.wait_event(self._early_ev)
@@ -405,6 +422,7 @@ class FusedTrainStep:
 
     EARLY_TOKEN_ADAM_WG = int(os.environ.get("RS_EARLY_TOKEN_ADAM_WG", "256"))
     REST_BEFORE_JOIN = os.environ.get("RS_ADAM_REST_BEFORE_JOIN", "0") != "0"
+    DEFER_HEAD_JOIN = os.environ.get("RS_DEFER_HEAD_JOIN", "0") != "0"
     EARLY_TOKEN_ON_MAIN = os.environ.get("RS_EARLY_TOKEN_MAIN", "0") != "0"
 
     def _early_token_update(self, name):
@@ -621,7 +639,7 @@ class FusedTrainStep:
                         sample()
                     self._compute(*inputs(k), split=self._inline_split(), update=True)
                     self._graph_exchange()
-                    self._update()
+                    self._update(defer=self.DEFER_HEAD_JOIN and k + 1 < self.steps_per_graph)
             finally:
                 self.loss_out, self.loss_val = base, base_val
         return compute
