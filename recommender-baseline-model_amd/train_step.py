@@ -233,7 +233,9 @@ class FusedTrainStep:
         self._early_small = os.environ.get("RS_EARLY_HEAD_ADAM_SMALL", "0") != "0"
         # ... and the token table's update (256M elements at cfg5) beside the grouped weight gradients: cfg5
         # 7,140 / 7,043 / 7,051 -> 7,144 / 7,167 / 7,195 seq/s (three interleaved rounds)
-        self._early_token = self._early_ok and os.environ.get("RS_EARLY_TOKEN_ADAM", "1") != "0"
+        # (not with a deferred head join: the next step's embedding reads the token table before its head)
+        self._early_token = (self._early_ok and os.environ.get("RS_EARLY_TOKEN_ADAM", "1") != "0"
+                             and not self.DEFER_HEAD_JOIN)
 
     # ---------------------------------------------------------------- pieces
     def _divisor(self, local_count):
