@@ -362,6 +362,10 @@ int rs_wall_clock_khz(int* khz);
 
 /* *seed_base += 1 on the stream (advances every dropout mask; capturable). */
 int rs_seed_advance(uint64_t* seed_base, void* stream);
+/* Upload an instantiated step graph (hipGraphExec_t) to the device ahead of its first launch (hipGraphUpload):
+ * graph preparation, no step runs.  Infrastructure of the captured training step (BS/trainers/base.py:114-123's
+ * loop body replayed as one graph), not a reference op. */
+int rs_graph_upload(void* graph_exec, void* stream);
 
 /* ---- fused SAS sublayers (bf16, d in {64, 128}; rowchain.hip) ----------------------------
  * One workgroup per CU stages the block's weights in LDS once, each wave carries 16 tokens

@@ -473,6 +473,11 @@ __global__ void seed_advance_kernel(uint64_t* s) {
   if (threadIdx.x == 0) *s += 1;
 }
 
+int rs_graph_upload(void* graph_exec, void* stream) {
+  if (!graph_exec) return RS_ERR_ARG;
+  return (int)hipGraphUpload((hipGraphExec_t)graph_exec, (hipStream_t)stream);
+}
+
 int rs_seed_advance(uint64_t* seed_base, void* stream) {
   hipLaunchKernelGGL(seed_advance_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, seed_base);
   return (int)hipGetLastError();

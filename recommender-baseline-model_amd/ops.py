@@ -459,6 +459,11 @@ def vocab_ce_bwd(h, E, bias, labels, ws, count, dl, rows_dev=None, dloss=None):
          ptr(count), ptr(dloss), ptr(ws), ptr(dl), ld(dl), stream())
 
 
+def graph_upload(graph):
+    """hipGraphUpload of a captured torch.cuda.CUDAGraph's executable (rs_graph_upload) on the current stream."""
+    call("rs_graph_upload", C.c_void_p(int(graph.raw_cuda_graph_exec())), stream())
+
+
 def seed_advance(seed_base):
     call("rs_seed_advance", ptr(seed_base), stream())
 

@@ -688,10 +688,16 @@ class FusedTrainStep:
         gc_on = gc.isenabled()
         gc.disable()
         try:
-            return self._capture_graphs_impl(compute, stamps, unrolled)
+            r = self._capture_graphs_impl(compute, stamps, unrolled)
         finally:
             if gc_on:
                 gc.enable()
+        if os.environ.get("RS_GRAPH_UPLOAD", "0") != "0":
+            # the executables go to the device now, not at their first replay (hipGraphUpload)
+            for g in self.graphs or ():
+                ops.graph_upload(g)
+            torch.cuda.synchronize()
+        return r
 
     def _capture_graphs_impl(self, compute, stamps=None, unrolled=False):
         self._stamps = stamps
