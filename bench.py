@@ -71,7 +71,7 @@ def parse():
                          "multi-process path with several ranks on one GPU)")
     ap.add_argument("--steps-per-graph", default="auto",
                     help="training steps unrolled into one graph replay (single GPU; 'auto' = the largest of "
-                         "10/8/5/4/2 dividing --steps, else 1); every step still runs on its own batch with its own "
+                         "20/10/8/5/4/2 dividing --steps, else 1); every step still runs on its own batch with its own "
                          "Adam update; warmup steps beyond a multiple of it run as eager steps")
     ap.add_argument("--roofline-replays", type=int, default=20,
                     help="eager training steps after the timed ones with HIP timing events around the dominant "
@@ -353,11 +353,12 @@ def main():
     stamps = None if sbuf is None else (sbuf, (dominant(cfg),))
 
     if args.steps_per_graph == "auto":
-        # the largest of 10 / 8 / 5 / 4 / 2 steps per replay that divides the timed count (a replay boundary costs
-        # ~25 us); the warmup need not be a multiple: its remainder runs as eager steps (below)
+        # the largest of 20 / 10 / 8 / 5 / 4 / 2 steps per replay that divides the timed count (a replay boundary costs
+        # ~25 us; the driver's 20 timed steps at cfg2: 20 per replay 422.9-430.4k against 10 per replay
+        # 418.2-426.2k seq/s, four interleaved rounds); the warmup need not be a multiple: its remainder runs as eager steps (below)
         # (data parallel: when the trainer captures its all-reduce inside the step graph -- SAS)
         unroll = (world == 1 or trainer.graph_collectives) and not args.no_graph
-        S = next((u for u in (10, 8, 5, 4, 2) if args.steps % u == 0), 1) if unroll else 1
+        S = next((u for u in (20, 10, 8, 5, 4, 2) if args.steps % u == 0), 1) if unroll else 1
     else:
         S = int(args.steps_per_graph)
         if S > 1 and ((world > 1 and not trainer.graph_collectives) or args.no_graph or args.steps % S):
