@@ -281,16 +281,18 @@ __device__ __forceinline__ float masked(const AttnLdsArgs& a, const float* km, i
   return apply_mask(mask_state(a, km, q, key), s);
 }
 
-// (sequence-head, split) of this workgroup.  Workgroups are dealt to the 8 XCDs round-robin in
-// dispatch order; the nsplit workgroups of one sequence stage the same K/V (or Q/dO) rows, so they
-// are given dispatch slots on ONE XCD and the second staging reads hit that XCD's L2.
+// (sequence-head, split) of this workgroup.  Workgroups are dealt to the 8 XCDs round-robin in dispatch order
+// (block b on XCC b % 8, fixed: tools/micro/xcd_probe.hip), so XCD x takes the x-th eighth of the sequence-heads
+// -- the rows the row-chain kernels give the same XCD (rowchain.hip tiles_of_wave) -- and the nsplit workgroups of
+// one sequence, which stage the same K/V (or Q/dO) rows, land on one XCD too.  The q/k/v the block-input kernel
+// just wrote and the o (dO) this launch writes for the block-output kernel then stay in one XCD's L2.
 // lin: the workgroup's linear index among the launch's workgroups of this pass (split fastest)
 __device__ __forceinline__ void block_coords(const AttnLdsArgs& a, int64_t lin, int64_t& bh, int& split) {
   const int ns = a.nsplit;
   const int64_t BH = a.B * a.H;
-  if (ns > 1 && BH % 8 == 0) {
+  if (BH % 8 == 0) {
     const int64_t xcd = lin & 7, slot = lin >> 3;
-    bh = (slot / ns) * 8 + xcd;
+    bh = xcd * (BH >> 3) + slot / ns;
     split = (int)(slot % ns);
   } else {
     bh = lin / ns;

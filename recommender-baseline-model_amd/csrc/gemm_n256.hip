@@ -12,12 +12,8 @@
 //
 //  * a 256 x 256 output tile (the whole N) per 8-wave workgroup: A streams from HBM exactly once; each wave owns a
 //    128 x 64 quadrant (8 x 4 accumulator tiles of mfma_f32_16x16x32_bf16: 3 fragment reads per 8 MFMAs);
-//  * 64-deep k stages, register-staged into two padded LDS images (one barrier per stage; the next stage's 16-B
-//    global loads are in flight under the current stage's 64 MFMAs per wave), k-major operands read with
-//    ds_read_b64_tr_b16 (the transposing LDS read);
-//  * interior tiles and full stages take unconditional loads through per-thread pointers; the last (partial)
-//    k stage and the last (partial) row tile take checked loads in separately instantiated code, so the main
-//    loop's loads never serialise behind a per-chunk branch;
+//  * 32-deep k stages loaded by LDS-DMA into four stage buffers, three in flight (below); k-major operands read
+//    with ds_read_b64_tr_b16 (the transposing LDS read);
 //  * dh's split-K workgroups are dealt so that the row tiles of one vocabulary slice share an XCD (its L2 holds
 //    the slice of E they all read);
 //  * the epilogue stages the fp32 tile through LDS in two 128-row halves and stores 1 KB rows.
@@ -29,18 +25,6 @@ namespace g256 {
 constexpr int BM = 256, BN = 256, BKT = 64, NTH = 512;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf4;
 
-template <bool KMAJ, int ROWS>
-struct Img {
-  // k-contiguous: [ROWS][BKT + 8];  k-major: [BKT][ROWS + 8]   (bf16 elements)
-  static constexpr int LD = KMAJ ? ROWS + 8 : BKT + 8;
-  static constexpr int ELEMS = (KMAJ ? BKT : ROWS) * LD;
-  static constexpr int GR = KMAJ ? BKT : ROWS;            // global rows per stage
-  static constexpr int CPR = (KMAJ ? ROWS : BKT) / 8;     // 16-B chunks per global row
-  static constexpr int NCH = GR * CPR;
-  static constexpr int PER_T = NCH / NTH;
-  static_assert(NCH % NTH == 0, "whole chunks per thread");
-};
-
 struct Args {
   int64_t M, K;                   // N = 256
   const __bf16* A; int64_t lda;   // A(m, k) = A[k*lda + m] (a_kmajor) or A[m*lda + k]
@@ -51,228 +35,8 @@ struct Args {
   const int* rows_dev;            // a_kmajor: bound on K; else bound on M (nullable)
 };
 
-// one operand's register stage: PER_T 16-B chunks per thread
-template <bool KMAJ, int ROWS>
-struct Stage {
-  using I = Img<KMAJ, ROWS>;
-  bf16x8 r[I::PER_T];
-  const __bf16* p;   // chunk 0's source; chunk i is I::GR / PER_T rows further (a wave-uniform offset)
-  int64_t step, ioff;
-  // interior: the thread's chunk pointer at the first stage; (r0, c0) = storage-orientation origin
-  __device__ __forceinline__ void init(const __bf16* base, int64_t ld, int64_t r0, int64_t c0, int tid) {
-    static_assert(NTH % I::CPR == 0, "chunk i of a thread = chunk 0 + NTH / CPR rows");
-    p = base + (r0 + tid / I::CPR) * ld + c0 + (tid % I::CPR) * 8;
-    ioff = (int64_t)(NTH / I::CPR) * ld;
-    step = KMAJ ? (int64_t)BKT * ld : (int64_t)BKT;
-  }
-  __device__ __forceinline__ void load_next() {
-#pragma unroll
-    for (int i = 0; i < I::PER_T; ++i) r[i] = *reinterpret_cast<const bf16x8*>(p + i * ioff);
-    p += step;
-  }
-  // checked: zero outside rows < rlim, cols < clim (storage orientation)
-  __device__ __forceinline__ void load_checked(const __bf16* base, int64_t ld, int64_t r0, int64_t c0, int64_t rlim,
-                                               int64_t clim, int tid) {
-#pragma unroll
-    for (int i = 0; i < I::PER_T; ++i) {
-      const int ch = tid + i * NTH;
-      const int64_t gr = r0 + ch / I::CPR, gc = c0 + (ch % I::CPR) * 8;
-      if (gr < rlim && gc + 8 <= clim) {
-        r[i] = *reinterpret_cast<const bf16x8*>(base + gr * ld + gc);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) r[i][j] = (gr < rlim && gc + j < clim) ? base[gr * ld + gc + j] : (__bf16)0.0f;
-      }
-    }
-  }
-  __device__ __forceinline__ void store(__bf16* img, int tid) const {
-#pragma unroll
-    for (int i = 0; i < I::PER_T; ++i) {
-      const int ch = tid + i * NTH;
-      *reinterpret_cast<bf16x8*>(img + (ch / I::CPR) * I::LD + (ch % I::CPR) * 8) = r[i];
-    }
-  }
-};
-
-// fragment of operand rows [row0, row0 + 16) for the 32-deep sub-step s of the stage image (MFMA operand map of
-// common.h: lane l holds row l&15, k = 8(l>>4) + j)
-template <bool KMAJ, int ROWS>
-__device__ __forceinline__ bf16x8 frag(const __bf16* img, int row0, int s, int lane) {
-  using I = Img<KMAJ, ROWS>;
-  const int g = lane >> 4, li = lane & 15;
-  if (!KMAJ) return *reinterpret_cast<const bf16x8*>(img + (row0 + li) * I::LD + 32 * s + 8 * g);
-  const int q = li >> 2, p = li & 3;
-  const __bf16* a0 = img + (32 * s + 8 * g + q) * I::LD + row0 + 4 * p;
-  const bf4 x = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf4*)a0);
-  const bf4 y = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf4*)(a0 + 4 * I::LD));
-  return __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7);
-}
-
-template <bool AK>
-__global__ __launch_bounds__(NTH) void gemm_n256_kernel(Args a) {
-  using IA = Img<AK, BM>;
-  using IB = Img<true, BN>;
-  constexpr int STAGE = IA::ELEMS + IB::ELEMS;
-  constexpr int LDC = BN + 4;
-  constexpr int LDS_BYTES = 2 * STAGE * 2 > (BM / 2) * LDC * 4 ? 2 * STAGE * 2 : (BM / 2) * LDC * 4;
-  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
-  __bf16* stage0 = reinterpret_cast<__bf16*>(smem);
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;      // 2 x 4 waves: quadrant rows wm*128, columns wn*64
-  constexpr int FM = 8, FN = 4;
-
-  // tiles: x = row tile, z = k split, dealt so that consecutive linear ids (one XCD) walk the row tiles of one
-  // split (they share that split's B rows); bijective over any workgroup count
-  const int64_t Mb = (!AK && a.rows_dev) ? min(a.M, (int64_t)*a.rows_dev) : a.M;
-  const int64_t Kb = (AK && a.rows_dev) ? min(a.K, (int64_t)*a.rows_dev) : a.K;
-  const unsigned tiles_m = (unsigned)((a.M + BM - 1) / BM);
-  unsigned tm, z;
-  {
-    const unsigned tot = gridDim.x, L = blockIdx.x, q = tot >> 3, r = tot & 7, x = L & 7;
-    const unsigned lg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (L >> 3);
-    z = lg / tiles_m;
-    tm = lg - z * tiles_m;
-  }
-  const int64_t m0 = (int64_t)tm * BM;
-  if (m0 >= Mb) return;                          // whole workgroup: a row tile past the device row count
-  const int64_t kbeg = (int64_t)z * a.k_per_split;
-  const int64_t kend = min(Kb, kbeg + a.k_per_split);
-  const int nk = kend > kbeg ? (int)((kend - kbeg + BKT - 1) / BKT) : 0;
-  const bool tail_partial = ((kend - kbeg) % BKT) != 0;
-
-  f32x4 acc[FM][FN], accb[2];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  accb[0] = accb[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  bf16x8 ones;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
-  const bool do_colsum = AK && a.colsum != nullptr;
-
-  Stage<AK, BM> sa;
-  Stage<true, BN> sb;
-  auto compute = [&](int kt) {
-    const __bf16* cur = stage0 + (kt & 1) * STAGE;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 fa[FM], fb[FN];
-#pragma unroll
-      for (int i = 0; i < FM; ++i) fa[i] = frag<AK, BM>(cur, wm * 128 + 16 * i, s, lane);
-#pragma unroll
-      for (int j = 0; j < FN; ++j) fb[j] = frag<true, BN>(cur + IA::ELEMS, wn * 64 + 16 * j, s, lane);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-      if (do_colsum) {   // the quadrant's m fragments 2wn, 2wn+1 (every row's sum formed once per row half);
-                         // compile-time fragment indices behind a wave-uniform test (a runtime index into fa[]
-                         // would send the fragments through scratch)
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-          if ((i >> 1) == wn) accb[i & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], ones, accb[i & 1], 0, 0, 0);
-      }
-    }
-  };
-  auto store_stage = [&](int kt) {
-    __bf16* nxt = stage0 + (kt & 1) * STAGE;
-    sa.store(nxt, tid);
-    sb.store(nxt + IA::ELEMS, tid);
-  };
-  // checked load of stage kt (A rows/cols bounded by the tile's valid m and the split's k end)
-  auto load_checked = [&](int kt) {
-    const int64_t k0 = kbeg + (int64_t)kt * BKT;
-    if (AK) sa.load_checked(a.A, a.lda, k0, m0, kend, a.M, tid);
-    else sa.load_checked(a.A, a.lda, m0, k0, a.M, kend, tid);
-    sb.load_checked(a.B, a.ldb, k0, 0, kend, BN, tid);
-  };
-  auto kloop = [&](auto edge_tag) {
-    constexpr bool EDGE = decltype(edge_tag)::value;   // partial row tile: every stage checked
-    if (!EDGE) {
-      if (AK) sa.init(a.A, a.lda, kbeg, m0, tid);
-      else sa.init(a.A, a.lda, m0, kbeg, tid);
-      sb.init(a.B, a.ldb, kbeg, 0, tid);
-    }
-    auto issue = [&](int kt, bool last) {
-      if (EDGE || (last && tail_partial)) load_checked(kt);
-      else {
-        sa.load_next();
-        sb.load_next();
-      }
-    };
-    issue(0, nk == 1);
-    store_stage(0);
-    __syncthreads();
-    int kt = 0;
-    // stages 1 .. nk-2 are whole: unconditional loads in flight under the MFMAs
-    for (; kt + 2 < nk; ++kt) {
-      if (EDGE) load_checked(kt + 1);
-      else {
-        sa.load_next();
-        sb.load_next();
-      }
-      compute(kt);
-      store_stage(kt + 1);
-      __syncthreads();
-    }
-    if (kt + 1 < nk) {       // the last stage (possibly partial)
-      issue(kt + 1, true);
-      compute(kt);
-      store_stage(kt + 1);
-      __syncthreads();
-      ++kt;
-    }
-    compute(kt);
-  };
-  if (nk > 0) {
-    if (m0 + BM <= a.M) kloop(std::integral_constant<bool, false>{});
-    else kloop(std::integral_constant<bool, true>{});
-  }
-
-  // ---- epilogue: two 128-row halves through LDS, 1 KB row stores
-  float* Cs = reinterpret_cast<float*>(smem);
-  float* Cz = a.C + (int64_t)z * a.cz;
-  const int g = lane >> 4, cl = lane & 15;
-  if (do_colsum && cl == 0) {
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t m = m0 + wm * 128 + 16 * (2 * wn + t) + 4 * g + r;
-        if (m < a.M) a.colsum[m] = accb[t][r];
-      }
-  }
-  constexpr int TPR = BN / 8, RPP = NTH / TPR;   // 32 threads per row, 16 rows per pass
-  const int c8 = (tid % TPR) * 8;
-#pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    __syncthreads();
-    if (wm == half) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) Cs[(16 * i + 4 * g + r) * LDC + wn * 64 + 16 * j + cl] = acc[i][j][r];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int row = tid / TPR; row < BM / 2; row += RPP) {
-      const int64_t m = m0 + half * 128 + row;
-      if (m >= a.M) break;
-      const float4 v0 = *reinterpret_cast<const float4*>(Cs + row * LDC + c8);
-      const float4 v1 = *reinterpret_cast<const float4*>(Cs + row * LDC + c8 + 4);
-      float* dst = Cz + m * a.ldc + c8;
-      *reinterpret_cast<float4*>(dst) = v0;
-      *reinterpret_cast<float4*>(dst + 4) = v1;
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------------------------------------------
-// LDS-DMA form (the default): 32-deep stages loaded by global_load_lds_dwordx4 straight into FOUR LDS stage buffers,
+// 32-deep stages loaded by global_load_lds_dwordx4 straight into FOUR LDS stage buffers,
 // three stages in flight -- no staging registers, and the HBM latency (~1-2 us under load) hidden behind three
 // stages of MFMAs (~0.4 us each) instead of one.  A DMA writes 1 KB lane-linear, so the images are unpadded and the
 // bank-conflict-free layouts are applied to the SOURCE address:
@@ -535,13 +299,8 @@ int rs_gemm_n256(int a_kmajor, int64_t M, int64_t K, const void* A, int64_t lda,
   }
   const dim3 grid((unsigned)(((M + g256::BM - 1) / g256::BM) * splits)), blk(g256::NTH);
   hipStream_t s = (hipStream_t)stream;
-#ifndef G256_REGSTAGE
   if (a_kmajor) hipLaunchKernelGGL(g256::gemm_n256_dma_kernel<true>, grid, blk, 0, s, a);
   else hipLaunchKernelGGL(g256::gemm_n256_dma_kernel<false>, grid, blk, 0, s, a);
-#else
-  if (a_kmajor) hipLaunchKernelGGL(g256::gemm_n256_kernel<true>, grid, blk, 0, s, a);
-  else hipLaunchKernelGGL(g256::gemm_n256_kernel<false>, grid, blk, 0, s, a);
-#endif
   return (int)hipGetLastError();
 }
 

@@ -9,9 +9,9 @@
 //
 //  * one workgroup per CU (NW = 8 waves) stages the block's three d x d weight matrices ONCE
 //    into LDS (110 KB at d = 128), then every wave runs its own 16-token chain with no
-//    workgroup barrier: 16-row tiles are dealt round robin over all workgroups
-//    (tile = b + G*(w + NW*k)), so at cfg2 (1,600 tiles) every CU gets 6-7 of them instead of
-//    one or two 64-row tiles (400 tiles on 256 CUs);
+//    workgroup barrier: 16-row tiles are dealt round robin over the workgroups of each XCD, each
+//    XCD taking one eighth of the rows (tiles_of_wave), so at cfg2 (1,600 tiles) every CU gets 6-7
+//    of them instead of one or two 64-row tiles (400 tiles on 256 CUs);
 //  * the activations never leave registers: every GEMM is computed TRANSPOSED,
 //    Y^T = W . X^T, with the weight as the MFMA A operand (LDS) and the 16 tokens as the B
 //    operand, so the accumulator (lane (g, cl) holds feature 16j + 4g + r of token cl) packed
@@ -260,6 +260,25 @@ __device__ __forceinline__ void ln_partials(const float* red, float* part, int t
 }
 
 __device__ __forceinline__ int64_t n_tiles(int64_t M) { return (M + TR - 1) / TR; }
+
+// The tiles of one wave: first, first + step, ... < end.  XCD-contiguous dealing: workgroup w runs on XCD w % 8
+// (blocks are dealt round-robin over the 8 XCDs: measured fixed, block b on XCC b % 8, tools/micro/xcd_probe.hip),
+// so XCD x takes the x-th eighth of the tiles -- the rows of sequences [x B / 8, (x + 1) B / 8) when 128 divides
+// M -- which is the sequence range the attention kernels give the same XCD (attention_lds.hip block_coords).  A
+// tensor one of them writes is then read by the other from that XCD's L2 (a 64 KB burst per workgroup right after
+// its producer: 1.24 us XCD-local against 2.6 us from another XCD, xcd_probe).  Placement is for speed only: every
+// tile has exactly one owner whatever the placement.
+struct TileRange {
+  int64_t first, step, end;
+};
+__device__ __forceinline__ TileRange tiles_of_wave(int64_t nt, int wave) {
+  const int64_t G = gridDim.x, w = blockIdx.x;
+  if (G >= 8 && G % 8 == 0) {
+    const int64_t x = w & 7, Gx = G >> 3;
+    return TileRange{x * nt / 8 + (w >> 3) + Gx * wave, Gx * NW, (x + 1) * nt / 8};
+  }
+  return TileRange{w + G * wave, G * NW, nt};
+}
 
 // ------------------------------------------------------------------ LDS layout
 // NM weight images, then NV fp32 vectors of D, then NR LayerNorm partial blocks red[NW][2][D]
@@ -567,8 +586,8 @@ __global__ __launch_bounds__(NT) void block_in_kernel(InArgs a) {
   const float* lv = reinterpret_cast<const float*>(smem + L::W);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
             cl = lane & 15;
-  const int64_t G = gridDim.x, nt = n_tiles(a.M);
-  int64_t t = blockIdx.x + G * wave;
+  const TileRange tr = tiles_of_wave(n_tiles(a.M), wave);
+  int64_t t = tr.first;
   const bool emb = a.e.etab != nullptr;
   const uint32_t es32 = emb && a.e.drop_p > 0.f ? seed32(eff_seed(a.e.salt, a.e.seed_base)) : 0u;
   int cnt = 0;
@@ -585,7 +604,7 @@ __global__ __launch_bounds__(NT) void block_in_kernel(InArgs a) {
     store_raw<D>(a.e.xout, D, T.m, T.ok, xr, g);
   };
   Raw<D> xr;
-  if (t < nt) load_x(xr, tile_of(t, a.M, cl));
+  if (t < tr.end) load_x(xr, tile_of(t, a.M, cl));
   {
     const bf16* const W[3] = {a.Wq, a.Wkv, a.Wkv + (int64_t)D * D};
     const int64_t ldw[3] = {D, D, D};
@@ -594,10 +613,10 @@ __global__ __launch_bounds__(NT) void block_in_kernel(InArgs a) {
     stage_v<D, 5>(reinterpret_cast<float*>(smem + L::W), V, tid);
   }
   __syncthreads();
-  for (; t < nt; t += G * NW) {
+  for (; t < tr.end; t += tr.step) {
     asm volatile("" ::: "memory");   // no hoisting of the loop-invariant weight fragment reads
     const Tile T = tile_of(t, a.M, cl);
-    if (t != blockIdx.x + G * wave) load_x(xr, T);
+    if (t != tr.first) load_x(xr, T);
     fwd_in_q<D>(xr, T, wslot(smem, 0, WB), lv, a.eps, a.Q, a.mean, a.rstd, a.q, lane);
     fwd_in_kv<D>(xr, T, wslot(smem, 1, WB), wslot(smem, 2, WB), lv, a.kv, lane);
   }
@@ -711,11 +730,11 @@ __global__ __launch_bounds__(NT) void block_out_kernel(OutArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
             cl = lane & 15;
   RCPROF(0);
-  const int64_t G = gridDim.x, nt = n_tiles(a.M);
+  const TileRange tr = tiles_of_wave(n_tiles(a.M), wave);
   const OutFwd of = out_fwd_of(a);
-  int64_t t = blockIdx.x + G * wave;
+  int64_t t = tr.first;
   Raw<D> orr, Qr;
-  if (t < nt) {
+  if (t < tr.end) {
     const int64_t mc = tile_of(t, a.M, cl).mc;
     load_raw<D>(orr, a.o, D, mc, g);
     load_raw<D>(Qr, a.Q, D, mc, g);
@@ -750,10 +769,10 @@ __global__ __launch_bounds__(NT) void block_out_kernel(OutArgs a) {
     hscale = 1.f / (a.h.divisor ? *a.h.divisor : c);
   }
   RCPROF(1);
-  for (; t < nt; t += G * NW) {
+  for (; t < tr.end; t += tr.step) {
     asm volatile("" ::: "memory");
     const Tile T = tile_of(t, a.M, cl);
-    if (t != blockIdx.x + G * wave) {
+    if (t != tr.first) {
       load_raw<D>(orr, a.o, D, T.mc, g);
       load_raw<D>(Qr, a.Q, D, T.mc, g);
     }
@@ -819,11 +838,11 @@ __global__ __launch_bounds__(NT) void block_out_bwd_kernel(OutBwdArgs a) {
   float* red = reinterpret_cast<float*>(smem + L::V);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
             cl = lane & 15;
-  const int64_t G = gridDim.x, nt = n_tiles(a.M);
+  const TileRange tr = tiles_of_wave(n_tiles(a.M), wave);
   const OutBwd ob = out_bwd_of(a);
-  int64_t t = blockIdx.x + G * wave;
+  int64_t t = tr.first;
   Raw<D> dr, hr;
-  if (t < nt) {
+  if (t < tr.end) {
     const int64_t mc = tile_of(t, a.M, cl).mc;
     load_raw<D>(dr, a.dxn, D, mc, g);
     load_raw<D>(hr, a.h1, D, mc, g);
@@ -837,10 +856,10 @@ __global__ __launch_bounds__(NT) void block_out_bwd_kernel(OutBwdArgs a) {
   }
   ln_zero(red, D, lane, wave);
   __syncthreads();
-  for (; t < nt; t += G * NW) {
+  for (; t < tr.end; t += tr.step) {
     asm volatile("" ::: "memory");
     const Tile T = tile_of(t, a.M, cl);
-    if (t != blockIdx.x + G * wave) {
+    if (t != tr.first) {
       load_raw<D>(dr, a.dxn, D, T.mc, g);
       load_raw<D>(hr, a.h1, D, T.mc, g);
     }
@@ -873,10 +892,10 @@ __global__ __launch_bounds__(NT) void block_in_bwd_kernel(InBwdArgs a) {
   float* red = reinterpret_cast<float*>(smem + L::V);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
             cl = lane & 15;
-  const int64_t G = gridDim.x, nt = n_tiles(a.M);
-  int64_t t = blockIdx.x + G * wave;
+  const TileRange tr = tiles_of_wave(n_tiles(a.M), wave);
+  int64_t t = tr.first;
   Raw<D> kr, vr;
-  if (t < nt) {
+  if (t < tr.end) {
     const int64_t mc = tile_of(t, a.M, cl).mc;
     load_raw<D>(kr, a.dkv, 2 * D, mc, g);
     load_raw<D>(vr, a.dkv + D, 2 * D, mc, g);
@@ -890,10 +909,10 @@ __global__ __launch_bounds__(NT) void block_in_bwd_kernel(InBwdArgs a) {
   }
   ln_zero(red, D, lane, wave);
   __syncthreads();
-  for (; t < nt; t += G * NW) {
+  for (; t < tr.end; t += tr.step) {
     asm volatile("" ::: "memory");
     const Tile T = tile_of(t, a.M, cl);
-    if (t != blockIdx.x + G * wave) {
+    if (t != tr.first) {
       load_raw<D>(kr, a.dkv, 2 * D, T.mc, g);
       load_raw<D>(vr, a.dkv + D, 2 * D, T.mc, g);
     }

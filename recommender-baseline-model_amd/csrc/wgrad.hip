@@ -219,131 +219,10 @@ __global__ __launch_bounds__(256, 2) void wgrad_group_kernel(Args a) {
   group_tile<T>(a, blockIdx.x, gridDim.x, smem);
 }
 
-// LDS-DMA form of a 128 x 128 (split, tile) -- the default for T = 128 (RS_WGRAD_DMA=0: the register ring above).
-// Both operands are k-major ([rows m][columns]): 32-row stages of dY[:, n0:n0+128] and X[:, c0:c0+128] go by
-// global_load_lds_dwordx4 into four LDS stage buffers in the 8-row x 32-column subtile layout of gemm_dma.h (read by
-// ds_read_b64_tr_b16), three stages in flight per wave, one raw barrier per stage; the row range's last partial
-// stage is zeroed in LDS past its end.  Each 32-row stage is one MFMA step in row order, as the ring's two 32-deep
-// sub-steps per 64-row stage: the same bits (tests/test_wgrad_gpu.py).
-__global__ __launch_bounds__(256, 2) void wgrad_group_dma_kernel(Args a) {
-  KStampBegin stamp_(a.ks);
-  using namespace gbf::dma;
-  constexpr int IMG = 32 * 128 * 2, DSTAGE = 2 * IMG, PPS = 4;   // per wave per stage: 2 pieces of each image
-  constexpr int FM = 4, FN = 4;
-  __shared__ __attribute__((aligned(1024))) char smem[NBUF * DSTAGE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), wm = wave >> 1,
-            wn = wave & 1;
-  unsigned bid = blockIdx.x;
-  {
-    const unsigned nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, x = bid & 7;
-    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
-  }
-  const int t = (int)(bid % (unsigned)a.ntiles);
-  const int s = (int)(bid / (unsigned)a.ntiles);
-  int pi = 0;
-#pragma unroll 1
-  for (int q = 1; q < a.nprob; ++q)
-    if (t >= a.p[q].tile0) pi = q;
-  const Prob& P = a.p[pi];
-  const int lt = t - P.tile0;
-  const int tn = lt / P.tiles_k, tk = lt - tn * P.tiles_k;
-  const int64_t n0 = (int64_t)tn * 128, c0 = (int64_t)tk * 128;
-  const int64_t kbeg = (int64_t)s * a.rows_per_split;
-  const int64_t kend = min(a.M, kbeg + a.rows_per_split);
-  const int nk = kend > kbeg ? (int)((kend - kbeg + DBK - 1) / DBK) : 0;
-  const bool do_colsum = tk == 0 && wn == 0;
-  const uint32_t lds0 = lds_u32(smem);
-
-  f32x4 acc[FM][FN], accb[FM];
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    accb[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  }
-  bf16x8 ones;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
-
-  // stage st's pieces of both images; rows past kend read row kend - 1 (zeroed in LDS before use)
-  auto issue = [&](int st) {
-    const uint32_t buf = lds0 + (uint32_t)((st % NBUF) * DSTAGE);
-    const int64_t r0 = kbeg + (int64_t)st * DBK;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int pc = 2 * wave + j, b = 1024 * pc + 16 * lane;
-      const int r = 8 * (b >> 11) + ((b >> 6) & 7);
-      const int ch = 4 * ((b >> 9) & 3) + (((b >> 4) & 3) ^ ((r >> 2) & 3));
-      const int64_t row = min(r0 + r, kend - 1);
-      dma16(P.dY + row * P.lddy + n0 + 8 * ch, __builtin_amdgcn_readfirstlane(buf + (uint32_t)pc * 1024));
-      dma16(P.X + row * P.ldx + c0 + 8 * ch, __builtin_amdgcn_readfirstlane(buf + IMG + (uint32_t)pc * 1024));
-    }
-  };
-  auto zero_tail = [&](int st) {
-    char* buf = smem + (st % NBUF) * DSTAGE;
-    const int kv = (int)(kend - (kbeg + (int64_t)st * DBK));   // valid rows of this stage, 1..31
-    for (int e = tid; e < (DBK - kv) * 128; e += 256) {
-      const int r = kv + e / 128, c = e % 128;
-      *reinterpret_cast<bf16*>(buf + km_off(r, c)) = (bf16)0.0f;
-      *reinterpret_cast<bf16*>(buf + IMG + km_off(r, c)) = (bf16)0.0f;
-    }
-  };
-  auto compute = [&](int st) {
-    const char* buf = smem + (st % NBUF) * DSTAGE;
-    bf16x8 fa[FM], fb[FN];
-#pragma unroll
-    for (int i = 0; i < FM; ++i) fa[i] = km_frag(buf, wm * 64 + 16 * i, lane);
-#pragma unroll
-    for (int j = 0; j < FN; ++j) fb[j] = km_frag(buf + IMG, wn * 64 + 16 * j, lane);
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-    if (do_colsum) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], ones, accb[i], 0, 0, 0);
-    }
-  };
-  const bool tail = ((kend - kbeg) % DBK) != 0;
-  for (int st = 0; st < min(nk, DIST); ++st) issue(st);
-  for (int st = 0; st < nk; ++st) {
-    const int after = min(nk - 1, st + DIST - 1) - st;
-    if (after >= 2) vm_wait<2 * PPS>();
-    else if (after == 1) vm_wait<PPS>();
-    else vm_wait<0>();
-    raw_barrier();
-    if (st + DIST < nk) issue(st + DIST);
-    if (tail && st == nk - 1) {
-      zero_tail(st);
-      raw_barrier();
-    }
-    compute(st);
-  }
-  vm_wait<0>();
-
-  float* S = a.slab + P.slab_off + (int64_t)s * ((int64_t)P.N * P.K + P.N);
-  const int g = lane >> 4, cl = lane & 15;
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t n = n0 + wm * 64 + 16 * i + 4 * g + r;
-#pragma unroll
-      for (int j = 0; j < FN; ++j) S[n * P.K + c0 + wn * 64 + 16 * j + cl] = acc[i][j][r];
-      if (do_colsum && cl == 0) S[(int64_t)P.N * P.K + n] = accb[i][r];
-    }
-}
-
-inline bool dma_enabled() {
-  const char* e = getenv("RS_WGRAD_DMA");
-  return e ? atoi(e) != 0 : false;   // default off: measured no faster (cfg2 31.9 -> 36.8 us, cfg3 175 -> 176 us)
-}
-
 // the grouped launch (T = output tile edge)
 inline void launch_group(const Args& a, int T, hipStream_t s) {
   const dim3 grid((unsigned)(a.ntiles * a.splits));
-  if (T == 128 && dma_enabled()) hipLaunchKernelGGL(wgrad_group_dma_kernel, grid, dim3(256), 0, s, a);
-  else if (T == 128) hipLaunchKernelGGL(wgrad_group_kernel<128>, grid, dim3(256), 0, s, a);
+  if (T == 128) hipLaunchKernelGGL(wgrad_group_kernel<128>, grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(wgrad_group_kernel<64>, grid, dim3(256), 0, s, a);
 }
 

@@ -287,12 +287,6 @@ class BERTEngine:
                 ops.linear_wgrad(dY, X, dW, slab, db=db)
 
         pending = None
-        # the upper half's weight gradients on a side stream once those blocks' backward is done, beside the lower
-        # blocks' backward (RS_BERT_WGRAD_SPLIT=1; the rest in the main grouped launch at the end).  Measured at
-        # cfg3 (three interleaved rounds): 44.5 / 44.2 / 44.5k -> 44.4 / 44.1 / 44.3k seq/s -- the lower blocks'
-        # latency-bound kernels lose as much to the co-running launch as it takes off the tail; off by default
-        split_at = L // 2 if (grouped and L >= 2 and os.environ.get("RS_BERT_WGRAD_SPLIT", "0") != "0") else None
-        early = None
         for i in reversed(range(L)):
             a = s["blocks"][i]
             pre = f"bert.transformer_blocks.{i}."
@@ -358,12 +352,6 @@ class BERTEngine:
                 ln_bwd(a["x"], dh, pre + "input_sublayer.norm.a_2", pre + "input_sublayer.norm.b_2", a["mu1"],
                        a["r1"], dx2, f"{i}i")
             dx = dx2
-            if split_at is not None and i == split_at:
-                # rows per split as for the whole set of blocks (same partials, same bits as one launch)
-                tl = sum(-(-p[0].shape[1] // 128) * -(-p[1].shape[1] // 128) for p in probs) // (L - split_at)
-                wrows = self._wgrad_rows(M, tl * L)
-                early = self._wgrad_side(probs, M, wrows)
-                probs = []
         if self._det_table():
             # token-table gradient by inverted index (rs_item_grad: sorted keys, per-row sums, no float
             # atomics -- deterministic); the index comes from the side stream when the step issued it
@@ -389,12 +377,9 @@ class BERTEngine:
         for c in range(0, len(probs), 16):              # rs_wgrad_grouped takes up to 16 problems
             chunk = probs[c:c + 16]
             shapes = [(p[0].shape[1], p[1].shape[1]) for p in chunk]
-            rows = wrows if early is not None else \
-                self._wgrad_rows(M, sum(-(-n // 128) * -(-k // 128) for n, k in shapes))
+            rows = self._wgrad_rows(M, sum(-(-n // 128) * -(-k // 128) for n, k in shapes))
             wslab = self.ws.get(f"wslab{c}", (ops.wgrad_grouped_slab_numel(shapes, M, rows),), torch.float32)
             ops.wgrad_grouped(chunk, M, rows, wslab, extra=ln_segs if c == 0 else ())
-        if early is not None:
-            torch.cuda.current_stream().wait_event(early[0])   # (early[1] kept the operands alive until here)
 
     def overwritten_grads(self):
         """(lo, hi) flat range whose gradient the fused step writes whole every step (out.weight then out.bias,
@@ -443,23 +428,6 @@ class BERTEngine:
             ev = torch.cuda.Event()
             ev.record(self._side)
         return ev, iws
-
-    def _wgrad_side(self, probs, M, rows):
-        """Grouped weight-gradient launch(es) of `probs` on the side stream, forked here: (done event, operands)."""
-        if getattr(self, "_wg_stream", None) is None:
-            self._wg_stream = torch.cuda.Stream(device=self.dev)
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream())
-        self._wg_stream.wait_event(ev)
-        with torch.cuda.stream(self._wg_stream):
-            for c in range(0, len(probs), 16):
-                chunk = probs[c:c + 16]
-                shapes = [(p[0].shape[1], p[1].shape[1]) for p in chunk]
-                wslab = self.ws.get(f"wslab_side{c}", (ops.wgrad_grouped_slab_numel(shapes, M, rows),), torch.float32)
-                ops.wgrad_grouped(chunk, M, rows, wslab)
-            done = torch.cuda.Event()
-            done.record(self._wg_stream)
-        return done, list(probs)
 
     @staticmethod
     def _wgrad_rows(M, tiles):

@@ -227,15 +227,11 @@ class FusedTrainStep:
                           and hasattr(self.engine, "overwritten_grads"))
         self._opt_stream = torch.cuda.Stream(device=self.flat.device) if self._early_ok else None
         self._early_done = []
-        self._pending_head_ev = None
-        # ... also below the unzeroed-head vocabulary size (cfg3's 27k classes: 6.8M elements) -- measured slower there
-        # (with the token table's early update: 44.2-44.4k -> 43.6-43.7k seq/s, three interleaved rounds), so off
-        self._early_small = os.environ.get("RS_EARLY_HEAD_ADAM_SMALL", "0") != "0"
+        # (below the unzeroed-head vocabulary size -- cfg3's 27k classes -- the early update measured slower: 44.2-44.4k
+        # -> 43.6-43.7k seq/s, three interleaved rounds; it runs only with the overwritten-gradient head)
         # ... and the token table's update (256M elements at cfg5) beside the grouped weight gradients: cfg5
         # 7,140 / 7,043 / 7,051 -> 7,144 / 7,167 / 7,195 seq/s (three interleaved rounds)
-        # (not with a deferred head join: the next step's embedding reads the token table before its head)
-        self._early_token = (self._early_ok and os.environ.get("RS_EARLY_TOKEN_ADAM", "1") != "0"
-                             and not self.DEFER_HEAD_JOIN)
+        self._early_token = self._early_ok and os.environ.get("RS_EARLY_TOKEN_ADAM", "1") != "0"
 
     # ---------------------------------------------------------------- pieces
     def _divisor(self, local_count):
@@ -289,20 +285,19 @@ class FusedTrainStep:
             return self._compute_impl(*batch, split=split)
         self.engine.after_head_grads = self._early_head_update
         self.engine.after_token_grads = self._early_token_update if self._early_token else None
-        self.engine.before_head = self._before_head
+        done = False
         try:
-            return self._compute_impl(*batch, split=split)
+            out = self._compute_impl(*batch, split=split)
+            done = True
+            return out
         finally:
             self.engine.after_head_grads = None
             self.engine.after_token_grads = None
-            self.engine.before_head = None
-
-    def _before_head(self):
-        """Engine hook (BERTEngine: right before the head reads out.weight): join the previous unrolled step's
-        out.weight update when its join was deferred (_update(defer=True))."""
-        if self._pending_head_ev is not None:
-            torch.cuda.current_stream().wait_event(self._pending_head_ev)
-            self._pending_head_ev = None
+            if not done:
+                # an aborted compute (e.g. a capture failing after the fork) must not leave a forked update for the
+                # next step's _update to join
+                self._early_ev = None
+                self._early_done = []
 
     def _compute_impl(self, *batch, split=None):
         """Forward + loss + backward into the flat gradient.  split(tag): called by the engine when the bucket
@@ -374,10 +369,7 @@ class FusedTrainStep:
         if self.l2:
             ops.l2_penalty(self.flat.data, self.flat.grad, self.l2_desc, self.l2, self.l2_ws, loss=loss, scale=scale)
 
-    def _update(self, defer=False):
-        """defer (an unrolled step that is not the graph's last, RS_DEFER_HEAD_JOIN): the early out.weight update is
-        joined by the NEXT step right before its head (_before_head), so its tail runs beside that step's encoder
-        forward instead of ending this step."""
+    def _update(self):
         sb = self.engine.seed_base
         if self.vshard is not None:
             # the sharded head normalised by the global count already; the loss is the global batch's
@@ -398,20 +390,8 @@ class FusedTrainStep:
                 assert tr is None and kp in (None, self._early_kp), (kp, self._early_kp)
                 cur = torch.cuda.current_stream()
                 done, self._early_done = self._early_done, []
-                if self.REST_BEFORE_JOIN or defer:
-                    # the remaining ranges (the token table: 256M elements at cfg5) on this stream with the full
-                    # grid, beside the tail of the out.weight update, which is joined only before the seed advance
-                    # (or, deferred, before the next step's head)
-                    cur.wait_event(self._early_prep_ev)
-                    self.opt.step_rest(self._early_kp, seed_base=None, done=done)
-                    if defer:
-                        self._pending_head_ev = self._early_ev
-                    else:
-                        cur.wait_event(self._early_ev)
-                    ops.seed_advance(sb)
-                else:
-                    cur.wait_event(self._early_ev)
-                    self.opt.step_rest(self._early_kp, seed_base=sb, done=done)
+                cur.wait_event(self._early_ev)
+                self.opt.step_rest(self._early_kp, seed_base=sb, done=done)
                 self._early_ev = None
             else:
                 self._l2(self.loss_out[2:3])
@@ -423,9 +403,6 @@ class FusedTrainStep:
     EARLY_HEAD_ADAM_WG = int(os.environ.get("RS_EARLY_HEAD_ADAM_WG", "256"))
 
     EARLY_TOKEN_ADAM_WG = int(os.environ.get("RS_EARLY_TOKEN_ADAM_WG", "256"))
-    REST_BEFORE_JOIN = os.environ.get("RS_ADAM_REST_BEFORE_JOIN", "0") != "0"
-    DEFER_HEAD_JOIN = os.environ.get("RS_DEFER_HEAD_JOIN", "0") != "0"
-    EARLY_TOKEN_ON_MAIN = os.environ.get("RS_EARLY_TOKEN_MAIN", "0") != "0"
 
     def _early_token_update(self, name):
         """Engine hook (BERTEngine: right after the token table's gradient, before the grouped weight gradients): that
@@ -439,19 +416,13 @@ class FusedTrainStep:
         kp = self._early_kp
         if not (hi <= kp[0] or lo >= kp[1]) or lo % 4:
             return
-        if self.EARLY_TOKEN_ON_MAIN:
-            # on the step's own stream, full grid: beside the head update still streaming on the side stream (the
-            # scalars it reads were prepared there first: join that prepare)
-            torch.cuda.current_stream().wait_event(self._early_prep_ev)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream())
+        self._opt_stream.wait_event(ev)
+        with torch.cuda.stream(self._opt_stream):
             self.opt.step_range(lo, hi, zero_grad=True, max_wg=self.EARLY_TOKEN_ADAM_WG)
-        else:
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream())
-            self._opt_stream.wait_event(ev)
-            with torch.cuda.stream(self._opt_stream):
-                self.opt.step_range(lo, hi, zero_grad=True, max_wg=self.EARLY_TOKEN_ADAM_WG)
-                self._early_ev = torch.cuda.Event()
-                self._early_ev.record(self._opt_stream)
+            self._early_ev = torch.cuda.Event()
+            self._early_ev.record(self._opt_stream)
         self._early_done.append((lo, hi))
 
     def _early_head_update(self):
@@ -462,19 +433,16 @@ class FusedTrainStep:
             return
         # the unzeroed-gradient contract (overwritten_grads) only at large vocabularies: elsewhere the early update
         # clears the range's gradient like the rest of the buffer
-        keep = self.engine.overwritten_grads() is not None
-        if not keep and not self._early_small:
+        if self.engine.overwritten_grads() is None:
             return
         self._early_kp = rng
         self._early_done = []
-        self._early_prep_ev = torch.cuda.Event()
         cur = torch.cuda.current_stream()
         ev = torch.cuda.Event()
         ev.record(cur)
         self._opt_stream.wait_event(ev)
         with torch.cuda.stream(self._opt_stream):
-            self.opt.step_keep_early(rng, max_wg=self.EARLY_HEAD_ADAM_WG, zero_grad=not keep,
-                                     prep_event=self._early_prep_ev)
+            self.opt.step_keep_early(rng, max_wg=self.EARLY_HEAD_ADAM_WG)
             self._early_ev = torch.cuda.Event()
             self._early_ev.record(self._opt_stream)
 
@@ -641,7 +609,7 @@ class FusedTrainStep:
                         sample()
                     self._compute(*inputs(k), split=self._inline_split(), update=True)
                     self._graph_exchange()
-                    self._update(defer=self.DEFER_HEAD_JOIN and k + 1 < self.steps_per_graph)
+                    self._update()
             finally:
                 self.loss_out, self.loss_val = base, base_val
         return compute
