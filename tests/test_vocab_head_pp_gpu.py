@@ -109,3 +109,79 @@ def test_vocab_head_pp_bwd_matches_lockstep_and_fp32(R, V1, d, live):
     tol = 2.0 ** -7 * ref.abs() + 1e-6 / float(cnt)
     assert bool(((d_pp[:live] - ref).abs() <= tol).all()), float((d_pp[:live] - ref).abs().max())
     assert bool(((d_pp[:live] - d_ls[:live]).abs() <= tol).all())
+
+
+def test_vocab_head_cfg5_vocabulary_full_path_matches_fp64():
+    """The whole bf16 vocabulary head at the cfg5 vocabulary (1,000,001 classes, d = 256) with 1,100 labelled rows --
+    35 of the ping-pong kernels' 32-row tiles (34 full + a partial one), rows with label 0 among them: the forward
+    (loss sum, count, per-row log-sum-exp), dlogits, dE = dlogits^T h with db (rs_gemm_n256, k-major), dh = dlogits
+    E (rs_gemm_n256 split over the vocabulary + rs_splitk_scatter_rows), against a float64 torch restatement of the
+    reference's CE over the full vocabulary (BS/models/bert.py:10,16, BS/trainers/bert.py:36-40), formed in 64k-class
+    chunks."""
+    import rbm_amd  # noqa: F401
+    from rbm_amd import ops
+    R, V1, d = 1100, 1_000_001, 256
+    g = torch.Generator(device="cuda").manual_seed(1100)
+    h = torch.randn(R, d, device="cuda", generator=g).bfloat16()
+    E = (0.06 * torch.randn(V1, d, device="cuda", generator=g)).bfloat16()
+    bias = 0.3 * torch.randn(V1, device="cuda", generator=g)
+    lab = torch.randint(1, V1, (R,), device="cuda", generator=g)
+    lab[::9] = 0
+    rows_dev = torch.tensor([R], dtype=torch.int32, device="cuda")
+    ws = torch.empty(ops.vocab_ce_ws_numel(R, V1), device="cuda")
+    out = torch.zeros(4, device="cuda")
+    ops.vocab_head_fwd(h, E, bias, lab, ws, out, rows_dev=rows_dev)
+    cnt = out[1:2].clone()
+    V1p = -(-V1 // 8) * 8
+    dl = torch.empty((R, V1p), device="cuda", dtype=torch.bfloat16)[:, :V1]
+    ops.vocab_head_bwd(h, E, bias, lab, ws, cnt, dl, rows_dev=rows_dev)
+    dE = torch.empty(V1, d, device="cuda")
+    db = torch.empty(V1, device="cuda")
+    ops.gemm_n256(dl, h, dE, True, V1, R, colsum=db, rows_dev=rows_dev)
+    sk = ops.gemm_n256_splits(R, V1)
+    slab = torch.empty(sk * R * d, device="cuda")
+    ops.gemm_n256(dl, E, slab.view(sk, R, d), False, R, V1, split=True, rows_dev=rows_dev)
+    dh = torch.empty(R, d, device="cuda", dtype=torch.bfloat16)
+    ops.splitk_scatter_rows(slab, sk, R, torch.arange(R, dtype=torch.int32, device="cuda"), dh)
+    torch.cuda.synchronize()
+    ntn = -(-V1 // 128)
+    lse_k = ws[R * ntn * 2 + R: R * ntn * 2 + 2 * R].double()
+    # float64 reference, 64k classes at a time
+    h64, keep = h.double(), (lab != 0)
+    n = float(keep.sum())
+    C = 1 << 16
+    m = torch.full((R,), -float("inf"), device="cuda", dtype=torch.float64)
+    s = torch.zeros(R, device="cuda", dtype=torch.float64)
+    tgt = torch.zeros(R, device="cuda", dtype=torch.float64)
+    for c0 in range(0, V1, C):
+        z = h64 @ E[c0:c0 + C].double().t() + bias[c0:c0 + C].double()
+        mc = torch.maximum(m, z.max(1).values)
+        s = s * torch.exp(m - mc) + torch.exp(z - mc[:, None]).sum(1)
+        m = mc
+        inside = (lab >= c0) & (lab < c0 + z.shape[1])
+        tgt[inside] = z[inside, lab[inside] - c0]
+    lse = m + torch.log(s)
+    loss = float((lse - tgt)[keep].sum())
+    dE64 = torch.empty(V1, d, device="cuda", dtype=torch.float64)
+    db64 = torch.empty(V1, device="cuda", dtype=torch.float64)
+    dh64 = torch.zeros(R, d, device="cuda", dtype=torch.float64)
+    err_dl = 0.0
+    for c0 in range(0, V1, C):
+        z = h64 @ E[c0:c0 + C].double().t() + bias[c0:c0 + C].double()
+        p = torch.exp(z - lse[:, None])
+        inside = (lab >= c0) & (lab < c0 + z.shape[1])
+        p[inside, lab[inside] - c0] -= 1.0
+        p *= keep[:, None].double() / n
+        err_dl = max(err_dl, float(((dl[:, c0:c0 + C].double() - p).abs() - 2.0 ** -8 * p.abs()).max()))
+        dE64[c0:c0 + C] = p.t() @ h64
+        db64[c0:c0 + C] = p.sum(0)
+        dh64 += p @ E[c0:c0 + C].double()
+    assert float(out[1]) == n
+    assert abs(float(out[0]) - loss) <= 2e-5 * abs(loss), (float(out[0]), loss)
+    assert float((lse_k - lse)[keep].abs().max()) <= 2e-4
+    assert err_dl <= 1e-6 / n, err_dl                           # dlogits: bf16 rounding of the exact value
+    rel64 = lambda a, b: float((a.double() - b).norm() / b.norm())   # noqa: E731
+    assert rel64(dE, dE64) < 1e-2, rel64(dE, dE64)
+    assert rel64(db, db64) < 1e-2, rel64(db, db64)
+    assert rel64(dh, dh64) < 1e-2, rel64(dh, dh64)
+    print("cfg5 head:", rel64(dE, dE64), rel64(db, db64), rel64(dh, dh64))

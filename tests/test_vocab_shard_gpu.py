@@ -27,7 +27,7 @@ def _free_port():
     return p
 
 
-def _model():
+def _model(V=V):
     import rbm_amd  # noqa: F401
     from rbm_amd.models import model_factory
     a = argparse.Namespace(model_code="bert", num_items=V, max_len=T, device="cuda", bert_hidden_units=D,
@@ -36,7 +36,7 @@ def _model():
     return model_factory(a)
 
 
-def _batches(world, steps):
+def _batches(world, steps, V=V):
     import rbm_amd.data as synth
     rng = np.random.default_rng(3)
     return [[synth.bert_batch(rng, BR, T, V, mask_prob=0.3) for _ in range(world)] for _ in range(steps)]
@@ -93,3 +93,72 @@ def test_vocab_sharded_head_equals_single_process(tmp_path, graph):
         if "linear_layers.1.bias" in k:
             continue    # attention key bias: analytically zero gradient, Adam amplifies rounding noise (see test_dp_gpu)
         assert rel(r0["sd"][k].float().numpy(), ref[k].float().numpy()) < 5e-3, (k, rel(r0["sd"][k].numpy(), ref[k].numpy()))
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# The sharded step's gradient against the ORACLE (oracle/bert.py: the float64 restatement of the reference's BERT4Rec
+# forward and CE(ignore_index=0), BS/models/bert.py:10,16, BS/trainers/bert.py:36-40) on the concatenated batch.
+# V = 100,000: 100,001 output rows, split at row 50,048 (128-aligned, inside one 256-entry forward vocabulary tile of
+# the ping-pong head); each rank's owned rows of out.weight / out.bias hold complete gradients of the global mean, the
+# rest of the buffer the all-reduced encoder gradients (FusedTrainStep.step up to the optimizer).
+
+VB = 100_000
+
+
+def _grad_worker(rank, world, port, out_dir):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rbm_amd.train_step import FusedTrainStep
+        m = _model(VB)
+        tr = FusedTrainStep(m, lr=0.0, vocab_shard=True, max_labelled=BR * T)
+        b = tuple(torch.from_numpy(x).cuda() for x in _batches(world, 1, VB)[0][rank])
+        tr.flat.grad.zero_()
+        tr._compute(*b, split=tr._eager_split, update=True)
+        tr.exchange.launch("final")
+        tr.exchange.finish()
+        torch.cuda.synchronize()
+        grads = {k: tr.flat.view(k, tr.flat.grad).detach().cpu().clone() for k in m.state_dict()}
+        torch.save({"v0": tr.vshard.v0, "v1": tr.vshard.v1, "loss": float(tr.loss_out[2].item()),
+                    "count": float(tr.loss_out[1].item()), "grads": grads}, os.path.join(out_dir, f"g{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_vocab_sharded_gradient_equals_oracle(tmp_path):
+    """Loss, labelled count and every gradient tensor (out.weight / out.bias assembled from the owners' rows) against
+    the float64 oracle on the concatenated batch, at the bf16 bars of the single-device BERT oracle tests
+    (test_bert.py: 3e-2 loss / per tensor); the attention key bias (analytically zero) against the gradient scale."""
+    from oracle import bert as obert
+    world = 2
+    mp.spawn(_grad_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    r = [torch.load(tmp_path / f"g{i}.pt", weights_only=True) for i in range(world)]
+    assert (r[0]["v0"], r[0]["v1"], r[1]["v0"], r[1]["v1"]) == (0, 50048, 50048, VB + 1)
+    assert r[0]["loss"] == r[1]["loss"] and r[0]["count"] == r[1]["count"]
+    b = _batches(world, 1, VB)[0]
+    tok = torch.from_numpy(np.concatenate([x[0] for x in b]))
+    lab = torch.from_numpy(np.concatenate([x[1] for x in b]))
+    assert r[0]["count"] == float((lab != 0).sum())
+    P = {k: v.detach().cpu().double() for k, v in _model(VB).state_dict().items()}
+    torch.set_num_threads(16)
+    l64, _, g64 = obert.loss_and_grads(P, tok, lab, 1, 2)
+    assert abs(r[0]["loss"] - float(l64)) <= 3e-2 * abs(float(l64)), (r[0]["loss"], float(l64))
+    scale = max(float(v.norm()) for v in g64.values())
+    errs = {}
+    for k, ref in g64.items():
+        if k in ("out.weight", "out.bias"):
+            g = torch.cat([r[i]["grads"][k][r[i]["v0"]:r[i]["v1"]] for i in range(world)])
+        else:
+            assert torch.equal(r[0]["grads"][k], r[1]["grads"][k]), k
+            g = r[0]["grads"][k]
+        g = g.double().numpy()
+        if "linear_layers.1.bias" in k:
+            assert np.linalg.norm(g) <= 1e-2 * scale, k
+            continue
+        errs[k] = rel(g, ref.numpy())
+    worst = max(errs, key=errs.get)
+    print("vocab-sharded head vs oracle: worst", worst, errs[worst])
+    assert errs[worst] < 3e-2, (worst, errs[worst])
