@@ -841,12 +841,19 @@ __global__ __launch_bounds__(NT) void block_out_bwd_kernel(OutBwdArgs a) {
   const TileRange tr = tiles_of_wave(n_tiles(a.M), wave);
   const OutBwd ob = out_bwd_of(a);
   int64_t t = tr.first;
-  Raw<D> dr, hr;
-  if (t < tr.end) {
-    const int64_t mc = tile_of(t, a.M, cl).mc;
+  // every input of the first tile is requested before the weight staging (its ~3 us burst then hides their latency;
+  // requested after the barrier they cost a second round trip)
+  Raw<D> dr, hr, xr, orr;
+  float mu = 0.f, rs = 0.f;
+  auto load_tile = [&](int64_t mc) {
     load_raw<D>(dr, a.dxn, D, mc, g);
     load_raw<D>(hr, a.h1, D, mc, g);
-  }
+    load_raw<D>(xr, a.x1, D, mc, g);
+    if (a.delta) load_raw<D>(orr, a.o, D, mc, g);
+    mu = a.mean2[mc];
+    rs = a.rstd2[mc];
+  };
+  if (t < tr.end) load_tile(tile_of(t, a.M, cl).mc);
   {
     const bf16* const W[3] = {a.W2T, a.W1T, a.WoT};
     const int64_t ldw[3] = {D, D, D};
@@ -859,14 +866,7 @@ __global__ __launch_bounds__(NT) void block_out_bwd_kernel(OutBwdArgs a) {
   for (; t < tr.end; t += tr.step) {
     asm volatile("" ::: "memory");
     const Tile T = tile_of(t, a.M, cl);
-    if (t != tr.first) {
-      load_raw<D>(dr, a.dxn, D, T.mc, g);
-      load_raw<D>(hr, a.h1, D, T.mc, g);
-    }
-    Raw<D> xr, orr;
-    load_raw<D>(xr, a.x1, D, T.mc, g);
-    if (a.delta) load_raw<D>(orr, a.o, D, T.mc, g);
-    const float mu = a.mean2[T.mc], rs = a.rstd2[T.mc];
+    if (t != tr.first) load_tile(T.mc);
     Raw<D> dzr, dar;
     bwd_out_a<D>(dr, hr, T, wslot(smem, 0, WB), ob, dzr, dar, lane);
     bwd_out_b<D>(dar, xr, dzr, orr, T, mu, rs, wslot(smem, 1, WB), wslot(smem, 2, WB), lv, ob, red, lane, wave);
@@ -894,12 +894,19 @@ __global__ __launch_bounds__(NT) void block_in_bwd_kernel(InBwdArgs a) {
             cl = lane & 15;
   const TileRange tr = tiles_of_wave(n_tiles(a.M), wave);
   int64_t t = tr.first;
-  Raw<D> kr, vr;
-  if (t < tr.end) {
-    const int64_t mc = tile_of(t, a.M, cl).mc;
+  // every input of the first tile is requested before the weight staging (as block_out_bwd)
+  Raw<D> kr, vr, qr, rr, xr;
+  float mu = 0.f, rs = 0.f;
+  auto load_tile = [&](int64_t mc) {
     load_raw<D>(kr, a.dkv, 2 * D, mc, g);
     load_raw<D>(vr, a.dkv + D, 2 * D, mc, g);
-  }
+    load_raw<D>(qr, a.dq, D, mc, g);
+    load_raw<D>(rr, a.dx1, D, mc, g);
+    load_raw<D>(xr, a.x, D, mc, g);
+    mu = a.mean1[mc];
+    rs = a.rstd1[mc];
+  };
+  if (t < tr.end) load_tile(tile_of(t, a.M, cl).mc);
   {
     const bf16* const W[3] = {a.WinT + D, a.WinT + 2 * D, a.WinT};   // Wk^T, Wv^T, Wq^T rows
     const int64_t ldw[3] = {a.ldwt, a.ldwt, a.ldwt};
@@ -912,16 +919,8 @@ __global__ __launch_bounds__(NT) void block_in_bwd_kernel(InBwdArgs a) {
   for (; t < tr.end; t += tr.step) {
     asm volatile("" ::: "memory");
     const Tile T = tile_of(t, a.M, cl);
-    if (t != tr.first) {
-      load_raw<D>(kr, a.dkv, 2 * D, T.mc, g);
-      load_raw<D>(vr, a.dkv + D, 2 * D, T.mc, g);
-    }
-    Raw<D> qr, rr, xr, dxr;
-    load_raw<D>(qr, a.dq, D, T.mc, g);
-    load_raw<D>(rr, a.dx1, D, T.mc, g);
-    load_raw<D>(xr, a.x, D, T.mc, g);
-    const float mu = a.mean1[T.mc], rs = a.rstd1[T.mc];
-    Raw<D> dxkv;
+    if (t != tr.first) load_tile(T.mc);
+    Raw<D> dxkv, dxr;
     bwd_in_a<D>(kr, vr, wslot(smem, 0, WB), wslot(smem, 1, WB), dxkv, lane);
     bwd_in_b<D>(qr, rr, xr, dxkv, T, mu, rs, wslot(smem, 2, WB), lv, red, dxr, lane, wave);
     store_raw<D>(a.dx, D, T.m, T.ok, dxr, g);
