@@ -253,12 +253,13 @@ def roofline(cfg, B, dtype, live_us=None, reps=50, labelled=None, live_expected=
     shapes = [(d, Fd), (Fd, d), (d, d), (3 * d, d)] * L        # W2, W1, Wo, Wqkv  (N, K)
     probs = [(rn(M, n), rn(M, k), torch.zeros(n, k, device="cuda"), torch.zeros(n, device="cuda"))
              for n, k in shapes]
-    rows = BERTEngine._wgrad_rows(M, sum((n // 128) * (k // 128) for n, k in shapes))
+    rows = BERTEngine._wgrad_rows(M, shapes)
     slab = torch.empty(ops.wgrad_grouped_slab_numel(shapes, M, rows), device="cuda")
     us = _time_on_stream(lambda: ops.wgrad_grouped(probs, M, rows, slab), reps, stream)
     flops = sum(2.0 * M * n * k for n, k in shapes)
     nbytes = sum(M * (n + k) * es + (n * k + n) * 4 * 2 for n, k in shapes)   # dY, X once; dW, db read+write
-    return _roof("rs_wgrad_grouped (wgrad_group_kernel + reduce_cols_kernel)", us, flops, nbytes, dtype,
+    kern = "wgrad_group256_kernel" if ops.wgrad_grouped_tile(shapes) == 256 else "wgrad_group_kernel"
+    return _roof(f"rs_wgrad_grouped ({kern} + reduce_cols_kernel)", us, flops, nbytes, dtype,
                  f"{len(shapes)} block weight gradients of M={M} token rows (d={d}, ff={Fd}, L={L}), "
                  f"{-(-M // rows)} row splits; 2 kernels per launch", live_us, live_expected, event_us)
 

@@ -484,6 +484,10 @@ typedef struct {
 } rs_reduce_segment;
 /* slab floats needed by rs_wgrad_grouped for these problems (splits = ceil(M / rows_per_split)). */
 int64_t rs_wgrad_grouped_slab_numel(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_t rows_per_split);
+/* output tile edge rs_wgrad_grouped uses for these problems (reads N and K only): 256 when every N and K is a
+ * multiple of 256 (the BERT d = 256 layer's weights), else 128 or 64; -1 on bad arguments.  Callers size the row
+ * splits by it (about one 256-tile workgroup per CU in total). */
+int rs_wgrad_grouped_tile(int nprob, const rs_wgrad_problem* probs);
 /* nprob <= 16 problems; rows_per_split % 64 == 0; the extra segments (<= 64, e.g. LayerNorm
  * affine partials from rs_sas_block_*_bwd) are summed into their outputs (+=) by the same
  * reduction launch.  Returns RS_ERR_UNSUPPORTED for shapes outside the contract. */

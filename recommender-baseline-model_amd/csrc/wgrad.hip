@@ -14,6 +14,7 @@
 //
 // Bias gradients ride on the same MFMAs (dY^T against a ones operand) in the k-tile-0 blocks.
 #include "gemm_bf16_impl.h"
+#include "dma256.h"
 
 namespace wg {
 
@@ -219,10 +220,162 @@ __global__ __launch_bounds__(256, 2) void wgrad_group_kernel(Args a) {
   group_tile<T>(a, blockIdx.x, gridDim.x, smem);
 }
 
+// 256 x 256 output tiles (every dimension of the problems a multiple of 256: the BERT d = 256 layer's QKV, output,
+// FFN1 and FFN2 weights).  With 128 x 128 tiles each 64-row stage moves 32 KB from L2 per 2.1 MFLOP and the 12,800-row
+// operands of width 1,024 / 768 are re-read by every 128-wide tile across them (FFN1's X 8x, dY 2x per split): the
+// launch ran at ~8.6 TB/s of L2->CU operand traffic (148 us at cfg3, 0.2 of MFMA).  A 256 x 256 tile halves the
+// stage bytes per flop and reads the 256-wide side once per split.  The tile is gemm_n256's (dma256.h): 8 waves,
+// each a 128 x 64 quadrant, 32-deep stages of both k-major operands by LDS-DMA into four buffers, three in flight;
+// bias column sums on MFMAs against ones (column tile 0); the fp32 partial tile staged through LDS into the split's
+// slab in the layout the grouped reduction sums (same slabs as the 64 / 128 tiles; summation order within a split
+// differs: 32-deep MFMA steps in row order).
+struct Args256 {
+  Prob p[MAXP];
+  int nprob, ntiles, splits, rows_per_split;
+  int64_t M;
+  float* slab;
+  KStamp ks;
+};
+__global__ __launch_bounds__(g256::NTH) void wgrad_group256_kernel(Args256 a) {
+  using namespace g256;
+  KStampBegin stamp_(a.ks);
+  constexpr int LDC = BN + 4;
+  constexpr int LDS_BYTES = NBUF * DSTAGE > (BM / 2) * LDC * 4 ? NBUF * DSTAGE : (BM / 2) * LDC * 4;
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  constexpr int FM = 8, FN = 4;
+  // XCD-contiguous (split, tile) ranges (as group_tile): the tiles of one row split, which share its operand rows,
+  // read them through one XCD's L2
+  unsigned bid = blockIdx.x;
+  {
+    const unsigned nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, x = bid & 7;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+  }
+  const int t = (int)(bid % (unsigned)a.ntiles);
+  const int s = (int)(bid / (unsigned)a.ntiles);
+  int pi = 0;
+#pragma unroll 1
+  for (int q = 1; q < a.nprob; ++q)
+    if (t >= a.p[q].tile0) pi = q;
+  const Prob& P = a.p[pi];
+  const int lt = t - P.tile0;
+  const int tm = lt / P.tiles_k, tn = lt - tm * P.tiles_k;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int64_t kbeg = (int64_t)s * a.rows_per_split;
+  const int64_t kend = min(a.M, kbeg + a.rows_per_split);
+  const int nk = kend > kbeg ? (int)((kend - kbeg + DBK - 1) / DBK) : 0;
+  const uint32_t lds0 = lds_u32(smem);
+  const bool do_colsum = tn == 0;
+
+  f32x4 acc[FM][FN], accb[2];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  accb[0] = accb[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
+
+  auto issue = [&](int st) {
+    const uint32_t buf = lds0 + (uint32_t)((st % NBUF) * DSTAGE);
+    const int64_t k0 = kbeg + (int64_t)st * DBK;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) km_piece(P.dY, P.lddy, k0, m0, kend, P.N, 2 * wave + j, lane, buf);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) km_piece(P.X, P.ldx, k0, n0, kend, P.K, 2 * wave + j, lane, buf + IMG_BYTES);
+  };
+  auto zero_tail = [&](int st) {
+    char* buf = smem + (st % NBUF) * DSTAGE;
+    const int kv = (int)(kend - (kbeg + (int64_t)st * DBK));
+    for (int e = tid; e < (DBK - kv) * 256; e += NTH) {
+      const int r = kv + e / 256, c = e % 256;
+      *reinterpret_cast<__bf16*>(buf + IMG_BYTES + km_off(r, c)) = (__bf16)0.0f;
+      *reinterpret_cast<__bf16*>(buf + km_off(r, c)) = (__bf16)0.0f;
+    }
+  };
+  auto compute = [&](int st) {
+    const char* buf = smem + (st % NBUF) * DSTAGE;
+    bf16x8 fa[FM], fb[FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) fa[i] = km_frag(buf, wm * 128 + 16 * i, lane);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) fb[j] = km_frag(buf + IMG_BYTES, wn * 64 + 16 * j, lane);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    if (do_colsum) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        if ((i >> 1) == wn) accb[i & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], ones, accb[i & 1], 0, 0, 0);
+    }
+  };
+  const bool tail = ((kend - kbeg) % DBK) != 0;
+  for (int st = 0; st < min(nk, DIST); ++st) issue(st);
+  for (int st = 0; st < nk; ++st) {
+    const int after = min(nk - 1, st + DIST - 1) - st;
+    if (after >= 2) vm_wait<8>();
+    else if (after == 1) vm_wait<4>();
+    else vm_wait<0>();
+    raw_barrier();
+    if (st + DIST < nk) issue(st + DIST);
+    if (tail && st == nk - 1) {
+      zero_tail(st);
+      raw_barrier();
+    }
+    compute(st);
+  }
+  vm_wait<0>();
+
+  // epilogue: the partial tile into split s's slab, [N][K] rows of the weight (+ the bias partial after them)
+  float* S = a.slab + P.slab_off + (int64_t)s * ((int64_t)P.N * P.K + P.N);
+  float* Cs = reinterpret_cast<float*>(smem);
+  const int g = lane >> 4, cl = lane & 15;
+  if (do_colsum && cl == 0) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) S[(int64_t)P.N * P.K + m0 + wm * 128 + 16 * (2 * wn + u) + 4 * g + r] = accb[u][r];
+  }
+  constexpr int TPR = BN / 8, RPP = NTH / TPR;
+  const int c8 = (tid % TPR) * 8;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    __syncthreads();
+    if (wm == half) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Cs[(16 * i + 4 * g + r) * LDC + wn * 64 + 16 * j + cl] = acc[i][j][r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int row = tid / TPR; row < BM / 2; row += RPP) {
+      const int64_t m = m0 + half * 128 + row;
+      const float4 v0 = *reinterpret_cast<const float4*>(Cs + row * LDC + c8);
+      const float4 v1 = *reinterpret_cast<const float4*>(Cs + row * LDC + c8 + 4);
+      float* dst = S + m * P.K + n0 + c8;
+      *reinterpret_cast<float4*>(dst) = v0;
+      *reinterpret_cast<float4*>(dst + 4) = v1;
+    }
+  }
+}
+
 // the grouped launch (T = output tile edge)
 inline void launch_group(const Args& a, int T, hipStream_t s) {
   const dim3 grid((unsigned)(a.ntiles * a.splits));
-  if (T == 128) hipLaunchKernelGGL(wgrad_group_kernel<128>, grid, dim3(256), 0, s, a);
+  if (T == 256) {
+    Args256 b;
+    static_assert(sizeof(b.p) == sizeof(a.p), "same problem table");
+    memcpy(b.p, a.p, sizeof(a.p));
+    b.nprob = a.nprob; b.ntiles = a.ntiles; b.splits = a.splits; b.rows_per_split = a.rows_per_split;
+    b.M = a.M; b.slab = a.slab; b.ks = a.ks;
+    hipLaunchKernelGGL(wgrad_group256_kernel, grid, dim3(g256::NTH), 0, s, b);
+  } else if (T == 128) hipLaunchKernelGGL(wgrad_group_kernel<128>, grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(wgrad_group_kernel<64>, grid, dim3(256), 0, s, a);
 }
 
@@ -458,14 +611,25 @@ int rs_reduce_segments(int nseg, const rs_reduce_segment* segs, int accumulate, 
 
 // the grouped launch's arguments (T = output tile edge) and its reduction segments (problems' W and bias
 // segments, then the caller's extra ones)
+// output tile edge of a grouped launch: 256 when every problem's N and K are multiples of 256 (RS_WGRAD_T256=0: at most
+// 128), else 128, else 64
+static int64_t wgrad_tile(int nprob, const rs_wgrad_problem* probs) {
+  static const bool t256 = [] {
+    const char* e = getenv("RS_WGRAD_T256");
+    return !e || atoi(e) != 0;
+  }();
+  int64_t T = t256 ? 256 : 128;
+  for (int q = 0; q < nprob; ++q)
+    while (probs[q].N % T || probs[q].K % T) T /= 2;
+  return T < 64 ? 64 : T;
+}
+
 static int wgrad_group_args(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_t rows_per_split, float* slab,
                             int64_t slab_numel, int nextra, const rs_reduce_segment* extra, wg::Args& a, int& T_,
                             rs_reduce_segment* segs, int& ns) {
   if (nprob <= 0 || nprob > wg::MAXP || M <= 0 || rows_per_split <= 0 || rows_per_split % 64 || !slab)
     return RS_ERR_ARG;
-  int64_t T = 128;
-  for (int q = 0; q < nprob; ++q)
-    if (probs[q].N % 128 || probs[q].K % 128) T = 64;
+  int64_t T = wgrad_tile(nprob, probs);
   const int64_t splits = cdiv(M, rows_per_split);
   a = wg::Args{};
   a.nprob = nprob;
@@ -502,6 +666,11 @@ static int wgrad_group_args(int nprob, const rs_wgrad_problem* probs, int64_t M,
 }
 
 extern "C" {
+
+int rs_wgrad_grouped_tile(int nprob, const rs_wgrad_problem* probs) {
+  if (nprob <= 0 || nprob > wg::MAXP || !probs) return -1;
+  return (int)wgrad_tile(nprob, probs);
+}
 
 int rs_wgrad_grouped(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_t rows_per_split, float* slab,
                      int64_t slab_numel, int nextra, const rs_reduce_segment* extra, void* stream) {

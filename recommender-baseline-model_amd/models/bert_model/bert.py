@@ -377,7 +377,7 @@ class BERTEngine:
         for c in range(0, len(probs), 16):              # rs_wgrad_grouped takes up to 16 problems
             chunk = probs[c:c + 16]
             shapes = [(p[0].shape[1], p[1].shape[1]) for p in chunk]
-            rows = self._wgrad_rows(M, sum(-(-n // 128) * -(-k // 128) for n, k in shapes))
+            rows = self._wgrad_rows(M, shapes)
             wslab = self.ws.get(f"wslab{c}", (ops.wgrad_grouped_slab_numel(shapes, M, rows),), torch.float32)
             ops.wgrad_grouped(chunk, M, rows, wslab, extra=ln_segs if c == 0 else ())
 
@@ -430,11 +430,14 @@ class BERTEngine:
         return ev, iws
 
     @staticmethod
-    def _wgrad_rows(M, tiles):
-        """rows per split of the grouped weight-gradient launch: about one and a half 128x128-tile workgroups
-        per CU in total (cfg3: 192 tiles x 2 splits; 4 splits measured 156 against 153 us for the launch, 1 split
-        219 us)."""
-        splits = max(1, round(384 / tiles))
+    def _wgrad_rows(M, shapes):
+        """rows per split of the grouped weight-gradient launch.  128 x 128 tiles: about one and a half workgroups per
+        CU in total (cfg3: 192 tiles x 2 splits; 4 splits measured 156 against 153 us for the launch, 1 split 219 us);
+        256 x 256 tiles (every dimension a multiple of 256, rs_wgrad_grouped_tile; one 8-wave workgroup per CU): about
+        one per CU (cfg3: 48 tiles x 5 splits)."""
+        t = ops.wgrad_grouped_tile(shapes)
+        tiles = sum(-(-n // t) * -(-k // t) for n, k in shapes)
+        splits = max(1, round((256 if t == 256 else 384) / tiles))
         return max(64, -(-(-(-M // splits)) // 64) * 64)
 
     # ---- eval scores at candidates (BS/trainers/bert.py:43-49 without the (B, T, V+1) logits) --------

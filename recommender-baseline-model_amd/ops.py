@@ -613,6 +613,17 @@ def _wgrad_grouped(problems, M, rows_per_split, slab, extra=(), pos=None):
          stream())
 
 
+def wgrad_grouped_tile(shapes):
+    """Output tile edge rs_wgrad_grouped uses for problems of these (N, K) shapes (256, 128 or 64)."""
+    arr = (_lib.WgradProblem * len(shapes))()
+    for i, (N, K) in enumerate(shapes):
+        arr[i] = _lib.WgradProblem(None, 0, None, 0, N, K, None, None)
+    t = int(_lib.lib().rs_wgrad_grouped_tile(len(shapes), arr))
+    if t <= 0:
+        raise RuntimeError("rs_wgrad_grouped_tile: bad arguments")
+    return t
+
+
 def wgrad_grouped_slab_numel(shapes, M, rows_per_split):
     """shapes: [(N, K)] of the problems."""
     splits = -(-M // rows_per_split)

@@ -146,7 +146,7 @@ def main():
         from rbm_amd.models.bert_model.bert import BERTEngine
         bshapes = [(d, ff), (ff, d), (d, d), (3 * d, d)] * 4
         bprobs = [(rn(M, n), rn(M, k), torch.zeros(n, k, device=dev), torch.zeros(n, device=dev)) for n, k in bshapes]
-        brows = BERTEngine._wgrad_rows(M, sum((n // 128) * (k // 128) for n, k in bshapes))
+        brows = BERTEngine._wgrad_rows(M, bshapes)
         bslab = torch.empty(ops.wgrad_grouped_slab_numel(bshapes, M, brows), device=dev)
         run("bert wgrad_grouped 16 problems", lambda: ops.wgrad_grouped(bprobs, M, brows, bslab),
             sum(M * (n + k) * es for n, k in bshapes), sum(2 * M * n * k for n, k in bshapes))
