@@ -200,6 +200,21 @@ __device__ __forceinline__ void ln_fwd(Act<D>& x, const float* gw, const float* 
   }
 }
 
+// sum over the 16 lanes of a DPP row (the 16 tokens of a lane group), pairing lanes as an xor butterfly over offsets
+// 1, 2, 4, 8 does -- quad permutes, then the half-row and row mirrors, which combine the same partial sums (the lanes
+// of a quad, of a half row, already agree) -- so every lane gets that butterfly's bits, from DPP operand moves instead
+// of __shfl_xor's ds_bpermute_b32 (an LDS-crossbar round trip each: ~260 per tile in the LayerNorm backwards)
+template <int CTRL> __device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<0xB1>(v);    // quad_perm [1, 0, 3, 2]: lane ^ 1
+  v += dpp_f<0x4E>(v);    // quad_perm [2, 3, 0, 1]: lane ^ 2
+  v += dpp_f<0x141>(v);   // row_half_mirror: the other quad of the half row
+  v += dpp_f<0x140>(v);   // row_mirror: the other half row
+  return v;
+}
+
 // LayerNorm backward (layernorm.hip ln_bwd, VAR 0), in place on dy: t = rstd*(dy*g - mean(dy*g))
 // - rstd^3*mean(dy*g*u)*u, u = x - mean (x as stored, bf16); dy zeroed on invalid tokens.  The dgamma/dbeta
 // terms of the tile's 16 tokens are summed by an xor tree over the lanes of a group as they are formed and added
@@ -218,12 +233,7 @@ __device__ __forceinline__ void ln_bwd(Act<D>& dy, const Raw<D>& xr, bool valid,
       const float gy = valid ? dy.v[j][e] : 0.f;
       const float u = (float)xr.v[j >> 1][4 * (j & 1) + e] - mu;
       const float gq = gy * w[e];
-      float pg = gy * (u * a), pb = gy;
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        pg += __shfl_xor(pg, o, 64);
-        pb += __shfl_xor(pb, o, 64);
-      }
+      const float pg = row16_sum(gy * (u * a)), pb = row16_sum(gy);
       if (cl == 0) {
         rw[feat(j, g, e)] += pg;
         rw[D + feat(j, g, e)] += pb;
