@@ -387,8 +387,7 @@ __global__ __launch_bounds__(NT) void attn_fwd_lds_kernel(AttnLdsArgs a) {
         }
       }
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = max_xor32(max_xor16(mx));
     float sm = 0.f;
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
@@ -401,8 +400,7 @@ __global__ __launch_bounds__(NT) void attn_fwd_lds_kernel(AttnLdsArgs a) {
         }
       }
     }
-    sm += __shfl_xor(sm, 16, 64);
-    sm += __shfl_xor(sm, 32, 64);
+    sm = add_xor32(add_xor16(sm));
     const float inv = 1.f / sm;
     if (g == 0 && qrow < a.T) a.lse[bh * a.T + qrow] = (mx + __builtin_amdgcn_logf(sm)) * LN2;
     // P^T (+ dropout: one hash per pair of adjacent keys), packed pairwise as the B operand of O^T = V^T P^T
@@ -538,8 +536,7 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnLdsArgs& a, int64_t l
 #pragma unroll
         for (int j = 0; j < 8; ++j) dl += (float)df[kc][j] * (float)of[kc][j];
       }
-      dl += __shfl_xor(dl, 16, 64);
-      dl += __shfl_xor(dl, 32, 64);  // delta = rowsum(dO * O) for query qrow
+      dl = add_xor32(add_xor16(dl));  // delta = rowsum(dO * O) for query qrow
       if (role != 1 && g == 0 && qrow < a.T) a.delta[bh * a.T + qrow] = dl;
     }
     const float lq2 = (qrow < a.T ? a.lse[bh * a.T + qrow] : 0.f) * LOG2E;
@@ -775,8 +772,7 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnLdsArgs& a, int64_t 
 #pragma unroll
         for (int j = 0; j < 8; ++j) dl += (float)dfv[j] * (float)of[kc][j];
       }
-      dl += __shfl_xor(dl, 16, 64);
-      dl += __shfl_xor(dl, 32, 64);
+      dl = add_xor32(add_xor16(dl));
       if (g == 0) dl_s[row] = row < T ? dl : 0.f;
     }
     __syncthreads();

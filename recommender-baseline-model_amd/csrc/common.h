@@ -135,6 +135,69 @@ __device__ __forceinline__ float group16_max(float v) {
   return v;
 }
 
+// Cross-lane steps without the LDS crossbar, for code that runs with ALL 64 lanes active (DPP and the permlane
+// swaps read an inactive lane's register as invalid; __shfl_xor's ds_bpermute_b32 reads it regardless -- but costs
+// an LDS round trip each): lane ^ 32 / ^ 16 by the gfx950 permlane swaps (the pair's two values summed in either
+// order: the same bits), lane ^ 8 / ^ 4 / ^ 2 / ^ 1 by DPP row moves -- row_ror:8 IS lane ^ 8 within a 16-lane row,
+// and once the lanes i, i ^ 8 agree row_ror:4 reads the value lane ^ 4 holds -- so each form returns, in every
+// lane, the bits of the xor butterfly it replaces.
+template <int CTRL> __device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+#define DPP_XOR1 0xB1    // quad_perm [1, 0, 3, 2]
+#define DPP_XOR2 0x4E    // quad_perm [2, 3, 0, 1]
+#define DPP_ROR4 0x124   // row_ror:4
+#define DPP_ROR8 0x128   // row_ror:8
+#define DPP_HALF_MIRROR 0x141
+#define DPP_MIRROR 0x140
+// v_permlane32_swap_b32 a, b: lanes 32-63 of a <-> lanes 0-31 of b; v_permlane16_swap_b32: the odd 16-lane rows of a
+// <-> the even rows of b.  With a = b = v the pair (a, b) then holds, per lane, v and the value of lane ^ 32 (^ 16).
+// Inline asm, two distinct registers: hipcc 7.2 folds __builtin_amdgcn_permlane*_swap(u, u) wrongly (the two
+// results taken as equal: every lane wrong, tools/micro/xlane_probe.hip).  s_nop 1: the VALU-write -> permlane-read
+// hazard's two wait states.
+__device__ __forceinline__ void pl32_swap(unsigned& a, unsigned& b) {
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+__device__ __forceinline__ void pl16_swap(unsigned& a, unsigned& b) {
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+__device__ __forceinline__ float add_xor32(float v) {
+  unsigned a = __builtin_bit_cast(unsigned, v), b = a;
+  pl32_swap(a, b);
+  return __builtin_bit_cast(float, a) + __builtin_bit_cast(float, b);
+}
+__device__ __forceinline__ float add_xor16(float v) {
+  unsigned a = __builtin_bit_cast(unsigned, v), b = a;
+  pl16_swap(a, b);
+  return __builtin_bit_cast(float, a) + __builtin_bit_cast(float, b);
+}
+__device__ __forceinline__ float max_xor32(float v) {
+  unsigned a = __builtin_bit_cast(unsigned, v), b = a;
+  pl32_swap(a, b);
+  return fmaxf(__builtin_bit_cast(float, a), __builtin_bit_cast(float, b));
+}
+__device__ __forceinline__ float max_xor16(float v) {
+  unsigned a = __builtin_bit_cast(unsigned, v), b = a;
+  pl16_swap(a, b);
+  return fmaxf(__builtin_bit_cast(float, a), __builtin_bit_cast(float, b));
+}
+// = group16_sum (butterfly order 8, 4, 2, 1), all lanes active
+__device__ __forceinline__ float group16_sum_full(float v) {
+  v += dpp_mov<DPP_ROR8>(v);
+  v += dpp_mov<DPP_ROR4>(v);
+  v += dpp_mov<DPP_XOR2>(v);
+  v += dpp_mov<DPP_XOR1>(v);
+  return v;
+}
+// the xor butterfly over offsets 1, 2, 4, 8 (that order), all lanes active
+__device__ __forceinline__ float row16_sum_up(float v) {
+  v += dpp_mov<DPP_XOR1>(v);
+  v += dpp_mov<DPP_XOR2>(v);
+  v += dpp_mov<DPP_HALF_MIRROR>(v);   // the other quad of the half row
+  v += dpp_mov<DPP_MIRROR>(v);        // the other half row
+  return v;
+}
+
 // ---------------------------------------------------------------- dropout RNG
 // Counter-based: keep(seed, idx) is a pure function of (site/step seed, element index), so the
 // backward pass regenerates every mask instead of storing it.  One 32-bit avalanche hash

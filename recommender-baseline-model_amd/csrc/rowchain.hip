@@ -167,11 +167,7 @@ __device__ __forceinline__ f32x4 vec4(const float* lv, int j, int g) {
 }
 __device__ __forceinline__ int feat(int j, int g, int r) { return 32 * (j >> 1) + 8 * g + 4 * (j & 1) + r; }
 // sum over the token's features: this lane's values, then the other 3 lane groups
-__device__ __forceinline__ float row_sum(float s) {
-  s += __shfl_xor(s, 16, 64);
-  s += __shfl_xor(s, 32, 64);
-  return s;
-}
+__device__ __forceinline__ float row_sum(float s) { return add_xor32(add_xor16(s)); }   // xor 16, then 32 (all lanes active)
 
 // torch.nn.LayerNorm (biased variance, eps inside the sqrt), in place; returns (mean, rstd)
 template <int D>
@@ -200,20 +196,10 @@ __device__ __forceinline__ void ln_fwd(Act<D>& x, const float* gw, const float* 
   }
 }
 
-// sum over the 16 lanes of a DPP row (the 16 tokens of a lane group), pairing lanes as an xor butterfly over offsets
-// 1, 2, 4, 8 does -- quad permutes, then the half-row and row mirrors, which combine the same partial sums (the lanes
-// of a quad, of a half row, already agree) -- so every lane gets that butterfly's bits, from DPP operand moves instead
-// of __shfl_xor's ds_bpermute_b32 (an LDS-crossbar round trip each: ~260 per tile in the LayerNorm backwards)
-template <int CTRL> __device__ __forceinline__ float dpp_f(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
-}
-__device__ __forceinline__ float row16_sum(float v) {
-  v += dpp_f<0xB1>(v);    // quad_perm [1, 0, 3, 2]: lane ^ 1
-  v += dpp_f<0x4E>(v);    // quad_perm [2, 3, 0, 1]: lane ^ 2
-  v += dpp_f<0x141>(v);   // row_half_mirror: the other quad of the half row
-  v += dpp_f<0x140>(v);   // row_mirror: the other half row
-  return v;
-}
+// sum over the 16 lanes of a DPP row (the 16 tokens of a lane group): common.h row16_sum_up, the xor butterfly's
+// bits from DPP operand moves instead of __shfl_xor's ds_bpermute_b32 (~260 LDS-crossbar round trips per tile in the
+// LayerNorm backwards).  Every caller runs with all 64 lanes active (wave-uniform tile loops).
+__device__ __forceinline__ float row16_sum(float v) { return row16_sum_up(v); }
 
 // LayerNorm backward (layernorm.hip ln_bwd, VAR 0), in place on dy: t = rstd*(dy*g - mean(dy*g))
 // - rstd^3*mean(dy*g*u)*u, u = x - mean (x as stored, bf16); dy zeroed on invalid tokens.  The dgamma/dbeta
