@@ -383,7 +383,7 @@ int rs_sas_block_in(int64_t M, int64_t d, const void* x, int64_t ldx, const floa
 /* The first block's input side with the embedding stage folded in (rowchain: one launch instead of two): x0 =
  * (item_emb[ids]*scale + pos_emb[t]) -> dropout(p, salt) -> *(ids != 0), exactly as rs_embed_fwd mode 0, stored
  * to x0 [M][d] and fed to rs_sas_block_in's chain; with count_ids, count_parts[rs_sas_block_in_count_parts(M)]
- * (int32) receives per-wave counts of count_ids != 0 (the BCE divisor for rs_sas_block_out_head).  d in {64, 128}
+ * (int32) receives per-workgroup counts of count_ids != 0 (the BCE divisor for rs_sas_block_out_head).  d in {64, 128}
  * and 16-byte aligned tables / x0, else RS_ERR_ARG. */
 int64_t rs_sas_block_in_count_parts(int64_t M);
 int rs_sas_block_in_embed(int64_t M, int64_t d, const int64_t* ids, int64_t T, const void* item_emb, const void* pos_emb,

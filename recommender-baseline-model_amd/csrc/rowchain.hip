@@ -529,7 +529,8 @@ __device__ __forceinline__ void bwd_out_b(const Raw<D>& dar, const Raw<D>& xr, c
 // The SAS embedding stage folded into the first block's input kernel (rs_sas_block_in_embed): the tile's
 // x = (item_emb[ids]·scale + pos_emb[t]) → dropout → ·(ids != 0) is formed in registers exactly as
 // embed_fwd_kernel forms it (same expression, same hash index r·d + c), stored (x0, the backward's LN1 input) and
-// fed to the chain; each wave also counts its tiles' valid positions (count_ids != 0) into count_parts[wave].
+// fed to the chain; each workgroup also counts its tiles' valid positions (count_ids != 0) into
+// count_parts[workgroup] (the head kernel's 256 workgroups then load one word per thread, not a dependent chain of 8).
 struct EmbIn {
   const int64_t* ids; const bf16* etab; const bf16* ptab; int64_t T;
   float scale, drop_p; uint64_t salt; const uint64_t* seed_base;
@@ -616,7 +617,17 @@ __global__ __launch_bounds__(NT) void block_in_kernel(InArgs a) {
     fwd_in_q<D>(xr, T, wslot(smem, 0, WB), lv, a.eps, a.Q, a.mean, a.rstd, a.q, lane);
     fwd_in_kv<D>(xr, T, wslot(smem, 1, WB), wslot(smem, 2, WB), lv, a.kv, lane);
   }
-  if (emb && a.e.cnt_parts && lane == 0) a.e.cnt_parts[blockIdx.x * NW + wave] = cnt;
+  if (emb && a.e.cnt_parts) {   // integer counts: exact in any order
+    __shared__ int wcnt[NW];
+    if (lane == 0) wcnt[wave] = cnt;
+    __syncthreads();
+    if (tid == 0) {
+      int c = 0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) c += wcnt[w];
+      a.e.cnt_parts[blockIdx.x] = c;
+    }
+  }
 }
 
 // The SAS output head riding in the LAST block's output kernel (rs_sas_block_out_head): every quantity of the head
@@ -789,6 +800,7 @@ __global__ __launch_bounds__(NT) void block_out_kernel(OutArgs a) {
     RCPROF(4);
     if (head && RC_HEAD_PREFETCH == 2) ip = head_rows<D>(a.h, T, er, nr, g);
     if (head) head_tile<D>(xr, er, nr, ip, T, lv + 5 * D, lv + 6 * D, a.h, hscale, red, hacc, lane, wave);
+    RCPROF(6);
   }
   RCPROF(5);
   if (head) {
@@ -1020,7 +1032,7 @@ int rs_sas_block_in(int64_t M, int64_t d, const void* x, int64_t ldx, const floa
   return (int)hipGetLastError();
 }
 
-int64_t rs_sas_block_in_count_parts(int64_t M) { return M > 0 ? rc::grid_for(M) * rc::NW : 0; }
+int64_t rs_sas_block_in_count_parts(int64_t M) { return M > 0 ? rc::grid_for(M) : 0; }
 
 int rs_sas_block_in_embed(int64_t M, int64_t d, const int64_t* ids, int64_t T, const void* item_emb, const void* pos_emb,
                           float scale, float drop_p, uint64_t salt, const uint64_t* seed_base, void* x0,

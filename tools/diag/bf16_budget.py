@@ -18,7 +18,7 @@ import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
-GROUPS = ("W", "Ax", "AQ", "Aqkv", "Ao", "Ax1", "Az", "Ah1", "G", "P", "DS", "LNG")
+GROUPS = ("W", "WE", "Ax", "AQ", "Aqkv", "Ao", "Ax1", "Az", "Ah1", "G", "P", "DS", "LNG")
 ON = set(GROUPS)
 
 
@@ -61,12 +61,12 @@ def ln(x, w, b, eps=1e-8):
 
 
 def forward(P, seq, pos, neg, L, heads):
-    W = lambda k: RF(P[k], "W")  # noqa: E731   bf16 compute copy of a weight (biases / LN params stay fp32)
+    W = lambda k: RF(P[k], "W")  # noqa: E731   bf16 compute copy of a block weight (MFMA operand)
     E = P["sas.item_emb.weight"]
     d = E.shape[1]
     B, T = seq.shape
-    Eb = RF(E, "W")
-    x = F.embedding(seq, Eb) * math.sqrt(d) + RF(P["sas.pos_emb.weight"], "W")[:T]
+    Eb = RF(E, "WE")                   # the tables' bf16 copies: the embedding gather and the tied logits (VALU)
+    x = F.embedding(seq, Eb) * math.sqrt(d) + RF(P["sas.pos_emb.weight"], "WE")[:T]
     keep = (seq != 0).unsqueeze(-1).double()
     x = x * keep
     x = RG(RF(x, "Ax"))                # x0 stored bf16; its gradient dx (block_in_bwd output) bf16

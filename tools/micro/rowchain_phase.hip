@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <vector>
+#include <string>
 
 static void pct(const char* name, std::vector<double> v) {
   if (v.empty()) return;
@@ -30,6 +31,26 @@ int main(int argc, char** argv) {
   hipMemset(b, 0, d * 4); hipMemset(lw, 0, d * 4); hipMemset(lb, 0, d * 4); hipMemset(ids, 1, M * 8);
   hipMemset(sb, 0, 8);
   const __bf16* Wb = (const __bf16*)W;
+  // --head (argv[2] = "head"): the last block's kernel with the SAS head (rs_sas_block_out_head), 3,416 items
+  const bool head = argc > 2 && std::string(argv[2]) == "head";
+  const int G = (int)rc::grid_for(M);
+  void *E, *f, *dx;
+  int64_t *pos, *neg;
+  int* cnt;
+  float *pl, *nl, *dpl, *dnl, *lnpart, *part;
+  hipMalloc(&E, 3417 * d * 2); hipMalloc(&f, M * d * 2); hipMalloc(&dx, M * d * 2);
+  hipMalloc(&pos, M * 8); hipMalloc(&neg, M * 8); hipMalloc(&cnt, G * 8 * 4);
+  hipMalloc(&pl, M * 4); hipMalloc(&nl, M * 4); hipMalloc(&dpl, M * 4); hipMalloc(&dnl, M * 4);
+  hipMalloc(&lnpart, G * 2 * d * 4); hipMalloc(&part, G * 3 * 4);
+  {
+    std::vector<int64_t> ip(M), in(M);
+    for (int64_t i = 0; i < M; ++i) { ip[i] = 1 + (i * 7919) % 3416; in[i] = 1 + (i * 104729) % 3416; }
+    hipMemcpy(pos, ip.data(), M * 8, hipMemcpyHostToDevice);
+    hipMemcpy(neg, in.data(), M * 8, hipMemcpyHostToDevice);
+    std::vector<int> c(G, 96);
+    hipMemcpy(cnt, c.data(), G * 4, hipMemcpyHostToDevice);
+    hipMemset(E, 0x3c, 3417 * d * 2);
+  }
   std::vector<unsigned long long> p(4096 * 8 * 16);
   hipEvent_t e0, e1;
   hipEventCreate(&e0); hipEventCreate(&e1);
@@ -37,14 +58,18 @@ int main(int argc, char** argv) {
   for (int it = 0; it < 20; ++it) {
     hipMemcpyToSymbol(HIP_SYMBOL(rc::g_rc_prof), p.data(), p.size() * 8);   // zero
     hipEventRecord(e0, 0);
-    rs_sas_block_out(M, d, o, Q, Wb, b, x1, lw, lb, 1e-8f, z, mu, rs, Wb + d * d, b, h1, Wb + 2 * d * d, b, xn, ids,
-                     0.2f, 3, 5, sb, 0);
+    if (head)
+      rs_sas_block_out_head(M, d, o, Q, Wb, b, x1, lw, lb, 1e-8f, z, mu, rs, Wb + d * d, b, h1, Wb + 2 * d * d, b, xn,
+                            ids, 0.2f, 3, 5, sb, E, pos, neg, lw, lb, cnt, G, nullptr, f, pl, nl, dpl, dnl, dx,
+                            lnpart, part, 0);
+    else
+      rs_sas_block_out(M, d, o, Q, Wb, b, x1, lw, lb, 1e-8f, z, mu, rs, Wb + d * d, b, h1, Wb + 2 * d * d, b, xn,
+                       ids, 0.2f, 3, 5, sb, 0);
     hipEventRecord(e1, 0);
     hipEventSynchronize(e1);
     hipEventElapsedTime(&ms, e0, e1);
   }
   hipMemcpyFromSymbol(p.data(), HIP_SYMBOL(rc::g_rc_prof), p.size() * 8);
-  const int G = (int)rc::grid_for(M);
   unsigned long long t0 = ~0ull, t1 = 0;
   for (int b_ = 0; b_ < G; ++b_)
     for (int w = 0; w < 8; ++w) {
@@ -75,5 +100,14 @@ int main(int argc, char** argv) {
   pct("GEMM W2 + stores (tile 1)", gb);
   pct("exit after first entry", ex);
   pct("wave lifetime", tot);
+  if (head) {
+    std::vector<double> hd;
+    for (int b_ = 0; b_ < G; ++b_)
+      for (int w = 0; w < 8; ++w) {
+        const unsigned long long* x = &p[((size_t)b_ * 8 + w) * 16];
+        if (x[6] && x[4]) hd.push_back((x[6] - x[4]) * u);
+      }
+    pct("head (tile 1)", hd);
+  }
   return 0;
 }
