@@ -566,11 +566,11 @@ int rs_sas_sample(const int64_t* user_offsets, const int64_t* user_items, int64_
                   int64_t* neg, void* stream);
 /* rs_bert_mask: one BERT4Rec training batch as BertTrainDataset builds it (BS/dataloaders/bert.py:77-110):
  * row b's user = perm[(cursor*batch + b) mod n_users] (perm nullable = identity), its last max_len items
- * cloze-masked (prob mask_prob; then 80 % [MASK] = num_items+1, 10 % a uniform item, 10 % kept;
+ * cloze-masked (prob mask_prob, a double: the reference's Python float; then 80 % [MASK] = num_items+1, 10 % a uniform item, 10 % kept;
  * label = the item, 0 elsewhere), left padded.  state[2] = {step seed, cursor} on the device, both
  * advanced by 1 before sampling (graph-capturable; reset state[1] to 0 at an epoch start). */
 int rs_bert_mask(const int64_t* user_offsets, const int64_t* user_items, int64_t n_users, int64_t num_items,
-                 int64_t batch, int64_t max_len, float mask_prob, const int64_t* perm, uint64_t* state, uint64_t salt,
+                 int64_t batch, int64_t max_len, double mask_prob, const int64_t* perm, uint64_t* state, uint64_t salt,
                  int64_t* tokens, int64_t* labels, void* stream);
 /* The same two samplers, also recording the draws each row consumed (tests replay the reference's construction
  * on them, oracle/sampling.py).  SAS: draws int64 [batch][1 + max_len*256] = {user, then per position the 256
@@ -581,7 +581,7 @@ int rs_sas_sample_draws(const int64_t* user_offsets, const int64_t* user_items, 
                         int64_t batch, int64_t max_len, uint64_t* seed_base, uint64_t salt, int64_t* seq, int64_t* pos,
                         int64_t* neg, int64_t* draws, void* stream);
 int rs_bert_mask_draws(const int64_t* user_offsets, const int64_t* user_items, int64_t n_users, int64_t num_items,
-                       int64_t batch, int64_t max_len, float mask_prob, const int64_t* perm, uint64_t* state,
+                       int64_t batch, int64_t max_len, double mask_prob, const int64_t* perm, uint64_t* state,
                        uint64_t salt, int64_t* tokens, int64_t* labels, int64_t* draws, void* stream);
 
 /* rs_rank_metrics: recalls_ndcgs_and_mrr_for_ks (BS/trainers/utils.py:28-57) over scores/labels

@@ -19,7 +19,7 @@ LIB_PATH = os.path.join(PKG, "librecsys_hip.so" if not os.environ.get("RS_LIB_VA
 
 F32, BF16 = 0, 1
 
-i32, i64, u64, f32, vp = C.c_int, C.c_int64, C.c_uint64, C.c_float, C.c_void_p
+i32, i64, u64, f32, f64, vp = C.c_int, C.c_int64, C.c_uint64, C.c_float, C.c_double, C.c_void_p
 
 
 class Epilogue(C.Structure):
@@ -133,9 +133,9 @@ SIGNATURES = {
                                    vp, i64, vp, i64, f32, u64, vp, vp, vp, i64, vp, vp, vp, vp],
     "rs_transpose_bf16": [i64, vp, i64, vp, vp, vp],
     "rs_sas_sample": [vp, vp, i64, i64, i64, i64, vp, u64, vp, vp, vp, vp],
-    "rs_bert_mask": [vp, vp, i64, i64, i64, i64, f32, vp, vp, u64, vp, vp, vp],
+    "rs_bert_mask": [vp, vp, i64, i64, i64, i64, f64, vp, vp, u64, vp, vp, vp],
     "rs_sas_sample_draws": [vp, vp, i64, i64, i64, i64, vp, u64, vp, vp, vp, vp, vp],
-    "rs_bert_mask_draws": [vp, vp, i64, i64, i64, i64, f32, vp, vp, u64, vp, vp, vp, vp],
+    "rs_bert_mask_draws": [vp, vp, i64, i64, i64, i64, f64, vp, vp, u64, vp, vp, vp, vp],
     "rs_splitk_scatter_rows": [i32, vp, i32, i64, i64, vp, i64, vp, i64, vp],
     "rs_rank_metrics": [vp, vp, i64, i64, i32, vp, vp, vp, vp],
     "rs_kernel_stamps": [vp, vp, i32],

@@ -112,7 +112,7 @@ __global__ void seed_step_kernel(uint64_t* s) {
 // their item with label 0; rows are left padded with 0.  state = {step seed, cursor}, advanced first.
 __global__ __launch_bounds__(256) void bert_mask_kernel(const int64_t* __restrict__ off,
                                                         const int64_t* __restrict__ items, int64_t n_users,
-                                                        int64_t num_items, int T, float p,
+                                                        int64_t num_items, int T, double p,
                                                         const int64_t* __restrict__ perm,
                                                         const uint64_t* __restrict__ state, uint64_t salt,
                                                         int64_t* __restrict__ tokens, int64_t* __restrict__ labels,
@@ -126,8 +126,8 @@ __global__ __launch_bounds__(256) void bert_mask_kernel(const int64_t* __restric
   const int64_t w0 = s0 + L - n, pad = T - n;
   const int64_t mask_token = num_items + 1;
   // the reference's decision (prob = rng.rand(); prob < mask_prob; prob /= mask_prob; < 0.8; < 0.9) in double on
-  // the 24-bit uniform k / 2^24, exactly as Python evaluates it on that value
-  const double pd = (double)p;
+  // the 24-bit uniform k / 2^24, exactly as Python evaluates it on that value (mask_prob arrives as the Python double)
+  const double pd = p;
   // draws (tests): per row {u, then per position (k, the replacement item), -1 on padding}
   int64_t* dr = draws ? draws + b * (1 + 2 * (int64_t)T) : nullptr;
   if (dr && threadIdx.x == 0) dr[0] = u;
@@ -254,9 +254,9 @@ int rs_sas_sample(const int64_t* user_offsets, const int64_t* user_items, int64_
 }
 
 int rs_bert_mask_draws(const int64_t* user_offsets, const int64_t* user_items, int64_t n_users, int64_t num_items,
-                       int64_t batch, int64_t max_len, float mask_prob, const int64_t* perm, uint64_t* state,
+                       int64_t batch, int64_t max_len, double mask_prob, const int64_t* perm, uint64_t* state,
                        uint64_t salt, int64_t* tokens, int64_t* labels, int64_t* draws, void* stream) {
-  if (n_users <= 0 || num_items <= 0 || batch <= 0 || max_len <= 0 || !(mask_prob >= 0.f && mask_prob <= 1.f) ||
+  if (n_users <= 0 || num_items <= 0 || batch <= 0 || max_len <= 0 || !(mask_prob >= 0.0 && mask_prob <= 1.0) ||
       !user_offsets || !user_items || !state || !tokens || !labels)
     return RS_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
@@ -267,7 +267,7 @@ int rs_bert_mask_draws(const int64_t* user_offsets, const int64_t* user_items, i
 }
 
 int rs_bert_mask(const int64_t* user_offsets, const int64_t* user_items, int64_t n_users, int64_t num_items,
-                 int64_t batch, int64_t max_len, float mask_prob, const int64_t* perm, uint64_t* state, uint64_t salt,
+                 int64_t batch, int64_t max_len, double mask_prob, const int64_t* perm, uint64_t* state, uint64_t salt,
                  int64_t* tokens, int64_t* labels, void* stream) {
   return rs_bert_mask_draws(user_offsets, user_items, n_users, num_items, batch, max_len, mask_prob, perm, state, salt,
                             tokens, labels, nullptr, stream);

@@ -27,6 +27,18 @@ them; every element is summed over the same ranks (two ranks: bit for bit the de
 cfg5 on 8 GPUs (1,000,002 x 256 fp32 table, 12,800 token ids per rank): 1,024 MB dense -> at most 102,400 rows x
 1 KB = 105 MB + 0.8 MB of ids.
 
+Sharded table optimizer (ShardedRows): the SAS item table is most of the gradient buffer (cfg4:
+54,543 x 128 fp32 = 27.9 of 28.7 MB) and every rank's Adam over it is the same work.  Instead of the dense all-reduce, the
+table's gradient is REDUCE-SCATTERED (each rank receives the global sum of its 1/N of the table), each rank runs Adam on
+that part only, and the updated compute rows (bf16, or fp32 without a bf16 copy) are ALL-GATHERED back before the next
+forward.  The fp32 master and Adam moments of the other ranks' parts are not kept current on this rank (they stay
+allocated: this is for exchange bytes and optimizer time, not memory); gather_masters() all-gathers them (checkpoints).
+Ring bytes sent per rank and step at cfg4 on 8 GPUs: dense all-reduce 2 x 7/8 x 28.7 MB = 50.2 MB; sharded: 7/8 x 27.9 MB
+reduce-scatter + 7/8 x 14.0 MB bf16 all-gather + 2 x 7/8 x 0.8 MB for the rest = 38.1 MB, and 1/8 of the table's Adam.
+The split is by elements (Adam and the copies are elementwise), in equal 64-element-aligned parts; the table's last few
+elements that do not fill a part ride in the dense all-reduce.  Under gloo (the CPU tests) the reduce-scatter is an
+all-reduce of the region whose own part is then used -- the same values -- since gloo has no reduce-scatter.
+
 The bucket helpers only move tensors (gloo on CPU in the tests); SparseRowExchange's index/pack kernels need the
 HIP library.
 """
@@ -101,11 +113,13 @@ class BucketedExchange:
     all-reduce asynchronously; finish() waits for every launched one (on the current stream for
     NCCL/RCCL: no host block) and checks that every bucket went out exactly once."""
 
-    def __init__(self, flat_grad, buckets, group=None, partial=False):
+    def __init__(self, flat_grad, buckets, group=None, partial=False, extra=None):
         """buckets: {tag: (lo, hi) or [(lo, hi), ...]}.  partial: the buckets may leave parts of the buffer out
-        (rank-owned regions, e.g. a vocabulary shard, or a table exchanged by SparseRowExchange); else they must
-        cover it."""
+        (rank-owned regions, e.g. a vocabulary shard, or a table exchanged by SparseRowExchange / ShardedRows); else
+        they must cover it.  extra: {tag: callable() -> work or None}, a further collective issued with that tag's
+        all-reduce (ShardedRows.scatter)."""
         self.flat_grad = flat_grad
+        self.extra = dict(extra or {})
         self.buckets = {t: ([r] if isinstance(r, tuple) else list(r)) for t, r in dict(buckets).items()}
         self.group = group
         spans = sorted(x for rs in self.buckets.values() for x in rs)
@@ -121,6 +135,10 @@ class BucketedExchange:
         self.sent.append(tag)
         for lo, hi in self.buckets[tag]:
             self.works.append(dist.all_reduce(self.flat_grad[lo:hi], group=self.group, async_op=True))
+        if tag in self.extra:
+            w = self.extra[tag]()
+            if w is not None:
+                self.works.append(w)
 
     def finish(self):
         assert sorted(self.sent) == sorted(self.buckets), (self.sent, list(self.buckets))
@@ -200,3 +218,105 @@ class SparseRowExchange:
 
     def unpack(self):
         self.ops.rows_unpack(self.g, self.index, self.compact)
+
+
+class ShardedRows:
+    """Reduce-scatter / rank-local Adam / all-gather of one table of a FlatParams buffer (see the module docstring).
+
+    The table's elements [lo, hi) (hi = lo + N x part, the largest N-fold multiple of 64 elements inside the table)
+    are cut into N equal parts; rank r owns [lo + r part, lo + (r + 1) part).  Per step: scatter() (collective, with
+    the dense all-reduce) -> Adam over ranges() -> zero_foreign() -> gather() (collective) of the compute copy."""
+
+    ALIGN = 64
+
+    def __init__(self, flat, name, group=None):
+        self.flat = flat
+        self.name = name
+        self.group = group
+        self.W = world(group)
+        self.rank = dist.get_rank(group) if self.W > 1 else 0
+        self.lo = flat.offsets[name]
+        n = 1
+        for s in flat.shapes[name]:
+            n *= s
+        self.table_end = self.lo + n
+        A = self.ALIGN
+        assert self.lo % A == 0, self.lo
+        self.part = (n // (self.W * A)) * A
+        self.hi = self.lo + self.W * self.part
+        self.own = (self.lo + self.rank * self.part, self.lo + (self.rank + 1) * self.part)
+        self.nccl = backend(group) == "nccl"
+
+    @staticmethod
+    def worthwhile(numel, n_ranks):
+        """Shard when every rank's part is at least 64k elements (smaller tables: the extra collective's latency
+        outweighs the bytes)."""
+        return n_ranks > 1 and numel // n_ranks >= 65536
+
+    def foreign(self):
+        """The sharded region's ranges this rank does not own."""
+        a, b = self.own
+        return [(x, y) for x, y in ((self.lo, a), (b, self.hi)) if y > x]
+
+    def dense_ranges(self, total):
+        """[0, total) without the sharded region (what the all-reduce and the full-buffer optimizer launch cover)."""
+        return [(x, y) for x, y in ((0, self.lo), (self.hi, total)) if y > x]
+
+    def adam_ranges(self, total):
+        """The optimizer's ranges: the dense parts first (the first launch prepares the step's scalars and writes the
+        transposed block weights: it must cover them), then the owned part."""
+        return self.dense_ranges(total) + [self.own]
+
+    @classmethod
+    def ring_bytes(cls, total, table, n_ranks, compute_bytes):
+        """(dense all-reduce bytes, sharded-table bytes) sent per rank and step by ring collectives: a buffer of
+        `total` fp32 elements holding a `table`-element table whose compute copy has `compute_bytes` bytes per
+        element.  Sharded: reduce-scatter (fp32) + all-gather (compute copy) of the parts, all-reduce of the rest."""
+        f = (n_ranks - 1) / n_ranks
+        sharded = n_ranks * ((table // (n_ranks * cls.ALIGN)) * cls.ALIGN)
+        return 2 * f * total * 4, f * sharded * (4 + compute_bytes) + 2 * f * (total - sharded) * 4
+
+    def bytes_per_step(self):
+        """ring_bytes for this buffer and table."""
+        f = self.flat
+        return self.ring_bytes(f.numel, self.table_end - self.lo, self.W, 2 if f.bf16 is not None else 4)
+
+    def scatter(self, async_op=True):
+        """Reduce-scatter(SUM) of the sharded region of the gradient, in place: the owned part receives the global
+        sum (RCCL: reduce_scatter_tensor; gloo: an all-reduce of the region)."""
+        g = self.flat.grad
+        if self.nccl:
+            a, b = self.own
+            return dist.reduce_scatter_tensor(g[a:b], g[self.lo:self.hi], group=self.group, async_op=async_op)
+        return dist.all_reduce(g[self.lo:self.hi], group=self.group, async_op=async_op)
+
+    def zero_foreign(self):
+        """Clear the gradient outside the owned part (the optimizer clears the owned part): the next backward
+        accumulates into zeros."""
+        for a, b in self.foreign():
+            self.flat.grad[a:b].zero_()
+
+    def gather(self, buf):
+        """All-gather of the sharded region of `buf` (every rank contributes its owned part), in place."""
+        a, b = self.own
+        full = buf[self.lo:self.hi]
+        if self.nccl:
+            dist.all_gather_into_tensor(full, buf[a:b], group=self.group)
+        else:
+            dist.all_gather(list(full.view(self.W, self.part).unbind(0)), buf[a:b].clone(), group=self.group)
+
+    def gather_compute(self):
+        """The step's all-gather: the rows the forward reads (the bf16 copy when there is one, else the master)."""
+        f = self.flat
+        self.gather(f.bf16 if f.bf16 is not None else f.data)
+
+    def gather_masters(self, bufs):
+        """All-gather the sharded region of each fp32 buffer (master weights, Adam moments): afterwards every rank
+        holds the full, current table (collective)."""
+        for b in bufs:
+            self.gather(b)
+
+    def stale_ranges(self):
+        """Ranges of the fp32 master that are not current on this rank after a step (bf16 copy: the foreign parts;
+        fp32 compute: none -- the master itself is gathered)."""
+        return self.foreign() if self.flat.bf16 is not None else []

@@ -39,6 +39,9 @@ class FlatParams:
         self.grad = torch.zeros(self.numel + AUX, dtype=torch.float32, device=self.device)
         self.aux = self.grad[self.numel:]
         self.bf16 = None
+        # ranges of the fp32 master that are not current on this rank (a data-parallel step that shards a table's
+        # optimizer, dp.ShardedRows: the compute copy of those rows was all-gathered, the master was not)
+        self.stale = []
         for n, p in named:
             if p.dtype != torch.float32:
                 raise TypeError(f"parameter {n} must be fp32 (master weights), got {p.dtype}")

@@ -170,8 +170,16 @@ class SASEngine:
 
     # compute-dtype weights
     def sync_compute_weights(self):
-        if self.flat.bf16 is not None:
-            ops.cast_bf16(self.flat.data, self.flat.bf16)
+        f = self.flat
+        if f.bf16 is not None:
+            if not f.stale:
+                ops.cast_bf16(f.data, f.bf16)
+            else:   # the compute copy of stale master rows (a sharded item table) is the current one: keep it
+                a = 0
+                for lo, hi in sorted(f.stale) + [(f.numel, f.numel)]:
+                    if lo > a:
+                        ops.cast_bf16(f.data[a:lo], f.bf16[a:lo])
+                    a = max(a, hi)
             if self._wT is not None:
                 self._refresh_transposed()
 

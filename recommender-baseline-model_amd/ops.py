@@ -327,10 +327,11 @@ def adam_step(p, g, m, v, p_bf16, state, hyper, zero_grad=False, max_wg=None):
 
 
 def adam_prepare_step(p, g, m, v, p_bf16, state, hyper, zero_grad=False, grad_divisor=None, seed_base=None,
-                      transposed=None, loss_sum=None, loss_out=None):
+                      transposed=None, loss_sum=None, loss_out=None, tbase=0):
     """adam_prepare + adam_step in one launch (state: double[144]; state[7], state[16 + 16 k] arrival counters).
     transposed: (desc int64 device [n][6] as transpose_bf16's, its host copy, dst bf16 tensor) -- the bf16
-    result of those matrices is also written transposed (p[0] is element 0 of the flat buffer)."""
+    result of those matrices is also written transposed; the descriptors' offsets are flat-buffer elements and
+    p[0] is element `tbase` of the flat buffer (every matrix must lie inside [tbase, tbase + p.numel()))."""
     if state.numel() < 144:
         raise ValueError("adam_prepare_step needs the 144-entry optimizer state")
     td, nt, wt = None, 0, None
@@ -338,18 +339,18 @@ def adam_prepare_step(p, g, m, v, p_bf16, state, hyper, zero_grad=False, grad_di
         td, host, wt = transposed
         nt = len(host)
         for rows, cols, off, lds, doff, ldd in host:
-            if lds % 4 or off % 4 or off + rows * lds > (p.numel() // 4) * 4 or doff + (cols - 1) * ldd + rows > wt.numel() \
-                    or rows * lds >= 2 ** 31:
+            if lds % 4 or off % 4 or tbase % 4 or off < tbase or off + rows * lds > tbase + (p.numel() // 4) * 4 \
+                    or doff + (cols - 1) * ldd + rows > wt.numel() or rows * lds >= 2 ** 31:
                 raise ValueError("adam_prepare_step: transposed matrix outside the buffers or misaligned")
         if p_bf16 is None:
             raise ValueError("adam_prepare_step: transposed copies need the bf16 output")
     if loss_out is not None:   # + loss_out = loss_sum / grad_divisor in the same launch
         call("rs_adam_prepare_step_loss", p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), ptr(p_bf16), ptr(state),
-             ptr(hyper), int(zero_grad), ptr(grad_divisor), ptr(seed_base), ptr(td), nt, 0, ptr(wt), ptr(loss_sum),
+             ptr(hyper), int(zero_grad), ptr(grad_divisor), ptr(seed_base), ptr(td), nt, int(tbase), ptr(wt), ptr(loss_sum),
              ptr(loss_out), stream())
         return
     call("rs_adam_prepare_step", p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), ptr(p_bf16), ptr(state), ptr(hyper),
-         int(zero_grad), ptr(grad_divisor), ptr(seed_base), ptr(td), nt, 0, ptr(wt), stream())
+         int(zero_grad), ptr(grad_divisor), ptr(seed_base), ptr(td), nt, int(tbase), ptr(wt), stream())
 
 
 L2_CHUNK = 16384

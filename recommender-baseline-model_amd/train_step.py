@@ -56,9 +56,11 @@ class FusedAdam:
         """One Adam update; also clears the gradient buffer (the next step accumulates from zero) and
         advances the dropout step seed when given.  ranges: [(lo, hi)] flat slices to update (default all; a
         vocabulary-sharded rank skips the output rows other ranks own).  loss = (sum, out): out = sum / grad_divisor
-        in the first launch.  keep = (lo, hi): a slice the backward OVERWRITES every step (BERT's out.weight /
-        out.bias with a large vocabulary): updated by its own launch that leaves its gradient in place -- no zero
-        written by this sweep, none read back by the next step's dE GEMM (2 GB per step at 1M items)."""
+        in the first launch.  transposed (the SAS block weights' transposed bf16 copies) rides in the first range's
+        launch, which must cover those matrices.  keep = (lo, hi): a slice the backward OVERWRITES every step
+        (BERT's out.weight / out.bias with a large vocabulary): updated by its own launch that leaves its gradient
+        in place -- no zero written by this sweep, none read back by the next step's dE GEMM (2 GB per step at 1M
+        items)."""
         f = self.flat
         segs = [(lo, hi, True) for lo, hi in (ranges or [(0, f.numel)])]
         if keep is not None and ranges is None:
@@ -70,7 +72,7 @@ class FusedAdam:
             if k == 0:   # the first range's launch also prepares the step's scalars (rs_adam_prepare_step)
                 ops.adam_prepare_step(f.data[lo:hi], f.grad[lo:hi], self.m[lo:hi], self.v[lo:hi], bf, self.state,
                                       self.hyper, zero_grad=zg, grad_divisor=grad_divisor, seed_base=seed_base,
-                                      transposed=transposed if lo == 0 else None,
+                                      transposed=transposed, tbase=lo,
                                       loss_sum=loss[0] if loss else None, loss_out=loss[1] if loss else None)
             else:
                 ops.adam_step(f.data[lo:hi], f.grad[lo:hi], self.m[lo:hi], self.v[lo:hi], bf, self.state,
@@ -143,7 +145,7 @@ class FusedStepLR:
 
 class FusedTrainStep:
     def __init__(self, model, lr=1e-3, weight_decay=0.0, process_group=None, dp=None, max_labelled=None,
-                 bucket_numel=None, overlap=None, vocab_shard=False, sparse_rows="auto"):
+                 bucket_numel=None, overlap=None, vocab_shard=False, sparse_rows="auto", shard_rows="auto"):
         """model: rbm_amd SASModel or BERTModel on a CUDA device.
         dp: data-parallel mode (default: torch.distributed initialised with world size > 1).
         max_labelled (BERT): upper bound on labelled rows per batch (sizes the compacted
@@ -153,7 +155,12 @@ class FusedTrainStep:
         vocab_shard (BERT, DP): out.weight / out.bias sharded over the ranks (rbm_amd.vocab_parallel).
         sparse_rows (BERT, DP with overlap): "auto" (default: when the gathered ids are at most half the table),
         "on" or "off" -- the token table's gradient is exchanged as the union of the rows the ranks touched
-        (dp.SparseRowExchange) instead of inside the dense buckets."""
+        (dp.SparseRowExchange) instead of inside the dense buckets.
+        shard_rows (SAS, DP): "auto" (default: when each rank's part of the item table is >= 64k elements), "on" or
+        "off" -- the item table's optimizer is sharded over the ranks (dp.ShardedRows): its gradient is
+        reduce-scattered, each rank updates its part, the compute rows are all-gathered.  The other ranks' parts of
+        the fp32 master and Adam moments are then not current on this rank: checkpoint() / gather_shards() gather
+        them (needs l2_emb == 0: the regulariser reads every master row)."""
         self.model = model
         self.kind = model.code()
         self.engine = model.sas.engine() if self.kind == "sas" else model.engine()
@@ -199,8 +206,23 @@ class FusedTrainStep:
         self.static = None
         self.steps_per_graph = 1
         self._stamps = None
-        self.exchange = dpx.BucketedExchange(self.flat.grad, self._buckets(), self.pg, partial=self.vshard is not None) \
-            if self.overlap else None
+        self.rshard = None
+        if self.dp and self.kind == "sas" and shard_rows != "off":
+            name = "item_emb.weight"
+            n = self.flat.view(name).numel()
+            if shard_rows == "on" or dpx.ShardedRows.worthwhile(n, dpx.world(self.pg)):
+                if self.l2:
+                    if shard_rows == "on":
+                        raise ValueError("shard_rows needs l2_emb == 0 (the regulariser reads every master row)")
+                else:
+                    self.rshard = dpx.ShardedRows(self.flat, name, self.pg)
+        self.exchange = None
+        if self.overlap:
+            b, extra = self._buckets(), None
+            if self.rshard is not None:
+                b, extra = dpx.carve(b, self.rshard.lo, self.rshard.hi), {"final": self.rshard.scatter}
+            self.exchange = dpx.BucketedExchange(self.flat.grad, b, self.pg, extra=extra,
+                                                 partial=self.vshard is not None or self.rshard is not None)
         # Under DP over RCCL the collectives are captured INSIDE the step graph (RCCL collectives are graph
         # capturable; thread-local capture mode lets the process group's watchdog poll meanwhile), so a replay is
         # forward + backward + exchange + Adam with no host round trip, and several steps unroll into one graph as
@@ -350,10 +372,18 @@ class FusedTrainStep:
         write_aux()
 
     def _exchange(self):
-        if self.dp:
+        if not self.dp:
+            return
+        if self.rshard is None:
             dpx.allreduce_grads(self.flat.grad, self.pg, self.bucket_numel)
+            return
+        for lo, hi in self.rshard.dense_ranges(self.flat.grad.numel()):
+            dpx.allreduce_grads(self.flat.grad[lo:hi], self.pg, self.bucket_numel)
+        self.rshard.scatter(async_op=False)
 
     def _adam_ranges(self):
+        if self.rshard is not None:
+            return self.rshard.adam_ranges(self.flat.numel)
         if self.vshard is None:
             return None
         f, vs = self.flat, self.vshard
@@ -369,7 +399,9 @@ class FusedTrainStep:
         if self.l2:
             ops.l2_penalty(self.flat.data, self.flat.grad, self.l2_desc, self.l2, self.l2_ws, loss=loss, scale=scale)
 
-    def _update(self):
+    def _update(self, post=True):
+        """The optimizer (graph-capturable).  post: then the sharded item table's all-gather (_post_update; a
+        collective -- the segmented DP graphs run it eagerly after the optimizer's graph instead)."""
         sb = self.engine.seed_base
         if self.vshard is not None:
             # the sharded head normalised by the global count already; the loss is the global batch's
@@ -380,12 +412,18 @@ class FusedTrainStep:
             kp = self.engine.overwritten_grads() if hasattr(self.engine, "overwritten_grads") else None
             if self.dp:
                 lsum, cnt = self.flat.aux[dpx.LOSS_SUM:dpx.LOSS_SUM + 1], self.flat.aux[dpx.COUNT:dpx.COUNT + 1]
+                rg = self._adam_ranges()
                 if self.l2:
                     torch.div(lsum, cnt, out=self.loss_val)
                     self._l2(self.loss_val, scale=cnt)
-                    self.opt.step(grad_divisor=cnt, seed_base=sb, transposed=tr, keep=kp)
+                    self.opt.step(grad_divisor=cnt, seed_base=sb, transposed=tr, keep=kp, ranges=rg)
                 else:   # the loss division rides in the optimizer's launch
-                    self.opt.step(grad_divisor=cnt, seed_base=sb, transposed=tr, loss=(lsum, self.loss_val), keep=kp)
+                    self.opt.step(grad_divisor=cnt, seed_base=sb, transposed=tr, loss=(lsum, self.loss_val), keep=kp,
+                                  ranges=rg)
+                if self.rshard is not None:
+                    self.rshard.zero_foreign()
+                    if post:
+                        self._post_update()
             elif self._early_ev is not None:
                 assert tr is None and kp in (None, self._early_kp), (kp, self._early_kp)
                 cur = torch.cuda.current_stream()
@@ -396,6 +434,12 @@ class FusedTrainStep:
             else:
                 self._l2(self.loss_out[2:3])
                 self.opt.step(seed_base=sb, transposed=tr, keep=kp)
+
+    def _post_update(self):
+        """Sharded item table: all-gather the updated compute rows; the other ranks' master rows are stale now."""
+        if self.rshard is not None:
+            self.rshard.gather_compute()
+            self.flat.stale = self.rshard.stale_ranges()
 
     # max workgroups of the early out.weight update: a bounded share of the CUs beside the encoder's backward.  cfg5
     # (two interleaved rounds, seq/s): end of step 6,776 / 6,607; early on 128 workgroups 6,573 / 6,444, 256: 7,184 /
@@ -463,8 +507,32 @@ class FusedTrainStep:
     def replicas_equal(self):
         """Data parallel: True iff every rank holds the same parameter bits (collective; call on every rank).  The
         replicas start equal and every step applies the same all-reduced gradient, so a difference means an
-        exchange went wrong (bench.py checks it after its warmup)."""
-        return dpx.replicas_equal(self.flat.data, self.pg) if self.dp else True
+        exchange went wrong (bench.py checks it after its warmup).  Sharded item table: the master outside the
+        table and the table's all-gathered compute rows (what every rank's next forward reads)."""
+        if not self.dp:
+            return True
+        if self.rshard is None:
+            return dpx.replicas_equal(self.flat.data, self.pg)
+        f, rs = self.flat, self.rshard
+        cb = f.bf16 if f.bf16 is not None else f.data
+        oks = [dpx.replicas_equal(f.data[a:b], self.pg) for a, b in rs.dense_ranges(f.numel)]
+        oks.append(dpx.replicas_equal(cb[rs.lo:rs.hi], self.pg))
+        return all(oks)
+
+    def gather_shards(self):
+        """Make this rank's parameters and Adam moments whole: the vocabulary shards (gather_vocab_shards) and the
+        sharded item table's master / moment rows.  Collective: call on every rank."""
+        self.gather_vocab_shards()
+        if self.rshard is not None:
+            torch.cuda.synchronize()
+            self.rshard.gather_masters([self.flat.data, self.opt.m, self.opt.v])
+            self.flat.stale = []
+
+    def masters_loaded(self):
+        """Call after writing the parameters directly (model.load_state_dict on every rank): the fp32 masters are
+        whole and current again, and the compute copy is re-derived from them."""
+        self.flat.stale = []
+        self.engine.sync_compute_weights()
 
     # ---------------------------------------------------------------- checkpoints
     def _param_slices(self):
@@ -483,6 +551,8 @@ class FusedTrainStep:
         """The optimizer state in torch.optim.Adam's state_dict() layout (param_groups from a real Adam over
         the same parameters; per-parameter 'step', 'exp_avg', 'exp_avg_sq'), so the reference trainer can
         resume from it (BS/trainers/base.py:255-259, 'optimizer_state_dict')."""
+        if self.rshard is not None:
+            self.gather_shards()
         torch.cuda.synchronize()
         hy = self.opt.hyper.cpu().tolist()
         ref = torch.optim.Adam(self.model.parameters(), lr=hy[0], betas=(hy[1], hy[2]), eps=hy[3], weight_decay=hy[4])
@@ -531,8 +601,8 @@ class FusedTrainStep:
 
     def checkpoint(self, epoch=None):
         """{'model_state_dict', 'optimizer_state_dict'[, 'epoch']} as the reference's loggers save it
-        (BS/trainers/base.py:255-259, BS/loggers.py:48-58).  Vocabulary-sharded: collective (all ranks)."""
-        self.gather_vocab_shards()
+        (BS/trainers/base.py:255-259, BS/loggers.py:48-58).  Sharded (vocabulary / item table): collective."""
+        self.gather_shards()
         d = {"model_state_dict": self.model.state_dict(), "optimizer_state_dict": self.optimizer_state_dict()}
         if epoch is not None:
             d["epoch"] = epoch
@@ -540,7 +610,7 @@ class FusedTrainStep:
 
     def load_checkpoint(self, d):
         self.model.load_state_dict(d["model_state_dict"])
-        self.engine.sync_compute_weights()
+        self.masters_loaded()
         self.load_optimizer_state_dict(d["optimizer_state_dict"])
 
     # ---------------------------------------------------------------- HIP graphs
@@ -731,7 +801,7 @@ class FusedTrainStep:
         if self.dp:
             self.g_update = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g_update, capture_error_mode=CAPTURE_MODE):
-                self._update()
+                self._update(post=False)
         segs = [seg[0] for seg in self.g_segments if seg[0] is not None] if self.g_segments else [self.g_compute]
         self.graphs = tuple(segs) + ((self.g_update,) if self.dp else ())
 
@@ -787,6 +857,8 @@ class FusedTrainStep:
     def _replay_graphs(self):
         if self.graph_collectives:
             self.g_compute.replay()
+            if self.rshard is not None:
+                self.flat.stale = self.rshard.stale_ranges()
             return self.loss_steps if self.steps_per_graph > 1 else self.loss_val
         if self.overlap:
             for g, tag, action in self.g_segments:
@@ -798,6 +870,7 @@ class FusedTrainStep:
                     self.exchange.launch(tag)  # RCCL all-reduce of the bucket, overlapping the next segment
             self.exchange.finish()
             self.g_update.replay()
+            self._post_update()
             return self.loss_val
         self.g_compute.replay()
         if self.steps_per_graph > 1:
@@ -805,6 +878,7 @@ class FusedTrainStep:
         if self.dp:
             self._exchange()            # RCCL all-reduce, eager, on the current stream
             self.g_update.replay()
+            self._post_update()
         return self.loss_val if self.dp else self.loss_out[2:3]
 
     def capture_sampled(self, sampler, warmup=2, stamps=None, steps_per_graph=1):

@@ -225,3 +225,83 @@ def test_sparse_exchange_sizing():
     assert not dp.SparseRowExchange.worthwhile(54_543, 128 * 50 * 3, 8)     # SAS cfg4 item table: dense
     cap = min(rows, 8 * n)
     assert cap * d * 4 == 104_857_600 and rows * d * 4 == 1_024_002_048
+
+
+def _rows_worker(rank, world, port, out_dir):
+    import sys
+    sys.path.insert(0, ROOT)
+    import rbm_amd  # noqa: F401
+    from rbm_amd import dp
+    from rbm_amd.flat import FlatParams
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.manual_seed(0)
+        mod = torch.nn.Module()
+        mod.item_emb = torch.nn.Embedding(1001, 3)          # 3,003 elements: 1,003 of them past the N x 64 parts
+        mod.lin = torch.nn.Linear(5, 7)
+        flat = FlatParams(mod, "cpu")
+        rs = dp.ShardedRows(flat, "item_emb.weight")
+        g = torch.Generator().manual_seed(rank)
+        flat.grad.copy_(torch.randn(flat.grad.numel(), generator=g))
+        ref = flat.grad.clone()
+        dist.all_reduce(ref)
+        ex = dp.BucketedExchange(flat.grad, dp.carve({"final": (0, flat.grad.numel())}, rs.lo, rs.hi), partial=True,
+                                 extra={"final": rs.scatter})
+        ex.launch("final")
+        ex.finish()
+        a, b = rs.own
+        got = {"own": (a, b), "lo": rs.lo, "hi": rs.hi, "dense": rs.dense_ranges(flat.numel),
+               "adam": rs.adam_ranges(flat.numel), "foreign": rs.foreign(),
+               "grad_own": flat.grad[a:b].clone(), "ref": ref}
+        rs.zero_foreign()
+        got["zeroed"] = all(bool((flat.grad[x:y] == 0).all()) for x, y in rs.foreign())
+        got["grad_dense"] = rs.dense_ranges(flat.grad.numel())
+        got["dense_grads"] = [flat.grad[x:y].clone() for x, y in got["grad_dense"]]
+        # the owner's update: each rank writes only its part, then the gather makes the region whole everywhere
+        flat.data[rs.lo:rs.hi] = -1.0
+        flat.data[a:b] = torch.arange(a, b, dtype=torch.float32)
+        rs.gather(flat.data)
+        got["data"] = flat.data[rs.lo:rs.hi].clone()
+        torch.save(got, os.path.join(out_dir, f"w{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_rows_scatter_gather(tmp_path, world):
+    """dp.ShardedRows (the sharded item-table optimizer of the SAS DP step): equal 64-aligned parts tile the sharded
+    region; after the exchange each rank's part holds the global gradient sum and the dense ranges (the table's tail
+    included) the all-reduced values; zero_foreign clears the rest; gather assembles the owners' parts everywhere."""
+    mp.spawn(_rows_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    parts = []
+    for r in range(world):
+        d = torch.load(tmp_path / f"w{r}.pt", weights_only=True)
+        a, b = d["own"]
+        parts.append((a, b))
+        assert (b - a) % 64 == 0 and b - a == (3003 // (world * 64)) * 64
+        # two ranks: a + b in either collective; three: gloo may associate the sums differently per buffer size
+        same = torch.equal if world == 2 else (lambda x, y: torch.allclose(x, y, rtol=1e-6, atol=1e-6))
+        assert same(d["grad_own"], d["ref"][a:b])
+        assert d["dense"][0] == (d["hi"], d["dense"][0][1]) and d["lo"] == 0
+        assert d["adam"] == d["dense"] + [(a, b)]
+        assert d["zeroed"]
+        assert d["grad_dense"][-1][1] == d["ref"].numel()          # the aux tail rides in the dense all-reduce
+        for got, (x, y) in zip(d["dense_grads"], d["grad_dense"]):
+            assert same(got, d["ref"][x:y])
+        assert torch.equal(d["data"], torch.arange(d["lo"], d["hi"], dtype=torch.float32))
+    assert parts[0][0] == 0 and all(p[1] == q[0] for p, q in zip(parts, parts[1:]))
+
+
+def test_sharded_rows_sizing():
+    """The cfg4 exchange (SAS, 54,543 x 128 item table, 8 GPUs) with the sharded item-table optimizer against the dense
+    all-reduce: ring bytes sent per rank and step."""
+    import sys
+    sys.path.insert(0, ROOT)
+    from rbm_amd import dp
+    n_item = 54_543 * 128
+    assert dp.ShardedRows.worthwhile(n_item, 8) and not dp.ShardedRows.worthwhile(n_item, 1)
+    assert not dp.ShardedRows.worthwhile(501 * 64, 2)
+    total = 7_187_328                        # the cfg4 flat buffer (fp32 elements, FlatParams layout)
+    dense, sharded = dp.ShardedRows.ring_bytes(total, n_item, 8, 2)
+    assert 50.0e6 < dense < 50.5e6 and 37.5e6 < sharded < 38.5e6, (dense, sharded)

@@ -220,3 +220,44 @@ def test_dp_large_vocab_unzeroed_head_grads_equal_zeroed(nccl_group):
         res.append((losses, tr.flat.data.detach().cpu().clone()))
     assert res[0][0] == res[1][0]
     assert torch.equal(res[0][1], res[1][1])
+
+
+def test_dp_sharded_item_table_equals_dense_rccl(nccl_group, monkeypatch):
+    """The sharded item-table optimizer (dp.ShardedRows: in-place RCCL reduce_scatter_tensor of the table's gradient,
+    Adam over the owned part, in-place all_gather_into_tensor of the bf16 rows) through RCCL -- eager, segmented
+    graphs, the collectives captured in the step graph, and two steps unrolled into one graph -- against the dense
+    all-reduce step: bit-identical losses and parameters (world size 1 here: the two-rank form against the oracle is
+    tests/test_dp_multirank_gpu.py::test_two_rank_sharded_item_table)."""
+    import rbm_amd  # noqa: F401
+    from rbm_amd.models import model_factory
+    from rbm_amd.train_step import FusedTrainStep
+    batches = _batches("sas", 4)
+    res = []
+    runs = (("off", "1", 1), ("on", "0", 1), ("on", "1", 1), ("on", "1", 2), ("off", None, 1), ("on", None, 1))
+    for shard, mode, S in runs:
+        monkeypatch.setenv("RS_DP_GRAPH_COLLECTIVES", mode or "1")
+        torch.manual_seed(5)
+        a = argparse.Namespace(model_code="sas", num_items=500, max_len=50, device="cuda", sas_hidden_units=128,
+                               sas_num_blocks=2, sas_heads=1, sas_dropout=0.1, l2_emb=0.0, rs_dtype="bf16")
+        tr = FusedTrainStep(model_factory(a), lr=1e-3, dp=True, shard_rows=shard)
+        assert (tr.rshard is not None) == (shard == "on")
+        if mode is None:                       # eager steps
+            losses = [float(tr.step(*b).item()) for b in batches]
+        else:
+            tr.capture(*batches[0], steps_per_graph=S)
+            if S == 1:
+                losses = [float(tr.replay(*b).item()) for b in batches]
+            else:
+                losses = []
+                for j in range(0, len(batches), S):
+                    packed = torch.stack([torch.stack(b) for b in batches[j:j + S]])
+                    losses += [float(x) for x in tr.replay_packed(packed).cpu()]
+        assert tr.replicas_equal()
+        tr.gather_shards()
+        torch.cuda.synchronize()
+        res.append((losses, tr.flat.data.detach().cpu().clone(), tr.flat.bf16.detach().cpu().clone()))
+    # the captured forms (warm-up steps before the measured ones) against the captured dense step; eager against eager
+    for k, ref in ((1, 0), (2, 0), (3, 0), (5, 4)):
+        assert res[k][0] == res[ref][0], (runs[k], res[k][0], res[ref][0])
+        assert torch.equal(res[k][1], res[ref][1]), runs[k]
+        assert torch.equal(res[k][2], res[ref][2]), runs[k]

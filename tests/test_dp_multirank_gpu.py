@@ -63,13 +63,13 @@ def _valid(kind, b):
 def _reset(tr, sd):
     """Back to the initial weights and a fresh optimizer (capture() ran warm-up steps)."""
     tr.model.load_state_dict(sd)
-    tr.engine.sync_compute_weights()
+    tr.masters_loaded()
     tr.opt.m.zero_()
     tr.opt.v.zero_()
     tr.opt.state.zero_()
 
 
-def _worker(rank, world, port, kind, dtype, out_dir):
+def _worker(rank, world, port, kind, dtype, out_dir, shard="off", l2=0.01):
     import sys
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
@@ -82,11 +82,12 @@ def _worker(rank, world, port, kind, dtype, out_dir):
         local = [tuple(torch.from_numpy(x).cuda() for x in b[rank]) for b in batches]
         out = {}
         for graph, overlap in MODES:
-            m = _model(kind, dtype)
+            m = _model(kind, dtype, l2=l2)
             sd0 = {k: v.detach().clone() for k, v in m.state_dict().items()}
             tr = FusedTrainStep(m, lr=1e-3, dp=True, overlap=overlap, bucket_numel=None if overlap else 1 << 30,
-                                max_labelled=BR * T if kind == "bert" else None)
+                                max_labelled=BR * T if kind == "bert" else None, shard_rows=shard)
             assert (tr.exchange is not None) == overlap
+            assert (tr.rshard is not None) == (shard == "on")
             if graph:
                 tr.capture(*local[0])
                 _reset(tr, sd0)
@@ -95,9 +96,14 @@ def _worker(rank, world, port, kind, dtype, out_dir):
                 losses.append(float((tr.replay(*b) if graph else tr.step(*b)).item()))
                 counts.append(float(tr.flat.aux[dpx.COUNT].item()))
             torch.cuda.synchronize()
-            out[f"{int(graph)}{int(overlap)}"] = {
-                "losses": losses, "counts": counts,
-                "sd": {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}}
+            rec = {"losses": losses, "counts": counts, "equal": tr.replicas_equal(),
+                   "stale": [list(r) for r in tr.flat.stale]}
+            tr.gather_shards()                 # the sharded item table's master / moment rows made whole
+            rec["sd"] = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+            rec["m"], rec["v"] = tr.opt.m.cpu().clone(), tr.opt.v.cpu().clone()
+            if tr.flat.bf16 is not None:
+                rec["bf16"] = tr.flat.bf16.float().cpu()
+            out[f"{int(graph)}{int(overlap)}"] = rec
         torch.save(out, os.path.join(out_dir, f"r{rank}.pt"))
     finally:
         dist.destroy_process_group()
@@ -268,3 +274,55 @@ def test_two_rank_gradient_equals_oracle(tmp_path, kind, dtype, overlap):
         worst = max(errs, key=errs.get)
         print(f"bert bf16: worst gradient {worst} {errs[worst]:.3g}")
         assert errs[worst] < 3e-2, (worst, errs[worst])
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# Sharded item-table optimizer (dp.ShardedRows, the cfg4 exchange): reduce-scatter of the table's gradient (gloo: an
+# all-reduce of the region, the same sums), Adam on each rank's half, all-gather of the compute rows.  With two ranks
+# every element's sum is a + b either way, so the sharded step must equal the dense-all-reduce DP step BIT FOR BIT
+# (weights, Adam moments after gather_shards, the bf16 compute copy), and -- fp32 -- the reference's single-device
+# step on the concatenated batch: the oracle's float64 loss and gradients (oracle/sas.py) + AdamOracle (the
+# reference's torch.optim.Adam, BS/trainers/base.py:225-228), BS/trainers/sas.py:49 for the global-batch mean.
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_two_rank_sharded_item_table(tmp_path, dtype):
+    world = 2
+    runs = {}
+    for shard in ("on", "off"):
+        d = tmp_path / shard
+        d.mkdir()
+        mp.spawn(_worker, args=(world, _free_port(), "sas", dtype, str(d), shard, 0.0), nprocs=world, join=True)
+        runs[shard] = [torch.load(d / f"r{r}.pt", weights_only=True) for r in range(world)]
+    on, off = runs["on"], runs["off"]
+    for mode in on[0]:
+        a, b, c = on[0][mode], on[1][mode], off[0][mode]
+        assert a["equal"] and b["equal"] and c["equal"], mode
+        if dtype == "bf16":       # the other rank's half of the fp32 master is stale until gather_shards
+            assert a["stale"] and b["stale"] and a["stale"] != b["stale"], (mode, a["stale"], b["stale"])
+        assert a["losses"] == b["losses"] == c["losses"], (mode, a["losses"], c["losses"])
+        for k in c["sd"]:
+            assert torch.equal(a["sd"][k], b["sd"][k]), (mode, k)
+            assert torch.equal(a["sd"][k], c["sd"][k]), (mode, k)          # sharded == dense exchange, bitwise
+        for key in ("m", "v") + (("bf16",) if dtype == "bf16" else ()):
+            assert torch.equal(a[key], b[key]) and torch.equal(a[key], c[key]), (mode, key)
+    if dtype != "fp32":
+        return
+    from oracle import sas as osas
+    from oracle.optim import AdamOracle
+    init = {k: v.detach().cpu().double() for k, v in _model("sas", dtype, l2=0.0).state_dict().items()}
+    P = {k: v.clone() for k, v in init.items()}
+    opt = AdamOracle(list(P.values()), lr=1e-3)
+    torch.set_num_threads(16)
+    ref_losses = []
+    for bt in _batches("sas", world):
+        cat = [torch.from_numpy(np.concatenate([x[i] for x in bt])) for i in range(3)]
+        l64, _, _, g = osas.loss_and_grads(P, *cat, 2, 1)
+        opt.step([g[k] for k in P])
+        ref_losses.append(float(l64))
+    for mode, a in on[0].items():
+        assert np.allclose(a["losses"], ref_losses, rtol=1e-5), (mode, a["losses"], ref_losses)
+        errs = {k: _update_err("sas", k, a["sd"][k], P[k].float(), init[k].float()) for k in P}
+        worst = max(errs, key=errs.get)
+        print(f"sharded item table {mode}: update error vs oracle max {errs[worst]:.3g} ({worst})")
+        assert errs[worst] < 1e-3, (mode, worst, errs[worst])
