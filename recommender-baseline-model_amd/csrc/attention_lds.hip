@@ -345,6 +345,9 @@ __global__ __launch_bounds__(NT) void attn_fwd_lds_kernel(AttnLdsArgs a) {
   __syncthreads();
   APROF(1);
   const uint64_t seed = eff_seed(a.seed, a.seed_base);
+  // the younger half at issue priority 1, as in the backward passes (cfg2 bench, three interleaved rounds: 459.2 /
+  // 463.1 / 462.2k -> 462.8 / 463.8 / 466.6k seq/s)
+  if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
 
   for (int qt = split + wave * a.nsplit; qt < nq; qt += NW * a.nsplit) {
     const int q0 = qt * 16;
@@ -515,6 +518,10 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnLdsArgs& a, int64_t l
   APROF(5);
   const uint64_t seed = eff_seed(a.seed, a.seed_base);
 
+  // the second-dispatched half of the workgroup (waves 4-7, each sharing a SIMD with one of waves 0-3) at issue
+  // priority 1 for the whole loop: it otherwise loses every arbitration to its older partner (phase stamps, B = 128,
+  // T = 200, tools/micro/attn_bwd_phase.hip, two interleaved rounds: span 25.99 / 25.85 -> 24.44 / 23.66 us)
+  if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
   int qt, cb, ce, role, slot;
   for (int it = 0; item(it, qt, cb, ce, role, slot); ++it) {
     const int q0 = qt * 16;
@@ -782,6 +789,7 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnLdsArgs& a, int64_t 
   const uint32_t s32 = seed32(seed), Tp = (uint32_t)(T + (T & 1));   // mask row pitch: even
 
   const float sl2 = a.scale * LOG2E;
+  if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);   // as the dQ pass
   int kt, cb, ce, role, slot;
   for (int it = 0; item(it, kt, cb, ce, role, slot); ++it) {
     const int64_t key = kt * 16 + cl;  // this lane's key

@@ -25,7 +25,6 @@ eps 1e-8), rs_gemm (MFMA, fused bias / ReLU / dropout / residual / row-mask epil
 rs_sampled_logits_fwd/bwd, rs_bce_*, split-K weight gradients.
 """
 import math
-import os
 
 import torch
 import torch.nn as nn
@@ -592,17 +591,6 @@ class SASEngine:
         wslab = self.ws.get("wslab", (ops.wgrad_grouped_slab_numel([(d, d)] * 4 * L + [(2 * d, d)] * L, M, rows),),
                             torch.float32)
         join, fork = None, None
-        mode = os.environ.get("RS_SAS_TAIL", "side")
-        if tail is not None and mode != "side":
-            if mode == "main_before":
-                tail(dx)
-            ops.wgrad_grouped(probs, M, rows, wslab, extra=segs, pos=pos(dx) if pos is not None else None)
-            if mode == "main_after":
-                tail(dx)
-            join = torch.cuda.Event()
-            join.record(torch.cuda.current_stream())
-            self._tail_join = join
-            return dx
         if tail is not None:
             fork = torch.cuda.Event()
             fork.record(torch.cuda.current_stream())
