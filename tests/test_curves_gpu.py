@@ -73,6 +73,8 @@ def test_sas_loss_curve_matches_reference_1000_steps():
     print("sas_curve fp32: max err", err.max(), "at", int(err.argmax()), "; max err / envelope", ratio.max(), "at",
           int(ratio.argmax()), "; global floor", floor.max())
     assert (err <= env).all(), (ratio.max(), int(ratio.argmax()), err[ratio.argmax()], env[ratio.argmax()])
+    # and the earlier global cap: never more than 1.5 x the reference's own largest fp32 drift
+    assert err.max() <= 1.5 * floor.max(), (err.max(), int(err.argmax()), floor.max())
 
     def ma(x):
         return np.convolve(x, np.ones(50) / 50, mode="valid")
