@@ -488,11 +488,18 @@ int64_t rs_wgrad_grouped_slab_numel(int nprob, const rs_wgrad_problem* probs, in
  * multiple of 256 (the BERT d = 256 layer's weights), else 128 or 64; -1 on bad arguments.  Callers size the row
  * splits by it (about one 256-tile workgroup per CU in total). */
 int rs_wgrad_grouped_tile(int nprob, const rs_wgrad_problem* probs);
+/* the same with the tile edge capped at max_tile (>= 64) */
+int rs_wgrad_grouped_tile_max(int nprob, const rs_wgrad_problem* probs, int max_tile);
 /* nprob <= 16 problems; rows_per_split % 64 == 0; the extra segments (<= 64, e.g. LayerNorm
  * affine partials from rs_sas_block_*_bwd) are summed into their outputs (+=) by the same
  * reduction launch.  Returns RS_ERR_UNSUPPORTED for shapes outside the contract. */
 int rs_wgrad_grouped(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_t rows_per_split, float* slab,
                      int64_t slab_numel, int nextra, const rs_reduce_segment* extra, void* stream);
+/* rs_wgrad_grouped with the output tile edge capped at max_tile (>= 64; rs_wgrad_grouped = 256): a launch that runs
+ * beside a streaming kernel (the BERT token table's optimizer update) takes 128-wide tiles -- the 256-wide form's
+ * one-workgroup-per-CU LDS-DMA pipeline measured 10x slower sharing the chip with it (cfg5). */
+int rs_wgrad_grouped_max(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_t rows_per_split, float* slab,
+                         int64_t slab_numel, int nextra, const rs_reduce_segment* extra, int max_tile, void* stream);
 
 /* rs_wgrad_grouped followed by rs_embed_bwd's positional part (bf16, SAS mode 0, scale 1, dpos +=): the
  * positional table's gradient rides in the grouped reduction's launch as T extra workgroups (grad_tail.hip). */

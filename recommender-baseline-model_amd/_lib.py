@@ -119,6 +119,8 @@ SIGNATURES = {
     "rs_reduce_segments": [i32, C.POINTER(ReduceSegment), i32, vp],
     "rs_wgrad_grouped_slab_numel": [i32, C.POINTER(WgradProblem), i64, i64],
     "rs_wgrad_grouped_tile": [i32, C.POINTER(WgradProblem)],
+    "rs_wgrad_grouped_tile_max": [i32, C.POINTER(WgradProblem), i32],
+    "rs_wgrad_grouped_max": [i32, C.POINTER(WgradProblem), i64, i64, vp, i64, i32, C.POINTER(ReduceSegment), i32, vp],
     "rs_item_index_ws_bytes": [i32, i64, i64, i64],
     "rs_item_index_build": [i32, vp, vp, vp, i64, i64, i64, vp, i64, vp],
     "rs_item_index_layout": [i32, i64, i64, i64, C.POINTER(i64)],

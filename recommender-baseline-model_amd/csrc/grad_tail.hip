@@ -65,7 +65,7 @@ int rs_wgrad_grouped_pos_stats(int nprob, const rs_wgrad_problem* probs, int64_t
   wg::Args a;
   int T, ns;
   rs_reduce_segment segs[2 * wg::MAXP + wg::MAXS];
-  if (int e = wgrad_group_args(nprob, probs, M, rows_per_split, slab, slab_numel, nextra, extra, a, T, segs, ns))
+  if (int e = wgrad_group_args(nprob, probs, M, rows_per_split, slab, slab_numel, nextra, extra, a, T, segs, ns, 256))
     return e;
   const bool vec = d % 8 == 0 && d / 8 <= 16 && ((uintptr_t)dx % 16) == 0;
   if (ns > wg::MAXS || !vec) {   // unfused: the functions one after the other

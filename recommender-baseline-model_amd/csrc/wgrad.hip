@@ -611,14 +611,10 @@ int rs_reduce_segments(int nseg, const rs_reduce_segment* segs, int accumulate, 
 
 // the grouped launch's arguments (T = output tile edge) and its reduction segments (problems' W and bias
 // segments, then the caller's extra ones)
-// output tile edge of a grouped launch: 256 when every problem's N and K are multiples of 256 (RS_WGRAD_T256=0: at most
-// 128), else 128, else 64
-static int64_t wgrad_tile(int nprob, const rs_wgrad_problem* probs) {
-  static const bool t256 = [] {
-    const char* e = getenv("RS_WGRAD_T256");
-    return !e || atoi(e) != 0;
-  }();
-  int64_t T = t256 ? 256 : 128;
+// output tile edge of a grouped launch: 256 when every problem's N and K are multiples of 256, else 128, else 64 --
+// at most max_tile (the caller's cap: a launch sharing the chip with a streaming kernel takes the 128-wide tiles)
+static int64_t wgrad_tile(int nprob, const rs_wgrad_problem* probs, int64_t max_tile) {
+  int64_t T = max_tile >= 256 ? 256 : max_tile >= 128 ? 128 : 64;
   for (int q = 0; q < nprob; ++q)
     while (probs[q].N % T || probs[q].K % T) T /= 2;
   return T < 64 ? 64 : T;
@@ -626,10 +622,10 @@ static int64_t wgrad_tile(int nprob, const rs_wgrad_problem* probs) {
 
 static int wgrad_group_args(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_t rows_per_split, float* slab,
                             int64_t slab_numel, int nextra, const rs_reduce_segment* extra, wg::Args& a, int& T_,
-                            rs_reduce_segment* segs, int& ns) {
+                            rs_reduce_segment* segs, int& ns, int64_t max_tile) {
   if (nprob <= 0 || nprob > wg::MAXP || M <= 0 || rows_per_split <= 0 || rows_per_split % 64 || !slab)
     return RS_ERR_ARG;
-  int64_t T = wgrad_tile(nprob, probs);
+  int64_t T = wgrad_tile(nprob, probs, max_tile);
   const int64_t splits = cdiv(M, rows_per_split);
   a = wg::Args{};
   a.nprob = nprob;
@@ -667,17 +663,23 @@ static int wgrad_group_args(int nprob, const rs_wgrad_problem* probs, int64_t M,
 
 extern "C" {
 
-int rs_wgrad_grouped_tile(int nprob, const rs_wgrad_problem* probs) {
-  if (nprob <= 0 || nprob > wg::MAXP || !probs) return -1;
-  return (int)wgrad_tile(nprob, probs);
+int rs_wgrad_grouped_tile_max(int nprob, const rs_wgrad_problem* probs, int max_tile) {
+  if (nprob <= 0 || nprob > wg::MAXP || !probs || max_tile < 64) return -1;
+  return (int)wgrad_tile(nprob, probs, max_tile);
 }
 
-int rs_wgrad_grouped(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_t rows_per_split, float* slab,
-                     int64_t slab_numel, int nextra, const rs_reduce_segment* extra, void* stream) {
+int rs_wgrad_grouped_tile(int nprob, const rs_wgrad_problem* probs) {
+  return rs_wgrad_grouped_tile_max(nprob, probs, 256);
+}
+
+int rs_wgrad_grouped_max(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_t rows_per_split, float* slab,
+                         int64_t slab_numel, int nextra, const rs_reduce_segment* extra, int max_tile, void* stream) {
   wg::Args a;
   int T, ns;
   rs_reduce_segment segs[2 * wg::MAXP + wg::MAXS];
-  if (int e = wgrad_group_args(nprob, probs, M, rows_per_split, slab, slab_numel, nextra, extra, a, T, segs, ns))
+  if (max_tile < 64) return RS_ERR_ARG;
+  if (int e = wgrad_group_args(nprob, probs, M, rows_per_split, slab, slab_numel, nextra, extra, a, T, segs, ns,
+                               max_tile))
     return e;
   a.ks = kstamp_next(RS_STAMP_WGRAD_GROUPED);
   hipStream_t s = (hipStream_t)stream;
@@ -685,6 +687,11 @@ int rs_wgrad_grouped(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   return launch_segments(ns, segs, 1, s, a.ks);
+}
+
+int rs_wgrad_grouped(int nprob, const rs_wgrad_problem* probs, int64_t M, int64_t rows_per_split, float* slab,
+                     int64_t slab_numel, int nextra, const rs_reduce_segment* extra, void* stream) {
+  return rs_wgrad_grouped_max(nprob, probs, M, rows_per_split, slab, slab_numel, nextra, extra, 256, stream);
 }
 
 }  // extern "C"

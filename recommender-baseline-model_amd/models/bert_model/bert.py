@@ -365,8 +365,11 @@ class BERTEngine:
             ops.embed_bwd(1, ids, T, dx, 1.0, hp, self.salt["emb"], sb, G("bert.embedding.token.weight"),
                           G("bert.embedding.position.pe.weight"))
         hook = getattr(self, "after_token_grads", None)
-        if hook is not None:
-            hook("bert.embedding.token.weight")   # the token table's gradient is final
+        # the token table's gradient is final; True: the trainer's optimizer update of it now runs beside the grouped
+        # weight gradients, which then take 128-wide tiles (the 256-wide form slowed 10x sharing the chip with that
+        # stream at cfg5: 1,377 against 280 us; cfg5 5.8k -> 7.07k seq/s)
+        beside = bool(hook("bert.embedding.token.weight")) if hook is not None else False
+        tmax = 128 if beside else 256
         ex, sp = getattr(self, "sparse_tok", None), getattr(self, "_split", None)
         if ex is not None and sp is not None:
             # data parallel, union-of-touched-rows exchange of the token table's gradient (dp.SparseRowExchange):
@@ -377,9 +380,9 @@ class BERTEngine:
         for c in range(0, len(probs), 16):              # rs_wgrad_grouped takes up to 16 problems
             chunk = probs[c:c + 16]
             shapes = [(p[0].shape[1], p[1].shape[1]) for p in chunk]
-            rows = self._wgrad_rows(M, shapes)
-            wslab = self.ws.get(f"wslab{c}", (ops.wgrad_grouped_slab_numel(shapes, M, rows),), torch.float32)
-            ops.wgrad_grouped(chunk, M, rows, wslab, extra=ln_segs if c == 0 else ())
+            rows = self._wgrad_rows(M, shapes, tmax)
+            wslab = self.ws.get(f"wslab{c}_{tmax}", (ops.wgrad_grouped_slab_numel(shapes, M, rows),), torch.float32)
+            ops.wgrad_grouped(chunk, M, rows, wslab, extra=ln_segs if c == 0 else (), max_tile=tmax)
 
     def overwritten_grads(self):
         """(lo, hi) flat range whose gradient the fused step writes whole every step (out.weight then out.bias,
@@ -430,12 +433,12 @@ class BERTEngine:
         return ev, iws
 
     @staticmethod
-    def _wgrad_rows(M, shapes):
+    def _wgrad_rows(M, shapes, max_tile=256):
         """rows per split of the grouped weight-gradient launch.  128 x 128 tiles: about one and a half workgroups per
         CU in total (cfg3: 192 tiles x 2 splits; 4 splits measured 156 against 153 us for the launch, 1 split 219 us);
         256 x 256 tiles (every dimension a multiple of 256, rs_wgrad_grouped_tile; one 8-wave workgroup per CU): about
         one per CU (cfg3: 48 tiles x 5 splits)."""
-        t = ops.wgrad_grouped_tile(shapes)
+        t = ops.wgrad_grouped_tile(shapes, max_tile)
         tiles = sum(-(-n // t) * -(-k // t) for n, k in shapes)
         splits = max(1, round((256 if t == 256 else 384) / tiles))
         return max(64, -(-(-(-M // splits)) // 64) * 64)

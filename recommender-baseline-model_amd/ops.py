@@ -582,13 +582,13 @@ def _segments(segs):
     return arr
 
 
-def wgrad_grouped(problems, M, rows_per_split, slab, extra=(), pos=None):
+def wgrad_grouped(problems, M, rows_per_split, slab, extra=(), pos=None, max_tile=256):
     ev = _ev_begin("wgrad_grouped")
-    _wgrad_grouped(problems, M, rows_per_split, slab, extra, pos)
+    _wgrad_grouped(problems, M, rows_per_split, slab, extra, pos, max_tile)
     _ev_end(ev)
 
 
-def _wgrad_grouped(problems, M, rows_per_split, slab, extra=(), pos=None):
+def _wgrad_grouped(problems, M, rows_per_split, slab, extra=(), pos=None, max_tile=256):
     """problems: [(dY, X, dW, db|None)] with dW [N][K] fp32 (+=); extra: reduce segments
     (src, stride, splits, n, out) summed (+=) in the same reduction launch.  pos: (ids, T, dx, drop_p, salt, seed_base, dpos) -- the SAS positional
     table's gradient (embed_bwd mode 0, scale 1, +=) then rides in the reduction launch (rs_wgrad_grouped_pos);
@@ -600,6 +600,7 @@ def _wgrad_grouped(problems, M, rows_per_split, slab, extra=(), pos=None):
         arr[i] = _lib.WgradProblem(ptr(dY), ld(dY), ptr(X), ld(X), N, K, ptr(dW), ptr(db) if db is not None else None)
     segs = _segments(list(extra))
     if pos is not None:
+        assert max_tile == 256, "the positional form takes the default tiles"
         ids, T, dx, drop_p, salt, seed_base, dpos, *st = pos
         if st:
             hp, hdiv, lout, *aux = st
@@ -610,16 +611,17 @@ def _wgrad_grouped(problems, M, rows_per_split, slab, extra=(), pos=None):
         call("rs_wgrad_grouped_pos", len(problems), arr, M, rows_per_split, ptr(slab), slab.numel(), len(extra),
              segs, ptr(ids), T, ptr(dx), dx.shape[-1], drop_p, salt, ptr(seed_base), ptr(dpos), stream())
         return
-    call("rs_wgrad_grouped", len(problems), arr, M, rows_per_split, ptr(slab), slab.numel(), len(extra), segs,
-         stream())
+    call("rs_wgrad_grouped_max", len(problems), arr, M, rows_per_split, ptr(slab), slab.numel(), len(extra), segs,
+         int(max_tile), stream())
 
 
-def wgrad_grouped_tile(shapes):
-    """Output tile edge rs_wgrad_grouped uses for problems of these (N, K) shapes (256, 128 or 64)."""
+def wgrad_grouped_tile(shapes, max_tile=256):
+    """Output tile edge rs_wgrad_grouped uses for problems of these (N, K) shapes (256, 128 or 64; at most
+    max_tile)."""
     arr = (_lib.WgradProblem * len(shapes))()
     for i, (N, K) in enumerate(shapes):
         arr[i] = _lib.WgradProblem(None, 0, None, 0, N, K, None, None)
-    t = int(_lib.lib().rs_wgrad_grouped_tile(len(shapes), arr))
+    t = int(_lib.lib().rs_wgrad_grouped_tile_max(len(shapes), arr, int(max_tile)))
     if t <= 0:
         raise RuntimeError("rs_wgrad_grouped_tile: bad arguments")
     return t

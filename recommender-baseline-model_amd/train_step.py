@@ -451,15 +451,15 @@ class FusedTrainStep:
     def _early_token_update(self, name):
         """Engine hook (BERTEngine: right after the token table's gradient, before the grouped weight gradients): that
         range's update follows the early head update on the side stream (same prepared scalars, gradient cleared),
-        beside the grouped weight-gradient launch; step_rest skips it."""
+        beside the grouped weight-gradient launch; step_rest skips it.  Returns True when it forked that update."""
         if self._early_ev is None:
-            return
+            return False
         f = self.flat
         lo = f.offsets[name]
         hi = min(lo + -(-f.view(name).numel() // 4) * 4, f.numel)
         kp = self._early_kp
         if not (hi <= kp[0] or lo >= kp[1]) or lo % 4:
-            return
+            return False
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream())
         self._opt_stream.wait_event(ev)
@@ -468,6 +468,7 @@ class FusedTrainStep:
             self._early_ev = torch.cuda.Event()
             self._early_ev.record(self._opt_stream)
         self._early_done.append((lo, hi))
+        return True
 
     def _early_head_update(self):
         """Engine hook (BERTEngine: right after the head's dE / dh): fork the out.weight / out.bias update onto the

@@ -83,8 +83,9 @@ def test_linear_wgrad_single_split_direct(M, N, K, acc):
     assert rel(db.cpu().numpy(), ref_b.cpu().numpy()) < 1e-5
 
 
-@pytest.mark.parametrize("M,rows,d", [(25600, 1280, 128), (12800, 6400, 256), (1000, 192, 128), (777, 128, 256)])
-def test_wgrad_grouped_bench_shapes(M, rows, d):
+@pytest.mark.parametrize("M,rows,d,tmax", [(25600, 1280, 128, 256), (12800, 6400, 256, 256), (1000, 192, 128, 256),
+                                           (777, 128, 256, 256), (12800, 3200, 256, 128)])
+def test_wgrad_grouped_bench_shapes(M, rows, d, tmax):
     """The grouped launch at the SAS shape (cfg2: 12 d x d weights... here 6, 20 splits) and the BERT layer's four
     weights (cfg3: QKV, output, FFN1, FFN2), with ragged last splits: every weight and bias gradient against float64,
     and two launches give the same bits (fixed-order split reduction)."""
@@ -99,7 +100,7 @@ def test_wgrad_grouped_bench_shapes(M, rows, d):
         probs = [(dY, X, torch.zeros(N, K, device="cuda"), torch.zeros(N, device="cuda"))
                  for (dY, X), (N, K) in zip(ops_in, shapes)]
         slab = torch.empty(ops.wgrad_grouped_slab_numel(shapes, M, rows), device="cuda")
-        ops.wgrad_grouped(probs, M, rows, slab)
+        ops.wgrad_grouped(probs, M, rows, slab, max_tile=tmax)   # tmax 128 at d = 256: the capped (beside) form
         torch.cuda.synchronize()
         outs.append([(dW.clone(), db.clone()) for _, _, dW, db in probs])
     for (a, b), (c, e) in zip(outs[0], outs[1]):
