@@ -16,7 +16,9 @@ import os
 import sys
 
 KEYS = {"rs_attn_bwd (attn_bwd_lds: dQ + dK/dV workgroups)": ["attn_bwd_lds_kernel"],
-        "rs_wgrad_grouped (wgrad_group_kernel + reduce_cols_kernel)": ["wgrad_group_kernel", "reduce_cols_kernel"]}
+        "rs_wgrad_grouped (wgrad_group_kernel + reduce_cols_kernel)": ["wgrad_group_kernel", "reduce_cols_kernel"],
+        "rs_wgrad_grouped (wgrad_group256_kernel + reduce_cols_kernel)": ["wgrad_group256_kernel",
+                                                                         "reduce_cols_kernel"]}
 
 
 def per_dispatch(root):
