@@ -47,8 +47,28 @@ __global__ void adam_prepare_kernel(double* state, const double* hyper, const fl
 // scalars itself, and the LAST workgroup to finish (arrival counter in state[7]) writes them back, advances
 // the step count and the dropout seed, and re-arms the counter.  One launch instead of two on the step's
 // critical path.
+// streaming float4 access; NT: nontemporal (slc / nt) loads and stores for the optimizer's single-use sweeps
+typedef float f4v __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ float4 ld4(const float* a, int64_t i) {
+  if (NT) {
+    const f4v x = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(a) + i);
+    return make_float4(x[0], x[1], x[2], x[3]);
+  }
+  return reinterpret_cast<const float4*>(a)[i];
+}
+template <bool NT>
+__device__ __forceinline__ void st4(float* a, int64_t i, float4 v) {
+  if (NT) {
+    const f4v x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<f4v*>(a) + i);
+  } else {
+    reinterpret_cast<float4*>(a)[i] = v;
+  }
+}
+
 // one float4 of the Adam update (torch.optim.Adam, BS/trainers/base.py:225-228) + its stores
-template <bool BF16OUT>
+template <bool BF16OUT, bool NT>
 __device__ __forceinline__ void adam4(int64_t i, float4 pp, float4 gg, float4 mm, float4 vv, float* __restrict__ p,
                                       float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
                                       __bf16* __restrict__ pb, AdamElem h,
@@ -65,9 +85,9 @@ __device__ __forceinline__ void adam4(int64_t i, float4 pp, float4 gg, float4 mm
     const float denom = sqrtf(Vv[j]) / bc2s + h.eps;
     P[j] = P[j] - step_size * (Mv[j] / denom);            // param.addcdiv_(exp_avg, denom, -step_size)
   }
-  reinterpret_cast<float4*>(p)[i] = pp;
-  reinterpret_cast<float4*>(m)[i] = mm;
-  reinterpret_cast<float4*>(v)[i] = vv;
+  st4<NT>(p, i, pp);
+  st4<NT>(m, i, mm);
+  st4<NT>(v, i, vv);
   // zero_grad: only where the gradient is not already zero -- the table rows no token of the step touched (most of
   // a large item / token table) keep their zeros without a store (4 of the 34 bytes per element)
   if (zero_grad && (__float_as_uint(gg.x) | __float_as_uint(gg.y) | __float_as_uint(gg.z) | __float_as_uint(gg.w)))
@@ -75,7 +95,13 @@ __device__ __forceinline__ void adam4(int64_t i, float4 pp, float4 gg, float4 mm
   if (BF16OUT) {
     bf16x4 o;
     o[0] = (__bf16)P[0]; o[1] = (__bf16)P[1]; o[2] = (__bf16)P[2]; o[3] = (__bf16)P[3];
-    reinterpret_cast<bf16x4*>(pb)[i] = o;
+    if (NT) {
+      uint64_t w;
+      __builtin_memcpy(&w, &o, 8);
+      __builtin_nontemporal_store(w, reinterpret_cast<uint64_t*>(pb) + i);
+    } else {
+      reinterpret_cast<bf16x4*>(pb)[i] = o;
+    }
     // transposed bf16 copies of matrices inside the buffer (the SAS backward's [in][out] block weights,
     // rs_transpose_bf16's desc layout): the 4 elements share a row (host checks lds % 4 == 0)
     // the descriptors' element span [tlo, thi) first: most of the buffer (the tables) is outside every matrix
@@ -99,7 +125,7 @@ __device__ __forceinline__ void adam4(int64_t i, float4 pp, float4 gg, float4 mm
   }
 }
 
-template <bool BF16OUT, bool PREP, int U>
+template <bool BF16OUT, bool PREP, int U, bool NT>
 __global__ __launch_bounds__(256) void adam_step_kernel(int64_t n, float* __restrict__ p, float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v,
                                                         __bf16* __restrict__ pb, double* __restrict__ state,
@@ -141,22 +167,22 @@ __global__ __launch_bounds__(256) void adam_step_kernel(int64_t n, float* __rest
     float4 pq[U], gq[U], mq[U], vq[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      pq[u] = reinterpret_cast<float4*>(p)[i + u * stride];
-      gq[u] = reinterpret_cast<const float4*>(g)[i + u * stride];
-      mq[u] = reinterpret_cast<float4*>(m)[i + u * stride];
-      vq[u] = reinterpret_cast<float4*>(v)[i + u * stride];
+      pq[u] = ld4<NT>(p, i + u * stride);
+      gq[u] = ld4<NT>(g, i + u * stride);
+      mq[u] = ld4<NT>(m, i + u * stride);
+      vq[u] = ld4<NT>(v, i + u * stride);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      adam4<BF16OUT>(i + u * stride, pq[u], gq[u], mq[u], vq[u], p, g, m, v, pb, h, step_size, bc2s, gs,
+      adam4<BF16OUT, NT>(i + u * stride, pq[u], gq[u], mq[u], vq[u], p, g, m, v, pb, h, step_size, bc2s, gs,
                      zero_grad, tdesc, ntd, tbase, wT, tlo, thi);
   }
   for (; i < n4; i += stride) {
-    float4 pp = reinterpret_cast<float4*>(p)[i];
-    float4 gg = reinterpret_cast<const float4*>(g)[i];
-    float4 mm = reinterpret_cast<float4*>(m)[i];
-    float4 vv = reinterpret_cast<float4*>(v)[i];
-    adam4<BF16OUT>(i, pp, gg, mm, vv, p, g, m, v, pb, h, step_size, bc2s, gs, zero_grad, tdesc, ntd,
+    float4 pp = ld4<NT>(p, i);
+    float4 gg = ld4<NT>(g, i);
+    float4 mm = ld4<NT>(m, i);
+    float4 vv = ld4<NT>(v, i);
+    adam4<BF16OUT, NT>(i, pp, gg, mm, vv, p, g, m, v, pb, h, step_size, bc2s, gs, zero_grad, tdesc, ntd,
                    tbase, wT, tlo, thi);
   }
   // tail
@@ -351,7 +377,15 @@ int rs_adam_prepare(double* state, const double* hyper, const float* grad_diviso
 }
 
 // two float4 groups in flight per thread (1 and 4 measured slower)
-#define ADAM_LAUNCH(BO, PR, ...) hipLaunchKernelGGL((adam_step_kernel<BO, PR, 2>), __VA_ARGS__)
+// nontemporal sweeps only for ranges far beyond the 256 MB Infinity Cache (cfg5's 256M-element out.weight and token
+// table: 1,535 -> 1,460-1,472 us per sweep alone, cfg5 7.03-7.11k -> 7.26-7.28k seq/s); below that the next step's
+// optimizer re-reads the masters / moments from that cache (cfg4's item table with nt hints: 636-639k -> 604-608k)
+#define ADAM_NT_MIN (64ll << 20)
+#define ADAM_LAUNCH(BO, PR, ...)                                                          \
+  do {                                                                                    \
+    if (n >= ADAM_NT_MIN) hipLaunchKernelGGL((adam_step_kernel<BO, PR, 2, true>), __VA_ARGS__); \
+    else hipLaunchKernelGGL((adam_step_kernel<BO, PR, 2, false>), __VA_ARGS__);           \
+  } while (0)
 
 int rs_adam_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, const double* state,
                  const double* hyper, int zero_grad, void* stream) {

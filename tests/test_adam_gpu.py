@@ -221,3 +221,43 @@ def test_step_lr_matches_torch_steplr_and_reaches_captured_graphs():
         runs.append(snaps)
     for x, y in zip(*runs):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_nontemporal_sweep_matches_the_cached_form(fused):
+    """Ranges of >= 64M elements take the nontemporal-hint form of the Adam kernel (misc.hip ADAM_NT_MIN: cfg5's
+    out.weight and token-table sweeps); the same elements updated as a shorter range (the cached form) give the same
+    bits, zero_grad included, over two steps at a 256-workgroup cap (the early sweeps' grid) and the full grid."""
+    import rbm_amd  # noqa: F401
+    from rbm_amd import ops
+    n, k = (64 << 20) + 4099, 1 << 20
+    g0 = torch.Generator(device="cuda").manual_seed(7)
+    p = torch.randn(n, generator=g0, device="cuda")
+    m, v = torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
+    pb = torch.empty(n, dtype=torch.bfloat16, device="cuda")
+    hyper = torch.tensor([1e-3, 0.9, 0.999, 1e-8, 0.01], dtype=torch.float64, device="cuda")
+    div = torch.tensor([2.0], device="cuda")
+    # two windows: the head of the range and its ragged tail
+    wins = [(0, k), (n - k - 3, n)]
+    small = [(p[a:b].clone(), m[a:b].clone(), v[a:b].clone(), torch.empty(b - a, dtype=torch.bfloat16, device="cuda"))
+             for a, b in wins]
+    st_big, st_small = torch.zeros(144, dtype=torch.float64, device="cuda"), torch.zeros(144, dtype=torch.float64, device="cuda")
+    for step in range(2):
+        g = torch.randn(n, generator=g0, device="cuda")
+        g[: n // 3] = 0.0   # untouched rows keep their zeros without a store
+        gs = [g[a:b].clone() for a, b in wins]
+        if fused:
+            ops.adam_prepare_step(p, g, m, v, pb, st_big, hyper, zero_grad=True, grad_divisor=div)
+        else:
+            ops.adam_prepare(st_big, hyper, div)
+            ops.adam_step(p, g, m, v, pb, st_big, hyper, zero_grad=True, max_wg=256 if step == 0 else None)
+        ops.adam_prepare(st_small, hyper, div)
+        for (sp, sm, sv, sb), sg in zip(small, gs):
+            ops.adam_step(sp, sg, sm, sv, sb, st_small, hyper, zero_grad=True)
+        assert int(torch.count_nonzero(g)) == 0
+        for (sp, sm, sv, sb), sg in zip(small, gs):
+            assert int(torch.count_nonzero(sg)) == 0
+    torch.cuda.synchronize()
+    for (a, b), (sp, sm, sv, sb) in zip(wins, small):
+        assert torch.equal(p[a:b], sp) and torch.equal(m[a:b], sm) and torch.equal(v[a:b], sv)
+        assert torch.equal(pb[a:b], sb)
