@@ -263,6 +263,22 @@ int rs_adam_prepare_step_loss(int64_t n, float* p, float* g, float* m, float* v,
                               const double* hyper, int zero_grad, const float* grad_divisor, uint64_t* seed_base,
                               const int64_t* tdesc, int ntd, int64_t tbase, void* wT, const float* loss_sum,
                               float* loss_out, void* stream);
+/* rs_adam_step_wg / rs_adam_prepare_step_loss over a range holding (part of) a table whose gradient only
+ * rs_item_grad_marked writes: table row r is launch element moff + r * 2^dshift (moff may be negative), mrows rows;
+ * a row with row_marks[r] != *epoch has a zero gradient this step, so its gradient is not read (nor cleared: it
+ * is zero already).  Same results bit for bit as the unmarked launches.  row_marks == NULL: the unmarked launch.
+ * row_marks: 16-byte aligned, (mrows + 15) / 16 * 16 + 16 + 1024 bytes, the bytes past the stamps zero (the
+ * sweep's scalar mark loads run up to 16 bytes past a row; unstamped rows' gradient loads read the zero tail).
+ * Only valid while nothing but the marked item gradient writes that table's gradient rows (single device, no
+ * l2 regulariser, no exchange). */
+int rs_adam_step_marked(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, const double* state,
+                        const double* hyper, int zero_grad, int max_wg, const uint8_t* row_marks, const uint8_t* epoch,
+                        int64_t moff, int64_t mrows, int dshift, void* stream);
+int rs_adam_prepare_step_marked(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, double* state,
+                                const double* hyper, int zero_grad, const float* grad_divisor, uint64_t* seed_base,
+                                const int64_t* tdesc, int ntd, int64_t tbase, void* wT, const float* loss_sum,
+                                float* loss_out, const uint8_t* row_marks, const uint8_t* epoch, int64_t moff,
+                                int64_t mrows, int dshift, void* stream);
 
 /* SASRec's parameter-norm regulariser, BS/trainers/sas.py:51-52 (loss += l2_emb * torch.norm(p) for every
  * parameter p): *loss += l2 * sum_seg ||p_seg||_2 and g += scale * l2 * p / ||p_seg|| (0 where the norm is 0,
@@ -536,6 +552,13 @@ int rs_item_index_layout(int nsrc, int64_t rows, int64_t table_rows, int64_t d, 
 int rs_item_grad(const void* ws, int nsrc, int64_t rows, int64_t table_rows, int64_t d, const void* dx, float scale,
                  float drop_p, uint64_t salt, const uint64_t* seed_base, const void* f, const float* w1,
                  const float* w2, float* dtable, void* stream);
+/* rs_item_grad that also marks the table rows it writes: row_marks[v] = epoch for every key v of the batch and
+ * *epoch_out = epoch, epoch = the low byte of *seed_base (0 without one): the step's stamp for rs_adam_*_marked.
+ * row_marks: the rs_adam_*_marked layout over table_rows (stamps: any initial contents). */
+int rs_item_grad_marked(const void* ws, int nsrc, int64_t rows, int64_t table_rows, int64_t d, const void* dx,
+                        float scale, float drop_p, uint64_t salt, const uint64_t* seed_base, const void* f,
+                        const float* w1, const float* w2, float* dtable, uint8_t* row_marks, uint8_t* epoch_out,
+                        void* stream);
 /* The same for fp32 dx, f (the fp32 parity path, any d): one workgroup per table row, entries in sorted order. */
 int rs_item_grad_f32(const void* ws, int nsrc, int64_t rows, int64_t table_rows, int64_t d, const float* dx, float scale,
                      float drop_p, uint64_t salt, const uint64_t* seed_base, const float* f, const float* w1,

@@ -79,9 +79,12 @@ SIGNATURES = {
     "rs_adam_prepare": [vp, vp, vp, vp, vp],
     "rs_adam_step": [i64, vp, vp, vp, vp, vp, vp, vp, i32, vp],
     "rs_adam_step_wg": [i64, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp],
+    "rs_adam_step_marked": [i64, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, vp, i64, i64, i32, vp],
     "rs_graph_upload": [vp, vp],
     "rs_adam_prepare_step": [i64, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, i32, i64, vp, vp],
     "rs_adam_prepare_step_loss": [i64, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, i32, i64, vp, vp, vp, vp],
+    "rs_adam_prepare_step_marked": [i64, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, i32, i64, vp, vp, vp, vp, vp,
+                                    i64, i64, i32, vp],
     "rs_cast_bf16": [i64, vp, vp, vp],
     "rs_l2_penalty": [vp, vp, vp, i64, f32, vp, vp, vp, vp],
     "rs_dropout_rowmask": [i32, vp, i64, i64, i64, f32, u64, vp, i64, vp, vp, vp, vp],
@@ -128,6 +131,7 @@ SIGNATURES = {
     "rs_sas_head_finish": [i64, vp, vp, vp, vp],
     "rs_sas_head_bwd": [i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "rs_item_grad": [vp, i32, i64, i64, i64, vp, f32, f32, u64, vp, vp, vp, vp, vp, vp],
+    "rs_item_grad_marked": [vp, i32, i64, i64, i64, vp, f32, f32, u64, vp, vp, vp, vp, vp, vp, vp, vp],
     "rs_item_grad_f32": [vp, i32, i64, i64, i64, vp, f32, f32, u64, vp, vp, vp, vp, vp, vp],
     "rs_wgrad_grouped_pos": [i32, C.POINTER(WgradProblem), i64, i64, vp, i64, i32, C.POINTER(ReduceSegment),
                              vp, i64, vp, i64, f32, u64, vp, vp, vp],

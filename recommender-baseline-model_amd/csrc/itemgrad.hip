@@ -481,6 +481,8 @@ struct GradArgs {
   const float* w2;
   float* dtable;
   const int* start;      // counting-sort path: start[v] = first sorted position of key v (v <= V); null on the radix path
+  uint8_t* marks;        // nullable: marks[v] = the step's stamp for every key v (rs_item_grad_marked)
+  uint8_t* epoch;        // ... and the stamp itself
 };
 
 // one workgroup per chunk of CH sorted entries.  Dependent global round trips: (keys, entries) ->
@@ -504,6 +506,12 @@ __device__ __forceinline__ void item_chunk(const GradArgs& a, int64_t chunk, Chu
   const int cnt = (int)min((int64_t)CH, a.n - base);
   const bool drop = a.drop_p > 0.f;
   const uint32_t s32 = drop ? seed32(eff_seed(a.salt, a.seed_base)) : 0u;
+  const uint8_t stamp = a.marks && a.seed_base ? (uint8_t)*a.seed_base : 0;
+  if (a.marks && tid < cnt) {
+    const uint32_t k = a.sk[base + tid];
+    if (k != 0) a.marks[k] = stamp;
+  }
+  if (a.marks && chunk == 0 && tid == 0) *a.epoch = stamp;
   if (tid < CH) {
     skey[tid + 1] = tid < cnt ? a.sk[base + tid] : 0xffffffffu;
     sent[tid] = tid < cnt ? a.sv[base + tid] : 0u;
@@ -828,7 +836,7 @@ static int item_grad_args(const void* ws, int nsrc, int64_t rows, int64_t table_
   const char* w = (const char*)ws;
   a = {(const uint32_t*)(w + L.sk), (const uint32_t*)(w + L.sv), (float*)(w + L.part),
        L.n, rows, (const __bf16*)dx, scale, drop_p, salt, seed_base, (const __bf16*)f, w1, w2, dtable,
-       L.cs ? (const int*)(w + L.start) : nullptr};
+       L.cs ? (const int*)(w + L.start) : nullptr, nullptr, nullptr};
   return 0;
 }
 
@@ -837,11 +845,22 @@ extern "C" {
 int rs_item_grad(const void* ws, int nsrc, int64_t rows, int64_t table_rows, int64_t d, const void* dx, float scale,
                  float drop_p, uint64_t salt, const uint64_t* seed_base, const void* f, const float* w1,
                  const float* w2, float* dtable, void* stream) {
+  return rs_item_grad_marked(ws, nsrc, rows, table_rows, d, dx, scale, drop_p, salt, seed_base, f, w1, w2, dtable,
+                             nullptr, nullptr, stream);
+}
+
+int rs_item_grad_marked(const void* ws, int nsrc, int64_t rows, int64_t table_rows, int64_t d, const void* dx,
+                        float scale, float drop_p, uint64_t salt, const uint64_t* seed_base, const void* f,
+                        const float* w1, const float* w2, float* dtable, uint8_t* row_marks, uint8_t* epoch_out,
+                        void* stream) {
   ig::GradArgs a;
   ig::Layout L;
+  if (!row_marks != !epoch_out) return RS_ERR_ARG;
   if (int e = item_grad_args(ws, nsrc, rows, table_rows, d, dx, scale, drop_p, salt, seed_base, f, w1, w2, dtable,
                              a, L))
     return e;
+  a.marks = row_marks;
+  a.epoch = epoch_out;
   hipStream_t s = (hipStream_t)stream;
   const dim3 g1((unsigned)L.nchunks), g2((unsigned)cdiv(L.nchunks, 4));
   if (d == 64) {

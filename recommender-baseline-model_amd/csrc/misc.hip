@@ -125,7 +125,40 @@ __device__ __forceinline__ void adam4(int64_t i, float4 pp, float4 gg, float4 mm
   }
 }
 
-template <bool BF16OUT, bool PREP, int U, bool NT>
+// rows of a table whose gradient only the item-gradient kernels write (rs_item_grad_marked): marks[row] == *epoch for
+// every row they wrote this step (and possibly for rows of an old step: harmless, their gradient reads as zero), so a
+// row without the mark has a zero gradient and the sweep skips its load -- 4 of the 30 bytes per element of a table
+// whose rows a batch mostly does not touch (cfg5's 1M-row token table, cfg4's 54k-row item table)
+struct RowMarks {
+  const uint8_t* marks;
+  const uint8_t* epoch;
+  const float* zeros;   // 1 KB of zeros after the marks (16-B aligned)
+  int64_t moff;       // launch element index of the table's row 0 (may be negative: the launch starts inside it)
+  int64_t mlo, mhi;   // launch element range covered by the table
+  int dshift;         // log2(row width)
+};
+
+// The marks of a wave's rows by SCALAR loads (constant address space, wave-uniform address): lgkmcnt-counted, so
+// consuming them does not wait for the wave's vector loads in flight (vmcnt retires in order -- a per-lane byte
+// load before the gradient load made every group wait for all earlier loads: two round trips per group).  A
+// wave's 64 float4 span 256 elements, at most 3 rows of >= 128: the 16 mark bytes from the row of its first
+// active lane (rounded down to 8) cover them (row_marks arrays carry 16 bytes of padding).
+typedef __attribute__((address_space(4))) const uint64_t* const_u64p;
+template <bool MK>
+__device__ __forceinline__ bool row_touched(int64_t i, const RowMarks& rm, uint8_t ep) {
+  if (!MK) return true;
+  const int64_t e = 4 * i;
+  const int64_t r = e >= rm.mlo ? (e - rm.moff) >> rm.dshift : 0;
+  const int rf = __builtin_amdgcn_readfirstlane((int)r) & ~7;
+  const const_u64p w = (const_u64p)(rm.marks + rf);
+  const uint64_t lo = w[0], hi = w[1];
+  const int k = (int)r - rf;
+  const uint64_t word = k < 8 ? lo : hi;
+  const uint8_t mk = (uint8_t)(word >> (8 * (k & 7)));
+  return !(e >= rm.mlo && e < rm.mhi) || mk == ep;
+}
+
+template <bool BF16OUT, bool PREP, int U, bool NT, bool MK>
 __global__ __launch_bounds__(256) void adam_step_kernel(int64_t n, float* __restrict__ p, float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v,
                                                         __bf16* __restrict__ pb, double* __restrict__ state,
@@ -133,8 +166,9 @@ __global__ __launch_bounds__(256) void adam_step_kernel(int64_t n, float* __rest
                                                         const float* __restrict__ divisor, uint64_t* seed_base,
                                                         const int64_t* __restrict__ tdesc, int ntd, int64_t tbase,
                                                         __bf16* __restrict__ wT, const float* __restrict__ lsum,
-                                                        float* __restrict__ lout) {
+                                                        float* __restrict__ lout, RowMarks rm) {
   const AdamElem h = adam_elem(hyper);
+  const uint8_t ep = MK ? *rm.epoch : 0;
   // data parallel: the step's reported loss = all-reduced loss sum / all-reduced count (the division torch.div did
   // in its own launch), by one thread: both inputs are final before this launch
   if (PREP && lout && blockIdx.x == 0 && threadIdx.x == 0) *lout = lsum[0] / divisor[0];
@@ -165,13 +199,26 @@ __global__ __launch_bounds__(256) void adam_step_kernel(int64_t n, float* __rest
   // U float4 per thread in flight: every load of the group is issued before the first store
   for (; i + (U - 1) * stride < n4; i += U * stride) {
     float4 pq[U], gq[U], mq[U], vq[U];
+    bool tq[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) tq[u] = row_touched<MK>(i + u * stride, rm, ep);
+    if (MK) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       pq[u] = ld4<NT>(p, i + u * stride);
-      gq[u] = ld4<NT>(g, i + u * stride);
+      // an unstamped row's lanes read zeros from the marks' zero tail (a hot 1 KB) instead of HBM: one load either
+      // way, no branch around it
+      gq[u] = MK ? *(tq[u] ? reinterpret_cast<const float4*>(g) + i + u * stride
+                           : reinterpret_cast<const float4*>(rm.zeros) + (threadIdx.x & 63))
+                 : ld4<NT>(g, i + u * stride);
       mq[u] = ld4<NT>(m, i + u * stride);
       vq[u] = ld4<NT>(v, i + u * stride);
     }
+    // marked: all U groups' loads issued before the first use (the scheduler otherwise sinks group u+1's loads and
+    // its mark loads below group u's update).  Unmarked: left to the scheduler, which issues group u+1's loads after
+    // group u's -- forcing all eight in flight measured slower (256M elements at 256 / 512 workgroups: 1,460-1,472
+    // -> 1,486-1,491 / 1,508-1,519 -> 1,621-1,624 us)
+    if (MK) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < U; ++u)
       adam4<BF16OUT, NT>(i + u * stride, pq[u], gq[u], mq[u], vq[u], p, g, m, v, pb, h, step_size, bc2s, gs,
@@ -179,7 +226,10 @@ __global__ __launch_bounds__(256) void adam_step_kernel(int64_t n, float* __rest
   }
   for (; i < n4; i += stride) {
     float4 pp = ld4<NT>(p, i);
-    float4 gg = ld4<NT>(g, i);
+    const bool tt = row_touched<MK>(i, rm, ep);
+    float4 gg = MK ? *(tt ? reinterpret_cast<const float4*>(g) + i
+                          : reinterpret_cast<const float4*>(rm.zeros) + (threadIdx.x & 63))
+                   : ld4<NT>(g, i);
     float4 mm = ld4<NT>(m, i);
     float4 vv = ld4<NT>(v, i);
     adam4<BF16OUT, NT>(i, pp, gg, mm, vv, p, g, m, v, pb, h, step_size, bc2s, gs, zero_grad, tdesc, ntd,
@@ -381,11 +431,32 @@ int rs_adam_prepare(double* state, const double* hyper, const float* grad_diviso
 // table: 1,535 -> 1,460-1,472 us per sweep alone, cfg5 7.03-7.11k -> 7.26-7.28k seq/s); below that the next step's
 // optimizer re-reads the masters / moments from that cache (cfg4's item table with nt hints: 636-639k -> 604-608k)
 #define ADAM_NT_MIN (64ll << 20)
-#define ADAM_LAUNCH(BO, PR, ...)                                                          \
-  do {                                                                                    \
-    if (n >= ADAM_NT_MIN) hipLaunchKernelGGL((adam_step_kernel<BO, PR, 2, true>), __VA_ARGS__); \
-    else hipLaunchKernelGGL((adam_step_kernel<BO, PR, 2, false>), __VA_ARGS__);           \
+#define ADAM_LAUNCH(BO, PR, ...)                                                                         \
+  do {                                                                                                   \
+    if (rm.marks) {                                                                                      \
+      if (n >= ADAM_NT_MIN) hipLaunchKernelGGL((adam_step_kernel<BO, PR, 2, true, true>), __VA_ARGS__, rm);  \
+      else hipLaunchKernelGGL((adam_step_kernel<BO, PR, 2, false, true>), __VA_ARGS__, rm);                \
+    } else {                                                                                             \
+      if (n >= ADAM_NT_MIN) hipLaunchKernelGGL((adam_step_kernel<BO, PR, 2, true, false>), __VA_ARGS__, rm); \
+      else hipLaunchKernelGGL((adam_step_kernel<BO, PR, 2, false, false>), __VA_ARGS__, rm);               \
+    }                                                                                                    \
   } while (0)
+
+// row_marks layout: mrows stamps, padding to 16 B + 16 (the scalar loads' overrun), then 1 KB of zeros
+#define ROW_MARKS_ZEROS(rows) ((((rows) + 15) / 16) * 16 + 16)
+// the marked table's rows inside launch elements [0, n): row r of the table is launch element moff + r << dshift
+static int row_marks(int64_t n, const uint8_t* marks, const uint8_t* epoch, int64_t moff, int64_t mrows, int dshift,
+                     RowMarks& rm) {
+  rm = RowMarks{nullptr, nullptr, nullptr, 0, 0, 0, 0};
+  if (!marks) return 0;
+  if (!epoch || mrows <= 0 || dshift < 2 || dshift > 16 || moff % 4 || (uintptr_t)marks % 16) return RS_ERR_ARG;
+  rm.marks = marks; rm.epoch = epoch; rm.moff = moff; rm.dshift = dshift;
+  rm.zeros = reinterpret_cast<const float*>(marks + ROW_MARKS_ZEROS(mrows));
+  rm.mlo = std::max<int64_t>(0, moff);
+  rm.mhi = std::min<int64_t>(n, moff + (mrows << dshift));
+  if (rm.mhi <= rm.mlo) rm.marks = nullptr;   // no overlap: the plain sweep
+  return 0;
+}
 
 int rs_adam_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, const double* state,
                  const double* hyper, int zero_grad, void* stream) {
@@ -394,7 +465,16 @@ int rs_adam_step(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16
 
 int rs_adam_step_wg(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, const double* state,
                     const double* hyper, int zero_grad, int max_wg, void* stream) {
+  return rs_adam_step_marked(n, p, g, m, v, p_bf16, state, hyper, zero_grad, max_wg, nullptr, nullptr, 0, 0, 0,
+                             stream);
+}
+
+int rs_adam_step_marked(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, const double* state,
+                        const double* hyper, int zero_grad, int max_wg, const uint8_t* row_marks_, const uint8_t* epoch,
+                        int64_t moff, int64_t mrows, int dshift, void* stream) {
   if (n <= 0 || max_wg <= 0 || ((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16) return RS_ERR_ARG;
+  RowMarks rm;
+  if (int e = row_marks(n, row_marks_, epoch, moff, mrows, dshift, rm)) return e;
   const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(cdiv(n / 4, 256), max_wg));
   hipStream_t s = (hipStream_t)stream;
   double* st = const_cast<double*>(state);   // read only without PREP
@@ -420,7 +500,18 @@ int rs_adam_prepare_step_loss(int64_t n, float* p, float* g, float* m, float* v,
                               const double* hyper, int zero_grad, const float* grad_divisor, uint64_t* seed_base,
                               const int64_t* tdesc, int ntd, int64_t tbase, void* wT, const float* loss_sum,
                               float* loss_out, void* stream) {
+  return rs_adam_prepare_step_marked(n, p, g, m, v, p_bf16, state, hyper, zero_grad, grad_divisor, seed_base, tdesc,
+                                     ntd, tbase, wT, loss_sum, loss_out, nullptr, nullptr, 0, 0, 0, stream);
+}
+
+int rs_adam_prepare_step_marked(int64_t n, float* p, float* g, float* m, float* v, void* p_bf16, double* state,
+                                const double* hyper, int zero_grad, const float* grad_divisor, uint64_t* seed_base,
+                                const int64_t* tdesc, int ntd, int64_t tbase, void* wT, const float* loss_sum,
+                                float* loss_out, const uint8_t* row_marks_, const uint8_t* epoch, int64_t moff,
+                                int64_t mrows, int dshift, void* stream) {
   if (n <= 0 || !state || ((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16) return RS_ERR_ARG;
+  RowMarks rm;
+  if (int e = row_marks(n, row_marks_, epoch, moff, mrows, dshift, rm)) return e;
   if (!loss_out != !loss_sum || (loss_out && !grad_divisor)) return RS_ERR_ARG;
   if (ntd < 0 || (ntd > 0 && (!tdesc || !wT || !p_bf16))) return RS_ERR_ARG;
   // at most 2048 workgroups: every workgroup pays an arrival atomic (the PREP step-count publication); 7k of

@@ -360,7 +360,7 @@ class BERTEngine:
                 torch.cuda.current_stream().wait_event(ev)
             ops.embed_bwd(1, ids, T, dx, 1.0, hp, self.salt["emb"], sb, None, G("bert.embedding.position.pe.weight"))
             ops.item_grad(iws, 1, M, dx, 1.0, hp, self.salt["emb"], sb, None, None, None,
-                          G("bert.embedding.token.weight"))
+                          G("bert.embedding.token.weight"), marks=getattr(self, "row_marks", None))
         else:
             ops.embed_bwd(1, ids, T, dx, 1.0, hp, self.salt["emb"], sb, G("bert.embedding.token.weight"),
                           G("bert.embedding.position.pe.weight"))
@@ -412,6 +412,19 @@ class BERTEngine:
 
     def _det_table(self):
         return self.dt == torch.bfloat16 and self.d in (64, 128, 256)
+
+    def enable_row_marks(self, min_rows=0):
+        """Stamp the rows the inverted-index gradient writes (rs_item_grad_marked) so the optimizer can skip the
+        gradient loads of the others: (table name, row marks u8 [rows], epoch u8 [1]), or None where that
+        gradient is not the index path's alone (fp32 / other widths) or the table is below min_rows."""
+        name = "bert.embedding.token.weight"
+        rows, d = self.flat.shapes[name]
+        if not self._det_table() or d & (d - 1) or rows < min_rows:
+            self.row_marks = None
+            return None
+        self.row_marks = (torch.zeros(ops.row_marks_bytes(rows), dtype=torch.uint8, device=self.dev),
+                          torch.zeros(1, dtype=torch.uint8, device=self.dev))
+        return (name,) + self.row_marks
 
     def _token_index(self, ids, side=True):
         """rs_item_index_build over the batch's token ids (the token-table gradient's inverted index); on a

@@ -423,7 +423,7 @@ class SASEngine:
 
             def item_grads(dx):
                 ops.item_grad(iws, 3, M, dx, math.sqrt(d), p, self.salt["emb"], sb, s["f"], dpl, dnl,
-                              G("item_emb.weight"))
+                              G("item_emb.weight"), marks=getattr(self, "row_marks", None))
             dx = self._backward_blocks_fused(s, dx, grad, segs, tail=item_grads,
                                              pos=lambda dx: (ids, T, dx, p, self.salt["emb"], sb,
                                                              G("pos_emb.weight")) + stats)
@@ -485,7 +485,20 @@ class SASEngine:
             iws = self.ws.get("itemidx", (ops.item_index_ws_bytes(3, M, V1, d),), torch.uint8)
             ops.item_index_build([ids, s["pos"], s["neg"]], V1, d, iws)
             ops.item_grad(iws, 3, M, dx, math.sqrt(d), p, self.salt["emb"], sb, s["f"], dpl, dnl,
-                          G("item_emb.weight"))
+                          G("item_emb.weight"), marks=getattr(self, "row_marks", None))
+
+    def enable_row_marks(self, min_rows=0):
+        """Stamp the rows the inverted-index gradient writes (rs_item_grad_marked) so the optimizer can skip the
+        gradient loads of the others: (table name, row marks u8 [rows], epoch u8 [1]), or None where that
+        gradient is not the index path's alone (fp32 / other widths) or the table is below min_rows."""
+        name = "item_emb.weight"
+        rows, d = self.flat.shapes[name]
+        if not (self.dt == torch.bfloat16 and d in (64, 128, 256)) or d & (d - 1) or rows < min_rows:
+            self.row_marks = None
+            return None
+        self.row_marks = (torch.zeros(ops.row_marks_bytes(rows), dtype=torch.uint8, device=self.dev),
+                          torch.zeros(1, dtype=torch.uint8, device=self.dev))
+        return (name,) + self.row_marks
 
     def _side_prologue(self, ids, pos, neg, after=None):
         """Work of the fused backward that depends only on the batch's keys and the weights, issued on a

@@ -317,7 +317,20 @@ def adam_prepare(state, hyper, grad_divisor=None, seed_base=None):
     call("rs_adam_prepare", ptr(state), ptr(hyper), ptr(grad_divisor), ptr(seed_base), stream())
 
 
-def adam_step(p, g, m, v, p_bf16, state, hyper, zero_grad=False, max_wg=None):
+def row_marks_bytes(rows):
+    """Size of a row-marks array (rs_item_grad_marked / rs_adam_*_marked): the rows' stamps, padding to 16 B + 16
+    (the sweep's scalar mark loads run past the last row) and a 1 KB zero tail (the unstamped rows' gradient
+    loads read it).  Allocate zeroed, 16-byte aligned."""
+    return (rows + 15) // 16 * 16 + 16 + 1024
+
+
+def adam_step(p, g, m, v, p_bf16, state, hyper, zero_grad=False, max_wg=None, marks=None):
+    """marks: (row_marks u8, epoch u8, moff, rows, dshift) of a marked table inside this range (rs_adam_step_marked)."""
+    if marks is not None:
+        rm, ep, moff, rows, dshift = marks
+        call("rs_adam_step_marked", p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), ptr(p_bf16), ptr(state), ptr(hyper),
+             int(zero_grad), int(max_wg or 8192), ptr(rm), ptr(ep), int(moff), int(rows), int(dshift), stream())
+        return
     if max_wg:
         call("rs_adam_step_wg", p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), ptr(p_bf16), ptr(state), ptr(hyper),
              int(zero_grad), int(max_wg), stream())
@@ -327,7 +340,7 @@ def adam_step(p, g, m, v, p_bf16, state, hyper, zero_grad=False, max_wg=None):
 
 
 def adam_prepare_step(p, g, m, v, p_bf16, state, hyper, zero_grad=False, grad_divisor=None, seed_base=None,
-                      transposed=None, loss_sum=None, loss_out=None, tbase=0):
+                      transposed=None, loss_sum=None, loss_out=None, tbase=0, marks=None):
     """adam_prepare + adam_step in one launch (state: double[144]; state[7], state[16 + 16 k] arrival counters).
     transposed: (desc int64 device [n][6] as transpose_bf16's, its host copy, dst bf16 tensor) -- the bf16
     result of those matrices is also written transposed; the descriptors' offsets are flat-buffer elements and
@@ -344,6 +357,12 @@ def adam_prepare_step(p, g, m, v, p_bf16, state, hyper, zero_grad=False, grad_di
                 raise ValueError("adam_prepare_step: transposed matrix outside the buffers or misaligned")
         if p_bf16 is None:
             raise ValueError("adam_prepare_step: transposed copies need the bf16 output")
+    if marks is not None:      # a marked table inside the range (rs_adam_prepare_step_marked)
+        rm, ep, moff, rows, dshift = marks
+        call("rs_adam_prepare_step_marked", p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), ptr(p_bf16), ptr(state),
+             ptr(hyper), int(zero_grad), ptr(grad_divisor), ptr(seed_base), ptr(td), nt, int(tbase), ptr(wt),
+             ptr(loss_sum), ptr(loss_out), ptr(rm), ptr(ep), int(moff), int(rows), int(dshift), stream())
+        return
     if loss_out is not None:   # + loss_out = loss_sum / grad_divisor in the same launch
         call("rs_adam_prepare_step_loss", p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), ptr(p_bf16), ptr(state),
              ptr(hyper), int(zero_grad), ptr(grad_divisor), ptr(seed_base), ptr(td), nt, int(tbase), ptr(wt), ptr(loss_sum),
@@ -669,8 +688,14 @@ def item_index_view(nsrc, rows, table_rows, d, ws):
     return sk, sv, start, int(out[3])
 
 
-def item_grad(ws, nsrc, rows, dx, scale, drop_p, salt, seed_base, f, w1, w2, dtable):
+def item_grad(ws, nsrc, rows, dx, scale, drop_p, salt, seed_base, f, w1, w2, dtable, marks=None):
+    """marks: (row_marks u8 [table_rows], epoch u8 [1]) -- rs_item_grad_marked stamps the rows it writes (bf16)."""
     table_rows, d = dtable.shape
+    if marks is not None and dx.dtype != torch.float32:
+        call("rs_item_grad_marked", ptr(ws), nsrc, rows, table_rows, d, ptr(dx), scale, drop_p, salt, ptr(seed_base),
+             ptr(f) if f is not None else None, ptr(w1) if w1 is not None else None,
+             ptr(w2) if w2 is not None else None, ptr(dtable), ptr(marks[0]), ptr(marks[1]), stream())
+        return
     # fp32 (the parity path): one workgroup per table row; bf16: the chunked kernels (d in {64, 128, 256})
     call("rs_item_grad_f32" if dx.dtype == torch.float32 else "rs_item_grad", ptr(ws), nsrc, rows, table_rows, d,
          ptr(dx), scale, drop_p, salt, ptr(seed_base),

@@ -47,6 +47,17 @@ class FusedAdam:
         # state[16 + 16 k], k < 8)]
         self.state = torch.zeros(144, dtype=torch.float64, device=dev)
         self.hyper = torch.tensor([lr, betas[0], betas[1], eps, weight_decay], dtype=torch.float64, device=dev)
+        # (table lo, rows, log2 d, row marks, epoch): a table whose gradient rows only the marked item gradient
+        # writes -- the sweep skips the gradient loads of the rows it did not stamp (rs_adam_*_marked)
+        self.marks = None
+
+    def _marks(self, lo, hi):
+        if self.marks is None:
+            return None
+        tlo, rows, dshift, rm, ep = self.marks
+        if hi <= tlo or lo >= tlo + (rows << dshift):
+            return None
+        return rm, ep, tlo - lo, rows, dshift
 
     def set_lr(self, lr):
         """StepLR hook (BS/trainers/base.py:40,87): lives on the device, so graph replays see it."""
@@ -73,10 +84,11 @@ class FusedAdam:
                 ops.adam_prepare_step(f.data[lo:hi], f.grad[lo:hi], self.m[lo:hi], self.v[lo:hi], bf, self.state,
                                       self.hyper, zero_grad=zg, grad_divisor=grad_divisor, seed_base=seed_base,
                                       transposed=transposed, tbase=lo,
-                                      loss_sum=loss[0] if loss else None, loss_out=loss[1] if loss else None)
+                                      loss_sum=loss[0] if loss else None, loss_out=loss[1] if loss else None,
+                                      marks=self._marks(lo, hi))
             else:
                 ops.adam_step(f.data[lo:hi], f.grad[lo:hi], self.m[lo:hi], self.v[lo:hi], bf, self.state,
-                              self.hyper, zero_grad=zg)
+                              self.hyper, zero_grad=zg, marks=self._marks(lo, hi))
 
 
     def step_keep_early(self, keep, max_wg=None, zero_grad=False, prep_event=None):
@@ -91,14 +103,14 @@ class FusedAdam:
             prep_event.record(torch.cuda.current_stream())
         bf = f.bf16[lo:hi] if f.bf16 is not None else None
         ops.adam_step(f.data[lo:hi], f.grad[lo:hi], self.m[lo:hi], self.v[lo:hi], bf, self.state, self.hyper,
-                      zero_grad=zero_grad, max_wg=max_wg)
+                      zero_grad=zero_grad, max_wg=max_wg, marks=self._marks(lo, hi))
 
     def step_range(self, lo, hi, zero_grad=True, max_wg=None):
         """rs_adam_step over [lo, hi) with the step's scalars already prepared (a step_keep_early step)."""
         f = self.flat
         bf = f.bf16[lo:hi] if f.bf16 is not None else None
         ops.adam_step(f.data[lo:hi], f.grad[lo:hi], self.m[lo:hi], self.v[lo:hi], bf, self.state, self.hyper,
-                      zero_grad=zero_grad, max_wg=max_wg)
+                      zero_grad=zero_grad, max_wg=max_wg, marks=self._marks(lo, hi))
 
     def step_rest(self, keep, seed_base=None, done=()):
         """The rest of a step_keep_early step: every range outside `keep` and the ranges in `done` (already updated
@@ -254,6 +266,17 @@ class FusedTrainStep:
         # ... and the token table's update (256M elements at cfg5) beside the grouped weight gradients: cfg5
         # 7,140 / 7,043 / 7,051 -> 7,144 / 7,167 / 7,195 seq/s (three interleaved rounds)
         self._early_token = self._early_ok and os.environ.get("RS_EARLY_TOKEN_ADAM", "1") != "0"
+        # single device, bf16: the item / token table's gradient rows come only from the inverted-index kernels,
+        # which stamp the rows they write; the optimizer then reads the gradient of those rows only (4 of its 30
+        # bytes per element elsewhere).  Not under data parallel (other ranks' rows arrive by the exchange) nor
+        # with the l2 regulariser (it writes every row); tables below ROW_MARKS_MIN rows are mostly touched.
+        if (not self.dp and not self.l2 and os.environ.get("RS_ROW_MARKS", "1") != "0"
+                and hasattr(self.engine, "enable_row_marks")):
+            r = self.engine.enable_row_marks(self.ROW_MARKS_MIN)
+            if r is not None:
+                name, rm, ep = r
+                rows, d = self.flat.shapes[name]
+                self.opt.marks = (self.flat.offsets[name], rows, d.bit_length() - 1, rm, ep)
 
     # ---------------------------------------------------------------- pieces
     def _divisor(self, local_count):
@@ -447,6 +470,8 @@ class FusedTrainStep:
     EARLY_HEAD_ADAM_WG = int(os.environ.get("RS_EARLY_HEAD_ADAM_WG", "256"))
 
     EARLY_TOKEN_ADAM_WG = int(os.environ.get("RS_EARLY_TOKEN_ADAM_WG", "256"))
+
+    ROW_MARKS_MIN = 16384
 
     def _early_token_update(self, name):
         """Engine hook (BERTEngine: right after the token table's gradient, before the grouped weight gradients): that
