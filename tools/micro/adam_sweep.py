@@ -1,5 +1,5 @@
 """Standalone Adam sweep rate: rs_adam_step_wg over n fp32 elements (+ bf16 copy) at several workgroup caps.
-Usage: python tools/micro/adam_sweep.py [n_millions]   (RS_ADAM_PIPE picks the loop form at library load)"""
+Usage: python tools/micro/adam_sweep.py [n_millions]   (ranges of >= 64M elements take the nontemporal form)"""
 import os, sys, torch
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
 import rbm_amd  # noqa: F401
@@ -23,4 +23,4 @@ for wg in [256, 512, 1024, 2048, 8192]:
         ops.adam_step(p, g, m, v, pb, state, hyper, max_wg=wg)
     e1.record(); torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / 5
-    print(f"pipe={os.environ.get('RS_ADAM_PIPE', '0')} n={n} wg={wg}: {us:.1f} us  {nbytes / us / 1e6:.2f} TB/s", flush=True)
+    print(f"n={n} wg={wg}: {us:.1f} us  {nbytes / us / 1e6:.2f} TB/s", flush=True)
