@@ -77,6 +77,7 @@ static void run(int B, int T) {
 int main() {
   run(128, 200);
   run(128, 64);
+  run(128, 50);
   run(64, 200);
   run(256, 200);
   return 0;
