@@ -148,14 +148,17 @@ template <bool MK>
 __device__ __forceinline__ bool row_touched(int64_t i, const RowMarks& rm, uint8_t ep) {
   if (!MK) return true;
   const int64_t e = 4 * i;
-  const int64_t r = e >= rm.mlo ? (e - rm.moff) >> rm.dshift : 0;
+  const bool inside = e >= rm.mlo && e < rm.mhi;
+  // lanes outside the table take row 0: every scalar load stays inside [0, mrows + 15] (a wave straddling the
+  // table's start holds rows 0..2 inside it; one straddling its end starts inside)
+  const int64_t r = inside ? (e - rm.moff) >> rm.dshift : 0;
   const int rf = __builtin_amdgcn_readfirstlane((int)r) & ~7;
   const const_u64p w = (const_u64p)(rm.marks + rf);
   const uint64_t lo = w[0], hi = w[1];
   const int k = (int)r - rf;
   const uint64_t word = k < 8 ? lo : hi;
   const uint8_t mk = (uint8_t)(word >> (8 * (k & 7)));
-  return !(e >= rm.mlo && e < rm.mhi) || mk == ep;
+  return !inside || mk == ep;
 }
 
 template <bool BF16OUT, bool PREP, int U, bool NT, bool MK>
