@@ -168,6 +168,16 @@ def main():
         run(f"vocab dh split-K={sk}", lambda: ops.gemm(dl, Wo, slab_dh, R, d, V1, False, True, ops.epilogue(),
                                                         split_k=sk, slab=slab_dh), R * V1 * es + V1 * d * es,
             2 * R * V1 * d)
+        if ops.vocab_head_supported(d):
+            # the bench's cfg5 roofline kernel at its shape (R = the batches' mean labelled count, bench.py roofline)
+            Rh = 1574 if V1 > 500000 else R
+            hh = rn(Rh, d)
+            labh = torch.randint(1, V1, (Rh,), device=dev, generator=g)
+            wsh = torch.empty(ops.vocab_ce_ws_numel(Rh, V1), device=dev)
+            outh = torch.empty(4, device=dev)
+            run("vocab_head_fwd (E-stationary, online-softmax partials)",
+                lambda: ops.vocab_head_fwd(hh, Wo, bo, labh, wsh, outh),
+                (V1 * d + Rh * d) * es + Rh * -(-V1 // 128) * 8, 2 * Rh * V1 * d)
         dWo = torch.zeros(V1, d, device=dev)
         slab_o = torch.empty(ops.wgrad_slab_numel(R, V1, d), device=dev)
         run("vocab wgrad+bias",lambda: ops.linear_wgrad(dl, h, dWo, slab_o, db=bo),

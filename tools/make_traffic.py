@@ -18,7 +18,9 @@ import sys
 KEYS = {"rs_attn_bwd (attn_bwd_lds: dQ + dK/dV workgroups)": ["attn_bwd_lds_kernel"],
         "rs_wgrad_grouped (wgrad_group_kernel + reduce_cols_kernel)": ["wgrad_group_kernel", "reduce_cols_kernel"],
         "rs_wgrad_grouped (wgrad_group256_kernel + reduce_cols_kernel)": ["wgrad_group256_kernel",
-                                                                         "reduce_cols_kernel"]}
+                                                                         "reduce_cols_kernel"],
+        "rs_vocab_head_fwd (E-tile-stationary logits + online-softmax partials)": ["pp_kernel<256, false>",
+                                                                                  "ce_tiles_kernel"]}
 
 
 def per_dispatch(root):
