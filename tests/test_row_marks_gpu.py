@@ -13,11 +13,14 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("prep", [False, True])
-@pytest.mark.parametrize("moff", [1000, -4 * 128 * 3])
-def test_marked_sweep_equals_unmarked(prep, moff):
+@pytest.mark.parametrize("moff", [1000, -4 * 128 * 3, 900_004 - 5000 * 64 + 12])
+@pytest.mark.parametrize("dshift", [6, 7, 8])
+def test_marked_sweep_equals_unmarked(prep, moff, dshift):
+    """moff: the table starts mid-wave inside the range, the range starts inside the table, the table runs past the
+    range's end; d = 64 / 128 / 256 (a wave's 256 elements span up to 5 / 3 / 2 rows)."""
     import rbm_amd  # noqa: F401
     from rbm_amd import ops
-    dshift, rows = 7, 5000              # d = 128
+    rows = 5000
     d = 1 << dshift
     n = 900_004
     gen = torch.Generator(device="cuda").manual_seed(3)
