@@ -78,6 +78,12 @@ def main():
     print(f"fork 2 spins early, side 1 || main 1    : {v:.1f} us  (edges cost {v - 5 * one:.1f})")
     v = timed(lambda: fork_join(3, 1, 2, 1, early=2))
     print(f"fork 2 spins early, side 1 || main 2    : {v:.1f} us  (vs 6 serial: {v - 6 * one:.1f})")
+    for k in (2, 4):
+        v = timed(lambda: fork_join(1, k, k, 1))
+        print(f"1 | fork: side {k} || main {k} | join | 1 : {v:.1f} us  (ideal {(2 + k) * one:.1f}, serial "
+              f"{(2 + 2 * k) * one:.1f})")
+    v = timed(lambda: fork_join(1, 2, 0, 3))
+    print(f"1 | fork: side 2 | join | 3 (main idle) : {v:.1f} us  (serial {6 * one:.1f})")
 
 
 if __name__ == "__main__":
