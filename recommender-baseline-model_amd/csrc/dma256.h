@@ -19,7 +19,10 @@ typedef __attribute__((ext_vector_type(4))) __bf16 bf4;
 // Every DMA source is clamped into the operand; the last (partial) stage zeroes its k rows / columns past the end in
 // LDS before use.  One raw s_barrier per stage (after this wave's counted vmcnt and lgkmcnt(0)) publishes the
 // stage and frees the buffer the next DMA overwrites.
-constexpr int DBK = 32, NBUF = 4, DIST = 3;
+#ifndef G256_DIST
+#define G256_DIST 3
+#endif
+constexpr int DBK = 32, DIST = G256_DIST, NBUF = DIST + 1;
 constexpr int KM_HALF = DBK * 128 * 2;          // bytes of one [32][128] half image
 constexpr int IMG_BYTES = DBK * 256 * 2;        // 16 KB: one operand's stage image
 constexpr int DSTAGE = 2 * IMG_BYTES;           // A + B
@@ -54,6 +57,14 @@ __device__ __forceinline__ void dma16(const void* gsrc, uint32_t dst) {
                : "memory");
 }
 template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory"); }
+// wait for the oldest stage of a wave's DMAs, `after` later stages (4 pieces each: 2 per operand) left in flight
+__device__ __forceinline__ void vm_wait_stages(int after) {
+  if (after >= 4) vm_wait<16>();
+  else if (after == 3) vm_wait<12>();
+  else if (after == 2) vm_wait<8>();
+  else if (after == 1) vm_wait<4>();
+  else vm_wait<0>();
+}
 __device__ __forceinline__ void raw_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();

@@ -123,9 +123,7 @@ __global__ __launch_bounds__(NTH) void gemm_n256_dma_kernel(Args a) {
   for (int t = 0; t < min(nk, DIST); ++t) issue(t);
   for (int t = 0; t < nk; ++t) {
     const int after = min(nk - 1, t + DIST - 1) - t;   // stages issued after t, allowed to stay in flight
-    if (after >= 2) vm_wait<8>();
-    else if (after == 1) vm_wait<4>();
-    else vm_wait<0>();
+    vm_wait_stages(after);
     raw_barrier();                                      // stage t landed everywhere; buffer (t - 1) % NBUF free
     if (t + DIST < nk) issue(t + DIST);
     if (tail && t == nk - 1) {

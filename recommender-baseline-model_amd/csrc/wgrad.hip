@@ -316,9 +316,7 @@ __global__ __launch_bounds__(g256::NTH) void wgrad_group256_kernel(Args256 a) {
   for (int st = 0; st < min(nk, DIST); ++st) issue(st);
   for (int st = 0; st < nk; ++st) {
     const int after = min(nk - 1, st + DIST - 1) - st;
-    if (after >= 2) vm_wait<8>();
-    else if (after == 1) vm_wait<4>();
-    else vm_wait<0>();
+    vm_wait_stages(after);
     raw_barrier();
     if (st + DIST < nk) issue(st + DIST);
     if (tail && st == nk - 1) {
