@@ -4,9 +4,11 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg5] [--batch B]
 
 BASELINE.json's metric is training sequences/sec for SASRec T=200 d=128 (configs[1] = cfg2,
-the default).  For N > 1 the driver launches one process per GPU (torchrun; RANK /
-LOCAL_RANK / WORLD_SIZE from the env): data parallel, RCCL all-reduce of the flat gradient
-(+ loss-sum/count aux) each step, weak scaling (B sequences per GPU).
+the default).  For N > 1 one process runs per GPU: either the driver's torchrun starts them
+(RANK / LOCAL_RANK / WORLD_SIZE from the env; WORLD_SIZE must equal --gpus), or `bench.py --gpus N`
+started alone launches the N ranks itself (torch.distributed.run children, before any GPU call).
+Data parallel, RCCL all-reduce of the flat gradient (+ loss-sum/count aux) each step, weak
+scaling (B sequences per GPU).
 
 One "step" = zero_grad + forward + loss + backward (+ all-reduce) + Adam on one synthetic batch
 already resident in HBM: the step is captured once in HIP graphs and replayed; each replay first
@@ -81,7 +83,56 @@ def parse():
     ap.add_argument("--sampler", default="host", choices=["host", "device"],
                     help="SAS: 'device' = batches drawn each step by the on-device WarpSampler "
                          "(rs_sas_sample) inside the step's graph, from synthetic user histories")
+    ap.add_argument("--launch-selftest", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
+
+
+# ------------------------------------------------------------------------------------ rank launcher
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` started WITHOUT a torchrun environment (no WORLD_SIZE): start the N data-parallel
+    ranks as child processes -- torch.distributed.run, one process per GPU, rendezvous on 127.0.0.1 -- and
+    return the worst exit status.  Called before anything touches the GPU (this process never initialises
+    HIP; the children do), and the children are started, never exec'd into.  The reference picks its device
+    count from the device list (`BS/utils.py:74-76`, `BS/trainers/base.py:32-34`)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")     # dmabuf IPC: RCCL / CUDA-tensor sharing across ranks
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def world_from_env(gpus):
+    """(world, rank, local_rank) of this process; under torchrun WORLD_SIZE must equal --gpus."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != gpus:
+        raise SystemExit(f"WORLD_SIZE={world} but --gpus {gpus}: start N ranks with `bench.py --gpus N` "
+                         f"(it launches them) or torchrun --nproc-per-node N ... bench.py --gpus N")
+    return world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def launch_selftest(args):
+    """CPU check of the launcher's plumbing (tests/test_bench_launch.py): every rank joins a gloo group of the
+    launched size, the ranks all-reduce their rank ids, and rank 0 prints one line with the live world size."""
+    world, rank, _ = world_from_env(args.gpus)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    t = torch.tensor([float(rank)])
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "parallelism": f"dp{world}", "rank_sum": t.item()}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def model_args(cfg, dtype, device):
@@ -265,6 +316,35 @@ def roofline(cfg, B, dtype, live_us=None, reps=50, labelled=None, live_expected=
 
 
 # ------------------------------------------------------------------------------------ CPU baseline
+def _cgroup_cpu_quota():
+    """CPUs granted by the cgroup's CPU quota (v2 cpu.max, v1 cfs_quota_us / cfs_period_us), None if unlimited."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = float(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = float(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
+def host_cpu_share():
+    """The CPU share this process may use, from what the host actually grants it: the scheduler affinity mask, the
+    cgroup CPU quota and the job's OMP_NUM_THREADS limit (the GPU box sets it to its per-GPU share); the baseline
+    runs on the smallest of them.  os.cpu_count() is the whole host's count and is reported, not used."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = _cgroup_cpu_quota()
+    omp = os.environ.get("OMP_NUM_THREADS")
+    omp = int(omp) if omp and omp.isdigit() and int(omp) > 0 else None
+    lim = [aff] + ([max(1, int(quota))] if quota else []) + ([omp] if omp else [])
+    return {"threads": max(1, min(lim)), "affinity_cpus": aff,
+            "cgroup_quota_cpus": round(quota, 2) if quota else None, "omp_num_threads": omp,
+            "host_logical_cpus": os.cpu_count()}
+
+
 def cpu_baseline(cfg, B, seconds):
     """The CPU oracle (PyTorch-CPU fp32 restatement of the reference math, torch bernoulli dropout
     at the config value like the reference) timed on this host's cores: full train steps
@@ -272,7 +352,8 @@ def cpu_baseline(cfg, B, seconds):
     from oracle import bert as obert
     from oracle import sas as osas
     from oracle.optim import AdamOracle
-    cores = max(1, min(16, os.cpu_count() or 1))     # the GPU box's CPU share is 16 threads (os.cpu_count: the host's)
+    share = host_cpu_share()
+    cores = share["threads"]
     try:
         import psutil
         physical = psutil.cpu_count(logical=False)
@@ -307,15 +388,21 @@ def cpu_baseline(cfg, B, seconds):
     return {"value": round(steps * Bc / dt, 2), "unit": "sequences/s", "cores": cores, "kind": "port",
             "sample": f"{steps} full train steps (fwd+loss+bwd+Adam, fp32, dropout {cfg['p']}) at batch {Bc} of the "
                       f"workload with the CPU oracle (oracle/{cfg['model']}.py), {dt:.1f} s on {cores} threads"
-                      f" (host: {os.cpu_count()} logical / {physical} physical cores)"}
+                      f" (host: {os.cpu_count()} logical / {physical} physical cores)",
+            "cpu_share": share}
 
 
 # ------------------------------------------------------------------------------------ main
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # N ranks requested without a launcher: start them (torch.distributed.run children) and report the worst rc
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if args.launch_selftest:
+        return launch_selftest(args)
+    world, rank, local = world_from_env(args.gpus)
     dev = local % max(1, torch.cuda.device_count())     # one GPU per rank (ranks > GPUs: gloo rehearsal only)
     torch.cuda.set_device(dev)
     if world > 1:
@@ -429,11 +516,13 @@ def main():
     for i in range(args.warmup % S):
         loss = eager(i)
     torch.cuda.synchronize()
+    replicas_checked = False
     if world > 1:
         # the replicas must hold the same parameter bits after the warmup steps (one all-reduced gradient per
         # step): checks the exchange -- in-graph or segmented -- end to end before anything is timed
         if not trainer.replicas_equal():
             raise SystemExit(f"rank {rank}: data-parallel replicas diverged during warmup")
+        replicas_checked = True
         dist.barrier()
     torch.cuda.synchronize()
     if sbuf is not None:
@@ -520,6 +609,11 @@ def main():
             line["config"]["labelled_rows_cap"] = max_lab
         if vshard:
             line["config"]["vocab_sharded_head"] = True
+        if world > 1:
+            # every rank compared its parameters with rank 0's after the warmup steps (SystemExit otherwise)
+            line["dp"] = {"backend": args.dist_backend, "replicas_equal_after_warmup": replicas_checked,
+                          "graph_collectives": bool(trainer.graph_collectives),
+                          "sharded_item_table": trainer.rshard is not None}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -264,7 +264,9 @@ int rs_adam_prepare_step_loss(int64_t n, float* p, float* g, float* m, float* v,
                               const int64_t* tdesc, int ntd, int64_t tbase, void* wT, const float* loss_sum,
                               float* loss_out, void* stream);
 /* rs_adam_step_wg / rs_adam_prepare_step_loss over a range holding (part of) a table whose gradient only
- * rs_item_grad_marked writes: table row r is launch element moff + r * 2^dshift (moff may be negative), mrows rows;
+ * rs_item_grad_marked writes: table row r is launch element moff + r * 2^dshift (moff may be negative), mrows rows,
+ * 5 <= dshift <= 16 (rows of at least 32 elements: a wave tests its rows' marks from one 16-byte window; smaller
+ * dshift returns RS_ERR_ARG);
  * a row with row_marks[r] != *epoch has a zero gradient this step, so its gradient is not read (nor cleared: it
  * is zero already).  Same results bit for bit as the unmarked launches.  row_marks == NULL: the unmarked launch.
  * row_marks: 16-byte aligned, (mrows + 15) / 16 * 16 + 16 + 1024 bytes, the bytes past the stamps zero (the

@@ -447,12 +447,15 @@ int rs_adam_prepare(double* state, const double* hyper, const float* grad_diviso
 
 // row_marks layout: mrows stamps, padding to 16 B + 16 (the scalar loads' overrun), then 1 KB of zeros
 #define ROW_MARKS_ZEROS(rows) ((((rows) + 15) / 16) * 16 + 16)
-// the marked table's rows inside launch elements [0, n): row r of the table is launch element moff + r << dshift
+// the marked table's rows inside launch elements [0, n): row r of the table is launch element moff + r << dshift.
+// A wave's mark test reads ONE 16-byte scalar window from its first active lane's row rounded down to 8: that
+// covers the wave's 256 elements only while they span <= 9 rows, i.e. rows of >= 32 elements (dshift >= 5)
+#define ROW_MARKS_MIN_DSHIFT 5
 static int row_marks(int64_t n, const uint8_t* marks, const uint8_t* epoch, int64_t moff, int64_t mrows, int dshift,
                      RowMarks& rm) {
   rm = RowMarks{nullptr, nullptr, nullptr, 0, 0, 0, 0};
   if (!marks) return 0;
-  if (!epoch || mrows <= 0 || dshift < 2 || dshift > 16 || moff % 4 || (uintptr_t)marks % 16) return RS_ERR_ARG;
+  if (!epoch || mrows <= 0 || dshift < ROW_MARKS_MIN_DSHIFT || dshift > 16 || moff % 4 || (uintptr_t)marks % 16) return RS_ERR_ARG;
   rm.marks = marks; rm.epoch = epoch; rm.moff = moff; rm.dshift = dshift;
   rm.zeros = reinterpret_cast<const float*>(marks + ROW_MARKS_ZEROS(mrows));
   rm.mlo = std::max<int64_t>(0, moff);

@@ -168,8 +168,8 @@ class FusedTrainStep:
         sparse_rows (BERT, DP with overlap): "auto" (default: when the gathered ids are at most half the table),
         "on" or "off" -- the token table's gradient is exchanged as the union of the rows the ranks touched
         (dp.SparseRowExchange) instead of inside the dense buckets.
-        shard_rows (SAS, DP): "auto" (default: when each rank's part of the item table is >= 64k elements), "on" or
-        "off" -- the item table's optimizer is sharded over the ranks (dp.ShardedRows): its gradient is
+        shard_rows (SAS, DP): "auto" (default: when each rank's part of the item table is >= 64k elements, gloo
+        only -- off over RCCL until a multi-GPU run verifies it), "on" or "off" -- the item table's optimizer is sharded over the ranks (dp.ShardedRows): its gradient is
         reduce-scattered, each rank updates its part, the compute rows are all-gathered.  The other ranks' parts of
         the fp32 master and Adam moments are then not current on this rank: checkpoint() / gather_shards() gather
         them (needs l2_emb == 0: the regulariser reads every master row)."""
@@ -219,10 +219,14 @@ class FusedTrainStep:
         self.steps_per_graph = 1
         self._stamps = None
         self.rshard = None
+        # "auto" stays off over RCCL: its in-place reduce-scatter / all-gather are checked at world size 1 and over
+        # gloo with two ranks only (one GPU reaches this builder, and RCCL refuses two ranks on one device), so the
+        # sharded form is an explicit opt-in there until a multi-GPU run pins it to the dense exchange
+        auto_ok = dpx.backend(self.pg) != "nccl" if self.dp else False
         if self.dp and self.kind == "sas" and shard_rows != "off":
             name = "item_emb.weight"
             n = self.flat.view(name).numel()
-            if shard_rows == "on" or dpx.ShardedRows.worthwhile(n, dpx.world(self.pg)):
+            if shard_rows == "on" or (auto_ok and dpx.ShardedRows.worthwhile(n, dpx.world(self.pg))):
                 if self.l2:
                     if shard_rows == "on":
                         raise ValueError("shard_rows needs l2_emb == 0 (the regulariser reads every master row)")
@@ -576,8 +580,9 @@ class FusedTrainStep:
     def optimizer_state_dict(self):
         """The optimizer state in torch.optim.Adam's state_dict() layout (param_groups from a real Adam over
         the same parameters; per-parameter 'step', 'exp_avg', 'exp_avg_sq'), so the reference trainer can
-        resume from it (BS/trainers/base.py:255-259, 'optimizer_state_dict')."""
-        if self.rshard is not None:
+        resume from it (BS/trainers/base.py:255-259, 'optimizer_state_dict').  With the sharded item table and stale
+        rows (after a step) this is COLLECTIVE: call it on every rank, not from rank 0 alone."""
+        if self.rshard is not None and self.flat.stale:
             self.gather_shards()
         torch.cuda.synchronize()
         hy = self.opt.hyper.cpu().tolist()
@@ -624,6 +629,14 @@ class FusedTrainStep:
             for buf in (self.flat.data, self.opt.m, self.opt.v):
                 self.vshard.gather_rows(self.flat.view(name, buf))
         self.engine.sync_compute_weights()
+
+    def state_dict(self):
+        """model.state_dict() with every row current: under a sharded optimizer (vocabulary / item table) the other
+        ranks' fp32 master rows are stale on this rank after a step (flat.stale), so they are gathered first.
+        Collective when sharded: call on every rank.  Read the weights through this (or checkpoint()), not through
+        model.state_dict() / model.parameters() directly, whenever shard_rows / vocab_shard is on."""
+        self.gather_shards()
+        return self.model.state_dict()
 
     def checkpoint(self, epoch=None):
         """{'model_state_dict', 'optimizer_state_dict'[, 'epoch']} as the reference's loggers save it

@@ -34,3 +34,22 @@ def test_bench_json_line(config):
     assert 0.5 < roof["avg_launch_us"] / roof["isolated_launch_us"] < 2.0
     cpu = d["cpu_baseline"]
     assert cpu["kind"] == "port" and cpu["value"] > 0 and cpu["cores"] >= 1
+
+
+def test_bench_two_ranks_gloo():
+    """`bench.py --gpus 2` started alone launches both data-parallel ranks itself (here: two processes on one GPU over
+    gloo; the driver's SCALE runs use RCCL on one GPU per rank): one JSON line, the live world size, the replicas'
+    parameters equal after the warmup steps, the whole-job value over both ranks."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+                        "--config", "cfg2", "--steps", "4", "--warmup", "2", "--roofline-replays", "2"],
+                       capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert REQUIRED <= set(d), REQUIRED - set(d)
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 256
+    assert d["dp"]["replicas_equal_after_warmup"] is True and d["dp"]["backend"] == "gloo"
+    assert abs(d["value"] - 256 / (d["ms_per_step"] * 1e-3)) < 0.01 * d["value"]
+    assert d["cpu_baseline"] is None                          # rank 0 at N = 1 only

@@ -149,3 +149,21 @@ def test_training_with_row_marks_equals_unmarked(kind, graph, monkeypatch):
     assert res[0][0] == res[1][0]
     for a, b in zip(res[0][1:], res[1][1:]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("dshift", [2, 4])
+def test_marked_sweep_rejects_narrow_rows(dshift):
+    """A wave tests its rows' marks from one 16-byte window of the marks array: rows narrower than 32 elements would
+    put more than 9 rows under one wave, so the ABI refuses them (RS_ERR_ARG -> RuntimeError) instead of skipping
+    stamped rows."""
+    import rbm_amd  # noqa: F401
+    from rbm_amd import ops
+    n, rows = 4096, 64
+    p, g, m, v = (torch.zeros(n, device="cuda") for _ in range(4))
+    pb = torch.empty(n, dtype=torch.bfloat16, device="cuda")
+    st = torch.zeros(144, dtype=torch.float64, device="cuda")
+    hyper = torch.tensor([1e-3, 0.9, 0.999, 1e-8, 0.0], dtype=torch.float64, device="cuda")
+    marks = torch.zeros(ops.row_marks_bytes(rows), dtype=torch.uint8, device="cuda")
+    epoch = torch.zeros(1, dtype=torch.uint8, device="cuda")
+    with pytest.raises(RuntimeError):
+        ops.adam_step(p, g, m, v, pb, st, hyper, zero_grad=True, max_wg=8, marks=(marks, epoch, 0, rows, dshift))
