@@ -97,3 +97,77 @@ def user_histories(rng, n_users, max_len, num_items, shape="ml-1m", zipf=None):
     zipf = zipf or ZipfItems(num_items)
     lens = history_lengths(rng, n_users, max_len, shape)
     return [zipf.sample(rng, int(n)).tolist() for n in lens]
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# Leave-one-out train / eval streams with sequential structure (the HR@10 parity run at the benchmarked shape).
+# Zipf-only histories teach a model item popularity and nothing else; here each item has a few fixed successors, so
+# ranking the held-out item needs the attention over the history.  Split and candidates follow the reference:
+# ``BS/dataloaders`` data_partition (train = all but the last two items, val = second last, test = last),
+# ``WarpSampler`` batches (``BS/dataloaders/sas.py:65-79``), ``SASEvalDataset`` (``:125-153``: the last max_len
+# items, left padding, candidates = answer + negatives) with ``RandomNegativeSampler``'s 100 negatives per user
+# (uniform over 1..V, not seen by the user, no repeats; ``BS/dataloaders/negative_samplers/random.py``).
+
+def loo_users(rng, n_users, max_len, num_items, follow=0.7, n_succ=3, shape="ml-1m", zipf=None):
+    """Per-user histories (train, val, test): history lengths as `history_lengths` + 2; the first item Zipf, each
+    next item one of its predecessor's `n_succ` fixed successors with probability `follow`, else Zipf."""
+    zipf = zipf or ZipfItems(num_items)
+    succ = zipf.sample(rng, (num_items + 1, n_succ))
+    lens = history_lengths(rng, n_users, max_len, shape) + 2
+    train, val, test = [], [], []
+    for n in lens.tolist():
+        h = np.empty(n, np.int64)
+        h[0] = zipf.sample(rng, 1)[0]
+        jump = rng.random(n) < follow
+        k = rng.integers(0, n_succ, size=n)
+        z = zipf.sample(rng, n)
+        for j in range(1, n):
+            h[j] = succ[h[j - 1], k[j]] if jump[j] else z[j]
+        train.append(h[:-2])
+        val.append(int(h[-2]))
+        test.append(int(h[-1]))
+    return train, val, test
+
+
+def loo_train_batch(rng, train, batch, max_len, num_items):
+    """One WarpSampler batch (seq, pos, neg) over the users' train histories: a uniform user, seq = its history
+    shifted by one, pos the next items, neg uniform items outside the history, the last max_len positions, left
+    padding."""
+    seq = np.zeros((batch, max_len), np.int64)
+    pos = np.zeros((batch, max_len), np.int64)
+    neg = np.zeros((batch, max_len), np.int64)
+    users = rng.integers(0, len(train), size=batch)
+    for b, u in enumerate(users.tolist()):
+        h = train[u]
+        n = min(len(h) - 1, max_len)
+        seen = set(h.tolist())
+        ng = rng.integers(1, num_items + 1, size=n)
+        for j in range(n):
+            while int(ng[j]) in seen and len(seen) < num_items:
+                ng[j] = rng.integers(1, num_items + 1)
+        seq[b, max_len - n:] = h[-n - 1:-1]
+        pos[b, max_len - n:] = h[-n:]
+        neg[b, max_len - n:] = ng
+    return seq, pos, neg
+
+
+def loo_eval_set(rng, train, val, test, max_len, num_items, n_neg=100):
+    """The test split as SASEvalDataset serves it: seq = (train + val)[-max_len:] left-padded, candidates = [test]
+    + n_neg negatives never seen by the user (no repeats), labels = [1, 0 ... 0].  Returns int64 arrays."""
+    U = len(train)
+    seq = np.zeros((U, max_len), np.int64)
+    cand = np.zeros((U, 1 + n_neg), np.int64)
+    for u in range(U):
+        h = np.append(train[u], val[u])[-max_len:]
+        seq[u, max_len - len(h):] = h
+        seen = set(train[u].tolist()) | {val[u], test[u]}
+        negs = []
+        while len(negs) < n_neg:
+            i = int(rng.integers(1, num_items + 1))
+            if i not in seen and i not in negs:
+                negs.append(i)
+        cand[u, 0] = test[u]
+        cand[u, 1:] = negs
+    labels = np.zeros_like(cand)
+    labels[:, 0] = 1
+    return seq, cand, labels

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build librecsys_hip.$NAME.so: SRC (a csrc/*.hip translation unit) recompiled with extra FLAGS, linked with the
-# other in-tree objects (run the normal build first).  For A/B timing with RS_LIB_VARIANT=$NAME (tools/ab_bench.sh).
+# other in-tree objects (run the normal build first).  For A/B timing with RS_LIB_VARIANT=$NAME (tools/gpu.sh ab).
 #   NAME=p1 SRC=rowchain.hip FLAGS="-DRC_HEAD_PREFETCH=1" bash tools/build_variant.sh
 set -e
 cd "$(dirname "$0")/.."

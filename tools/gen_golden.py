@@ -12,7 +12,9 @@ The reference never travels to the GPU box; this script refuses to run when
 ``/root/reference`` is absent.  Nothing is written into the reference tree:
 bytecode writing is disabled and the CWD is switched to a temp dir.
 
-    python tools/gen_golden.py            # all fixtures
+    python tools/gen_golden.py                 # all fixtures
+    python tools/gen_golden.py --bench-curve   # the 1000-step loss curve at the benchmarked shape
+    python tools/gen_golden.py --bench-hr      # 1000 training steps + HR@10 at the benchmarked configuration
 """
 import argparse
 import os
@@ -232,8 +234,76 @@ def metrics_case(name):
     print(name, m["Recall@10"], m["NDCG@10"])
 
 
+def _hashes(sd):
+    """sha256 of each tensor's float32 bytes: pins an initialisation without storing it."""
+    import hashlib
+    return {k: hashlib.sha256(v.detach().cpu().float().numpy().tobytes()).hexdigest() for k, v in sd.items()}
+
+
+def _ref_eval(model, seq, cand, labels, ks, chunk=512):
+    """The reference's validate() scoring (BS/trainers/sas.py:56-62: model.predict on the candidates) over the whole
+    eval set, ranked once by its recalls_ndcgs_and_mrr_for_ks (BS/trainers/utils.py:28-57)."""
+    model.eval()
+    with torch.no_grad():
+        sc = torch.cat([model.predict(torch.from_numpy(seq[i:i + chunk]), torch.from_numpy(cand[i:i + chunk]))
+                        for i in range(0, len(seq), chunk)])
+    model.train()
+    return sc.numpy(), recalls_ndcgs_and_mrr_for_ks(sc, torch.from_numpy(labels), ks)
+
+
+HR = dict(V=3416, T=200, d=128, L=2, h=1, B=128, p=0.2, steps=1000, lr=1e-3, users=6040, init_seed=8, data_seed=11,
+          batch_seed=12, eval_seed=13)
+
+
+def sas_hr_bench(name="sas_hr_bench"):
+    """HR@10 at the benchmarked configuration (BASELINE configs[1]: V 3,416, T 200, d 128, 2 blocks, 1 head, B 128,
+    dropout 0.2): the reference's own SASModel trained by its own calculate_loss + Adam for 1000 steps on
+    leave-one-out WarpSampler batches (rbm_amd.data.loo_*), then evaluated as its validate() does on all users with
+    1 + 100 candidates.  Stores the reference's init hashes, final weights, losses and metrics (init and final)."""
+    c = HR
+    V, T, d, L, h, B = c["V"], c["T"], c["d"], c["L"], c["h"], c["B"]
+    ks = [1, 5, 10, 20]
+    train, val, test = synth.loo_users(np.random.default_rng(c["data_seed"]), c["users"], T, V)
+    seq, cand, labels = synth.loo_eval_set(np.random.default_rng(c["eval_seed"]), train, val, test, T, V)
+    torch.manual_seed(c["init_seed"])
+    args = sas_args(V, T, d, L, h, p=c["p"])
+    model = model_factory(args)
+    model.train()
+    out = {k: np.float64(v) if isinstance(v, float) else np.int64(v) for k, v in c.items()}
+    out["ks"] = np.array(ks)
+    out.update({"init_sha/" + k: np.array(v) for k, v in _hashes(model.state_dict()).items()})
+    out["eval_checksum"] = np.int64(int((seq * 31 + 7).sum() + (cand * 131).sum()))
+    sc0, m0 = _ref_eval(model, seq, cand, labels, ks)
+    out.update({"m0/" + k: np.float64(v) for k, v in m0.items()})
+    opt = torch.optim.Adam(model.parameters(), lr=c["lr"], weight_decay=0)   # BS/trainers/base.py:225-228
+    fake = _FakeSAS(model, args)
+    rng = np.random.default_rng(c["batch_seed"])
+    losses, csum = [], 0
+    for i in range(c["steps"]):                                              # BS/trainers/base.py:114-123
+        batch = synth.loo_train_batch(rng, train, B, T, V)
+        csum += int(sum(((j + 1) * x).sum() for j, x in enumerate(batch)) % (1 << 40))
+        opt.zero_grad()
+        loss = SASTrainer.calculate_loss(fake, batch)
+        losses.append(loss.item())
+        loss.backward()
+        opt.step()
+        if i % 100 == 0:
+            print(name, "step", i, losses[-1], flush=True)
+    out["batch_checksum"] = np.int64(csum)
+    out["losses"] = np.array(losses, np.float64)
+    out.update(_pack("final/", model.state_dict()))
+    sc1, m1 = _ref_eval(model, seq, cand, labels, ks)
+    out.update({"m/" + k: np.float64(v) for k, v in m1.items()})
+    out["scores_head"] = sc1[:512]                   # the reference's fp32 scores of the first 512 users
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), **out)
+    print(name, "Recall@10 init", m0["Recall@10"], "trained", m1["Recall@10"], "loss", losses[0], "->", losses[-1])
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
+    if "--bench-hr" in sys.argv:
+        sas_hr_bench()
+        raise SystemExit(0)
     if "--bench-curve" in sys.argv:
         # the benchmarked SAS shape (BASELINE configs[1]: ML-1M items, T = 200, d = 128, 2 blocks, 1 head)
         sas_curve("sas_curve_bench", V=3416, T=200, d=128, L=2, h=1, B=16, steps=1000, seed=8, final=False,

@@ -1,5 +1,5 @@
 #!/usr/bin/env python
-"""profiles/traffic.json from rocprofv3 PMC passes (tools/gpu_pmc.sh output directory).
+"""profiles/traffic.json from rocprofv3 PMC passes (tools/gpu.sh pmc / traffic output directory).
 
     python tools/make_traffic.py gpurun_out/<tag> CONFIG [profiles/traffic.json]
 
