@@ -7,27 +7,9 @@
 //   rs_colsum                        bias gradients (sum over token rows), deterministic
 //   rs_dropout_rowmask               dropout/timeline-mask backward for SAS FFN dropout2
 //                                    (BS/models/sas_model/sas.py:17,84)
+#include "adam_math.h"
 #include "common.h"
 #include "../../include/recsys_hip.h"
-
-// Bias corrections of step t exactly as torch.optim.Adam forms them (BS/trainers/base.py:225-228; the
-// single-tensor path, torch/optim/adam.py): the hyperparameters are Python doubles there, bias_correction1 =
-// 1 - beta1 ** step, step_size = lr / bias_correction1, bias_correction2_sqrt = sqrt(1 - beta2 ** step) in double,
-// each cast to float where it meets the fp32 tensors.  hyper is double[5] for that reason: with fp32 betas,
-// 1 - 0.999f is 1.3e-5 (relative) off torch's float(1 - 0.999) -- a systematic bias in every v update and in
-// sqrt(bc2) that a 1000-step curve amplified.
-struct AdamScalars { float step_size, bc2s, gs; };
-__device__ __forceinline__ AdamScalars adam_scalars(double t, const double* hyper, const float* divisor) {
-  const double lr = hyper[0], b1 = hyper[1], b2 = hyper[2];
-  const double bc1 = 1.0 - pow(b1, t), bc2 = 1.0 - pow(b2, t);
-  return {(float)(lr / bc1), (float)sqrt(bc2), divisor ? 1.f / divisor[0] : 1.f};
-}
-// the per-element scalars: float(beta2) (exp_avg_sq.mul_(beta2)), float(1 - beta1) (lerp weight), float(1 - beta2)
-// (addcmul value), float(eps), float(weight_decay)
-struct AdamElem { float b2, omb1, omb2, eps, wd; };
-__device__ __forceinline__ AdamElem adam_elem(const double* hyper) {
-  return {(float)hyper[2], (float)(1.0 - hyper[1]), (float)(1.0 - hyper[2]), (float)hyper[3], (float)hyper[4]};
-}
 
 __device__ __forceinline__ void adam_commit(double* state, double t, AdamScalars c, uint64_t* seed_base) {
   if (seed_base) *seed_base += 1;   // next step's dropout masks (rs_seed_advance folded in)
@@ -77,14 +59,7 @@ __device__ __forceinline__ void adam4(int64_t i, float4 pp, float4 gg, float4 mm
                                       __bf16* __restrict__ wT, int64_t tlo, int64_t thi) {
   float* P = &pp.x; float* G = &gg.x; float* Mv = &mm.x; float* Vv = &vv.x;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    float gj = gs == 1.f ? G[j] : G[j] * gs;
-    if (h.wd != 0.f) gj = gj + h.wd * P[j];
-    Mv[j] = Mv[j] + h.omb1 * (gj - Mv[j]);                // exp_avg.lerp_(grad, 1-beta1)
-    Vv[j] = Vv[j] * h.b2 + h.omb2 * gj * gj;              // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
-    const float denom = sqrtf(Vv[j]) / bc2s + h.eps;
-    P[j] = P[j] - step_size * (Mv[j] / denom);            // param.addcdiv_(exp_avg, denom, -step_size)
-  }
+  for (int j = 0; j < 4; ++j) adam_elem_update(P[j], G[j], Mv[j], Vv[j], h, step_size, bc2s, gs);
   st4<NT>(p, i, pp);
   st4<NT>(m, i, mm);
   st4<NT>(v, i, vv);
@@ -241,12 +216,7 @@ __global__ __launch_bounds__(256) void adam_step_kernel(int64_t n, float* __rest
   // tail
   if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
     const int64_t j = n4 * 4 + threadIdx.x;
-    float gj = gs == 1.f ? g[j] : g[j] * gs;
-    if (h.wd != 0.f) gj = gj + h.wd * p[j];
-    m[j] = m[j] + h.omb1 * (gj - m[j]);
-    v[j] = v[j] * h.b2 + h.omb2 * gj * gj;
-    const float denom = sqrtf(v[j]) / bc2s + h.eps;
-    p[j] = p[j] - step_size * (m[j] / denom);
+    adam_elem_update(p[j], g[j], m[j], v[j], h, step_size, bc2s, gs);
     if (BF16OUT) pb[j] = (__bf16)p[j];
     if (zero_grad) g[j] = 0.f;
   }

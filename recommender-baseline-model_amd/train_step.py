@@ -333,6 +333,7 @@ class FusedTrainStep:
         if not (self._early_ok and update):
             return self._compute_impl(*batch, split=split)
         self.engine.after_head_grads = self._early_head_update
+        self.engine.head_adam = self._fused_head_update if self._fused_head_ok() else None
         self.engine.after_token_grads = self._early_token_update if self._early_token else None
         done = False
         try:
@@ -341,6 +342,7 @@ class FusedTrainStep:
             return out
         finally:
             self.engine.after_head_grads = None
+            self.engine.head_adam = None
             self.engine.after_token_grads = None
             if not done:
                 # an aborted compute (e.g. a capture failing after the fork) must not leave a forked update for the
@@ -498,6 +500,37 @@ class FusedTrainStep:
             self._early_ev.record(self._opt_stream)
         self._early_done.append((lo, hi))
         return True
+
+    def _fused_head_ok(self):
+        """The large-vocabulary head's dE with out.weight's Adam in its epilogue (rs_gemm_n256_adam)?
+        RS_FUSED_HEAD_ADAM=0 (read per step, for A/B): dE into the gradient buffer and the early sweep instead."""
+        f = self.flat
+        return (os.environ.get("RS_FUSED_HEAD_ADAM", "1") != "0" and f.bf16 is not None
+                and self.engine.overwritten_grads() is not None and f.shapes["out.weight"][1] == 256)
+
+    def _fused_head_update(self, dl, hl, cap, cnt):
+        """Engine hook (BERTEngine, after dh, in place of _early_head_update): fork onto the optimizer's side stream
+        rs_adam_prepare (the step's scalars, no seed advance), dE = dlogits^T h with out.weight's Adam update in the
+        GEMM's epilogue (its gradient never stored) and out.bias's gradient as column sums, then out.bias's update.
+        The same bits as dE into the gradient buffer + _early_head_update (tests/test_bert.py
+        ::test_bert_fused_head_adam_equals_sweep); _update joins it."""
+        rng = self.engine.head_grad_range()
+        f, o = self.flat, self.opt
+        self._early_kp = rng
+        self._early_done = []
+        cur = torch.cuda.current_stream()
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        self._opt_stream.wait_event(ev)
+        with torch.cuda.stream(self._opt_stream):
+            ops.adam_prepare(o.state, o.hyper)
+            V1 = f.shapes["out.weight"][0]
+            w = "out.weight"
+            ops.gemm_n256_adam(dl, hl, V1, cap, f.view(w), f.view(w, o.m), f.view(w, o.v), f.view(w, f.bf16), o.state,
+                               o.hyper, colsum=f.view("out.bias", f.grad), rows_dev=cnt)
+            o.step_range(f.offsets["out.bias"], rng[1], zero_grad=False)
+            self._early_ev = torch.cuda.Event()
+            self._early_ev.record(self._opt_stream)
 
     def _early_head_update(self):
         """Engine hook (BERTEngine: right after the head's dE / dh): fork the out.weight / out.bias update onto the
