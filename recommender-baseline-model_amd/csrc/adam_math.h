@@ -22,13 +22,16 @@ __device__ __forceinline__ AdamElem adam_elem(const double* hyper) {
   return {(float)hyper[2], (float)(1.0 - hyper[1]), (float)(1.0 - hyper[2]), (float)hyper[3], (float)hyper[4]};
 }
 // one element: gradient scale (1 / the data-parallel count), weight decay, exp_avg.lerp_(grad, 1-beta1),
-// exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2), param.addcdiv_(exp_avg, sqrt(exp_avg_sq) / bc2s + eps, -step_size)
+// exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2), param.addcdiv_(exp_avg, sqrt(exp_avg_sq) / bc2s + eps, -step_size).
+// Every fused multiply-add is spelled out and no other contraction is allowed: the compiler's own contraction
+// choices differed between the sweep and the GEMM epilogue inlining this (1 ulp in 0.5 % of the parameters).
 __device__ __forceinline__ void adam_elem_update(float& P, float G, float& Mv, float& Vv, const AdamElem& h,
                                                  float step_size, float bc2s, float gs) {
+#pragma clang fp contract(off)
   float gj = gs == 1.f ? G : G * gs;
-  if (h.wd != 0.f) gj = gj + h.wd * P;
-  Mv = Mv + h.omb1 * (gj - Mv);
-  Vv = Vv * h.b2 + h.omb2 * gj * gj;
+  if (h.wd != 0.f) gj = __builtin_fmaf(h.wd, P, gj);
+  Mv = __builtin_fmaf(h.omb1, gj - Mv, Mv);
+  Vv = __builtin_fmaf(h.omb2 * gj, gj, Vv * h.b2);
   const float denom = sqrtf(Vv) / bc2s + h.eps;
-  P = P - step_size * (Mv / denom);
+  P = __builtin_fmaf(-step_size, Mv / denom, P);
 }

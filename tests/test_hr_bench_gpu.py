@@ -11,7 +11,12 @@ BS/dataloaders/sas.py:125-153) on all 6,040 users with 1 + 100 candidates by rec
 (a) the HIP eval path (SASModel.predict -> rs_candidate_scores, rs_rank_metrics) on the reference's trained weights
     gives the reference's metrics: fp32 the same hit count at every k, bf16 HR@10 within a stated few users;
 (b) the FUSED TRAINER (the benchmarked bf16 step, and the fp32 parity mode) from the reference's initial weights
-    over the same 1000 batches ends at the reference-trained model's HR@10 within 0.01."""
+    over the same 1000 batches ends at the reference-trained model's HR@10 within 0.01.
+
+Measured (MI355X): the reference trains HR@10 0.166 -> 0.886 (5,353 of 6,040 users hit).  (a) fp32: the same hits at
+k = 1 / 5 / 10 / 20, scores 7e-7 from the reference's; bf16: HR@10 the same 5,353 hits (k = 1: 4,122 vs 4,126),
+scores 1.2e-2.  (b) bf16 fused trainer HR@10 0.8877 (gap +0.0015), NDCG@10 0.7833 vs 0.7838, last-100-step mean loss
+0.51927 vs 0.51914; fp32 fused trainer 0.8882 (gap +0.0020)."""
 import argparse
 
 import numpy as np

@@ -5,7 +5,7 @@
 # runs on the GPU in that call).
 #
 #   bash tools/gpu.sh suite                      pytest -m gpu, then __graft_entry__.smoke()
-#   bash tools/gpu.sh tests "<pytest args>"      a subset of the GPU tests
+#   bash tools/gpu.sh tests <pytest args...>     a subset of the GPU tests
 #   bash tools/gpu.sh bench cfg2 cfg4 ...        the default bench line per config (CPU baseline included)
 #   bash tools/gpu.sh profile cfg2 ...           rocprofv3 --kernel-trace --stats of bench.py + one step's timeline
 #   bash tools/gpu.sh traffic cfg2 cfg3 cfg4     HBM bytes of the roofline kernels (FETCH_SIZE / WRITE_SIZE passes)
@@ -33,7 +33,7 @@ suite() {
 }
 
 tests() {
-  timeout -k 10 ${LIMIT:-900} python -u -m pytest -x -v --timeout 240 --timeout-method thread $1 \
+  timeout -k 10 ${LIMIT:-900} python -u -m pytest -x -v -rP --timeout 240 --timeout-method thread "$@" \
     > "$OUT/pytest.log" 2>&1; rc=$?
   grep -E "PASSED|FAILED|ERROR|passed|failed" "$OUT/pytest.log" | tail -${TAILN:-40}
   return $rc
@@ -105,7 +105,7 @@ ab() {
 
 case "$mode" in
   suite) suite ;;
-  tests) tests "$1" ;;
+  tests) tests "$@" ;;
   bench) bench "$@" ;;
   profile) profile "$@" ;;
   traffic) traffic "$@" ;;
