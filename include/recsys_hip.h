@@ -224,10 +224,11 @@ int rs_gemm_n256(int a_kmajor, int64_t M, int64_t K, const void* A, int64_t lda,
  * p / m / v (fp32) and p_bf16 (the compute copy) at row stride ldp, the step's scalars from state (rs_adam_prepare
  * of this step: state[1..3]) and hyper.  Same bits as rs_gemm_n256 into a gradient buffer followed by rs_adam_step
  * over those rows; the gradient itself is never written (the 1M-item head's 1 GB per step, written and read back).
- * colsum (the bias gradient) as rs_gemm_n256. */
+ * colsum (the bias gradient) as rs_gemm_n256.  max_wg > 0: at most that many workgroups, each walking row tiles (the
+ * launch then leaves CUs to work beside it); 0: one workgroup per row tile. */
 int rs_gemm_n256_adam(int64_t M, int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb, float* p, float* m,
                       float* v, void* p_bf16, int64_t ldp, const double* state, const double* hyper, float* colsum,
-                      const int* rows_dev, void* stream);
+                      const int* rows_dev, int max_wg, void* stream);
 
 /* Eval scores at candidate ids (replaces SAS.predict's item_emb(candidates).matmul(final_feat), BS/models/sas_model/
  * sas.py:107-118, and BERTTrainer.calculate_metrics' logits[:, -1, :].gather(1, candidates), BS/trainers/bert.py:

@@ -46,25 +46,18 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f4v ntl(const float* a) { return __builtin_nontemporal_load(reinterpret_cast<const f4v*>(a)); }
 __device__ __forceinline__ void nts(float* a, f4v x) { __builtin_nontemporal_store(x, reinterpret_cast<f4v*>(a)); }
 
-template <bool AK, bool ADAM = false>
-__global__ __launch_bounds__(NTH) void gemm_n256_dma_kernel(Args a) {
-  constexpr int LDC = BN + 4;
-  constexpr int LDS_BYTES = NBUF * DSTAGE > (BM / 2) * LDC * 4 ? NBUF * DSTAGE : (BM / 2) * LDC * 4;
-  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+constexpr int LDC = BN + 4;
+constexpr int LDS_BYTES = NBUF * DSTAGE > (BM / 2) * LDC * 4 ? NBUF * DSTAGE : (BM / 2) * LDC * 4;
+
+// one 256 x 256 output tile (row tile tm, k split z)
+template <bool AK, bool ADAM>
+__device__ __forceinline__ void n256_tile(const Args& a, char* smem, unsigned tm, unsigned z) {
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
   constexpr int FM = 8, FN = 4;
 
   const int64_t Mb = (!AK && a.rows_dev) ? min(a.M, (int64_t)*a.rows_dev) : a.M;
   const int64_t Kb = (AK && a.rows_dev) ? min(a.K, (int64_t)*a.rows_dev) : a.K;
-  const unsigned tiles_m = (unsigned)((a.M + BM - 1) / BM);
-  unsigned tm, z;
-  {
-    const unsigned tot = gridDim.x, L = blockIdx.x, q = tot >> 3, r = tot & 7, x = L & 7;
-    const unsigned lg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (L >> 3);
-    z = lg / tiles_m;
-    tm = lg - z * tiles_m;
-  }
   const int64_t m0 = (int64_t)tm * BM;
   if (m0 >= Mb) return;
   const int64_t kbeg = (int64_t)z * a.k_per_split;
@@ -242,6 +235,25 @@ __global__ __launch_bounds__(NTH) void gemm_n256_dma_kernel(Args a) {
   }
 }
 
+template <bool AK, bool ADAM = false>
+__global__ __launch_bounds__(NTH) void gemm_n256_dma_kernel(Args a) {
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const unsigned tiles_m = (unsigned)((a.M + BM - 1) / BM);
+  if constexpr (ADAM) {
+    // a bounded grid walking the row tiles (rs_gemm_n256_adam's max_wg): the launch runs beside the encoder's
+    // backward and must leave it CUs (one 8-wave workgroup of ~133 KB LDS per CU)
+    for (unsigned tm = blockIdx.x; tm < tiles_m; tm += gridDim.x) {
+      n256_tile<AK, ADAM>(a, smem, tm, 0);
+      __syncthreads();
+    }
+  } else {
+    const unsigned tot = gridDim.x, L = blockIdx.x, q = tot >> 3, r = tot & 7, x = L & 7;
+    const unsigned lg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (L >> 3);
+    const unsigned z = lg / tiles_m;
+    n256_tile<AK, ADAM>(a, smem, lg - z * tiles_m, z);
+  }
+}
+
 // the k split of a k-contiguous product (dh): as many splits as fill the 256 CUs with whole row tiles, each a
 // multiple of the 64-deep stage
 static void splits_for(int64_t M, int64_t K, int& splits, int64_t& kps) {
@@ -288,14 +300,15 @@ int rs_gemm_n256(int a_kmajor, int64_t M, int64_t K, const void* A, int64_t lda,
 // BS/trainers/base.py:225-228): see recsys_hip.h
 int rs_gemm_n256_adam(int64_t M, int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb, float* p, float* m,
                       float* v, void* p_bf16, int64_t ldp, const double* state, const double* hyper, float* colsum,
-                      const int* rows_dev, void* stream) {
+                      const int* rows_dev, int max_wg, void* stream) {
   if (M <= 0 || K <= 0 || !A || !B || !p || !m || !v || !p_bf16 || !state || !hyper || ldb < 256 || ldp < 256 ||
       lda < M || (lda % 8) || (ldb % 8) || (ldp % 8) || ((uintptr_t)A % 16) || ((uintptr_t)B % 16) ||
       ((uintptr_t)p % 16) || ((uintptr_t)m % 16) || ((uintptr_t)v % 16) || ((uintptr_t)p_bf16 % 16))
     return RS_ERR_ARG;
   g256::Args a{M, K, (const __bf16*)A, lda, (const __bf16*)B, ldb, nullptr, ldp, 0, K, colsum, rows_dev,
                p, m, v, (__bf16*)p_bf16, state, hyper};
-  const dim3 grid((unsigned)((M + g256::BM - 1) / g256::BM)), blk(g256::NTH);
+  const int64_t tiles = (M + g256::BM - 1) / g256::BM;
+  const dim3 grid((unsigned)(max_wg > 0 ? std::min<int64_t>(tiles, max_wg) : tiles)), blk(g256::NTH);
   hipLaunchKernelGGL((g256::gemm_n256_dma_kernel<true, true>), grid, blk, 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }

@@ -264,6 +264,11 @@ class FusedTrainStep:
                           and os.environ.get("RS_EARLY_HEAD_ADAM", "1") != "0"
                           and hasattr(self.engine, "overwritten_grads"))
         self._opt_stream = torch.cuda.Stream(device=self.flat.device) if self._early_ok else None
+        # the token table's early update when the fused head update (a long bounded-grid launch) holds _opt_stream
+        self._tok_stream = torch.cuda.Stream(device=self.flat.device) if self._early_ok else None
+        self._tok_ev = None
+        self._fused_active = False
+        self._prep_ev = None
         self._early_done = []
         # (below the unzeroed-head vocabulary size -- cfg3's 27k classes -- the early update measured slower: 44.2-44.4k
         # -> 43.6-43.7k seq/s, three interleaved rounds; it runs only with the overwritten-gradient head)
@@ -348,6 +353,8 @@ class FusedTrainStep:
                 # an aborted compute (e.g. a capture failing after the fork) must not leave a forked update for the
                 # next step's _update to join
                 self._early_ev = None
+                self._tok_ev = None
+                self._fused_active = False
                 self._early_done = []
 
     def _compute_impl(self, *batch, split=None):
@@ -458,6 +465,10 @@ class FusedTrainStep:
                 cur = torch.cuda.current_stream()
                 done, self._early_done = self._early_done, []
                 cur.wait_event(self._early_ev)
+                if self._tok_ev is not None:
+                    cur.wait_event(self._tok_ev)
+                    self._tok_ev = None
+                self._fused_active = False
                 self.opt.step_rest(self._early_kp, seed_base=sb, done=done)
                 self._early_ev = None
             else:
@@ -493,13 +504,26 @@ class FusedTrainStep:
             return False
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream())
-        self._opt_stream.wait_event(ev)
-        with torch.cuda.stream(self._opt_stream):
-            self.opt.step_range(lo, hi, zero_grad=True, max_wg=self.EARLY_TOKEN_ADAM_WG)
-            self._early_ev = torch.cuda.Event()
-            self._early_ev.record(self._opt_stream)
+        if self._fused_active:
+            # the fused head update still holds _opt_stream: the table's sweep starts now on its own stream (the step's
+            # scalars were prepared on _opt_stream before the head update's launch, so wait for that point)
+            self._tok_stream.wait_event(ev)
+            self._tok_stream.wait_event(self._prep_ev)
+            with torch.cuda.stream(self._tok_stream):
+                self.opt.step_range(lo, hi, zero_grad=True, max_wg=self.EARLY_TOKEN_ADAM_WG)
+                self._tok_ev = torch.cuda.Event()
+                self._tok_ev.record(self._tok_stream)
+        else:
+            self._opt_stream.wait_event(ev)
+            with torch.cuda.stream(self._opt_stream):
+                self.opt.step_range(lo, hi, zero_grad=True, max_wg=self.EARLY_TOKEN_ADAM_WG)
+                self._early_ev = torch.cuda.Event()
+                self._early_ev.record(self._opt_stream)
         self._early_done.append((lo, hi))
         return True
+
+    # workgroups of the fused head update (one 8-wave workgroup per CU): the rest of the CUs run the encoder's backward
+    FUSED_HEAD_WG = int(os.environ.get("RS_FUSED_HEAD_WG", "128"))
 
     def _fused_head_ok(self):
         """The large-vocabulary head's dE with out.weight's Adam in its epilogue (rs_gemm_n256_adam)?
@@ -524,10 +548,13 @@ class FusedTrainStep:
         self._opt_stream.wait_event(ev)
         with torch.cuda.stream(self._opt_stream):
             ops.adam_prepare(o.state, o.hyper)
+            self._prep_ev = torch.cuda.Event()
+            self._prep_ev.record(self._opt_stream)
+            self._fused_active = True
             V1 = f.shapes["out.weight"][0]
             w = "out.weight"
             ops.gemm_n256_adam(dl, hl, V1, cap, f.view(w), f.view(w, o.m), f.view(w, o.v), f.view(w, f.bf16), o.state,
-                               o.hyper, colsum=f.view("out.bias", f.grad), rows_dev=cnt)
+                               o.hyper, colsum=f.view("out.bias", f.grad), rows_dev=cnt, max_wg=self.FUSED_HEAD_WG)
             o.step_range(f.offsets["out.bias"], rng[1], zero_grad=False)
             self._early_ev = torch.cuda.Event()
             self._early_ev.record(self._opt_stream)

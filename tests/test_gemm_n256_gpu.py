@@ -57,11 +57,12 @@ def test_dh_split_matches_float64(R, V, count):
     assert torch.equal(again[:, :m], slab[:, :m])
 
 
-@pytest.mark.parametrize("R,V,count", [(1750, 5000, None), (300, 70001, 200), (130, 257, None)])
-def test_dE_adam_epilogue_equals_gemm_then_sweep(R, V, count):
+@pytest.mark.parametrize("R,V,count,max_wg", [(1750, 5000, None, 0), (300, 70001, 200, 64), (130, 257, None, 1),
+                                              (1750, 5000, None, 7)])
+def test_dE_adam_epilogue_equals_gemm_then_sweep(R, V, count, max_wg):
     """rs_gemm_n256_adam (dE with torch.optim.Adam applied to the parameter rows in the epilogue) = rs_gemm_n256 into
     a gradient buffer followed by rs_adam_step over those rows: the same bits in p, m, v, the bf16 copy and the bias
-    column sums."""
+    column sums -- one workgroup per row tile (max_wg 0) or a bounded grid walking them."""
     import rbm_amd  # noqa: F401
     from rbm_amd import ops
     dl = _bf((R, V), 1e-2, seed=5, pad_cols=(-V) % 64)
@@ -81,7 +82,7 @@ def test_dE_adam_epilogue_equals_gemm_then_sweep(R, V, count):
         st[0] = 6.0
         ops.adam_prepare(st, hyper)
         if fused:
-            ops.gemm_n256_adam(dl, h, V, R, p, m, v, pb, st, hyper, colsum=db, rows_dev=rows)
+            ops.gemm_n256_adam(dl, h, V, R, p, m, v, pb, st, hyper, colsum=db, rows_dev=rows, max_wg=max_wg)
         else:
             gr = torch.empty(V, 256, device="cuda")
             ops.gemm_n256(dl, h, gr, True, V, R, colsum=db, rows_dev=rows)
