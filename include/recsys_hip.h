@@ -219,16 +219,6 @@ int rs_splitk_scatter_rows(int dtype, const float* slab, int splits, int64_t cap
 int rs_gemm_n256_splits(int64_t M, int64_t K);
 int rs_gemm_n256(int a_kmajor, int64_t M, int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb, float* C,
                  int64_t ldc, int split, int64_t c_split_stride, float* colsum, const int* rows_dev, void* stream);
-/* rs_gemm_n256 with a_kmajor = 1 (dE = dlogits^T h, BS/models/bert.py:10,16) whose epilogue applies
- * torch.optim.Adam (BS/trainers/base.py:225-228) to the M x 256 parameter rows instead of storing the gradient:
- * p / m / v (fp32) and p_bf16 (the compute copy) at row stride ldp, the step's scalars from state (rs_adam_prepare
- * of this step: state[1..3]) and hyper.  Same bits as rs_gemm_n256 into a gradient buffer followed by rs_adam_step
- * over those rows; the gradient itself is never written (the 1M-item head's 1 GB per step, written and read back).
- * colsum (the bias gradient) as rs_gemm_n256.  max_wg > 0: at most that many workgroups, each walking row tiles (the
- * launch then leaves CUs to work beside it); 0: one workgroup per row tile. */
-int rs_gemm_n256_adam(int64_t M, int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb, float* p, float* m,
-                      float* v, void* p_bf16, int64_t ldp, const double* state, const double* hyper, float* colsum,
-                      const int* rows_dev, int max_wg, void* stream);
 
 /* Eval scores at candidate ids (replaces SAS.predict's item_emb(candidates).matmul(final_feat), BS/models/sas_model/
  * sas.py:107-118, and BERTTrainer.calculate_metrics' logits[:, -1, :].gather(1, candidates), BS/trainers/bert.py:

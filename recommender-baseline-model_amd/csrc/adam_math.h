@@ -1,6 +1,6 @@
-// torch.optim.Adam's per-element update (BS/trainers/base.py:225-228; the single-tensor path of torch/optim/adam.py),
-// shared by the optimizer sweeps (misc.hip) and the vocabulary head's dE GEMM with the update in its epilogue
-// (gemm_n256.hip): one definition, so both produce the same bits.
+// torch.optim.Adam's per-element update (BS/trainers/base.py:225-228; the single-tensor path of torch/optim/adam.py)
+// for the optimizer sweeps (misc.hip): one definition, every fused multiply-add spelled out, so any kernel that
+// inlines it produces the same bits.
 #pragma once
 #include "common.h"
 
@@ -24,7 +24,8 @@ __device__ __forceinline__ AdamElem adam_elem(const double* hyper) {
 // one element: gradient scale (1 / the data-parallel count), weight decay, exp_avg.lerp_(grad, 1-beta1),
 // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2), param.addcdiv_(exp_avg, sqrt(exp_avg_sq) / bc2s + eps, -step_size).
 // Every fused multiply-add is spelled out and no other contraction is allowed: the compiler's own contraction
-// choices differed between the sweep and the GEMM epilogue inlining this (1 ulp in 0.5 % of the parameters).
+// choices differed between two kernels inlining the same expression (1 ulp in 0.5 % of the parameters; round 6's
+// dE GEMM with the update in its epilogue, measured and removed: DESIGN.md §4).
 __device__ __forceinline__ void adam_elem_update(float& P, float G, float& Mv, float& Vv, const AdamElem& h,
                                                  float step_size, float bc2s, float gs) {
 #pragma clang fp contract(off)

@@ -16,11 +16,7 @@
 //    with ds_read_b64_tr_b16 (the transposing LDS read);
 //  * dh's split-K workgroups are dealt so that the row tiles of one vocabulary slice share an XCD (its L2 holds
 //    the slice of E they all read);
-//  * the epilogue stages the fp32 tile through LDS in two 128-row halves and stores 1 KB rows -- or, for dE at one
-//    device (rs_gemm_n256_adam), applies torch.optim.Adam to those out.weight rows right there (adam_math.h, the
-//    optimizer sweep's per-element math): the 1 GB fp32 gradient of a 1M-item head is then never written nor read
-//    back by a separate sweep (2 GB of the step's HBM traffic).
-#include "adam_math.h"
+//  * the epilogue stages the fp32 tile through LDS in two 128-row halves and stores 1 KB rows.
 #include "common.h"
 #include "dma256.h"
 #include "../../include/recsys_hip.h"
@@ -35,29 +31,27 @@ struct Args {
   int64_t cz, k_per_split;
   float* colsum;                  // a_kmajor: colsum[m] = sum_k A(m, k) (nullable)
   const int* rows_dev;            // a_kmajor: bound on K; else bound on M (nullable)
-  // Adam epilogue (ADAM): C is the gradient of the parameter rows p[m * ldc + n] (fp32 master, moments m / v, bf16
-  // compute copy pb); the step's scalars from state[1..3] (rs_adam_prepare), the hyperparameters from hyper
-  float *p, *m, *v;
-  __bf16* pb;
-  const double *state, *hyper;
 };
 
-typedef float f4v __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ f4v ntl(const float* a) { return __builtin_nontemporal_load(reinterpret_cast<const f4v*>(a)); }
-__device__ __forceinline__ void nts(float* a, f4v x) { __builtin_nontemporal_store(x, reinterpret_cast<f4v*>(a)); }
-
-constexpr int LDC = BN + 4;
-constexpr int LDS_BYTES = NBUF * DSTAGE > (BM / 2) * LDC * 4 ? NBUF * DSTAGE : (BM / 2) * LDC * 4;
-
-// one 256 x 256 output tile (row tile tm, k split z)
-template <bool AK, bool ADAM>
-__device__ __forceinline__ void n256_tile(const Args& a, char* smem, unsigned tm, unsigned z) {
+template <bool AK>
+__global__ __launch_bounds__(NTH) void gemm_n256_dma_kernel(Args a) {
+  constexpr int LDC = BN + 4;
+  constexpr int LDS_BYTES = NBUF * DSTAGE > (BM / 2) * LDC * 4 ? NBUF * DSTAGE : (BM / 2) * LDC * 4;
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
   constexpr int FM = 8, FN = 4;
 
   const int64_t Mb = (!AK && a.rows_dev) ? min(a.M, (int64_t)*a.rows_dev) : a.M;
   const int64_t Kb = (AK && a.rows_dev) ? min(a.K, (int64_t)*a.rows_dev) : a.K;
+  const unsigned tiles_m = (unsigned)((a.M + BM - 1) / BM);
+  unsigned tm, z;
+  {
+    const unsigned tot = gridDim.x, L = blockIdx.x, q = tot >> 3, r = tot & 7, x = L & 7;
+    const unsigned lg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (L >> 3);
+    z = lg / tiles_m;
+    tm = lg - z * tiles_m;
+  }
   const int64_t m0 = (int64_t)tm * BM;
   if (m0 >= Mb) return;
   const int64_t kbeg = (int64_t)z * a.k_per_split;
@@ -155,14 +149,6 @@ __device__ __forceinline__ void n256_tile(const Args& a, char* smem, unsigned tm
   }
   constexpr int TPR = BN / 8, RPP = NTH / TPR;
   const int c8 = (tid % TPR) * 8;
-  AdamElem ah{};
-  float step_size = 0.f, bc2s = 1.f, gs = 1.f;
-  if constexpr (ADAM) {
-    ah = adam_elem(a.hyper);
-    step_size = (float)a.state[1];
-    bc2s = (float)a.state[2];
-    gs = (float)a.state[3];
-  }
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     __syncthreads();
@@ -175,53 +161,6 @@ __device__ __forceinline__ void n256_tile(const Args& a, char* smem, unsigned tm
           for (int r = 0; r < 4; ++r) Cs[(16 * i + 4 * g + r) * LDC + wn * 64 + 16 * j + cl] = acc[i][j][r];
     }
     __syncthreads();
-    if constexpr (ADAM) {
-      // two rows per thread and round: both rows' p / m / v loads are in flight before the first update
-#pragma unroll 1
-      for (int row = tid / TPR; row < BM / 2; row += 2 * RPP) {
-        f4v pq[2][2], mq[2][2], vq[2][2];
-        int64_t off[2];
-        bool live[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int64_t mr = m0 + half * 128 + row + u * RPP;
-          live[u] = mr < a.M;
-          off[u] = (live[u] ? mr : m0) * a.ldc + c8;
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            pq[u][h] = ntl(a.p + off[u] + 4 * h);
-            mq[u][h] = ntl(a.m + off[u] + 4 * h);
-            vq[u][h] = ntl(a.v + off[u] + 4 * h);
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          if (!live[u]) continue;
-          const float* cr = Cs + (row + u * RPP) * LDC + c8;
-          bf16x8 o;
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const float4 gq = *reinterpret_cast<const float4*>(cr + 4 * h);
-            const float G[4] = {gq.x, gq.y, gq.z, gq.w};
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              float P = pq[u][h][j], Mv = mq[u][h][j], Vv = vq[u][h][j];
-              adam_elem_update(P, G[j], Mv, Vv, ah, step_size, bc2s, gs);
-              pq[u][h][j] = P; mq[u][h][j] = Mv; vq[u][h][j] = Vv;
-              o[4 * h + j] = (__bf16)P;
-            }
-            nts(a.p + off[u] + 4 * h, pq[u][h]);
-            nts(a.m + off[u] + 4 * h, mq[u][h]);
-            nts(a.v + off[u] + 4 * h, vq[u][h]);
-          }
-          uint64_t w[2];
-          __builtin_memcpy(w, &o, 16);
-          __builtin_nontemporal_store(w[0], reinterpret_cast<uint64_t*>(a.pb + off[u]));
-          __builtin_nontemporal_store(w[1], reinterpret_cast<uint64_t*>(a.pb + off[u]) + 1);
-        }
-      }
-      continue;
-    }
 #pragma unroll
     for (int row = tid / TPR; row < BM / 2; row += RPP) {
       const int64_t m = m0 + half * 128 + row;
@@ -232,25 +171,6 @@ __device__ __forceinline__ void n256_tile(const Args& a, char* smem, unsigned tm
       *reinterpret_cast<float4*>(dst) = v0;
       *reinterpret_cast<float4*>(dst + 4) = v1;
     }
-  }
-}
-
-template <bool AK, bool ADAM = false>
-__global__ __launch_bounds__(NTH) void gemm_n256_dma_kernel(Args a) {
-  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
-  const unsigned tiles_m = (unsigned)((a.M + BM - 1) / BM);
-  if constexpr (ADAM) {
-    // a bounded grid walking the row tiles (rs_gemm_n256_adam's max_wg): the launch runs beside the encoder's
-    // backward and must leave it CUs (one 8-wave workgroup of ~133 KB LDS per CU)
-    for (unsigned tm = blockIdx.x; tm < tiles_m; tm += gridDim.x) {
-      n256_tile<AK, ADAM>(a, smem, tm, 0);
-      __syncthreads();
-    }
-  } else {
-    const unsigned tot = gridDim.x, L = blockIdx.x, q = tot >> 3, r = tot & 7, x = L & 7;
-    const unsigned lg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (L >> 3);
-    const unsigned z = lg / tiles_m;
-    n256_tile<AK, ADAM>(a, smem, lg - z * tiles_m, z);
   }
 }
 
@@ -282,8 +202,7 @@ int rs_gemm_n256(int a_kmajor, int64_t M, int64_t K, const void* A, int64_t lda,
       (lda % 8) || (ldb % 8) || (ldc % 4) || ((uintptr_t)A % 16) || ((uintptr_t)B % 16) || ((uintptr_t)C % 16))
     return RS_ERR_ARG;
   if (a_kmajor ? lda < M : lda < K) return RS_ERR_ARG;
-  g256::Args a{M, K, (const __bf16*)A, lda, (const __bf16*)B, ldb, C, ldc, c_split_stride, K, colsum, rows_dev,
-               nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  g256::Args a{M, K, (const __bf16*)A, lda, (const __bf16*)B, ldb, C, ldc, c_split_stride, K, colsum, rows_dev};
   int splits = 1;
   if (split) {
     g256::splits_for(M, K, splits, a.k_per_split);
@@ -293,23 +212,6 @@ int rs_gemm_n256(int a_kmajor, int64_t M, int64_t K, const void* A, int64_t lda,
   hipStream_t s = (hipStream_t)stream;
   if (a_kmajor) hipLaunchKernelGGL(g256::gemm_n256_dma_kernel<true>, grid, blk, 0, s, a);
   else hipLaunchKernelGGL(g256::gemm_n256_dma_kernel<false>, grid, blk, 0, s, a);
-  return (int)hipGetLastError();
-}
-
-// dE = dlogits^T h with torch.optim.Adam applied to the out.weight rows in the epilogue (BS/models/bert.py:10,16 +
-// BS/trainers/base.py:225-228): see recsys_hip.h
-int rs_gemm_n256_adam(int64_t M, int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb, float* p, float* m,
-                      float* v, void* p_bf16, int64_t ldp, const double* state, const double* hyper, float* colsum,
-                      const int* rows_dev, int max_wg, void* stream) {
-  if (M <= 0 || K <= 0 || !A || !B || !p || !m || !v || !p_bf16 || !state || !hyper || ldb < 256 || ldp < 256 ||
-      lda < M || (lda % 8) || (ldb % 8) || (ldp % 8) || ((uintptr_t)A % 16) || ((uintptr_t)B % 16) ||
-      ((uintptr_t)p % 16) || ((uintptr_t)m % 16) || ((uintptr_t)v % 16) || ((uintptr_t)p_bf16 % 16))
-    return RS_ERR_ARG;
-  g256::Args a{M, K, (const __bf16*)A, lda, (const __bf16*)B, ldb, nullptr, ldp, 0, K, colsum, rows_dev,
-               p, m, v, (__bf16*)p_bf16, state, hyper};
-  const int64_t tiles = (M + g256::BM - 1) / g256::BM;
-  const dim3 grid((unsigned)(max_wg > 0 ? std::min<int64_t>(tiles, max_wg) : tiles)), blk(g256::NTH);
-  hipLaunchKernelGGL((g256::gemm_n256_dma_kernel<true, true>), grid, blk, 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
 

@@ -554,15 +554,9 @@ class BERTEngine:
                 dl = self.ws.get("dlogits", (cap, self.V1p), self.dt)[:, :self.V1]
             ops.ce_bwd(logits, lab, count, None, wce, dl, rows_dev=cnt)
         big_dE, big_dh = self._n256_head()
-        # head_adam (FusedTrainStep, one device, the 1M-item head): dE runs AFTER dh, forked beside the encoder's
-        # backward, with out.weight's Adam update in its epilogue (rs_gemm_n256_adam) -- the 1 GB fp32 gradient is
-        # never stored nor read back; dh must read out.weight before that update rewrites it
-        head_adam = getattr(self, "head_adam", None) if big_dE and split is None else None
         # out.weight / out.bias get their whole gradient here: written, not accumulated (no read of the old
         # values; see overwritten_grads)
-        if head_adam is not None:
-            pass
-        elif big_dE:  # 256-wide tiles: dlogits streams once (gemm_n256.hip)
+        if big_dE:  # 256-wide tiles: dlogits streams once (gemm_n256.hip)
             ops.gemm_n256(dl, hl, self.flat.view("out.weight", grad), True, self.V1, cap,
                           colsum=self.flat.view("out.bias", grad), rows_dev=cnt)
         else:
@@ -587,12 +581,9 @@ class BERTEngine:
             slab_d = self.ws.get("slab_dh", (sk * cap * d,), torch.float32)
             ops.gemm(dl, self.W("out.weight"), slab_d, cap, d, self.V1, False, True, ops.epilogue(rows_dev=cnt),
                      split_k=sk, slab=slab_d)
-        if head_adam is not None:
-            head_adam(dl, hl, cap, cnt)  # fork: dE + out.weight's Adam, then out.bias's
-        else:
-            hook = getattr(self, "after_head_grads", None)
-            if hook is not None:
-                hook()                  # out.weight / out.bias are final and no longer read this step
+        hook = getattr(self, "after_head_grads", None)
+        if hook is not None:
+            hook()                      # out.weight / out.bias are final and no longer read this step
         dxL = self._buf((M, d))
         ops.splitk_scatter_rows(slab_d, sk, cap, rank, dxL)
         self.encode_backward(s, dxL, grad)

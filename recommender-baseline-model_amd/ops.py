@@ -717,14 +717,6 @@ def gemm_n256(A, B, C, a_kmajor, M, K, split=False, colsum=None, rows_dev=None):
          ptr(colsum), ptr(rows_dev), stream())
 
 
-def gemm_n256_adam(A, B, M, K, p, m, v, pb, state, hyper, colsum=None, rows_dev=None, max_wg=0):
-    """dE = A^T B (A k-major: A(m, k) = A[k, m]) with torch.optim.Adam applied to the (M, 256) parameter rows p / m / v
-    / pb in the epilogue (rs_gemm_n256_adam): the step's scalars must be prepared in `state` (adam_prepare).
-    max_wg > 0: a bounded grid walking the row tiles."""
-    call("rs_gemm_n256_adam", M, K, ptr(A), ld(A), ptr(B), ld(B), ptr(p), ptr(m), ptr(v), ptr(pb), ld(p), ptr(state),
-         ptr(hyper), ptr(colsum), ptr(rows_dev), int(max_wg), stream())
-
-
 def candidate_scores(h, E, cand, bias=None):
     """(B, C) fp32 scores <h[b], E[cand[b, c]]> (+ bias[cand[b, c]]): rs_candidate_scores.  h: (B, d) rows (row stride
     may exceed d), E: (V, d) in h's dtype, cand: (B, C) int64 on the device; raises on an id outside [0, V) like

@@ -264,11 +264,6 @@ class FusedTrainStep:
                           and os.environ.get("RS_EARLY_HEAD_ADAM", "1") != "0"
                           and hasattr(self.engine, "overwritten_grads"))
         self._opt_stream = torch.cuda.Stream(device=self.flat.device) if self._early_ok else None
-        # the token table's early update when the fused head update (a long bounded-grid launch) holds _opt_stream
-        self._tok_stream = torch.cuda.Stream(device=self.flat.device) if self._early_ok else None
-        self._tok_ev = None
-        self._fused_active = False
-        self._prep_ev = None
         self._early_done = []
         # (below the unzeroed-head vocabulary size -- cfg3's 27k classes -- the early update measured slower: 44.2-44.4k
         # -> 43.6-43.7k seq/s, three interleaved rounds; it runs only with the overwritten-gradient head)
@@ -338,7 +333,6 @@ class FusedTrainStep:
         if not (self._early_ok and update):
             return self._compute_impl(*batch, split=split)
         self.engine.after_head_grads = self._early_head_update
-        self.engine.head_adam = self._fused_head_update if self._fused_head_ok() else None
         self.engine.after_token_grads = self._early_token_update if self._early_token else None
         done = False
         try:
@@ -347,14 +341,11 @@ class FusedTrainStep:
             return out
         finally:
             self.engine.after_head_grads = None
-            self.engine.head_adam = None
             self.engine.after_token_grads = None
             if not done:
                 # an aborted compute (e.g. a capture failing after the fork) must not leave a forked update for the
                 # next step's _update to join
                 self._early_ev = None
-                self._tok_ev = None
-                self._fused_active = False
                 self._early_done = []
 
     def _compute_impl(self, *batch, split=None):
@@ -465,10 +456,6 @@ class FusedTrainStep:
                 cur = torch.cuda.current_stream()
                 done, self._early_done = self._early_done, []
                 cur.wait_event(self._early_ev)
-                if self._tok_ev is not None:
-                    cur.wait_event(self._tok_ev)
-                    self._tok_ev = None
-                self._fused_active = False
                 self.opt.step_rest(self._early_kp, seed_base=sb, done=done)
                 self._early_ev = None
             else:
@@ -504,60 +491,13 @@ class FusedTrainStep:
             return False
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream())
-        if self._fused_active:
-            # the fused head update still holds _opt_stream: the table's sweep starts now on its own stream (the step's
-            # scalars were prepared on _opt_stream before the head update's launch, so wait for that point)
-            self._tok_stream.wait_event(ev)
-            self._tok_stream.wait_event(self._prep_ev)
-            with torch.cuda.stream(self._tok_stream):
-                self.opt.step_range(lo, hi, zero_grad=True, max_wg=self.EARLY_TOKEN_ADAM_WG)
-                self._tok_ev = torch.cuda.Event()
-                self._tok_ev.record(self._tok_stream)
-        else:
-            self._opt_stream.wait_event(ev)
-            with torch.cuda.stream(self._opt_stream):
-                self.opt.step_range(lo, hi, zero_grad=True, max_wg=self.EARLY_TOKEN_ADAM_WG)
-                self._early_ev = torch.cuda.Event()
-                self._early_ev.record(self._opt_stream)
-        self._early_done.append((lo, hi))
-        return True
-
-    # workgroups of the fused head update (one 8-wave workgroup per CU): the rest of the CUs run the encoder's backward
-    FUSED_HEAD_WG = int(os.environ.get("RS_FUSED_HEAD_WG", "128"))
-
-    def _fused_head_ok(self):
-        """The large-vocabulary head's dE with out.weight's Adam in its epilogue (rs_gemm_n256_adam)?
-        RS_FUSED_HEAD_ADAM=0 (read per step, for A/B): dE into the gradient buffer and the early sweep instead."""
-        f = self.flat
-        return (os.environ.get("RS_FUSED_HEAD_ADAM", "1") != "0" and f.bf16 is not None
-                and self.engine.overwritten_grads() is not None and f.shapes["out.weight"][1] == 256)
-
-    def _fused_head_update(self, dl, hl, cap, cnt):
-        """Engine hook (BERTEngine, after dh, in place of _early_head_update): fork onto the optimizer's side stream
-        rs_adam_prepare (the step's scalars, no seed advance), dE = dlogits^T h with out.weight's Adam update in the
-        GEMM's epilogue (its gradient never stored) and out.bias's gradient as column sums, then out.bias's update.
-        The same bits as dE into the gradient buffer + _early_head_update (tests/test_bert.py
-        ::test_bert_fused_head_adam_equals_sweep); _update joins it."""
-        rng = self.engine.head_grad_range()
-        f, o = self.flat, self.opt
-        self._early_kp = rng
-        self._early_done = []
-        cur = torch.cuda.current_stream()
-        ev = torch.cuda.Event()
-        ev.record(cur)
         self._opt_stream.wait_event(ev)
         with torch.cuda.stream(self._opt_stream):
-            ops.adam_prepare(o.state, o.hyper)
-            self._prep_ev = torch.cuda.Event()
-            self._prep_ev.record(self._opt_stream)
-            self._fused_active = True
-            V1 = f.shapes["out.weight"][0]
-            w = "out.weight"
-            ops.gemm_n256_adam(dl, hl, V1, cap, f.view(w), f.view(w, o.m), f.view(w, o.v), f.view(w, f.bf16), o.state,
-                               o.hyper, colsum=f.view("out.bias", f.grad), rows_dev=cnt, max_wg=self.FUSED_HEAD_WG)
-            o.step_range(f.offsets["out.bias"], rng[1], zero_grad=False)
+            self.opt.step_range(lo, hi, zero_grad=True, max_wg=self.EARLY_TOKEN_ADAM_WG)
             self._early_ev = torch.cuda.Event()
             self._early_ev.record(self._opt_stream)
+        self._early_done.append((lo, hi))
+        return True
 
     def _early_head_update(self):
         """Engine hook (BERTEngine: right after the head's dE / dh): fork the out.weight / out.bias update onto the

@@ -288,8 +288,7 @@ def test_bert_large_vocab_overwritten_head_grads_match_zeroed():
             tr.step(tok, lab)
         torch.cuda.synchronize()
         params.append(tr.flat.data.clone())
-        if keep:   # the kept range holds the last step's gradient (out.bias's; out.weight's is never stored when
-            # dE applies its Adam update in place, rs_gemm_n256_adam), the rest is zero
+        if keep:   # the kept range holds the last step's gradient, the rest is zero
             lo, hi = tr.engine.overwritten_grads()
             assert float(tr.flat.grad[lo:hi].abs().sum()) > 0
             assert float(tr.flat.grad[:lo].abs().sum()) == 0
@@ -335,38 +334,3 @@ def test_bert_early_head_adam_equals_end_of_step(graph, monkeypatch):
 
 
 
-
-@pytest.mark.parametrize("graph", [False, True])
-def test_bert_fused_head_adam_equals_sweep(graph, monkeypatch):
-    """dE with out.weight's Adam update in the GEMM epilogue (rs_gemm_n256_adam, forked after dh beside the encoder's
-    backward; FusedTrainStep._fused_head_update) gives the same bits as dE into the gradient buffer followed by the
-    early sweep (RS_FUSED_HEAD_ADAM=0): master weights, both moments, the bf16 compute copy and the step count, three
-    steps eager and two unrolled graph replays (the 256-wide head GEMMs forced on at 70k items)."""
-    import rbm_amd.data as synth
-    from rbm_amd.train_step import FusedTrainStep
-    V, T, B = 70000, 40, 8
-    rng = np.random.default_rng(9)
-    batches = [tuple(torch.from_numpy(t).cuda() for t in synth.bert_batch(rng, B, T, V, mask_prob=0.2))
-               for _ in range(4)]
-    monkeypatch.setenv("RS_N256_HEAD", "1")
-    res = []
-    for fused in ("1", "0"):
-        monkeypatch.setenv("RS_FUSED_HEAD_ADAM", fused)
-        torch.manual_seed(0)
-        m = _bert(V, T, 256, 1, 2, 0.1, "bf16", seed=12)
-        tr = FusedTrainStep(m, lr=1e-3, max_labelled=128)
-        assert tr._early_ok and tr._fused_head_ok() == (fused == "1")
-        tr.engine.seed_base.fill_(31)
-        if graph:
-            tr.capture(*batches[0], warmup=1, steps_per_graph=2)
-            pk = lambda bs: torch.stack([torch.stack(b) for b in bs])   # noqa: E731  [S, 2, B, T]
-            losses = [tr.replay_packed(pk(batches[0:2])).cpu().tolist(),
-                      tr.replay_packed(pk(batches[2:4])).cpu().tolist()]
-        else:
-            losses = [float(tr.step(tok, lab).item()) for tok, lab in batches[:3]]
-        torch.cuda.synchronize()
-        res.append((losses, tr.flat.data.clone(), tr.opt.m.clone(), tr.opt.v.clone(), tr.flat.bf16.clone(),
-                    tr.opt.state[:4].clone()))
-    assert res[0][0] == res[1][0]
-    for a, b in zip(res[0][1:], res[1][1:]):
-        assert torch.equal(a, b)
