@@ -211,24 +211,27 @@ def _grad_worker(rank, world, port, kind, dtype, overlap, out_dir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind,dtype,overlap", [("sas", "fp32", True), ("sas", "bf16", True), ("sas", "bf16", False),
-                                                ("bert", "fp32", True), ("bert", "bf16", True)])
-def test_two_rank_gradient_equals_oracle(tmp_path, kind, dtype, overlap):
+@pytest.mark.parametrize("kind,dtype,overlap,world", [("sas", "fp32", True, 2), ("sas", "bf16", True, 2),
+                                                      ("sas", "bf16", False, 2), ("bert", "fp32", True, 2),
+                                                      ("bert", "bf16", True, 2), ("sas", "fp32", True, 4),
+                                                      ("sas", "bf16", True, 3), ("bert", "bf16", True, 3)])
+def test_multi_rank_gradient_equals_oracle(tmp_path, kind, dtype, overlap, world):
     """fp32: the exchanged gradient within the parity bars of the single-device tests (loss 1e-5, every gradient
     tensor 1e-4 norm-relative: the reference's own fp32-vs-fp64 drift is 1e-4 - 1.7e-3); bf16: the bars of the bf16
     single-device oracle tests (SAS: conftest.check_bf16_grads against the bf16-storage emulation and the exact math;
     BERT: 3e-2 per tensor, test_bert.py GRAD_TOL_BF16).  The attention key bias has an analytically zero gradient:
-    held against the global gradient scale."""
+    held against the global gradient scale.  Two ranks and three / four (processes on one GPU over gloo): with more
+    than two ranks the all-reduce's summation order is no longer a + b, and every rank must still hold the same bits."""
     from conftest import check_bf16_grads, rel
-    world = 2
     mp.spawn(_grad_worker, args=(world, _free_port(), kind, dtype, overlap, str(tmp_path)), nprocs=world, join=True)
-    r0 = torch.load(tmp_path / "g0.pt", weights_only=True)
-    r1 = torch.load(tmp_path / "g1.pt", weights_only=True)
+    rs = [torch.load(tmp_path / f"g{r}.pt", weights_only=True) for r in range(world)]
+    r0 = rs[0]
     b = _batches(kind, world)[0]
     cat = [torch.from_numpy(np.concatenate([x[i] for x in b])) for i in range(len(b[0]))]
-    assert r0["count"] == r1["count"] == float(sum(_valid(kind, x) for x in b))
-    for k in r0["grads"]:
-        assert torch.equal(r0["grads"][k], r1["grads"][k]), k          # the exchange left the ranks equal
+    assert all(r["count"] == float(sum(_valid(kind, x) for x in b)) for r in rs)
+    for r in rs[1:]:
+        for k in r0["grads"]:
+            assert torch.equal(r0["grads"][k], r["grads"][k]), k       # the exchange left the ranks equal
     P = {k: v.detach().cpu().double() for k, v in _model(kind, dtype, l2=0.0).state_dict().items()}
     torch.set_num_threads(16)
     g = {k: v.double().numpy() for k, v in r0["grads"].items()}
@@ -239,6 +242,7 @@ def test_two_rank_gradient_equals_oracle(tmp_path, kind, dtype, overlap):
         from oracle import bert as obert
         l64, _, g64 = obert.loss_and_grads(P, *cat, 2, 2)
     l64 = float(l64)
+    tag = f"{kind} {dtype} world={world}"
     scale = max(float(v.norm()) for v in g64.values())
     d = 64
     if dtype == "fp32":
@@ -254,7 +258,7 @@ def test_two_rank_gradient_equals_oracle(tmp_path, kind, dtype, overlap):
                 a, x = np.concatenate([a[:d], a[2 * d:]]), np.concatenate([x[:d], x[2 * d:]])
             errs[k] = rel(a, x)
         worst = max(errs, key=errs.get)
-        print(f"{kind} fp32 overlap={overlap}: worst gradient {worst} {errs[worst]:.3g}")
+        print(f"{tag} overlap={overlap}: worst gradient {worst} {errs[worst]:.3g}")
         assert errs[worst] < 1e-4, (worst, errs[worst])
     elif kind == "sas":
         from oracle import sas as osas
@@ -262,7 +266,7 @@ def test_two_rank_gradient_equals_oracle(tmp_path, kind, dtype, overlap):
         _, _, _, ge = osas.loss_and_grads(P, *cat, 2, 1, emu=osas.BF16Storage())
         out = check_bf16_grads(lambda n: g[n], {k: ge[k] for k in g64}, g64, d,
                                kbias=lambda n: n.endswith("in_proj_bias"))
-        print("sas bf16 overlap=%s: worst vs emulation" % overlap, max(out.items(), key=lambda kv: kv[1][0]))
+        print(f"{tag} overlap={overlap}: worst vs emulation", max(out.items(), key=lambda kv: kv[1][0]))
     else:
         assert abs(r0["loss"] - l64) <= 3e-2 * abs(l64), (r0["loss"], l64)
         errs = {}
@@ -272,7 +276,7 @@ def test_two_rank_gradient_equals_oracle(tmp_path, kind, dtype, overlap):
                 continue
             errs[k] = rel(g[k], r.numpy())
         worst = max(errs, key=errs.get)
-        print(f"bert bf16: worst gradient {worst} {errs[worst]:.3g}")
+        print(f"{tag}: worst gradient {worst} {errs[worst]:.3g}")
         assert errs[worst] < 3e-2, (worst, errs[worst])
 
 
@@ -325,4 +329,41 @@ def test_two_rank_sharded_item_table(tmp_path, dtype):
         errs = {k: _update_err("sas", k, a["sd"][k], P[k].float(), init[k].float()) for k in P}
         worst = max(errs, key=errs.get)
         print(f"sharded item table {mode}: update error vs oracle max {errs[worst]:.3g} ({worst})")
+        assert errs[worst] < 1e-3, (mode, worst, errs[worst])
+
+
+def test_three_rank_sharded_item_table_equals_oracle(tmp_path):
+    """The sharded item-table optimizer over THREE ranks (the table's 32,064 elements in three 64-aligned parts of
+    10,688; with three ranks a reduce-scatter sum is no longer a + b), fp32, every mode (eager / graph x overlapped / one
+    all-reduce): replicas bit-identical after gather_shards, and the trained weights equal the reference's
+    single-device steps on the concatenated batch (oracle float64 loss and gradients + AdamOracle) at the bars of the
+    two-rank test."""
+    world = 3
+    mp.spawn(_worker, args=(world, _free_port(), "sas", "fp32", str(tmp_path), "on", 0.0), nprocs=world, join=True)
+    rs = [torch.load(tmp_path / f"r{r}.pt", weights_only=True) for r in range(world)]
+    for mode in rs[0]:
+        assert all(r[mode]["equal"] for r in rs), mode
+        for r in rs[1:]:
+            assert r[mode]["losses"] == rs[0][mode]["losses"], mode
+            for k in rs[0][mode]["sd"]:
+                assert torch.equal(r[mode]["sd"][k], rs[0][mode]["sd"][k]), (mode, k)
+            for key in ("m", "v"):
+                assert torch.equal(r[mode][key], rs[0][mode][key]), (mode, key)
+    from oracle import sas as osas
+    from oracle.optim import AdamOracle
+    init = {k: v.detach().cpu().double() for k, v in _model("sas", "fp32", l2=0.0).state_dict().items()}
+    P = {k: v.clone() for k, v in init.items()}
+    opt = AdamOracle(list(P.values()), lr=1e-3)
+    torch.set_num_threads(16)
+    ref_losses = []
+    for bt in _batches("sas", world):
+        cat = [torch.from_numpy(np.concatenate([x[i] for x in bt])) for i in range(3)]
+        l64, _, _, g = osas.loss_and_grads(P, *cat, 2, 1)
+        opt.step([g[k] for k in P])
+        ref_losses.append(float(l64))
+    for mode, a in rs[0].items():
+        assert np.allclose(a["losses"], ref_losses, rtol=1e-5), (mode, a["losses"], ref_losses)
+        errs = {k: _update_err("sas", k, a["sd"][k], P[k].float(), init[k].float()) for k in P}
+        worst = max(errs, key=errs.get)
+        print(f"sharded item table, 3 ranks, {mode}: update error vs oracle max {errs[worst]:.3g} ({worst})")
         assert errs[worst] < 1e-3, (mode, worst, errs[worst])
