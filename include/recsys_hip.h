@@ -71,6 +71,17 @@ int rs_gemm(int dtype, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t
             const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int c_f32,
             const rs_epilogue* epi, int split_k, float* slab, void* stream);
 
+/* C = epi(LN(X) W^T) with the BERT LayerNorm (variant 1 of rs_layernorm_fwd: gamma (x - mean) / (std_unbiased + eps)
+ * + beta) formed in the GEMM's prologue (bf16 X / W / C, K = d = 256, N % 128 == 0; epilogues: bias, bias + GELU
+ * (+ dropout, aux_out = the pre-activation)).  h (bf16 [M][ldh]), mean, rinv (fp32 [M]) receive the LayerNorm output
+ * and row statistics exactly as rs_layernorm_fwd writes them (each nullable); C is bit-identical to rs_layernorm_fwd
+ * + rs_gemm.  RS_ERR_UNSUPPORTED for other shapes / epilogues (the caller runs the two launches).
+ * Replaces: utils/sublayer.py:16-18's norm(x) feeding attention/multi_head.py:18-19 (the q/k/v Linears) and
+ * utils/feed_forward.py:15-16 (w_1 + GELU + dropout). */
+int rs_gemm_ln(int64_t M, int64_t N, int64_t K, const void* X, int64_t ldx, const float* gamma, const float* beta,
+               float eps, const void* W, int64_t ldw, void* C, int64_t ldc, const rs_epilogue* epi, void* h,
+               int64_t ldh, float* mean, float* rinv, void* stream);
+
 /* out[i] (+)= sum_z slab[z*n+i], fixed order (deterministic split-K finish). */
 int rs_reduce_slabs(const float* slab, int splits, int64_t n, float* out, int accumulate, void* stream);
 /* Same over slabs of n0+n1 floats: the first n0 columns go to out0, the rest to out1. */

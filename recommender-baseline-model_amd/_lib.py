@@ -49,6 +49,7 @@ ACT_NONE, ACT_RELU, ACT_GELU, ACT_RELU_BWD, ACT_GELU_BWD = 0, 1, 2, 3, 4
 # name -> argtypes (all return int)
 SIGNATURES = {
     "rs_gemm": [i32, i32, i32, i64, i64, i64, vp, i64, vp, i64, vp, i64, i32, C.POINTER(Epilogue), i32, vp, vp],
+    "rs_gemm_ln": [i64, i64, i64, vp, i64, vp, vp, f32, vp, i64, vp, i64, C.POINTER(Epilogue), vp, i64, vp, vp, vp],
     "rs_reduce_slabs": [vp, i32, i64, vp, i32, vp],
     "rs_reduce_slabs2": [vp, i32, i64, vp, i64, vp, i32, vp],
     "rs_linear_wgrad": [i32, i64, i64, i64, vp, i64, vp, i64, vp, vp, i32, i32, vp, vp, vp],

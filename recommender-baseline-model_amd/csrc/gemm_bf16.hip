@@ -34,6 +34,7 @@ hipError_t launch_any(GemmArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_fwd(GemmArgs& a, hipStream_t s);    // gemm_bf16_fwd.hip
+hipError_t launch_fwd_ln(GemmArgs& a, hipStream_t s); // gemm_bf16_fwd.hip
 hipError_t launch_dgrad(GemmArgs& a, hipStream_t s);  // gemm_bf16_dgrad.hip
 
 }  // namespace gbf
@@ -60,3 +61,28 @@ hipError_t gemm_bf16_launch(int ak, int bk, GemmArgs& a, hipStream_t s) {
   }
   return launch_any<true, false, EC_GENERIC>(a, s);
 }
+
+extern "C" {
+
+// C = epi(LN(X) W^T), the BERT LayerNorm (variant 1: a_2 (x - mean) / (std_unbiased + eps) + b_2,
+// BS/models/bert_modules/utils/layer_norm.py:14-17) formed in the GEMM's prologue -- replaces rs_layernorm_fwd +
+// rs_gemm for the sublayers' LN -> Linear pairs (utils/sublayer.py:16-18 into attention/multi_head.py:18-19 and
+// utils/feed_forward.py:15-16).  See recsys_hip.h.
+int rs_gemm_ln(int64_t M, int64_t N, int64_t K, const void* X, int64_t ldx, const float* gamma, const float* beta,
+               float eps, const void* W, int64_t ldw, void* C, int64_t ldc, const rs_epilogue* epi, void* h,
+               int64_t ldh, float* mean, float* rinv, void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || !X || !W || !C || !gamma || !beta || !epi) return RS_ERR_ARG;
+  GemmArgs a{};
+  a.M = M; a.N = N; a.K = K; a.A = X; a.lda = ldx; a.B = W; a.ldb = ldw; a.C = C; a.ldc = ldc;
+  a.c_f32 = 0; a.split_k = 1; a.k_per_split = K;
+  a.epi = *epi;
+  a.ln.gamma = gamma; a.ln.beta = beta; a.ln.eps = eps; a.ln.h = h; a.ln.ldh = ldh; a.ln.mean = mean;
+  a.ln.rinv = rinv;
+  const rs_epilogue& e = a.epi;
+  a.vec_ok = (a.ldc % 8 == 0) && ((uintptr_t)a.C % 16 == 0) && (!e.bias || (uintptr_t)e.bias % 16 == 0) &&
+             (!(e.aux || e.aux_out) || (e.ldaux % 8 == 0 && (uintptr_t)(e.aux ? e.aux : e.aux_out) % 16 == 0));
+  const hipError_t r = gbf::launch_fwd_ln(a, (hipStream_t)stream);
+  return r == hipErrorNotSupported ? RS_ERR_UNSUPPORTED : (int)r;
+}
+
+}  // extern "C"

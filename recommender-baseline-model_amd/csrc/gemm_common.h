@@ -35,6 +35,18 @@ struct GemmArgs {
     int64_t ntn;
   } ce;
   KStamp ks;  // (bf16 path) in-kernel begin/end stamps of this launch (bench.py timing), buf null = off
+  // (bf16 DMA path, rs_gemm_ln) A = BERT LayerNorm of the rows of A formed in the GEMM's prologue: gamma / beta
+  // (fp32, K = d entries), eps; the column-tile-0 workgroups also store the LayerNorm output h (bf16, ldh) and the
+  // row statistics mean / rinv (each nullable)
+  struct {
+    const float* gamma;
+    const float* beta;
+    float eps;
+    void* h;
+    int64_t ldh;
+    float* mean;
+    float* rinv;
+  } ln;
 };
 
 

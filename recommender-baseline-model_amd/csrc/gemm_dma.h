@@ -92,14 +92,25 @@ __device__ __forceinline__ bf16x8 km_frag(const char* img, int col0, int lane) {
   return __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-template <bool BK, int BM, int EC>
+// LNA: the A operand is the BERT LayerNorm (BS/models/bert_modules/utils/layer_norm.py:14-17) of the rows of X
+// (a.A, K = d = 256), formed in the prologue instead of by a launch of its own (rs_layernorm_fwd variant 1 +
+// rs_gemm): thread t holds row t / 4's 16-B chunks 4 j + t % 4 (j = 0..7: stage j's chunk of that row), so
+// (a) the row statistics follow ln_fwd_v_kernel's arithmetic exactly -- per-chunk sums in element order, then the
+//     32-chunk butterfly (chunk c with c ^ 16, ^ 8, ^ 4 inside the thread, ^ 2 and ^ 1 by lane shuffles) -- and the
+//     normalised values, hence the GEMM, are bit-identical to the two-launch form;
+// (b) stage j's A image is one 16-B LDS write per thread (the k-contiguous swizzled layout), issued with the
+//     stage's B DMA; no A DMAs at all;
+// (c) the column-tile-0 workgroups store h and (mean, rinv) after the main loop (stores count in vmcnt: issued
+//     earlier they would lengthen the stage waits).
+template <bool BK, int BM, int EC, bool LNA = false>
 __global__ __launch_bounds__(NTH, 2) void gemm_dma_kernel(GemmArgs a) {
   KStampBegin stamp_b_(a.ks);
   KStampEnd stamp_e_(a.ks);
+  static_assert(!LNA || (BM == 64 && !BK), "the LayerNorm prologue: forward orientation, 64-row tiles");
   constexpr int IMG_A = BM * DBK * 2, DSTAGE = IMG_A + IMG_B;
   constexpr int LDC = BN + 4, HR = 64;            // epilogue: 64 rows of the fp32 tile per LDS pass
   constexpr int LDS_BYTES = NBUF * DSTAGE > HR * LDC * 4 ? NBUF * DSTAGE : HR * LDC * 4;
-  constexpr int PA = BM / 64, PB = 2, PPS = PA + PB;   // DMA pieces per wave per stage (A, B)
+  constexpr int PA = LNA ? 0 : BM / 64, PB = 2, PPS = PA + PB;   // DMA pieces per wave per stage (A, B)
   constexpr int FM = BM / 32, FN = 4;
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -139,9 +150,15 @@ __global__ __launch_bounds__(NTH, 2) void gemm_dma_kernel(GemmArgs a) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
+  // LNA: this thread's normalised A chunks (row lr, chunk 4 j + lq of stage j), kept for the h store
+  bf16x8 hq[LNA ? 8 : 1];
+  const int lr = tid >> 2, lq = tid & 3;
   auto issue = [&](int t) {
     const uint32_t buf = lds0 + (uint32_t)((t % NBUF) * DSTAGE);
     const int64_t k0 = (int64_t)t * DBK;
+    if constexpr (LNA) {
+      *reinterpret_cast<bf16x8*>(smem + (t % NBUF) * DSTAGE + 64 * lr + 16 * ((uint32_t)lq ^ kc_swz(lr))) = hq[t];
+    }
 #pragma unroll
     for (int j = 0; j < PA; ++j) kc_piece(A, a.lda, m0, k0, a.M, wave * PA + j, lane, buf);
 #pragma unroll
@@ -164,7 +181,82 @@ __global__ __launch_bounds__(NTH, 2) void gemm_dma_kernel(GemmArgs a) {
       for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
   };
 
-  for (int t = 0; t < min(nk, DIST); ++t) issue(t);
+  float ln_mu = 0.f, ln_r = 0.f;
+  if constexpr (LNA) {
+    // the row's chunks and the matching gamma / beta, then the first stages' B DMAs: every load before the stats
+    const int64_t xr = min(m0 + lr, a.M - 1);
+    const __bf16* xp = A + xr * a.lda + 8 * lq;
+    bf16x8 xv[8];
+    float4 gq[8][2], bq[8][2];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xv[j] = *reinterpret_cast<const bf16x8*>(xp + 32 * j);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        gq[j][h] = *reinterpret_cast<const float4*>(a.ln.gamma + 32 * j + 8 * lq + 4 * h);
+        bq[j][h] = *reinterpret_cast<const float4*>(a.ln.beta + 32 * j + 8 * lq + 4 * h);
+      }
+#pragma unroll
+    for (int t = 0; t < DIST; ++t) {                    // B only (the A writes need the stats)
+#pragma unroll
+      for (int j = 0; j < PB; ++j) kc_piece(B, a.ldb, n0, (int64_t)t * DBK, a.N, wave * PB + j, lane,
+                                            lds0 + (uint32_t)(t * DSTAGE) + IMG_A);
+    }
+    vm_wait<DIST * PB>();                               // the x / gamma / beta loads (older than the DMAs)
+    float s[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s[j] = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[j] += (float)xv[j][e];
+    }
+    // ln_fwd_v_kernel<bf16, 32, 1, 1>: group_sum<32> over the row's 32 chunk sums, chunk c in lane c; here
+    // chunk c = 4 j + lq: c ^ 16 / ^ 8 / ^ 4 = j ^ 4 / ^ 2 / ^ 1 (this thread), c ^ 2 / ^ 1 = lanes tid ^ 2 / ^ 1
+    auto tree = [&](float* v) {
+      float l1[4], l2[2];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) l1[j] = v[j] + v[j + 4];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) l2[j] = l1[j] + l1[j + 2];
+      float l3 = l2[0] + l2[1];
+      l3 += __shfl_xor(l3, 2, 64);
+      l3 += __shfl_xor(l3, 1, 64);
+      return l3;
+    };
+    const float mu = tree(s) / 256.f;
+    float qs[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      qs[j] = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float u = (float)xv[j][e] - mu;
+        qs[j] += u * u;
+      }
+    }
+    const float q = tree(qs);
+    const float rinv = 1.0f / (sqrtf(q / 255.f) + a.ln.eps);
+    ln_mu = mu;
+    ln_r = rinv;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float gm[8] = {gq[j][0].x, gq[j][0].y, gq[j][0].z, gq[j][0].w, gq[j][1].x, gq[j][1].y, gq[j][1].z,
+                           gq[j][1].w};
+      const float bt[8] = {bq[j][0].x, bq[j][0].y, bq[j][0].z, bq[j][0].w, bq[j][1].x, bq[j][1].y, bq[j][1].z,
+                           bq[j][1].w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float u = (float)xv[j][e] - mu;
+        hq[j][e] = (__bf16)(gm[e] * (u * rinv) + bt[e]);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < DIST; ++t)
+      *reinterpret_cast<bf16x8*>(smem + t * DSTAGE + 64 * lr + 16 * ((uint32_t)lq ^ kc_swz(lr))) = hq[t];
+  } else {
+    for (int t = 0; t < min(nk, DIST); ++t) issue(t);
+  }
   for (int t = 0; t < nk; ++t) {
     const int after = min(nk - 1, t + DIST - 1) - t;   // stages issued after t, allowed to stay in flight
     if (after >= 2) vm_wait<2 * PPS>();
@@ -173,6 +265,21 @@ __global__ __launch_bounds__(NTH, 2) void gemm_dma_kernel(GemmArgs a) {
     raw_barrier();                                      // stage t landed everywhere; buffer (t - 1) % NBUF free
     if (t + DIST < nk) issue(t + DIST);
     compute(t);
+  }
+  if constexpr (LNA) {
+    // column tile 0: the LayerNorm output and its row statistics (the backward's operands)
+    const int64_t row = m0 + lr;
+    if (tn == 0 && row < Mb) {
+      if (a.ln.h) {
+        __bf16* hp = reinterpret_cast<__bf16*>(a.ln.h) + row * a.ln.ldh + 8 * lq;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) *reinterpret_cast<bf16x8*>(hp + 32 * j) = hq[j];
+      }
+      if (lq == 0) {
+        if (a.ln.mean) a.ln.mean[row] = ln_mu;
+        if (a.ln.rinv) a.ln.rinv[row] = ln_r;
+      }
+    }
   }
 
   // ---- epilogue through LDS, 64 rows per pass
@@ -339,6 +446,19 @@ hipError_t launch(GemmArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((gemm_dma_kernel<BK, 64, EC>), dim3((unsigned)(cdiv(a.M, 64) * (a.N / BN))), dim3(NTH), 0, s,
                        a);
   }
+  return hipGetLastError();
+}
+
+// C = epi(LN(X) W^T) with the LayerNorm in the prologue (gemm_dma_kernel LNA): K = 256 (the whole row in one tile
+// row), N % 128 == 0, no split; hipErrorNotSupported otherwise
+template <int EC>
+hipError_t launch_ln(GemmArgs& a, hipStream_t s) {
+  if (a.split_k != 1 || a.N % BN || a.K != 256 || a.lda % 8 || a.ldb % 8 || ((uintptr_t)a.A & 15) ||
+      ((uintptr_t)a.B & 15) || !a.ln.gamma || !a.ln.beta || ((uintptr_t)a.ln.gamma & 15) ||
+      ((uintptr_t)a.ln.beta & 15) || (a.ln.h && (a.ln.ldh % 8 || ((uintptr_t)a.ln.h & 15))))
+    return hipErrorNotSupported;
+  hipLaunchKernelGGL((gemm_dma_kernel<false, 64, EC, true>), dim3((unsigned)(cdiv(a.M, 64) * (a.N / BN))), dim3(NTH),
+                     0, s, a);
   return hipGetLastError();
 }
 

@@ -214,12 +214,17 @@ class BERTEngine:
         for i in range(L):
             pre = f"bert.transformer_blocks.{i}."
             h, mu1, r1 = e((M, d)), e((M,), torch.float32), e((M,), torch.float32)
-            ops.layernorm_fwd(x, self.Wf(pre + "input_sublayer.norm.a_2"), self.Wf(pre + "input_sublayer.norm.b_2"),
-                              LN_EPS, h, mu1, r1, 1)
             qkv = e((M, 3 * d))
-            if self.qkv_fused:
+            g1, b1 = self.Wf(pre + "input_sublayer.norm.a_2"), self.Wf(pre + "input_sublayer.norm.b_2")
+            # LN1 inside the QKV GEMM's prologue (rs_gemm_ln: h, mean, rinv as rs_layernorm_fwd writes them)
+            if self.qkv_fused and self._ln_gemm() and ops.linear_fwd_ln(x, g1, b1, LN_EPS, self.Wqkv(i), qkv, h, mu1,
+                                                                        r1, bias=self.bqkv(i)):
+                pass
+            elif self.qkv_fused:
+                ops.layernorm_fwd(x, g1, b1, LN_EPS, h, mu1, r1, 1)
                 ops.linear_fwd(h, self.Wqkv(i), qkv, bias=self.bqkv(i))
             else:
+                ops.layernorm_fwd(x, g1, b1, LN_EPS, h, mu1, r1, 1)
                 for j in range(3):
                     ops.linear_fwd(h, self.W(self._qkv(i, j, "weight")), qkv[:, j * d:(j + 1) * d],
                                    bias=self.Wf(self._qkv(i, j, "bias")))
@@ -231,12 +236,15 @@ class BERTEngine:
                            bias=self.Wf(pre + "attention.output_linear.bias"), drop_p=hp,
                            drop_seed=self.salt[f"res1{i}"], seed_base=sb, drop_ld=d, resid=x)
             h2, mu2, r2 = e((M, d)), e((M,), torch.float32), e((M,), torch.float32)
-            ops.layernorm_fwd(x1, self.Wf(pre + "output_sublayer.norm.a_2"),
-                              self.Wf(pre + "output_sublayer.norm.b_2"), LN_EPS, h2, mu2, r2, 1)
+            g2, b2 = self.Wf(pre + "output_sublayer.norm.a_2"), self.Wf(pre + "output_sublayer.norm.b_2")
             a_pre, g = e((M, Fd)), e((M, Fd))
-            ops.linear_fwd(h2, self.W(pre + "feed_forward.w_1.weight"), g, bias=self.Wf(pre + "feed_forward.w_1.bias"),
-                           act=ops.ACT_GELU, aux_out=a_pre, drop_p=hp, drop_seed=self.salt[f"ffn{i}"], seed_base=sb,
-                           drop_ld=Fd)
+            ffn1 = dict(bias=self.Wf(pre + "feed_forward.w_1.bias"), act=ops.ACT_GELU, aux_out=a_pre, drop_p=hp,
+                        drop_seed=self.salt[f"ffn{i}"], seed_base=sb, drop_ld=Fd)
+            # LN2 inside the FFN1 GEMM's prologue
+            if not (self._ln_gemm() and ops.linear_fwd_ln(x1, g2, b2, LN_EPS, self.W(pre + "feed_forward.w_1.weight"),
+                                                          g, h2, mu2, r2, **ffn1)):
+                ops.layernorm_fwd(x1, g2, b2, LN_EPS, h2, mu2, r2, 1)
+                ops.linear_fwd(h2, self.W(pre + "feed_forward.w_1.weight"), g, **ffn1)
             xn = e((M, d))
             ops.linear_fwd(g, self.W(pre + "feed_forward.w_2.weight"), xn, bias=self.Wf(pre + "feed_forward.w_2.bias"),
                            drop_p=hp, drop_seed=self.salt[f"res2{i}"], seed_base=sb, drop_ld=d, resid=x1,
@@ -409,6 +417,11 @@ class BERTEngine:
         if ob != ow + -(-self.V1 * self.d // A) * A or end > f.numel or ow % 4 or end % 4:
             return None
         return ow, min(end, f.numel)
+
+    def _ln_gemm(self):
+        """The sublayers' LayerNorms inside the GEMMs they feed (rs_gemm_ln: bf16, d = 256)?  RS_GEMM_LN=0 (read per
+        call, for A/B): rs_layernorm_fwd + rs_gemm, the same bits."""
+        return self.dt == torch.bfloat16 and self.d == 256 and os.environ.get("RS_GEMM_LN", "1") != "0"
 
     def _det_table(self):
         return self.dt == torch.bfloat16 and self.d in (64, 128, 256)

@@ -136,6 +136,25 @@ def linear_fwd(X, W, Y, bias=None, **epi_kw):
     gemm(X, W, Y, M, N, K, False, False, epilogue(bias=bias, **epi_kw))
 
 
+RS_ERR_UNSUPPORTED = 1002
+
+
+def linear_fwd_ln(X, gamma, beta, eps, W, Y, h=None, mean=None, rinv=None, bias=None, **epi_kw):
+    """Y = epi(LN(X) W^T) with the BERT LayerNorm (variant 1) in the GEMM's prologue (rs_gemm_ln); h / mean / rinv
+    receive what rs_layernorm_fwd would write.  Returns False (nothing launched) when the shape or epilogue is not
+    one the fused kernel covers -- the caller then runs layernorm_fwd + linear_fwd."""
+    M, K = X.shape
+    N = W.shape[0]
+    e = epilogue(bias=bias, **epi_kw)
+    rc = _lib.lib().rs_gemm_ln(M, N, K, ptr(X), ld(X), ptr(gamma), ptr(beta), eps, ptr(W), ld(W), ptr(Y), ld(Y),
+                               C.byref(e), ptr(h), ld(h) if h is not None else 0, ptr(mean), ptr(rinv), stream())
+    if rc == RS_ERR_UNSUPPORTED:
+        return False
+    if rc != 0:
+        raise RuntimeError(f"rs_gemm_ln failed with code {rc}")
+    return True
+
+
 def linear_dgrad(dY, W, dX, **epi_kw):
     """dX = dY W (+ epilogue).  dY [M,N], W [N,K], dX [M,K]."""
     M, N = dY.shape

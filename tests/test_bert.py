@@ -334,3 +334,34 @@ def test_bert_early_head_adam_equals_end_of_step(graph, monkeypatch):
 
 
 
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graph", [False, True])
+def test_bert_ln_in_gemm_equals_separate_launches(graph, monkeypatch):
+    """The sublayers' LayerNorms inside the QKV / FFN1 GEMMs (rs_gemm_ln, RS_GEMM_LN=1) give the same bits as
+    rs_layernorm_fwd + rs_gemm (RS_GEMM_LN=0) over whole training steps: losses, parameters, Adam moments (d = 256,
+    dropout on, eager and graph-replayed)."""
+    import rbm_amd.data as synth
+    from rbm_amd.train_step import FusedTrainStep
+    V, T, B = 3000, 64, 8
+    rng = np.random.default_rng(17)
+    batches = [tuple(torch.from_numpy(t).cuda() for t in synth.bert_batch(rng, B, T, V, mask_prob=0.2))
+               for _ in range(3)]
+    res = []
+    for on in ("1", "0"):
+        monkeypatch.setenv("RS_GEMM_LN", on)
+        torch.manual_seed(0)
+        m = _bert(V, T, 256, 2, 2, 0.1, "bf16", seed=5)
+        tr = FusedTrainStep(m, lr=1e-3, max_labelled=B * T)
+        tr.engine.seed_base.fill_(41)
+        if graph:
+            tr.capture(*batches[0], warmup=1)
+            losses = [float(tr.replay(*b).item()) for b in batches[1:]]
+        else:
+            losses = [float(tr.step(*b).item()) for b in batches]
+        torch.cuda.synchronize()
+        res.append((losses, tr.flat.data.clone(), tr.opt.m.clone(), tr.opt.v.clone()))
+    assert res[0][0] == res[1][0]
+    for a, b in zip(res[0][1:], res[1][1:]):
+        assert torch.equal(a, b)

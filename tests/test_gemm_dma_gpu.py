@@ -162,3 +162,41 @@ def test_wgrad_direct_bitwise(R, V, count, accumulate):
     k = R if count is None else count
     ref = dl[:k].double().t() @ h[:k].double() + (0.5 if accumulate else 0.0)
     assert rel(outs[1][0].double().cpu().numpy(), ref.cpu().numpy()) < 2e-6
+
+
+@pytest.mark.parametrize("M", [12800, 1000, 37])
+@pytest.mark.parametrize("kind", ["qkv", "ffn1", "ffn1_eval"])
+def test_gemm_ln_equals_layernorm_then_gemm(M, kind):
+    """rs_gemm_ln (the BERT LayerNorm formed in the DMA GEMM's prologue) = rs_layernorm_fwd (variant 1) + rs_gemm, bit
+    for bit: the product, the LayerNorm output h and the row statistics -- QKV (bias) and FFN1 (bias + GELU + dropout
+    + pre-activation; eval: no dropout) at the cfg3 shapes, ragged M (a partial last row tile)."""
+    import rbm_amd  # noqa: F401
+    from rbm_amd import ops
+    d = 256
+    N = 768 if kind == "qkv" else 1024
+    x = _bf((M, d), 2.0, seed=11) + 0.3
+    W = _bf((N, d), 0.05, seed=12)
+    g = torch.Generator(device="cuda").manual_seed(13)
+    gamma = 1.0 + 0.1 * torch.randn(d, device="cuda", generator=g)
+    beta = 0.1 * torch.randn(d, device="cuda", generator=g)
+    bias = 0.1 * torch.randn(N, device="cuda", generator=g)
+    sb = torch.tensor([12345], dtype=torch.int64, device="cuda")
+    kw = dict(bias=bias)
+    if kind != "qkv":
+        kw.update(act=ops.ACT_GELU, drop_p=0.1 if kind == "ffn1" else 0.0, drop_seed=77, seed_base=sb, drop_ld=N)
+    outs = []
+    for fused in (True, False):
+        y = torch.full((M, N), float("nan"), device="cuda").bfloat16()
+        h = torch.full((M, d), float("nan"), device="cuda").bfloat16()
+        mu, r = torch.full((M,), float("nan"), device="cuda"), torch.full((M,), float("nan"), device="cuda")
+        aux = torch.full((M, N), float("nan"), device="cuda").bfloat16() if kind != "qkv" else None
+        kk = dict(kw, aux_out=aux) if aux is not None else kw
+        if fused:
+            assert ops.linear_fwd_ln(x, gamma, beta, 1e-6, W, y, h, mu, r, **kk)
+        else:
+            ops.layernorm_fwd(x, gamma, beta, 1e-6, h, mu, r, 1)
+            ops.linear_fwd(h, W, y, **kk)
+        torch.cuda.synchronize()
+        outs.append((y, h, mu, r) + ((aux,) if aux is not None else ()))
+    for name, a, b in zip(("y", "h", "mean", "rinv", "aux"), *outs):
+        assert torch.equal(a, b), (name, float((a.float() - b.float()).abs().max()), int((a != b).sum()))
