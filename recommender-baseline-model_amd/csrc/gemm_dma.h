@@ -183,6 +183,8 @@ __global__ __launch_bounds__(NTH, 2) void gemm_dma_kernel(GemmArgs a) {
 
   float ln_mu = 0.f, ln_r = 0.f;
   if constexpr (LNA) {
+    // ln_fwd_v_kernel's arithmetic, contraction spelled out the same way (fmaf where it has fmaf, nothing else)
+#pragma clang fp contract(off)
     // the row's chunks and the matching gamma / beta, then the first stages' B DMAs: every load before the stats
     const int64_t xr = min(m0 + lr, a.M - 1);
     const __bf16* xp = A + xr * a.lda + 8 * lq;
@@ -232,7 +234,7 @@ __global__ __launch_bounds__(NTH, 2) void gemm_dma_kernel(GemmArgs a) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float u = (float)xv[j][e] - mu;
-        qs[j] += u * u;
+        qs[j] = __builtin_fmaf(u, u, qs[j]);
       }
     }
     const float q = tree(qs);
@@ -248,7 +250,7 @@ __global__ __launch_bounds__(NTH, 2) void gemm_dma_kernel(GemmArgs a) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float u = (float)xv[j][e] - mu;
-        hq[j][e] = (__bf16)(gm[e] * (u * rinv) + bt[e]);
+        hq[j][e] = (__bf16)__builtin_fmaf(gm[e], u * rinv, bt[e]);
       }
     }
 #pragma unroll

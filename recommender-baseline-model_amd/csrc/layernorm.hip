@@ -148,6 +148,9 @@ __global__ __launch_bounds__(256) void ln_fwd_v_kernel(const T* __restrict__ X, 
                                                        const float* __restrict__ gamma, const float* __restrict__ beta,
                                                        float eps, T* __restrict__ Y, int64_t ldy,
                                                        float* __restrict__ mean_out, float* __restrict__ rinv_out) {
+  // contraction spelled out (fmaf below, nothing else fused): gemm_dma.h's LayerNorm prologue repeats this
+  // arithmetic and must produce the same bits
+#pragma clang fp contract(off)
   constexpr int V = Vec<T>::N, RPW = 64 / LPR;
   const int lane = threadIdx.x & 63, sub = lane % LPR;
   const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR;
@@ -168,7 +171,7 @@ __global__ __launch_bounds__(256) void ln_fwd_v_kernel(const T* __restrict__ X, 
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       const float u = v[i][j] - mu;
-      q += u * u;
+      q = __builtin_fmaf(u, u, q);
     }
   q = group_sum<LPR>(q);
   const float rinv = VAR == 0 ? 1.0f / sqrtf(q / (float)d + eps) : 1.0f / (sqrtf(q / (float)(d - 1)) + eps);
@@ -186,7 +189,7 @@ __global__ __launch_bounds__(256) void ln_fwd_v_kernel(const T* __restrict__ X, 
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       const float u = v[i][j] - mu;
-      o[j] = VAR == 0 ? u * rinv * gm[j] + bt[j] : gm[j] * (u * rinv) + bt[j];
+      o[j] = VAR == 0 ? __builtin_fmaf(u * rinv, gm[j], bt[j]) : __builtin_fmaf(gm[j], u * rinv, bt[j]);
     }
     store_chunk<T>(y + c0, o);
   }
