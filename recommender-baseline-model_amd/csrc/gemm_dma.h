@@ -259,14 +259,22 @@ __global__ __launch_bounds__(NTH, 2) void gemm_dma_kernel(GemmArgs a) {
   } else {
     for (int t = 0; t < min(nk, DIST); ++t) issue(t);
   }
-  for (int t = 0; t < nk; ++t) {
-    const int after = min(nk - 1, t + DIST - 1) - t;   // stages issued after t, allowed to stay in flight
+  auto step = [&](int t, int nkk) {
+    const int after = min(nkk - 1, t + DIST - 1) - t;  // stages issued after t, allowed to stay in flight
     if (after >= 2) vm_wait<2 * PPS>();
     else if (after == 1) vm_wait<PPS>();
     else vm_wait<0>();
     raw_barrier();                                      // stage t landed everywhere; buffer (t - 1) % NBUF free
-    if (t + DIST < nk) issue(t + DIST);
+    if (t + DIST < nkk) issue(t + DIST);
     compute(t);
+  };
+  if constexpr (LNA) {
+    // K = 256: eight stages, unrolled so the register chunks hq[t] are indexed statically (a runtime index would
+    // put the array in scratch memory)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) step(t, 8);
+  } else {
+    for (int t = 0; t < nk; ++t) step(t, nk);
   }
   if constexpr (LNA) {
     // column tile 0: the LayerNorm output and its row statistics (the backward's operands)
