@@ -109,7 +109,8 @@ __global__ __launch_bounds__(NTH, 2) void gemm_dma_kernel(GemmArgs a) {
   static_assert(!LNA || (BM == 64 && !BK), "the LayerNorm prologue: forward orientation, 64-row tiles");
   constexpr int IMG_A = BM * DBK * 2, DSTAGE = IMG_A + IMG_B;
   constexpr int LDC = BN + 4, HR = 64;            // epilogue: 64 rows of the fp32 tile per LDS pass
-  constexpr int LDS_BYTES = NBUF * DSTAGE > HR * LDC * 4 ? NBUF * DSTAGE : HR * LDC * 4;
+  constexpr int LDS_MAIN = NBUF * DSTAGE > HR * LDC * 4 ? NBUF * DSTAGE : HR * LDC * 4;
+  constexpr int LDS_BYTES = LDS_MAIN + (LNA ? 2 * 256 * 4 : 0);   // LNA: gamma, beta (fp32) after the stages
   constexpr int PA = LNA ? 0 : BM / 64, PB = 2, PPS = PA + PB;   // DMA pieces per wave per stage (A, B)
   constexpr int FM = BM / 32, FN = 4;
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
@@ -189,16 +190,13 @@ __global__ __launch_bounds__(NTH, 2) void gemm_dma_kernel(GemmArgs a) {
     const int64_t xr = min(m0 + lr, a.M - 1);
     const __bf16* xp = A + xr * a.lda + 8 * lq;
     bf16x8 xv[8];
-    float4 gq[8][2], bq[8][2];
 #pragma unroll
     for (int j = 0; j < 8; ++j) xv[j] = *reinterpret_cast<const bf16x8*>(xp + 32 * j);
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        gq[j][h] = *reinterpret_cast<const float4*>(a.ln.gamma + 32 * j + 8 * lq + 4 * h);
-        bq[j][h] = *reinterpret_cast<const float4*>(a.ln.beta + 32 * j + 8 * lq + 4 * h);
-      }
+    // gamma / beta to LDS (one float4 per thread: 128 threads each), read back per chunk for the normalisation
+    // (held in registers they pushed the kernel to 172 VGPRs: two workgroups per CU instead of three)
+    float* lnp = reinterpret_cast<float*>(smem + LDS_MAIN);
+    const float4 gb = tid < 64 ? reinterpret_cast<const float4*>(a.ln.gamma)[tid]
+                               : reinterpret_cast<const float4*>(a.ln.beta)[(tid - 64) & 63];
 #pragma unroll
     for (int t = 0; t < DIST; ++t) {                    // B only (the A writes need the stats)
 #pragma unroll
@@ -206,6 +204,7 @@ __global__ __launch_bounds__(NTH, 2) void gemm_dma_kernel(GemmArgs a) {
                                             lds0 + (uint32_t)(t * DSTAGE) + IMG_A);
     }
     vm_wait<DIST * PB>();                               // the x / gamma / beta loads (older than the DMAs)
+    if (tid < 128) reinterpret_cast<float4*>(lnp)[tid] = gb;
     float s[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -241,12 +240,15 @@ __global__ __launch_bounds__(NTH, 2) void gemm_dma_kernel(GemmArgs a) {
     const float rinv = 1.0f / (sqrtf(q / 255.f) + a.ln.eps);
     ln_mu = mu;
     ln_r = rinv;
+    __syncthreads();                                    // gamma / beta in LDS
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float gm[8] = {gq[j][0].x, gq[j][0].y, gq[j][0].z, gq[j][0].w, gq[j][1].x, gq[j][1].y, gq[j][1].z,
-                           gq[j][1].w};
-      const float bt[8] = {bq[j][0].x, bq[j][0].y, bq[j][0].z, bq[j][0].w, bq[j][1].x, bq[j][1].y, bq[j][1].z,
-                           bq[j][1].w};
+      const int c0 = 32 * j + 8 * lq;
+      const float4 g0 = *reinterpret_cast<const float4*>(lnp + c0), g1 = *reinterpret_cast<const float4*>(lnp + c0 + 4);
+      const float4 b0 = *reinterpret_cast<const float4*>(lnp + 256 + c0);
+      const float4 b1 = *reinterpret_cast<const float4*>(lnp + 256 + c0 + 4);
+      const float gm[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+      const float bt[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float u = (float)xv[j][e] - mu;
