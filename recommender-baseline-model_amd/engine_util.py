@@ -49,3 +49,22 @@ class Workspace:
             t = torch.empty(shape, dtype=dtype, device=self.device)
             self.bufs[name] = t
         return t
+
+
+# Events created while a stream is capturing a HIP graph are kept alive until that capture has ended
+# (FusedTrainStep._capture_graphs releases them after instantiation): a per-step event dropped mid-capture -- the
+# next unrolled step replacing it, a local going out of scope -- is otherwise destroyed while the capture still tracks
+# it as a dependency source.
+_CAPTURE_EVENTS = []
+
+
+def capture_event():
+    """torch.cuda.Event() for a fork / join inside a step; held until the end of the capture when one is running."""
+    ev = torch.cuda.Event()
+    if torch.cuda.is_current_stream_capturing():
+        _CAPTURE_EVENTS.append(ev)
+    return ev
+
+
+def release_capture_events():
+    _CAPTURE_EVENTS.clear()

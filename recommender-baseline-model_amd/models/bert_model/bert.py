@@ -30,7 +30,7 @@ import torch
 import torch.nn as nn
 
 from ... import ops
-from ...engine_util import Workspace, as_ids, compute_dtype, require_cuda, site_salt
+from ...engine_util import Workspace, as_ids, capture_event, compute_dtype, require_cuda, site_salt
 from ...flat import ALIGN, FlatParams
 
 LN_EPS = 1e-6  # utils/layer_norm.py:8
@@ -454,7 +454,7 @@ class BERTEngine:
         self._side.wait_stream(cur)
         with torch.cuda.stream(self._side):
             ops.item_index_build([ids], rows, self.d, iws)
-            ev = torch.cuda.Event()
+            ev = capture_event()
             ev.record(self._side)
         return ev, iws
 

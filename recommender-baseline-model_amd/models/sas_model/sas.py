@@ -30,7 +30,7 @@ import torch
 import torch.nn as nn
 
 from ... import ops
-from ...engine_util import Workspace, as_ids, compute_dtype, require_cuda, site_salt
+from ...engine_util import Workspace, as_ids, capture_event, compute_dtype, require_cuda, site_salt
 from ...flat import FlatParams
 
 LN_EPS = 1e-8
@@ -222,7 +222,7 @@ class SASEngine:
         fused = ops.sas_block_fused_ok(d, self.dt)
         side = fused and training and pos is not None
         if side:
-            fork = torch.cuda.Event()
+            fork = capture_event()
             fork.record()
         x = e("x0", (M, d))
         # the fused training step: the head's forward and backward inside the last block's output kernel, the
@@ -520,7 +520,7 @@ class SASEngine:
             self._side_refreshed = not self.adam_transposes or self._wT is None
             if self._side_refreshed:
                 self._refresh_transposed()
-            ev = torch.cuda.Event()
+            ev = capture_event()
             ev.record(self._side)
         return ev, iws
 
@@ -605,7 +605,7 @@ class SASEngine:
                             torch.float32)
         join, fork = None, None
         if tail is not None:
-            fork = torch.cuda.Event()
+            fork = capture_event()
             fork.record(torch.cuda.current_stream())
         # the grouped launch is captured BEFORE the side branch: a HIP graph keeps a node's first child on its
         # queue, so the weight gradients follow the blocks' backward with no cross-queue hop (side branch
@@ -615,7 +615,7 @@ class SASEngine:
             self._side.wait_event(fork)
             with torch.cuda.stream(self._side):
                 tail(dx)
-                join = torch.cuda.Event()
+                join = capture_event()
                 join.record(self._side)
             self._tail_join = join
         return dx

@@ -28,6 +28,7 @@ import torch
 
 from . import dp as dpx
 from . import ops
+from .engine_util import capture_event, release_capture_events
 
 
 # thread-local capture: the process group's watchdog thread polls its collectives' events while a step graph is
@@ -499,7 +500,7 @@ class FusedTrainStep:
         kp = self._early_kp
         if not (hi <= kp[0] or lo >= kp[1]) or lo % 4:
             return False
-        ev = torch.cuda.Event()
+        ev = capture_event()
         ev.record(torch.cuda.current_stream())
         if self._tok_stream is not None:
             # after the table's gradient (ev) and the step's prepared scalars (_prep_ev, on _opt_stream)
@@ -507,13 +508,13 @@ class FusedTrainStep:
             self._tok_stream.wait_event(self._prep_ev)
             with torch.cuda.stream(self._tok_stream):
                 self.opt.step_range(lo, hi, zero_grad=True, max_wg=self.EARLY_TOKEN_ADAM_WG)
-                self._tok_ev = torch.cuda.Event()
+                self._tok_ev = capture_event()
                 self._tok_ev.record(self._tok_stream)
         else:
             self._opt_stream.wait_event(ev)
             with torch.cuda.stream(self._opt_stream):
                 self.opt.step_range(lo, hi, zero_grad=True, max_wg=self.EARLY_TOKEN_ADAM_WG)
-                self._early_ev = torch.cuda.Event()
+                self._early_ev = capture_event()
                 self._early_ev.record(self._opt_stream)
         self._early_done.append((lo, hi))
         return True
@@ -531,13 +532,13 @@ class FusedTrainStep:
         self._early_kp = rng
         self._early_done = []
         cur = torch.cuda.current_stream()
-        ev = torch.cuda.Event()
+        ev = capture_event()
         ev.record(cur)
         self._opt_stream.wait_event(ev)
-        self._prep_ev = torch.cuda.Event()
+        self._prep_ev = capture_event()
         with torch.cuda.stream(self._opt_stream):
             self.opt.step_keep_early(rng, max_wg=self.EARLY_HEAD_ADAM_WG, prep_event=self._prep_ev)
-            self._early_ev = torch.cuda.Event()
+            self._early_ev = capture_event()
             self._early_ev.record(self._opt_stream)
 
     # ---------------------------------------------------------------- one step
@@ -787,6 +788,7 @@ class FusedTrainStep:
         try:
             r = self._capture_graphs_impl(compute, stamps, unrolled)
         finally:
+            release_capture_events()     # the graphs are instantiated: the capture's fork / join events may go
             if gc_on:
                 gc.enable()
         if os.environ.get("RS_GRAPH_UPLOAD", "1") != "0":
