@@ -395,9 +395,6 @@ int rs_seed_advance(uint64_t* seed_base, void* stream);
  * graph preparation, no step runs.  Infrastructure of the captured training step (BS/trainers/base.py:114-123's
  * loop body replayed as one graph), not a reference op. */
 int rs_graph_upload(void* graph_exec, void* stream);
-/* *out = a new non-blocking HIP stream (hipStreamCreateWithFlags), owned by the caller for the process lifetime: the
- * trainer's side streams that must not alias another queue (torch's stream pool reuses its 32 streams round robin). */
-int rs_stream_create(void** out);
 
 /* ---- fused SAS sublayers (bf16, d in {64, 128}; rowchain.hip) ----------------------------
  * One workgroup per CU stages the block's weights in LDS once, each wave carries 16 tokens

@@ -82,7 +82,6 @@ SIGNATURES = {
     "rs_adam_step_wg": [i64, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp],
     "rs_adam_step_marked": [i64, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, vp, i64, i64, i32, vp],
     "rs_graph_upload": [vp, vp],
-    "rs_stream_create": [vp],
     "rs_adam_prepare_step": [i64, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, i32, i64, vp, vp],
     "rs_adam_prepare_step_loss": [i64, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, i32, i64, vp, vp, vp, vp],
     "rs_adam_prepare_step_marked": [i64, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, i32, i64, vp, vp, vp, vp, vp,

@@ -579,16 +579,6 @@ int rs_graph_upload(void* graph_exec, void* stream) {
   return (int)hipGraphUpload((hipGraphExec_t)graph_exec, (hipStream_t)stream);
 }
 
-// a HIP stream of its own (non-blocking), outside torch's stream pool -- whose 32 streams per priority are handed out
-// round robin, so a pool stream of one trainer may be the same queue as another's or as the graph capture stream
-int rs_stream_create(void** out) {
-  if (!out) return RS_ERR_ARG;
-  hipStream_t s = nullptr;
-  const hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
-  *out = (void*)s;
-  return (int)e;
-}
-
 int rs_seed_advance(uint64_t* seed_base, void* stream) {
   hipLaunchKernelGGL(seed_advance_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, seed_base);
   return (int)hipGetLastError();

@@ -498,22 +498,6 @@ def vocab_ce_bwd(h, E, bias, labels, ws, count, dl, rows_dev=None, dloss=None):
          ptr(count), ptr(dloss), ptr(ws), ptr(dl), ld(dl), stream())
 
 
-_OWN_STREAMS = {}
-
-
-def own_stream(device, tag):
-    """A HIP stream of this process's own (rs_stream_create), one per (device, tag), wrapped as a torch stream: never
-    one of torch's pool streams, which are reused round robin (a trainer's side stream could otherwise be another
-    trainer's, or the graph-capture stream)."""
-    key = (torch.device(device).index or 0, tag)
-    if key not in _OWN_STREAMS:
-        h = C.c_void_p()
-        with torch.cuda.device(key[0]):
-            call("rs_stream_create", C.byref(h))
-        _OWN_STREAMS[key] = torch.cuda.ExternalStream(h.value, device=torch.device("cuda", key[0]))
-    return _OWN_STREAMS[key]
-
-
 def graph_upload(graph):
     """hipGraphUpload of a captured torch.cuda.CUDAGraph's executable (rs_graph_upload) on the current stream."""
     call("rs_graph_upload", C.c_void_p(int(graph.raw_cuda_graph_exec())), stream())

@@ -268,7 +268,7 @@ class FusedTrainStep:
         # the token table's early update on a stream of its own: it starts right after the table's gradient instead of
         # queueing behind the out.weight sweep still running on _opt_stream (RS_EARLY_TOKEN_OWN_STREAM=0: behind it)
         self._tok_own = os.environ.get("RS_EARLY_TOKEN_OWN_STREAM", "1") != "0"
-        self._tok_stream = ops.own_stream(self.flat.device, "tok") if self._early_ok and self._tok_own else None
+        self._tok_stream = torch.cuda.Stream(device=self.flat.device) if self._early_ok and self._tok_own else None
         self._tok_ev = None
         self._prep_ev = None
         self._early_done = []
