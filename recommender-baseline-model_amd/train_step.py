@@ -265,12 +265,7 @@ class FusedTrainStep:
                           and os.environ.get("RS_EARLY_HEAD_ADAM", "1") != "0"
                           and hasattr(self.engine, "overwritten_grads"))
         self._opt_stream = torch.cuda.Stream(device=self.flat.device) if self._early_ok else None
-        # the token table's early update on a stream of its own: it starts right after the table's gradient instead of
-        # queueing behind the out.weight sweep still running on _opt_stream (RS_EARLY_TOKEN_OWN_STREAM=0: behind it)
-        self._tok_own = os.environ.get("RS_EARLY_TOKEN_OWN_STREAM", "1") != "0"
-        self._tok_stream = torch.cuda.Stream(device=self.flat.device) if self._early_ok and self._tok_own else None
-        self._tok_ev = None
-        self._prep_ev = None
+
         self._early_done = []
         # (below the unzeroed-head vocabulary size -- cfg3's 27k classes -- the early update measured slower: 44.2-44.4k
         # -> 43.6-43.7k seq/s, three interleaved rounds; it runs only with the overwritten-gradient head)
@@ -353,7 +348,6 @@ class FusedTrainStep:
                 # an aborted compute (e.g. a capture failing after the fork) must not leave a forked update for the
                 # next step's _update to join
                 self._early_ev = None
-                self._tok_ev = None
                 self._early_done = []
 
     def _compute_impl(self, *batch, split=None):
@@ -464,9 +458,6 @@ class FusedTrainStep:
                 cur = torch.cuda.current_stream()
                 done, self._early_done = self._early_done, []
                 cur.wait_event(self._early_ev)
-                if self._tok_ev is not None:
-                    cur.wait_event(self._tok_ev)
-                    self._tok_ev = None
                 self.opt.step_rest(self._early_kp, seed_base=sb, done=done)
                 self._early_ev = None
             else:
@@ -502,20 +493,11 @@ class FusedTrainStep:
             return False
         ev = capture_event()
         ev.record(torch.cuda.current_stream())
-        if self._tok_stream is not None:
-            # after the table's gradient (ev) and the step's prepared scalars (_prep_ev, on _opt_stream)
-            self._tok_stream.wait_event(ev)
-            self._tok_stream.wait_event(self._prep_ev)
-            with torch.cuda.stream(self._tok_stream):
-                self.opt.step_range(lo, hi, zero_grad=True, max_wg=self.EARLY_TOKEN_ADAM_WG)
-                self._tok_ev = capture_event()
-                self._tok_ev.record(self._tok_stream)
-        else:
-            self._opt_stream.wait_event(ev)
-            with torch.cuda.stream(self._opt_stream):
-                self.opt.step_range(lo, hi, zero_grad=True, max_wg=self.EARLY_TOKEN_ADAM_WG)
-                self._early_ev = capture_event()
-                self._early_ev.record(self._opt_stream)
+        self._opt_stream.wait_event(ev)
+        with torch.cuda.stream(self._opt_stream):
+            self.opt.step_range(lo, hi, zero_grad=True, max_wg=self.EARLY_TOKEN_ADAM_WG)
+            self._early_ev = capture_event()
+            self._early_ev.record(self._opt_stream)
         self._early_done.append((lo, hi))
         return True
 
@@ -535,9 +517,8 @@ class FusedTrainStep:
         ev = capture_event()
         ev.record(cur)
         self._opt_stream.wait_event(ev)
-        self._prep_ev = capture_event()
         with torch.cuda.stream(self._opt_stream):
-            self.opt.step_keep_early(rng, max_wg=self.EARLY_HEAD_ADAM_WG, prep_event=self._prep_ev)
+            self.opt.step_keep_early(rng, max_wg=self.EARLY_HEAD_ADAM_WG)
             self._early_ev = capture_event()
             self._early_ev.record(self._opt_stream)
 
