@@ -950,12 +950,11 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkv_ds_kernel(AttnLdsArgs akv) {
 
 // dS mode, launch 2: dQ = dS K (scale inside dS) for one (sequence, head) and 32 queries per workgroup, key chunks
 // of 32 up to the causal bound.  Computed transposed, dQ^T[dh][q] = sum_k K^T[dh][k] dS^T[k][q]: both operands are
-// A-style fragments of row-major LDS images (K [key][dh], dS^T [key][query]) read by ds_read_b64_tr_b16 with the same
-// permuted k order; the accumulator lane holds 4 consecutive dh of one query (one 8-B store).  4 waves: wave w owns
-// dh tiles DTW w .. DTW w + DTW - 1 for both 16-query tiles.  Every chunk's operands are requested up front (T <=
-// 256: at most 8 chunks, 12 VGPRs each at Dh = 128), so the chunk loop waits on one memory round trip in all, not one
-// per chunk; the images are double-buffered in LDS.
-constexpr int DQD_NT = 256, DQD_LDS_S = 32 + 16, DQD_MAXC = 8;
+// A-style fragments of the row-major LDS images (K [key][dh], dS^T [key][query]) read by ds_read_b64_tr_b16 with the
+// same permuted k order; the accumulator lane holds 4 consecutive dh of one query (one 8-B store).  4 waves: wave w
+// owns dh tiles 2w, 2w + 1 (Dh = 128; DH / 64 tiles per wave in general) for both 16-query tiles.  The next chunk's
+// operands are loaded into registers while this one's MFMAs run (double-buffered images).
+constexpr int DQD_NT = 256, DQD_LDS_S = 32 + 16;
 template <int DH>
 __global__ __launch_bounds__(DQD_NT) void attn_dq_ds_kernel(AttnLdsArgs a) {
   KStampEnd end_(a.ks);
@@ -971,50 +970,52 @@ __global__ __launch_bounds__(DQD_NT) void attn_dq_ds_kernel(AttnLdsArgs a) {
   const int nkc = (kend + 31) / 32;
   const bf16* Kg = a.k + b * a.T * a.ldk + h * DH;
   const bf16* Sg = a.ds + (int64_t)bh * a.ds_rows * a.ds_ld + q0;
+  // this thread's pieces: K rows (kr, column chunk kq) and, threads < 128, dS^T row sr columns 8 sq..8 sq + 7
   typedef __attribute__((ext_vector_type(4))) unsigned u4;
-  u4 kv[DQD_MAXC][KPT], sv[DQD_MAXC];
-  // this thread's pieces of chunk kc: K row kr column chunk kq (KPT of them); threads < 128 the dS^T row tid / 4,
-  // columns 8 (tid % 4) ..; rows past T read row T - 1 and are zeroed (no branch around a load)
+  u4 kv[KPT], sv = {0u, 0u, 0u, 0u};
+  auto load = [&](int kc) {
 #pragma unroll
-  for (int kc = 0; kc < DQD_MAXC; ++kc) {
-    if (kc < nkc) {
-#pragma unroll
-      for (int j = 0; j < KPT; ++j) {
-        const int piece = tid + j * DQD_NT, kr = piece / (DH / 8), kq = piece % (DH / 8);
-        const int key = 32 * kc + kr;
-        kv[kc][j] = *reinterpret_cast<const u4*>(Kg + (int64_t)min(key, T - 1) * a.ldk + 8 * kq);
-        const unsigned keep = key < T ? 0xffffffffu : 0u;
-        kv[kc][j] &= keep;
-      }
-      const int key = 32 * kc + (tid >> 2);
-      sv[kc] = *reinterpret_cast<const u4*>(Sg + (int64_t)min(key, T - 1) * a.ds_ld + 8 * (tid & 3));
-      const unsigned keep = (key < T && tid < 128) ? 0xffffffffu : 0u;
-      sv[kc] &= keep;
+    for (int j = 0; j < KPT; ++j) {
+      const int piece = tid + j * DQD_NT, kr = piece / (DH / 8), kq = piece % (DH / 8);
+      const int key = 32 * kc + kr;
+      kv[j] = *reinterpret_cast<const u4*>(Kg + (int64_t)min(key, T - 1) * a.ldk + 8 * kq);
+      if (key >= T) kv[j] = (u4){0u, 0u, 0u, 0u};
     }
-  }
+    if (tid < 128) {
+      const int sr = tid >> 2, sq = tid & 3, key = 32 * kc + sr;
+      sv = *reinterpret_cast<const u4*>(Sg + (int64_t)min(key, (int)a.ds_rows - 1) * a.ds_ld + 8 * sq);
+      if (key >= T) sv = (u4){0u, 0u, 0u, 0u};
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+      const int piece = tid + j * DQD_NT, kr = piece / (DH / 8), kq = piece % (DH / 8);
+      *reinterpret_cast<u4*>(&Ks[buf][kr * LDK + 8 * kq]) = kv[j];
+    }
+    if (tid < 128) *reinterpret_cast<u4*>(&Ss[buf][(tid >> 2) * DQD_LDS_S + 8 * (tid & 3)]) = sv;
+  };
   f32x4 acc[DTW][2];
 #pragma unroll
   for (int i = 0; i < DTW; ++i) acc[i][0] = acc[i][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int kc = 0; kc < nkc; ++kc) {
+    const int buf = kc & 1;
+    if (kc + 1 < nkc) load(kc + 1);
+    bf16x8 fk[DTW], fs[2];
 #pragma unroll
-  for (int kc = 0; kc < DQD_MAXC; ++kc) {
-    if (kc < nkc) {
-      const int buf = kc & 1;
+    for (int i = 0; i < DTW; ++i) fk[i] = tr_frag(Ks[buf], LDK, 0, 16 * (DTW * wave + i), lane);
 #pragma unroll
-      for (int j = 0; j < KPT; ++j) {
-        const int piece = tid + j * DQD_NT, kr = piece / (DH / 8), kq = piece % (DH / 8);
-        *reinterpret_cast<u4*>(&Ks[buf][kr * LDK + 8 * kq]) = kv[kc][j];
-      }
-      if (tid < 128) *reinterpret_cast<u4*>(&Ss[buf][(tid >> 2) * DQD_LDS_S + 8 * (tid & 3)]) = sv[kc];
-      __syncthreads();   // chunk kc's images written; the reads of chunk kc - 2 (the same buffer) are long done
-      bf16x8 fk[DTW], fs[2];
+    for (int qt = 0; qt < 2; ++qt) fs[qt] = tr_frag(Ss[buf], DQD_LDS_S, 0, 16 * qt, lane);
 #pragma unroll
-      for (int i = 0; i < DTW; ++i) fk[i] = tr_frag(Ks[buf], LDK, 0, 16 * (DTW * wave + i), lane);
+    for (int i = 0; i < DTW; ++i)
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) fs[qt] = tr_frag(Ss[buf], DQD_LDS_S, 0, 16 * qt, lane);
-#pragma unroll
-      for (int i = 0; i < DTW; ++i)
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt) acc[i][qt] = mfma16(fk[i], fs[qt], acc[i][qt]);
+      for (int qt = 0; qt < 2; ++qt) acc[i][qt] = mfma16(fk[i], fs[qt], acc[i][qt]);
+    if (kc + 1 < nkc) {
+      store(buf ^ 1);
+      __syncthreads();
     }
   }
 #pragma unroll
