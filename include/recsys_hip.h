@@ -171,17 +171,6 @@ int rs_attn_bwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t Dh, const vo
                 const void* dout, int64_t lddo, const float* lse, void* dq, int64_t lddq, void* dk,
                 int64_t lddk, void* dv, int64_t lddv, float scale, int mask_kind, const int64_t* ids,
                 float drop_p, uint64_t seed, const uint64_t* seed_base, float* ws, void* stream);
-/* rs_attn_bwd in two launches for bf16, T <= 256, Dh 64 / 128: the dK/dV pass alone on two (or more) workgroups per
- * (sequence, head), storing dS^T (bf16, softmax scale included) into ds on the way, then dQ = dS K from it -- no second
- * recomputation of the softmax and its gradient, and both launches spread over all CUs.  ds: rs_attn_bwd_ds_bytes
- * bytes, 16-B aligned (0 bytes: this path does not apply and rs_attn_bwd's runs).  Replaces the same autograd of
- * F.multi_head_attention_forward (BS/models/sas_model/sas.py:75) / attention/single.py:13-35 as rs_attn_bwd. */
-int64_t rs_attn_bwd_ds_bytes(int64_t B, int64_t T, int64_t H, int64_t Dh);
-int rs_attn_bwd_ds(int dtype, int64_t B, int64_t T, int64_t H, int64_t Dh, const void* q, int64_t ldq,
-                   const void* k, int64_t ldk, const void* v, int64_t ldv, const void* o, int64_t ldo,
-                   const void* dout, int64_t lddo, const float* lse, void* dq, int64_t lddq, void* dk,
-                   int64_t lddk, void* dv, int64_t lddv, float scale, int mask_kind, const int64_t* ids,
-                   float drop_p, uint64_t seed, const uint64_t* seed_base, float* ws, void* ds, void* stream);
 
 /* SAS sampled tied logits (sas.py:93-100): pl[m] = <f[m], E[pos[m]]>, nl likewise (fp32 out). */
 int rs_sampled_logits_fwd(int dtype, const void* f, int64_t M, int64_t d, const void* E,

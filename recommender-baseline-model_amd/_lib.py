@@ -65,9 +65,6 @@ SIGNATURES = {
     "rs_attn_row_delta": [i32, i64, i64, i64, i64, vp, i64, vp, i64, vp, vp],
     "rs_attn_bwd": [i32, i64, i64, i64, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, i64,
                     vp, i64, f32, i32, vp, f32, u64, vp, vp, vp],
-    "rs_attn_bwd_ds": [i32, i64, i64, i64, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, i64,
-                    vp, i64, f32, i32, vp, f32, u64, vp, vp, vp, vp],
-    "rs_attn_bwd_ds_bytes": [i64, i64, i64, i64],
     "rs_sampled_logits_fwd": [i32, vp, i64, i64, vp, vp, vp, vp, vp, vp],
     "rs_sampled_logits_bwd": [i32, vp, i64, i64, vp, vp, vp, vp, vp, vp, i32, vp, vp],
     "rs_bce_fwd": [vp, vp, vp, i64, vp, vp, vp, vp],
@@ -160,8 +157,7 @@ RESTYPES = {"rs_wgrad_grouped_slab_numel": C.c_int64, "rs_sas_block_parts": C.c_
             "rs_touched_rows_ws_numel": C.c_int64, "rs_item_index_ws_bytes": C.c_int64,
             "rs_vocab_ce_ws_numel": C.c_int64,
             "rs_sas_block_in_count_parts": C.c_int64,
-            "rs_sas_block_grid": C.c_int64, "rs_layernorm_bwd_nparts": C.c_int64,
-            "rs_attn_bwd_ds_bytes": C.c_int64}
+            "rs_sas_block_grid": C.c_int64, "rs_layernorm_bwd_nparts": C.c_int64}
 
 _lib = None
 

@@ -437,8 +437,7 @@ hipError_t attn_lds_bwd(int64_t B, int64_t T, int64_t H, int64_t Dh, const void*
                         int64_t ldk, const void* v, int64_t ldv, const void* o, int64_t ldo, const void* dout,
                         int64_t lddo, const float* lse, void* dq, int64_t lddq, void* dk, int64_t lddk, void* dv,
                         int64_t lddv, float scale, int mask_kind, const int64_t* ids, float drop_p, uint64_t seed,
-                        const uint64_t* seed_base, float* delta, hipStream_t s, void* ds = nullptr);
-int64_t attn_lds_ds_bytes(int64_t B, int64_t T, int64_t H);
+                        const uint64_t* seed_base, float* delta, hipStream_t s);
 
 // bf16 storage with T <= 256 takes the LDS-resident kernels (attention_lds.hip); fp32 (the
 // parity mode) and anything else the register/LDS-chunk kernels above.
@@ -510,13 +509,6 @@ __global__ __launch_bounds__(256) void row_delta_v8_kernel(int64_t M, int64_t T,
   }
 }
 
-static int attn_bwd_generic(int dtype, int64_t B, int64_t T, int64_t H, int64_t Dh, const void* q, int64_t ldq,
-                            const void* k, int64_t ldk, const void* v, int64_t ldv, const void* o, int64_t ldo,
-                            const void* dout, int64_t lddo, const float* lse, void* dq, int64_t lddq, void* dk,
-                            int64_t lddk, void* dv, int64_t lddv, float scale, int mask_kind, const int64_t* ids,
-                            float drop_p, uint64_t seed, const uint64_t* seed_base, float* ws, int vec,
-                            void* stream);
-
 extern "C" {
 
 int rs_attn_row_delta(int dtype, int64_t B, int64_t T, int64_t H, int64_t Dh, const void* dout, int64_t lddo,
@@ -577,44 +569,6 @@ int rs_attn_bwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t Dh, const vo
     return (int)attn_lds_bwd(B, T, H, Dh, q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, dq, lddq, dk, lddk, dv,
                              lddv, scale, mask_kind | delta_in, ids, drop_p, seed, seed_base, ws, (hipStream_t)stream);
   // the generic kernels always form delta themselves (into ws)
-  return attn_bwd_generic(dtype, B, T, H, Dh, q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, dq, lddq, dk, lddk, dv,
-                          lddv, scale, mask_kind, ids, drop_p, seed, seed_base, ws, vec, stream);
-}
-
-int64_t rs_attn_bwd_ds_bytes(int64_t B, int64_t T, int64_t H, int64_t Dh) {
-  if (B <= 0 || T <= 0 || H <= 0 || (Dh != 64 && Dh != 128) || !attn_lds_supported(T, Dh)) return 0;
-  return attn_lds_ds_bytes(B, T, H);
-}
-
-// rs_attn_bwd with the dS-materialising LDS path: the dK/dV pass on nsplit workgroups per (sequence, head) stores
-// dS^T into ds (rs_attn_bwd_ds_bytes), then dQ = dS K; other shapes / dtypes take rs_attn_bwd's paths (ds unused)
-int rs_attn_bwd_ds(int dtype, int64_t B, int64_t T, int64_t H, int64_t Dh, const void* q, int64_t ldq,
-                   const void* k, int64_t ldk, const void* v, int64_t ldv, const void* o, int64_t ldo,
-                   const void* dout, int64_t lddo, const float* lse, void* dq, int64_t lddq, void* dk,
-                   int64_t lddk, void* dv, int64_t lddv, float scale, int mask_kind, const int64_t* ids,
-                   float drop_p, uint64_t seed, const uint64_t* seed_base, float* ws, void* ds, void* stream) {
-  const int64_t lds[8] = {ldq, ldk, ldv, ldo, lddo, lddq, lddk, lddv};
-  const int delta_in = mask_kind & RS_ATTN_DELTA_IN;
-  const int mk = mask_kind & ~RS_ATTN_DELTA_IN;
-  int c = check(B, T, H, Dh);
-  if (c) return c;
-  if (mk == 1 && !ids) return RS_ERR_ARG;
-  const void* ptrs[8] = {q, k, v, o, dout, dq, dk, dv};
-  const int vec = vec_ok(dtype, Dh, ptrs, 8, lds, 8);
-  if (ds && ((uintptr_t)ds % 16) == 0 && rs_attn_bwd_ds_bytes(B, T, H, Dh) > 0 && vec &&
-      use_lds_path(dtype, B * H, T, Dh))
-    return (int)attn_lds_bwd(B, T, H, Dh, q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, dq, lddq, dk, lddk, dv,
-                             lddv, scale, mk | delta_in, ids, drop_p, seed, seed_base, ws, (hipStream_t)stream, ds);
-  return rs_attn_bwd(dtype, B, T, H, Dh, q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, dq, lddq, dk, lddk, dv, lddv,
-                     scale, mask_kind, ids, drop_p, seed, seed_base, ws, stream);
-}
-
-static int attn_bwd_generic(int dtype, int64_t B, int64_t T, int64_t H, int64_t Dh, const void* q, int64_t ldq,
-                            const void* k, int64_t ldk, const void* v, int64_t ldv, const void* o, int64_t ldo,
-                            const void* dout, int64_t lddo, const float* lse, void* dq, int64_t lddq, void* dk,
-                            int64_t lddk, void* dv, int64_t lddv, float scale, int mask_kind, const int64_t* ids,
-                            float drop_p, uint64_t seed, const uint64_t* seed_base, float* ws, int vec,
-                            void* stream) {
   AttnArgs a = {};
   a.B = B; a.T = T; a.H = H; a.Dh = (int)Dh; a.vec = vec;
   a.q = q; a.ldq = ldq; a.k = k; a.ldk = ldk; a.v = v; a.ldv = ldv;

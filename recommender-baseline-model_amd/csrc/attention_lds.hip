@@ -56,9 +56,6 @@ struct AttnLdsArgs {
   // partial goes to LDS slot `slot`), 2 = upper half (adds that slot's partial, then writes the tile)
   int use_plan;
   uint32_t plan[PLAN_S][8][PLAN_I];
-  // dS mode (rs_attn_bwd_ds): the dK/dV pass also stores dS^T (bf16, scale included) as ds[bh][key][query] with
-  // ds_rows >= the 16-rounded key count and ds_ld >= the 32-rounded query count; the dQ = dS K launch reads it
-  bf16* ds; int64_t ds_rows, ds_ld;
 };
 #define DQ_SLOTS 4    // fp32 partial dQ tiles (8 KB each at Dh = 128)
 #define DKV_SLOTS 3   // bf16 partial (dK, dV) tiles (8 KB each at Dh = 128)
@@ -870,11 +867,6 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnLdsArgs& a, int64_t 
       pds(2 * c + 1, sB, dB, pdB, dsB);
       const bf16x8 bp = pack8(pdA, pdB);
       const bf16x8 bds = pack8(dsA, dsB);
-      if (a.ds) {   // dS^T row of this lane's key, queries 32 c + 4 g + r and 32 c + 16 + 4 g + r (the dK operand's bits)
-        bf16* dsr = a.ds + ((int64_t)bh * a.ds_rows + ki) * a.ds_ld + 32 * c + 4 * g;
-        *reinterpret_cast<bf4*>(dsr) = __builtin_shufflevector(bds, bds, 0, 1, 2, 3);
-        *reinterpret_cast<bf4*>(dsr + 16) = __builtin_shufflevector(bds, bds, 4, 5, 6, 7);
-      }
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         dv[dt] = mfma16(tr_frag(dOs, LD, 32 * c, 16 * dt, lane), bp, dv[dt]);
@@ -938,99 +930,6 @@ __global__ __launch_bounds__(NT) void attn_bwd_lds_kernel(AttnLdsArgs aq, AttnLd
   const int64_t nq = (int64_t)aq.nsplit * aq.B * aq.H;
   if ((int64_t)blockIdx.x < nq) attn_bwd_dq_body<DH>(aq, blockIdx.x);
   else attn_bwd_dkv_body<DH>(akv, blockIdx.x - nq, !akv.delta_in);
-}
-
-// dS mode, launch 1: the dK/dV pass alone, nsplit workgroups per (sequence, head), storing dS^T on the way (its
-// KStampBegin opens the attention backward's stamp; launch 2's KStampEnd closes it)
-template <int DH>
-__global__ __launch_bounds__(NT) void attn_bwd_dkv_ds_kernel(AttnLdsArgs akv) {
-  KStampBegin begin_(akv.ks);
-  attn_bwd_dkv_body<DH>(akv, blockIdx.x, !akv.delta_in);
-}
-
-// dS mode, launch 2: dQ = dS K (scale inside dS) for one (sequence, head) and 32 queries per workgroup, key chunks
-// of 32 up to the causal bound.  Computed transposed, dQ^T[dh][q] = sum_k K^T[dh][k] dS^T[k][q]: both operands are
-// A-style fragments of the row-major LDS images (K [key][dh], dS^T [key][query]) read by ds_read_b64_tr_b16 with the
-// same permuted k order; the accumulator lane holds 4 consecutive dh of one query (one 8-B store).  4 waves: wave w
-// owns dh tiles 2w, 2w + 1 (Dh = 128; DH / 64 tiles per wave in general) for both 16-query tiles.  The next chunk's
-// operands are loaded into registers while this one's MFMAs run (double-buffered images).
-constexpr int DQD_NT = 256, DQD_LDS_S = 32 + 16;
-template <int DH>
-__global__ __launch_bounds__(DQD_NT) void attn_dq_ds_kernel(AttnLdsArgs a) {
-  KStampEnd end_(a.ks);
-  constexpr int LDK = Img<DH>::LD, DTW = DH / 64;          // dh tiles per wave
-  constexpr int KPT = 32 * DH / 8 / DQD_NT;                 // 16-B K pieces per thread per chunk (DH = 128: 2)
-  __shared__ __attribute__((aligned(16))) bf16 Ks[2][32 * LDK];
-  __shared__ __attribute__((aligned(16))) bf16 Ss[2][32 * DQD_LDS_S];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
-  const int64_t bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
-  const int T = (int)a.T, q0 = 32 * (int)blockIdx.x;
-  if (q0 >= T) return;
-  const int kend = a.mask_kind == 0 ? min(q0 + 32, T) : T;
-  const int nkc = (kend + 31) / 32;
-  const bf16* Kg = a.k + b * a.T * a.ldk + h * DH;
-  const bf16* Sg = a.ds + (int64_t)bh * a.ds_rows * a.ds_ld + q0;
-  // this thread's pieces: K rows (kr, column chunk kq) and, threads < 128, dS^T row sr columns 8 sq..8 sq + 7
-  typedef __attribute__((ext_vector_type(4))) unsigned u4;
-  u4 kv[KPT], sv = {0u, 0u, 0u, 0u};
-  auto load = [&](int kc) {
-#pragma unroll
-    for (int j = 0; j < KPT; ++j) {
-      const int piece = tid + j * DQD_NT, kr = piece / (DH / 8), kq = piece % (DH / 8);
-      const int key = 32 * kc + kr;
-      kv[j] = *reinterpret_cast<const u4*>(Kg + (int64_t)min(key, T - 1) * a.ldk + 8 * kq);
-      if (key >= T) kv[j] = (u4){0u, 0u, 0u, 0u};
-    }
-    if (tid < 128) {
-      const int sr = tid >> 2, sq = tid & 3, key = 32 * kc + sr;
-      sv = *reinterpret_cast<const u4*>(Sg + (int64_t)min(key, (int)a.ds_rows - 1) * a.ds_ld + 8 * sq);
-      if (key >= T) sv = (u4){0u, 0u, 0u, 0u};
-    }
-  };
-  auto store = [&](int buf) {
-#pragma unroll
-    for (int j = 0; j < KPT; ++j) {
-      const int piece = tid + j * DQD_NT, kr = piece / (DH / 8), kq = piece % (DH / 8);
-      *reinterpret_cast<u4*>(&Ks[buf][kr * LDK + 8 * kq]) = kv[j];
-    }
-    if (tid < 128) *reinterpret_cast<u4*>(&Ss[buf][(tid >> 2) * DQD_LDS_S + 8 * (tid & 3)]) = sv;
-  };
-  f32x4 acc[DTW][2];
-#pragma unroll
-  for (int i = 0; i < DTW; ++i) acc[i][0] = acc[i][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  load(0);
-  store(0);
-  __syncthreads();
-  for (int kc = 0; kc < nkc; ++kc) {
-    const int buf = kc & 1;
-    if (kc + 1 < nkc) load(kc + 1);
-    bf16x8 fk[DTW], fs[2];
-#pragma unroll
-    for (int i = 0; i < DTW; ++i) fk[i] = tr_frag(Ks[buf], LDK, 0, 16 * (DTW * wave + i), lane);
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) fs[qt] = tr_frag(Ss[buf], DQD_LDS_S, 0, 16 * qt, lane);
-#pragma unroll
-    for (int i = 0; i < DTW; ++i)
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt) acc[i][qt] = mfma16(fk[i], fs[qt], acc[i][qt]);
-    if (kc + 1 < nkc) {
-      store(buf ^ 1);
-      __syncthreads();
-    }
-  }
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const int q = q0 + 16 * qt + cl;
-    if (q >= T) continue;
-    bf16* dq = a.dq + (b * a.T + q) * a.lddq + h * DH;
-#pragma unroll
-    for (int i = 0; i < DTW; ++i) {
-      bf4 w;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) w[r] = (bf16)acc[i][qt][r];
-      *reinterpret_cast<bf4*>(dq + 16 * (DTW * wave + i) + 4 * g) = w;
-    }
-  }
 }
 
 // ------------------------------------------------------------------ launchers
@@ -1179,28 +1078,10 @@ static hipError_t bwd_t(AttnLdsArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// dS mode: the dK/dV pass alone on nsplit workgroups per (sequence, head) (dS^T stored), then dQ = dS K
-template <int DH>
-static hipError_t bwd_ds_t(AttnLdsArgs& a, hipStream_t s) {
-  const int nq = (int)cdiv(a.T, 16);
-  AttnLdsArgs akv = a;
-  akv.nsplit = pick_split(a.B * a.H, nq);
-  constexpr int DT = DH / 16;
-  const size_t lds_kv = dkv_lds_bytes<DH>((int)a.T), ext_kv = (size_t)DKV_SLOTS * 2 * DT * 4 * 64 * 2 + 16;
-  akv.use_plan = a.mask_kind == 0 && nq >= 8 && lds_kv + ext_kv <= 160 * 1024 && make_plan(akv, nq, true, DKV_SLOTS);
-  const size_t bkv = lds_kv + (akv.use_plan ? ext_kv : 0);
-  hipLaunchKernelGGL((attn_bwd_dkv_ds_kernel<DH>), dim3((unsigned)(akv.nsplit * a.B * a.H)), dim3(NT), bkv, s, akv);
-  hipLaunchKernelGGL((attn_dq_ds_kernel<DH>), dim3((unsigned)cdiv(a.T, 32), (unsigned)(a.B * a.H)), dim3(DQD_NT), 0, s,
-                     a);
-  return hipGetLastError();
-}
-
 template <int DH>
 static void set_lds_limits() {
   hipFuncSetAttribute((const void*)attn_fwd_lds_kernel<DH>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipFuncSetAttribute((const void*)attn_bwd_lds_kernel<DH>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipFuncSetAttribute((const void*)attn_bwd_dkv_ds_kernel<DH>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                      160 * 1024);
 }
 
 static void init_once() {
@@ -1232,7 +1113,7 @@ hipError_t attn_lds_bwd(int64_t B, int64_t T, int64_t H, int64_t Dh, const void*
                         int64_t ldk, const void* v, int64_t ldv, const void* o, int64_t ldo, const void* dout,
                         int64_t lddo, const float* lse, void* dq, int64_t lddq, void* dk, int64_t lddk, void* dv,
                         int64_t lddv, float scale, int mask_kind, const int64_t* ids, float drop_p, uint64_t seed,
-                        const uint64_t* seed_base, float* delta, hipStream_t s, void* ds) {
+                        const uint64_t* seed_base, float* delta, hipStream_t s) {
   init_once();
   AttnLdsArgs a = {};
   a.B = B; a.T = T; a.H = H;
@@ -1244,17 +1125,7 @@ hipError_t attn_lds_bwd(int64_t B, int64_t T, int64_t H, int64_t Dh, const void*
   a.lse = const_cast<float*>(lse); a.delta = delta; a.scale = scale; a.mask_kind = mask_kind; a.ids = ids;
   a.drop_p = drop_p; a.seed = seed; a.seed_base = seed_base;
   a.ks = kstamp_next(RS_STAMP_ATTN_BWD);
-  if (ds) {
-    a.ds = (bf16*)ds;
-    a.ds_rows = cdiv(T, 16) * 16;
-    a.ds_ld = cdiv(T, 32) * 32;
-    if (Dh == 128) return bwd_ds_t<128>(a, s);
-    if (Dh == 64) return bwd_ds_t<64>(a, s);
-    return hipErrorNotSupported;
-  }
   if (Dh == 128) return bwd_t<128>(a, s);
   if (Dh == 64) return bwd_t<64>(a, s);
   return bwd_t<32>(a, s);
 }
-
-int64_t attn_lds_ds_bytes(int64_t B, int64_t T, int64_t H) { return B * H * cdiv(T, 16) * 16 * cdiv(T, 32) * 32 * 2; }

@@ -260,44 +260,14 @@ def attn_row_delta(B, T, H, Dh, do, o, delta):
     call("rs_attn_row_delta", dtype_code(do), B, T, H, Dh, ptr(do), ld(do), ptr(o), ld(o), ptr(delta), stream())
 
 
-_DS_WS = {}
-_DS_OLD = []
-
-
-def _attn_ds_ws(B, T, H, Dh, device):
-    """The dS workspace of rs_attn_bwd_ds (one per device, grown outside graph capture; None: the merged one-launch
-    backward, rs_attn_bwd).  RS_ATTN_BWD_DS=0 (read per call, for A/B): always the merged launch."""
-    if os.environ.get("RS_ATTN_BWD_DS", "1") == "0":
-        return None
-    n = int(_lib.lib().rs_attn_bwd_ds_bytes(B, T, H, Dh))
-    if n <= 0:
-        return None
-    key = torch.device(device).index or 0
-    buf = _DS_WS.get(key)
-    if buf is None or buf.numel() < n:
-        if torch.cuda.is_current_stream_capturing():
-            return None        # first seen inside a capture: the merged launch (never allocate into a graph pool)
-        # the smaller buffer stays referenced: a graph captured with it keeps writing there on every replay
-        _DS_OLD.append(buf)
-        _DS_WS[key] = buf = torch.empty(n, dtype=torch.uint8, device=device)
-    return buf
-
-
 def attn_bwd(B, T, H, Dh, q, k, v, o, do, lse, dq, dk, dv, scale, mask_kind, ids, drop_p, seed, seed_base, ws,
              delta_in=False):
-    """delta_in: ws already holds delta = rowsum(dO * O) per (b, h, t) (sas_block_out_bwd with o=).  bf16 at
-    Dh 64 / 128: the dS-materialising form (rs_attn_bwd_ds: the dK/dV pass stores dS^T, then dQ = dS K)."""
+    """delta_in: ws already holds delta = rowsum(dO * O) per (b, h, t) (sas_block_out_bwd with o=)."""
     mk = mask_kind | (RS_ATTN_DELTA_IN if delta_in else 0)
-    ds = _attn_ds_ws(B, T, H, Dh, q.device) if q.dtype == torch.bfloat16 else None
     ev = _ev_begin("attn_bwd")
-    if ds is not None:
-        call("rs_attn_bwd_ds", dtype_code(q), B, T, H, Dh, ptr(q), ld(q), ptr(k), ld(k), ptr(v), ld(v), ptr(o), ld(o),
-             ptr(do), ld(do), ptr(lse), ptr(dq), ld(dq), ptr(dk), ld(dk), ptr(dv), ld(dv), scale, mk, ptr(ids),
-             drop_p, seed, ptr(seed_base), ptr(ws), ptr(ds), stream())
-    else:
-        call("rs_attn_bwd", dtype_code(q), B, T, H, Dh, ptr(q), ld(q), ptr(k), ld(k), ptr(v), ld(v), ptr(o), ld(o),
-             ptr(do), ld(do), ptr(lse), ptr(dq), ld(dq), ptr(dk), ld(dk), ptr(dv), ld(dv), scale, mk, ptr(ids),
-             drop_p, seed, ptr(seed_base), ptr(ws), stream())
+    call("rs_attn_bwd", dtype_code(q), B, T, H, Dh, ptr(q), ld(q), ptr(k), ld(k), ptr(v), ld(v), ptr(o), ld(o),
+         ptr(do), ld(do), ptr(lse), ptr(dq), ld(dq), ptr(dk), ld(dk), ptr(dv), ld(dv), scale, mk, ptr(ids),
+         drop_p, seed, ptr(seed_base), ptr(ws), stream())
     _ev_end(ev)
 
 
