@@ -86,9 +86,21 @@ def ce_loss(logits, labels):
     return F.cross_entropy(logits.reshape(-1, logits.shape[-1]), labels.reshape(-1), ignore_index=0)
 
 
-def loss_and_grads(P, x_ids, labels, num_blocks, heads, p=0.0, hp=0.0, masks=None):
+def loss_and_grads(P, x_ids, labels, num_blocks, heads, p=0.0, hp=0.0, masks=None, labelled_only=False):
+    """(loss, logits, {name: gradient}).  labelled_only: the output layer on the labelled rows alone (logits
+    (R, V+1) in row-major order of the labelled positions) -- the same loss and gradients, since CrossEntropyLoss's
+    ignore_index rows (BS/trainers/bert.py:36-40) neither enter the mean nor receive a logit gradient; what a 1M-class
+    vocabulary needs to stay within the CPU's memory and seconds (pinned against the full form on the goldens,
+    tests/test_oracle.py)."""
     leaves = {k: v.detach().clone().requires_grad_(True) for k, v in P.items()}
-    logits = forward(leaves, x_ids, num_blocks, heads, p, hp, masks)
-    loss = ce_loss(logits, labels)
+    if labelled_only:
+        h = encode(leaves, x_ids, num_blocks, heads, p, hp, masks)
+        lab = labels.reshape(-1)
+        rows = torch.nonzero(lab != 0).flatten()
+        logits = h.reshape(-1, h.shape[-1])[rows] @ leaves["out.weight"].T + leaves["out.bias"]
+        loss = F.cross_entropy(logits, lab[rows])
+    else:
+        logits = forward(leaves, x_ids, num_blocks, heads, p, hp, masks)
+        loss = ce_loss(logits, labels)
     loss.backward()
     return loss.detach(), logits.detach(), {k: v.grad for k, v in leaves.items()}

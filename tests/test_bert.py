@@ -148,7 +148,7 @@ def _bert(V, T, d, L, h, p, dtype, seed):
     return model_factory(a)
 
 
-def _bert_step_vs_oracle(m, tok, lab, L, h, p, cap=None, seed=4242):
+def _bert_step_vs_oracle(m, tok, lab, L, h, p, cap=None, seed=4242, labelled_only=False):
     """One fused bf16 training step's loss and gradient (FusedTrainStep._compute, before the optimizer) against the
     fp64 oracle replaying the step's dropout masks.  Returns (loss, oracle loss, {name: norm-relative error})."""
     from oracle import bert as obert
@@ -166,7 +166,8 @@ def _bert_step_vs_oracle(m, tok, lab, L, h, p, cap=None, seed=4242):
     masks = {k: v.cpu().double() for k, v in bert_masks(tr.engine, B, T, sb).items()} if p > 0 else None
     P = {k: v.detach().cpu().double() for k, v in m.state_dict().items()}
     torch.set_num_threads(16)
-    l64, _, g64 = obert.loss_and_grads(P, tok.cpu(), lab.cpu(), L, h, p=p, hp=p, masks=masks)
+    l64, _, g64 = obert.loss_and_grads(P, tok.cpu(), lab.cpu(), L, h, p=p, hp=p, masks=masks,
+                                       labelled_only=labelled_only)
     scale = max(float(g.norm()) for g in g64.values())
     worst = {}
     for k, r in g64.items():
@@ -234,6 +235,27 @@ def test_bert_cfg5_bench_step_matches_oracle():
     assert 0 < n_lab <= 128
     loss, l64, worst = _bert_step_vs_oracle(m, tok, lab, L, 2, 0.1, cap=128)
     print("cfg5 bf16 step: loss", loss, l64, "worst", max(worst.items(), key=lambda kv: kv[1]))
+    assert abs(loss - l64) < FWD_TOL_BF16 * abs(l64), (loss, l64)
+    bad = {k: v for k, v in worst.items() if v >= GRAD_TOL_BF16}
+    assert not bad, bad
+
+
+@pytest.mark.gpu
+def test_bert_cfg5_bench_cap_step_matches_oracle():
+    """The same 1M-item step at the bench's own batch (64) and labelled-row cap (1,792): ~1,450 labelled rows, so
+    the head's row tiles, the dE / dh GEMMs' row dimension and the token table's inverted index run at the
+    benchmarked size (the batch-1 test above fits one tile).  The fp64 oracle applies the output layer to the
+    labelled rows only (oracle.bert.loss_and_grads(labelled_only=True): the same loss and gradients, pinned against
+    its full form on the goldens), which keeps its logits at R x 1M (~12 GB fp64; ~60 GB host memory in all)."""
+    import rbm_amd.data as synth
+    V, T, B, L = 1_000_000, 200, 64, 4
+    m = _bert(V, T, 256, L, 2, 0.1, "bf16", seed=5)
+    rng = np.random.default_rng(8)
+    tok, lab = (torch.from_numpy(t).cuda() for t in synth.bert_batch(rng, B, T, V, mask_prob=0.2))
+    n_lab = int((lab != 0).sum())
+    assert 1024 < n_lab <= 1792, n_lab
+    loss, l64, worst = _bert_step_vs_oracle(m, tok, lab, L, 2, 0.1, cap=1792, labelled_only=True)
+    print("cfg5 bf16 step, rows", n_lab, ": loss", loss, l64, "worst", max(worst.items(), key=lambda kv: kv[1]))
     assert abs(loss - l64) < FWD_TOL_BF16 * abs(l64), (loss, l64)
     bad = {k: v for k, v in worst.items() if v >= GRAD_TOL_BF16}
     assert not bad, bad

@@ -56,6 +56,25 @@ def test_bert_oracle_matches_reference(name):
         assert rel(g, ref) < 1e-4, k
 
 
+@pytest.mark.parametrize("name", ["bert_tiny", "bert_mid"])
+def test_bert_oracle_labelled_rows_head_equals_full(name):
+    """The oracle's labelled-rows output layer (what the 1M-class tests use) against its full form and the
+    reference's goldens: same loss, logits of the labelled rows, every gradient."""
+    z = load_golden(name)
+    P = golden_params(z)
+    tok, lab = torch.from_numpy(z["tokens"]), torch.from_numpy(z["labels"])
+    loss, logits, grads = obert.loss_and_grads(P, tok, lab, int(z["L"]), int(z["h"]), labelled_only=True)
+    full = z["logits"].reshape(-1, z["logits"].shape[-1])[lab.reshape(-1).numpy() != 0]
+    assert logits.shape == full.shape and rel(logits, full) < 1e-5
+    assert abs(loss.item() - float(z["loss"])) < 1e-5 * max(1.0, float(z["loss"]))
+    _, _, g_full = obert.loss_and_grads(P, tok, lab, int(z["L"]), int(z["h"]))
+    for k, g in grads.items():
+        if float(g_full[k].norm()) == 0:
+            assert float(g.norm()) == 0, k
+            continue
+        assert rel(g, g_full[k]) < 1e-5, k     # fp32 parameters: the summation order of the head's reductions
+
+
 def test_adam_oracle_matches_torch():
     torch.manual_seed(0)
     p0 = [torch.randn(7, 5), torch.randn(11)]
