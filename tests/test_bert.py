@@ -205,14 +205,17 @@ def test_bert_cfg3_bench_step_matches_oracle():
     """BASELINE configs[2] at its benchmarked shape and dtype: BERT4Rec, 26,744 items, T = 200, d = 256, 4 blocks,
     2 heads, dropout 0.1 at every site (injected into the oracle), bf16 fused training step -- grouped weight
     gradients (rs_wgrad_grouped), LayerNorm-backward dropout fusion, delta-in attention backward, the
-    vocabulary-tile-stationary head -- at a reduced batch (B = 4; the kernels' per-row work is batch-independent)
-    against the fp64 oracle (BS/models/bert.py:10,16, BS/trainers/bert.py:30-41)."""
+    vocabulary-tile-stationary head -- at the bench's batch (64) and labelled-row cap (1,792) against the fp64
+    oracle (BS/models/bert.py:10,16, BS/trainers/bert.py:30-41; its output layer on the labelled rows only, the same
+    loss and gradients)."""
     import rbm_amd.data as synth
     m = _bert(26744, 200, 256, 4, 2, 0.1, "bf16", seed=3)
     rng = np.random.default_rng(7)
-    tok, lab = (torch.from_numpy(t).cuda() for t in synth.bert_batch(rng, 4, 200, 26744, mask_prob=0.2))
-    loss, l64, worst = _bert_step_vs_oracle(m, tok, lab, 4, 2, 0.1, cap=256)
-    print("cfg3 bf16 step: loss", loss, l64, "worst", max(worst.items(), key=lambda kv: kv[1]))
+    tok, lab = (torch.from_numpy(t).cuda() for t in synth.bert_batch(rng, 64, 200, 26744, mask_prob=0.2))
+    n_lab = int((lab != 0).sum())
+    assert 1024 < n_lab <= 1792, n_lab
+    loss, l64, worst = _bert_step_vs_oracle(m, tok, lab, 4, 2, 0.1, cap=1792, labelled_only=True)
+    print("cfg3 bf16 step, rows", n_lab, ": loss", loss, l64, "worst", max(worst.items(), key=lambda kv: kv[1]))
     assert abs(loss - l64) < FWD_TOL_BF16 * abs(l64), (loss, l64)
     bad = {k: v for k, v in worst.items() if v >= GRAD_TOL_BF16}
     assert not bad, bad
