@@ -794,7 +794,7 @@ namespace ig {
 // ahead by the first FB threads (their entry loads two batches ahead), and every column thread issues all FB of its
 // value loads before summing them in order -- one round trip per batch.  A Zipf-hot item holds thousands of
 // entries; one dependent load chain per entry made that row's workgroup the whole launch (cfg2 fp32: 1.58 ms of a
-// 3.7 ms step).  Same order, same arithmetic: the same bits as that chain.
+// 3.7 ms step).  Same summation order and per-term arithmetic as that chain.
 constexpr int FB = 64;
 __global__ __launch_bounds__(256) void item_rows_f32_kernel(GradArgs a, const float* __restrict__ dx,
                                                             const float* __restrict__ f, int64_t d) {
