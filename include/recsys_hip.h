@@ -572,7 +572,8 @@ int rs_item_grad_marked(const void* ws, int nsrc, int64_t rows, int64_t table_ro
                         float scale, float drop_p, uint64_t salt, const uint64_t* seed_base, const void* f,
                         const float* w1, const float* w2, float* dtable, uint8_t* row_marks, uint8_t* epoch_out,
                         void* stream);
-/* The same for fp32 dx, f (the fp32 parity path, any d): one workgroup per table row, entries in sorted order. */
+/* The same for fp32 dx, f (the fp32 parity path, any d): each key run summed in sorted-entry order inside 32-entry
+ * chunks, a run crossing chunks as its chunk partials in chunk order (the index workspace's partial region). */
 int rs_item_grad_f32(const void* ws, int nsrc, int64_t rows, int64_t table_rows, int64_t d, const float* dx, float scale,
                      float drop_p, uint64_t salt, const uint64_t* seed_base, const float* f, const float* w1,
                      const float* w2, float* dtable, void* stream);

@@ -787,99 +787,115 @@ int rs_item_index_build(int nsrc, const int64_t* keys0, const int64_t* keys1, co
 }  // extern "C"
 
 namespace ig {
-// fp32 parity path: one workgroup per table row (key v >= 1), its entries summed in the index's sorted order --
-// deterministic like the bf16 chunk kernels (which the fp32 path's float-atomic scatter was not: each fp32 run of
-// a training curve was its own chaotic draw), with the atomic kernels' per-term arithmetic (embedding.hip).
-// The run is walked in batches of FB entries: the batch's (row, source, weight) are decoded into LDS one batch
-// ahead by the first FB threads (their entry loads two batches ahead), and every column thread issues all FB of its
-// value loads before summing them in order -- one round trip per batch.  A Zipf-hot item holds thousands of
-// entries; one dependent load chain per entry made that row's workgroup the whole launch (cfg2 fp32: 1.58 ms of a
-// 3.7 ms step).  Same summation order and per-term arithmetic as that chain.
-constexpr int FB = 64;
-__global__ __launch_bounds__(256) void item_rows_f32_kernel(GradArgs a, const float* __restrict__ dx,
-                                                            const float* __restrict__ f, int64_t d) {
-  __shared__ int sm_m[2][FB];
-  __shared__ int sm_src[2][FB];
-  __shared__ float sm_w[2][FB];
+// fp32 parity path, the bf16 path's chunk structure with fp32 rows and any width d: one workgroup per chunk of CH
+// sorted entries sums each key run inside the chunk in entry order (the per-term arithmetic of the atomic kernels,
+// embedding.hip); a run wholly inside the chunk goes to its table row (the row's only writer), a run crossing the
+// chunk's edge leaves a partial in the chunk's slot (0: the run at its head, 1: the run at its tail), and
+// item_span_f32_kernel adds a crossing run's partials in chunk order.  Deterministic -- the fp32 path's earlier
+// float-atomic scatter made every fp32 training curve its own chaotic draw -- and parallel over chunks: the previous
+// form (one workgroup per table row, its entries in one sequential chain) spent 0.7-1.6 ms of cfg2's fp32 step on
+// the Zipf-hottest item's ~6,000 entries.
+__device__ __forceinline__ float f32_term(const GradArgs& a, const float* __restrict__ dx, const float* __restrict__ f,
+                                          int src, int64_t m, float w, float raw, int64_t d, int64_t c, uint64_t seed) {
+  if (src == 0) {
+    float t = raw * w;                      // dx * scale
+    if (a.drop_p > 0.f) t *= drop_mul(a.drop_p, seed, (uint64_t)(m * d + c));
+    return t;
+  }
+  return w * raw;                           // w1[m] * f or w2[m] * f
+}
+
+__global__ __launch_bounds__(256) void item_chunk_f32_kernel(GradArgs a, const float* __restrict__ dx,
+                                                             const float* __restrict__ f, int64_t d) {
+  __shared__ uint32_t skey[CH + 2];   // [0]: the key before the chunk, [1 .. cnt]: the chunk's, [cnt + 1]: the next
+  __shared__ int sm_m[CH];
+  __shared__ int sm_src[CH];
+  __shared__ float sm_w[CH];
   const int tid = threadIdx.x;
-  const int64_t v = (int64_t)blockIdx.x + 1;
-  int64_t b, e;                            // [first entry with key >= v, first with key > v)
-  if (a.start) {
-    b = a.start[v];
-    e = a.start[v + 1];
-  } else {
-    b = 0;
-    e = a.n;
-    for (int64_t hi = a.n; b < hi;) {
-      const int64_t mid = (b + hi) >> 1;
-      if ((int64_t)a.sk[mid] < v) b = mid + 1;
-      else hi = mid;
+  const int64_t chunk = blockIdx.x, base = chunk * CH;
+  const int cnt = (int)min((int64_t)CH, a.n - base);
+  if (tid < cnt) {
+    skey[tid + 1] = a.sk[base + tid];
+    const uint32_t ent = a.sv[base + tid];
+    const int src = (int)(ent / (uint64_t)a.rows);
+    const int64_t m = (int64_t)ent - (int64_t)src * a.rows;
+    sm_m[tid] = (int)m;
+    sm_src[tid] = src;
+    sm_w[tid] = src == 0 ? a.scale : (src == 1 ? a.w1[m] : a.w2[m]);
+  }
+  if (tid == CH) skey[0] = base > 0 ? a.sk[base - 1] : 0xffffffffu;
+  if (tid == CH + 1) skey[cnt + 1] = base + cnt < a.n ? a.sk[base + cnt] : 0xffffffffu;
+  __syncthreads();
+  const uint64_t seed = eff_seed(a.salt, a.seed_base);
+  for (int64_t c = tid; c < d; c += blockDim.x) {
+    float raw[CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      raw[j] = 0.f;
+      if (j < cnt) {
+        const int64_t m = sm_m[j];
+        raw[j] = sm_src[j] == 0 ? dx[m * d + c] : f[m * d + c];
+      }
     }
-    for (int64_t lo = b; lo < e;) {
+    float acc = 0.f;
+    int rs = 0;                               // the current run's first entry in the chunk
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      if (j < cnt) {
+        acc += f32_term(a, dx, f, sm_src[j], sm_m[j], sm_w[j], raw[j], d, c, seed);
+        const uint32_t k = skey[j + 1];
+        if (j + 1 == cnt || skey[j + 2] != k) {        // the run ends at entry j of this chunk
+          if (k != 0) {                                 // padding_idx 0: no gradient
+            const bool from_before = rs == 0 && skey[0] == k;
+            const bool past_end = j + 1 == cnt && skey[cnt + 1] == k;
+            if (!from_before && !past_end) a.dtable[(int64_t)k * d + c] += acc;
+            else a.part[(chunk * 2 + (rs == 0 ? 0 : 1)) * d + c] = acc;
+          }
+          acc = 0.f;
+          rs = j + 1;
+        }
+      }
+    }
+  }
+}
+
+// one wave per chunk: the chunk holding the first entry of a run that continues past it sums the run's partials in
+// chunk order and adds them to the table row
+__global__ __launch_bounds__(256) void item_span_f32_kernel(GradArgs a, int64_t nchunks, int64_t d) {
+  const int lane = threadIdx.x & 63;
+  const int64_t ch = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (ch >= nchunks) return;
+  const int64_t base = ch * CH, last = min(a.n, base + CH) - 1;
+  const uint32_t k = a.sk[last];
+  if (k == 0 || last + 1 >= a.n || a.sk[last + 1] != k) return;     // no run continues past this chunk
+  const bool head_here = a.sk[base] != k;
+  if (!head_here && base > 0 && a.sk[base - 1] == k) return;         // the run started in an earlier chunk
+  int64_t e;                                                         // first entry past the run
+  if (a.start) {
+    e = a.start[k + 1];
+  } else {
+    int64_t lo = last + 1;
+    e = a.n;
+    while (lo < e) {
       const int64_t mid = (lo + e) >> 1;
-      if ((int64_t)a.sk[mid] <= v) lo = mid + 1;
+      if (a.sk[mid] <= k) lo = mid + 1;
       else e = mid;
     }
   }
-  if (b >= e) return;
-  const uint64_t seed = eff_seed(a.salt, a.seed_base);
-  const int nb = (int)((e - b + FB - 1) / FB);
-  // decoder thread j < FB: entry j of batch `bat` -> (row, source, weight) in LDS slot bat & 1
-  auto decode = [&](uint32_t ent, int bat) {
-    const int src = (int)(ent / (uint64_t)a.rows);
-    const int64_t m = (int64_t)ent - (int64_t)src * a.rows;
-    sm_m[bat & 1][tid] = (int)m;
-    sm_src[bat & 1][tid] = src;
-    sm_w[bat & 1][tid] = src == 0 ? a.scale : (src == 1 ? a.w1[m] : a.w2[m]);
-  };
-  for (int64_t c0 = 0; c0 < d; c0 += blockDim.x) {
-    const int64_t c = c0 + tid;
-    uint32_t nxt = 0;                      // decoder: the entry of batch 1
-    if (tid < FB) {
-      if (b + tid < e) decode(a.sv[b + tid], 0);
-      if (nb > 1 && b + FB + tid < e) nxt = a.sv[b + FB + tid];
-    }
-    __syncthreads();
-    float acc = 0.f;
-    for (int bat = 0; bat < nb; ++bat) {
-      const int64_t k0 = b + (int64_t)bat * FB;
-      const int n = (int)min((int64_t)FB, e - k0);
-      const int sl = bat & 1;
-      float raw[FB];
+  const int64_t cl = (e - 1) / CH;                                   // the run's last chunk
+  const int own = head_here ? 1 : 0;
+  for (int64_t c = lane; c < d; c += 64) {
+    float acc = a.part[(ch * 2 + own) * d + c];
+    int64_t cc = ch + 1;
+    for (; cc + 7 <= cl; cc += 8) {
+      float u[8];
 #pragma unroll
-      for (int j = 0; j < FB; ++j) {
-        raw[j] = 0.f;
-        if (j < n && c < d) {
-          const int64_t m = sm_m[sl][j];
-          raw[j] = sm_src[sl][j] == 0 ? dx[m * d + c] : f[m * d + c];
-        }
-      }
-      // decoder: batch bat + 1 into the other slot (its readers finished at the barrier that ended batch bat - 1),
-      // batch bat + 2's entries requested
-      if (tid < FB && bat + 1 < nb) {
-        if (k0 + FB + tid < e) decode(nxt, bat + 1);
-        nxt = (bat + 2 < nb && k0 + 2 * FB + tid < e) ? a.sv[k0 + 2 * FB + tid] : 0u;
-      }
-      if (c < d) {
+      for (int t = 0; t < 8; ++t) u[t] = a.part[((cc + t) * 2) * d + c];
 #pragma unroll
-        for (int j = 0; j < FB; ++j) {
-          if (j < n) {
-            const int64_t m = sm_m[sl][j];
-            float t;
-            if (sm_src[sl][j] == 0) {
-              t = raw[j] * sm_w[sl][j];
-              if (a.drop_p > 0.f) t *= drop_mul(a.drop_p, seed, (uint64_t)(m * d + c));
-            } else {
-              t = sm_w[sl][j] * raw[j];
-            }
-            acc += t;
-          }
-        }
-      }
-      __syncthreads();
+      for (int t = 0; t < 8; ++t) acc += u[t];
     }
-    if (c < d) a.dtable[v * d + c] += acc;
-    __syncthreads();
+    for (; cc <= cl; ++cc) acc += a.part[(cc * 2) * d + c];
+    a.dtable[(int64_t)k * d + c] += acc;
   }
 }
 }  // namespace ig
@@ -945,8 +961,11 @@ int rs_item_grad_f32(const void* ws, int nsrc, int64_t rows, int64_t table_rows,
                              a, L))
     return e;
   if (d <= 0 || table_rows < 2) return table_rows < 2 ? 0 : RS_ERR_ARG;
-  hipLaunchKernelGGL(ig::item_rows_f32_kernel, dim3((unsigned)(table_rows - 1)), dim3(d >= 256 ? 256 : (d >= 128 ? 128 : 64)),
-                     0, (hipStream_t)stream, a, dx, f, d);
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t nch = cdiv(L.n, ig::CH);
+  hipLaunchKernelGGL(ig::item_chunk_f32_kernel, dim3((unsigned)nch), dim3(d > 128 ? 256 : (d > 64 ? 128 : 64)), 0, s,
+                     a, dx, f, d);
+  hipLaunchKernelGGL(ig::item_span_f32_kernel, dim3((unsigned)cdiv(nch, 4)), dim3(256), 0, s, a, nch, d);
   return (int)hipGetLastError();
 }
 

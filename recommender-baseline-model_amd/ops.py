@@ -715,7 +715,7 @@ def item_grad(ws, nsrc, rows, dx, scale, drop_p, salt, seed_base, f, w1, w2, dta
              ptr(f) if f is not None else None, ptr(w1) if w1 is not None else None,
              ptr(w2) if w2 is not None else None, ptr(dtable), ptr(marks[0]), ptr(marks[1]), stream())
         return
-    # fp32 (the parity path): one workgroup per table row; bf16: the chunked kernels (d in {64, 128, 256})
+    # fp32 (the parity path): chunk + span kernels at any width; bf16: the LDS chunk kernels (d in {64, 128, 256})
     call("rs_item_grad_f32" if dx.dtype == torch.float32 else "rs_item_grad", ptr(ws), nsrc, rows, table_rows, d,
          ptr(dx), scale, drop_p, salt, ptr(seed_base),
          ptr(f) if f is not None else None, ptr(w1) if w1 is not None else None,

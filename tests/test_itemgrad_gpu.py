@@ -125,3 +125,41 @@ def test_item_index_is_the_stable_sort(nsrc, M, V1, pad, path):
     ops.item_index_build(dev, V1, d, ws2)
     sk2, sv2, _, _ = ops.item_index_view(nsrc, M, V1, d, ws2)
     assert torch.equal(sk2, sk) and torch.equal(sv2, sv)
+
+
+# the fp32 parity path (rs_item_grad_f32: chunk sums + chunk-order span sums, any width): Zipf-hot keys spanning
+# many chunks, padding keys, odd widths, both index paths
+@pytest.mark.parametrize("M,V1,d,p", [(25600, 3417, 128, 0.2), (25600, 3417, 50, 0.0), (777, 50, 256, 0.1),
+                                      (64, 5, 96, 0.0), (6400, 54543, 128, 0.2), (5000, 300, 300, 0.0)])
+def test_item_grad_f32_matches_atomic_scatter(M, V1, d, p):
+    import rbm_amd  # noqa: F401
+    from rbm_amd import ops
+    ids, pos, neg, dx, f, dpl, dnl = _inputs(M, V1, d, seed=M + d + 1)
+    dx, f = dx.float(), f.float()
+    T = 200 if M % 200 == 0 else M
+    seed_base = torch.full((1,), 7, dtype=torch.int64, device="cuda")
+    salt, scale = 12345, float(np.sqrt(d))
+    base = torch.randn(V1, d, device="cuda")
+    ours = base.clone()
+    ws = torch.empty(ops.item_index_ws_bytes(3, M, V1, d), dtype=torch.uint8, device="cuda")
+    ops.item_index_build([ids, pos, neg], V1, d, ws)
+    ops.item_grad(ws, 3, M, dx, scale, p, salt, seed_base, f, dpl, dnl, ours)
+    ref = base.clone()
+    ops.embed_bwd(0, ids, T, dx, scale, p, salt, seed_base, ref, None)
+    E = torch.randn(V1, d, device="cuda")
+    df = torch.empty(M, d, device="cuda")
+    ops.sampled_logits_bwd(f, E, pos, neg, dpl, dnl, df, ref)
+    torch.cuda.synchronize()
+    assert rel(ours.cpu().numpy(), ref.cpu().numpy()) < 1e-5   # both fp32 sums, different orders
+    assert torch.equal(ours[0], base[0])                         # padding row untouched
+    if p == 0.0:
+        t = base.double().clone()
+        for k, w, src in ((ids, None, dx), (pos, dpl, f), (neg, dnl, f)):
+            rows = src.double() * (scale if w is None else w.double()[:, None])
+            keep = k != 0
+            t.index_add_(0, k[keep], rows[keep])
+        assert rel(ours.cpu().numpy(), t.cpu().numpy()) < 1e-5
+    again = base.clone()
+    ops.item_index_build([ids, pos, neg], V1, d, ws)
+    ops.item_grad(ws, 3, M, dx, scale, p, salt, seed_base, f, dpl, dnl, again)
+    assert torch.equal(again, ours)                              # reproducible bit for bit
