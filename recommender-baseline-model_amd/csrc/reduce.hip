@@ -68,8 +68,18 @@ __global__ __launch_bounds__(256) void reduce_slabs_scalar_kernel(const float* _
   const int col = threadIdx.x % C, grp = threadIdx.x / C;
   const int64_t i = (int64_t)blockIdx.x * C + col;
   float s = 0.f;
-  if (i < n)
-    for (int z = grp; z < splits; z += G) s += slab[(int64_t)z * n + i];
+  if (i < n) {
+    // eight splits' loads in flight, summed in the same order (z = grp, grp + G, ...): the same bits as one at a time
+    int z = grp;
+    for (; z + 7 * G < splits; z += 8 * G) {
+      float u[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) u[t] = slab[(int64_t)(z + t * G) * n + i];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) s += u[t];
+    }
+    for (; z < splits; z += G) s += slab[(int64_t)z * n + i];
+  }
   __shared__ float red[G][C];
   red[grp][col] = s;
   __syncthreads();
