@@ -480,8 +480,12 @@ __global__ __launch_bounds__(NTH, 1) void pp_kernel(Args a) {
     }
   }
   // flat item f (in processing order) -> (local vocabulary tile, row tile)
-  auto item_vt = [&](int f) { const int ff = f + rot < F ? f + rot : f + rot - F; return ff / nloc; };
-  auto item_u = [&](int f) { const int ff = f + rot < F ? f + rot : f + rot - F; return ff - (ff / nloc) * nloc; };
+  // ff / nloc by a multiply-shift (nloc is the workgroup's constant; exact while ff * nloc < 2^40, i.e. always here:
+  // ff < F = tiles x nloc) instead of an integer division sequence ~10 times per interval per wave
+  const uint64_t dmag = (1ull << 40) / (uint64_t)nloc + 1;
+  auto div_nloc = [&](int ff) { return (int)(((uint64_t)ff * dmag) >> 40); };
+  auto item_vt = [&](int f) { const int ff = f + rot < F ? f + rot : f + rot - F; return div_nloc(ff); };
+  auto item_u = [&](int f) { const int ff = f + rot < F ? f + rot : f + rot - F; return ff - div_nloc(ff) * nloc; };
 
   // items fa, fa + 1 -> h buffers fa % NBUF, (fa + 1) % NBUF: 2 * PIECES DMA pieces dealt over the 8 waves.  A
   // wave's pieces j all have j = wave (mod 8), so its lanes' (row in piece, swizzled chunk) are fixed: lane row
@@ -638,14 +642,23 @@ __global__ __launch_bounds__(NTH, 1) void pp_kernel(Args a) {
       const float scr = le == -2 ? 0.f : sc;
       const int64_t offl = (int64_t)le - vb;             // the label's entry among this lane's rows
       const int off = le < 0 || offl < 0 || offl >= 64 ? -1 : (int)offl;
+      // element pairs on packed FMA / add / mul (the same operations per element, so the same bits)
+      typedef __attribute__((ext_vector_type(2))) float f2;
+      const f2 l2 = {1.4426950408889634f, 1.4426950408889634f}, nl = {-Ll, -Ll}, s2 = {scr, scr};
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         bf4 o;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float ea = __builtin_fmaf(acc[i][j][r], 1.4426950408889634f, -Ll);
-          const float e = VPP_EXPT == 1 ? ea : __builtin_amdgcn_exp2f(ea);
-          o[r] = (bf16)((e - (off == 16 * i + r ? 1.f : 0.f)) * scr);
+        for (int r = 0; r < 4; r += 2) {
+          const f2 a = {acc[i][j][r], acc[i][j][r + 1]};
+          const f2 ea = __builtin_elementwise_fma(a, l2, nl);
+          f2 e;
+          e.x = VPP_EXPT == 1 ? ea.x : __builtin_amdgcn_exp2f(ea.x);
+          e.y = VPP_EXPT == 1 ? ea.y : __builtin_amdgcn_exp2f(ea.y);
+          const f2 oh = {off == 16 * i + r ? 1.f : 0.f, off == 16 * i + r + 1 ? 1.f : 0.f};
+          const f2 t = (e - oh) * s2;
+          o[r] = (bf16)t.x;
+          o[r + 1] = (bf16)t.y;
         }
         *reinterpret_cast<bf4*>(st + (16 * j + cl) * SLD + 16 * i + 4 * g) = o;
       }
