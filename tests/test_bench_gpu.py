@@ -36,12 +36,13 @@ def test_bench_json_line(config):
     assert cpu["kind"] == "port" and cpu["value"] > 0 and cpu["cores"] >= 1
 
 
-def test_bench_two_ranks_gloo():
-    """`bench.py --gpus 2` started alone launches both data-parallel ranks itself (here: two processes on one GPU over
-    gloo; the driver's SCALE runs use RCCL on one GPU per rank): one JSON line, the live world size, the replicas'
-    parameters equal after the warmup steps, the whole-job value over both ranks."""
+@pytest.mark.parametrize("n", [2, 8])
+def test_bench_ranks_gloo(n):
+    """`bench.py --gpus N` started alone launches its data-parallel ranks itself (here: N processes on one GPU over
+    gloo, N = 8 the scaling run's rank count; the driver's SCALE runs use RCCL on one GPU per rank): one JSON line,
+    the live world size, the replicas' parameters equal after the warmup steps, the whole-job value over all ranks."""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--dist-backend", "gloo",
                         "--config", "cfg2", "--steps", "4", "--warmup", "2", "--roofline-replays", "2"],
                        capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -49,7 +50,7 @@ def test_bench_two_ranks_gloo():
     assert len(lines) == 1, r.stdout[-2000:]
     d = json.loads(lines[0])
     assert REQUIRED <= set(d), REQUIRED - set(d)
-    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 256
+    assert d["n_gpus"] == n and d["config"]["parallelism"] == f"dp{n}" and d["config"]["global_batch"] == 128 * n
     assert d["dp"]["replicas_equal_after_warmup"] is True and d["dp"]["backend"] == "gloo"
-    assert abs(d["value"] - 256 / (d["ms_per_step"] * 1e-3)) < 0.01 * d["value"]
+    assert abs(d["value"] - 128 * n / (d["ms_per_step"] * 1e-3)) < 0.01 * d["value"]
     assert d["cpu_baseline"] is None                          # rank 0 at N = 1 only

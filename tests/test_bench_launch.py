@@ -1,7 +1,7 @@
 """bench.py's rank launcher (CPU): `bench.py --gpus N` without a torchrun environment starts N data-parallel ranks
 itself, every rank joins one process group of the launched size, and exactly one line (rank 0's) reports the live
 world size.  Under a launcher, WORLD_SIZE must equal --gpus.  The GPU half (the real step over gloo on one GPU) is
-tests/test_bench_gpu.py::test_bench_two_ranks_gloo."""
+tests/test_bench_gpu.py::test_bench_ranks_gloo."""
 import json
 import os
 import subprocess

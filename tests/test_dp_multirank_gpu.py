@@ -214,14 +214,16 @@ def _grad_worker(rank, world, port, kind, dtype, overlap, out_dir):
 @pytest.mark.parametrize("kind,dtype,overlap,world", [("sas", "fp32", True, 2), ("sas", "bf16", True, 2),
                                                       ("sas", "bf16", False, 2), ("bert", "fp32", True, 2),
                                                       ("bert", "bf16", True, 2), ("sas", "fp32", True, 4),
-                                                      ("sas", "bf16", True, 3), ("bert", "bf16", True, 3)])
+                                                      ("sas", "bf16", True, 3), ("bert", "bf16", True, 3),
+                                                      ("sas", "bf16", True, 8), ("bert", "bf16", True, 8)])
 def test_multi_rank_gradient_equals_oracle(tmp_path, kind, dtype, overlap, world):
     """fp32: the exchanged gradient within the parity bars of the single-device tests (loss 1e-5, every gradient
     tensor 1e-4 norm-relative: the reference's own fp32-vs-fp64 drift is 1e-4 - 1.7e-3); bf16: the bars of the bf16
     single-device oracle tests (SAS: conftest.check_bf16_grads against the bf16-storage emulation and the exact math;
     BERT: 3e-2 per tensor, test_bert.py GRAD_TOL_BF16).  The attention key bias has an analytically zero gradient:
-    held against the global gradient scale.  Two ranks and three / four (processes on one GPU over gloo): with more
-    than two ranks the all-reduce's summation order is no longer a + b, and every rank must still hold the same bits."""
+    held against the global gradient scale.  Two ranks and three / four / eight (processes on one GPU over gloo; eight
+    = the scaling run's rank count on the benchmarked path): with more than two ranks the all-reduce's summation order
+    is no longer a + b, and every rank must still hold the same bits."""
     from conftest import check_bf16_grads, rel
     mp.spawn(_grad_worker, args=(world, _free_port(), kind, dtype, overlap, str(tmp_path)), nprocs=world, join=True)
     rs = [torch.load(tmp_path / f"g{r}.pt", weights_only=True) for r in range(world)]
